@@ -1,0 +1,109 @@
+/*
+ * flr.h — C ABI of the MI355X-native federated-round engine (gfx950).
+ *
+ * Every entry point takes plain device pointers, element counts and a
+ * hipStream_t passed as `void*` (NULL = the legacy default stream).  Nothing
+ * here allocates: scratch space is caller-provided (query the size with the
+ * matching *_workspace function).  Calls are stream-ordered and return as soon
+ * as the work is enqueued.  Results are deterministic: fixed reduction order,
+ * no float atomics, so 1/2/4/8-GPU runs give bit-identical outputs.
+ *
+ * Each function names the reference interface it replaces
+ * (Shashank8834/multimodal-fl-security, paths relative to its repo root).
+ *
+ * Matrix convention ("client matrix"): X is K rows (clients, in global client
+ * order) × P fp32 coordinates (the client's parameters flattened in
+ * `model.parameters()` order, krum.py:55-57), row stride `ldx` elements.
+ */
+#ifndef FLR_H
+#define FLR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define FLR_OK 0
+#define FLR_ERR_ARG (-1)          /* invalid argument (shape, null pointer) */
+#define FLR_ERR_HIP (-2)          /* a HIP runtime call or launch failed    */
+#define FLR_ERR_UNSUPPORTED (-3)  /* shape outside what the kernels handle   */
+#define FLR_ERR_WORKSPACE (-4)    /* workspace too small or misaligned       */
+#define FLR_ERR_KRUM_N (-5)       /* n < 2f+3 (krum.py:153-157)             */
+
+const char* flr_version(void);
+const char* flr_status_string(int status);
+/* Last HIP error string recorded by a failing call on this thread. */
+const char* flr_last_error(void);
+
+/* ---- a9: Krum pairwise l2 ---------------------------------------------
+ * Replaces KrumDefense._compute_distances (src/defenses/krum.py:73-99):
+ *   D[i][j] = float32(||X_i - X_j||_2) stored as float64, D[i][i] = 0.
+ * Engine: centred Gram matrix on MFMA (bf16 hi/lo split, fp32 accumulate),
+ * fixed-order fp64 reduction of per-segment partials.  Any K >= 1.
+ */
+size_t flr_pairwise_l2_workspace(int64_t K, int64_t P);
+int flr_pairwise_l2(const float* X, int64_t K, int64_t P, int64_t ldx,
+                    double* D, void* workspace, size_t workspace_bytes,
+                    void* stream);
+
+/* Direct-difference VALU variant (same contract, exact fp32 differences);
+ * a slower second implementation used to cross-check the MFMA path. */
+size_t flr_pairwise_l2_direct_workspace(int64_t K, int64_t P);
+int flr_pairwise_l2_direct(const float* X, int64_t K, int64_t P, int64_t ldx,
+                           double* D, void* workspace, size_t workspace_bytes,
+                           void* stream);
+
+/* ---- a10: Krum score + selection --------------------------------------
+ * Replaces KrumDefense._krum_score + the argsort in aggregate
+ * (src/defenses/krum.py:101-131, 149-176):
+ *   m = K - f - 2; scores[i] = numpy-pairwise-sum(sort(D[i])[1 : m+1]);
+ *   order = argsort(scores) (ties broken by lower client index).
+ * D: device fp64 K×K (row-major, ld = K). scores: device fp64 [K];
+ * order: device int32 [K].  Returns FLR_ERR_KRUM_N if K < 2f+3.
+ */
+int flr_krum_select(const double* D, int64_t K, int64_t f, double* scores,
+                    int32_t* order, void* stream);
+
+/* ---- a11: Multi-Krum mean ---------------------------------------------
+ * Replaces the Multi-Krum average (src/defenses/krum.py:182-192):
+ *   out = (((0 + X[rows[0]]) + X[rows[1]]) + ...) / divisor   (fp32, in order)
+ * rows: device int32 [m] (e.g. the first m entries of `order`); divisor is
+ * the reference's multi_k (== m unless multi_k > K).
+ */
+int flr_rows_mean(const float* X, int64_t K, int64_t P, int64_t ldx,
+                  const int32_t* rows, int64_t m, int64_t divisor, float* out,
+                  void* stream);
+
+/* ---- a14: FedAvg -------------------------------------------------------
+ * Replaces NoDefense.aggregate (src/defenses/base_defense.py:80-97) and the
+ * inline FedAvg of experiments/run_experiments.py:246-254:
+ *   out = (sum_i fl(n_i * X_i)) / sum_i n_i     (fp32, client order)
+ * num_examples: device int64 [K].
+ */
+int flr_fedavg(const float* X, int64_t K, int64_t P, int64_t ldx,
+               const int64_t* num_examples, float* out, void* stream);
+
+/* ---- a12: coordinate-wise trimmed mean ---------------------------------
+ * Replaces TrimmedMeanDefense.aggregate (src/defenses/trimmed_mean.py:48-90)
+ * for one fixed t (= max(1, int(K*trim_ratio)), computed by the caller):
+ *   out[p] = mean(sort(X[:,p])[t : K-t])   (torch's cascade-sum order)
+ * Requires K - 2t >= 1 (the caller falls back to the median otherwise).
+ */
+int flr_trimmed_mean(const float* X, int64_t K, int64_t P, int64_t ldx,
+                     int64_t t, float* out, void* stream);
+
+/* ---- a13: coordinate-wise lower median ---------------------------------
+ * Replaces MedianDefense.aggregate / _coordinate_wise_median
+ * (src/defenses/trimmed_mean.py:92-103, 141-166): torch.median(dim=0)[0]
+ * = sort(X[:,p])[(K-1)/2]. Bit-exact (selection, no arithmetic).
+ */
+int flr_median_lower(const float* X, int64_t K, int64_t P, int64_t ldx,
+                     float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLR_H */

@@ -1,0 +1,37 @@
+// Internal helpers shared by the flr HIP translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/flr.h"
+
+namespace flr {
+
+// Records the last HIP error text for flr_last_error().
+void set_last_error(const char* where, hipError_t e);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Checks the launch that was just enqueued.
+inline int launch_status(const char* where) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_last_error(where, e);
+    return FLR_ERR_HIP;
+  }
+  return FLR_OK;
+}
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+__host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// fp32 add/mul/div with no contraction (the reference computes each op as a
+// separate rounded torch op, so FMA contraction would break bit parity).
+__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float div_rn(float a, float b) { return __fdiv_rn(a, b); }
+
+}  // namespace flr

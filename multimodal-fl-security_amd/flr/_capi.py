@@ -1,0 +1,103 @@
+"""ctypes binding of the flr C ABI (``include/flr.h``, ``lib/libflr.so``).
+
+The library is the product path: every aggregation op in :mod:`flr.ops`
+calls through here.  There is no CPU or PyTorch fallback — if the shared
+library is missing or fails to load, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("FLR_LIB", os.path.join(_PKG_ROOT, "lib", "libflr.so"))
+HEADER_PATH = os.path.join(os.path.dirname(_PKG_ROOT), "include", "flr.h")
+
+FLR_OK = 0
+FLR_ERR_ARG = -1
+FLR_ERR_HIP = -2
+FLR_ERR_UNSUPPORTED = -3
+FLR_ERR_WORKSPACE = -4
+FLR_ERR_KRUM_N = -5
+
+_c_void_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_size_t = ctypes.c_size_t
+_int = ctypes.c_int
+
+# name -> (restype, argtypes); must list every function include/flr.h declares.
+SIGNATURES = {
+    "flr_version": (ctypes.c_char_p, []),
+    "flr_status_string": (ctypes.c_char_p, [_int]),
+    "flr_last_error": (ctypes.c_char_p, []),
+    "flr_pairwise_l2_workspace": (_size_t, [_i64, _i64]),
+    "flr_pairwise_l2": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "flr_pairwise_l2_direct_workspace": (_size_t, [_i64, _i64]),
+    "flr_pairwise_l2_direct": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "flr_krum_select": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),
+    "flr_rows_mean": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _i64, _c_void_p, _c_void_p]),
+    "flr_fedavg": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),
+    "flr_trimmed_mean": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p]),
+    "flr_median_lower": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class FlrError(RuntimeError):
+    """A C-ABI call returned a non-zero status."""
+
+    def __init__(self, fn: str, status: int, detail: str = ""):
+        self.status = status
+        msg = f"{fn} failed: {status_string(status)} ({status})"
+        if detail:
+            msg += f": {detail}"
+        super().__init__(msg)
+
+
+def lib() -> ctypes.CDLL:
+    """Load libflr.so once; raise loudly if it is absent (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"flr native library not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C "
+                "multimodal-fl-security_amd/csrc). There is no CPU fallback.")
+        # torch must be imported first so its libamdhip64.so.7 is the runtime
+        # this library binds to (same SONAME -> one HIP runtime per process).
+        import torch  # noqa: F401
+        handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+        return _lib
+
+
+def status_string(status: int) -> str:
+    try:
+        return lib().flr_status_string(status).decode()
+    except Exception:  # pragma: no cover - only when the lib is unusable
+        return "unknown"
+
+
+def check(fn: str, status: int) -> None:
+    if status != FLR_OK:
+        detail = ""
+        if status == FLR_ERR_HIP:
+            detail = lib().flr_last_error().decode()
+        raise FlrError(fn, status, detail)
+
+
+def call(fn: str, *args) -> int:
+    status = getattr(lib(), fn)(*args)
+    check(fn, status)
+    return status

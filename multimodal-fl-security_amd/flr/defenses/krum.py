@@ -1,0 +1,86 @@
+"""Krum / Multi-Krum (mirror of src/defenses/krum.py:14-237).
+
+Pipeline on the device, no host round trip until the selected indices are
+published: flr_pairwise_l2 (K×K fp64 distances, krum.py:73-99) ->
+flr_krum_select (scores + argsort, krum.py:101-131, 149-176) ->
+flr_rows_mean over the first multi_k rows of the order (krum.py:182-192).
+Single Krum (multi_k == 1) returns the caller's own list for the selected
+client, as the reference does (krum.py:178-181).
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List
+
+import torch
+
+from .. import ops
+from ..matrix import ClientMatrix
+from .base_defense import BaseDefense, Updates, as_matrix, source_device
+
+
+class KrumDefense(BaseDefense):
+    def __init__(self, defense_config: Dict[str, Any]):
+        super().__init__(defense_config)
+        self.num_malicious = defense_config.get("num_malicious", 1)
+        self.multi_k = defense_config.get("multi_k", 1)
+        self.pairwise_method = defense_config.get("pairwise_method", "gram")
+        self.selected_clients: List[int] = []
+        self.rejected_clients: List[int] = []
+        self.client_scores: List[float] = []
+        # device-side results of the last call (engine consumers use these)
+        self.distances = None
+        self.scores_device = None
+        self.order_device = None
+
+    def select(self, cm: ClientMatrix) -> torch.Tensor:
+        """Distances, scores and order on the device; returns the int32 order."""
+        n, f = cm.K, self.num_malicious
+        if n < 2 * f + 3:  # krum.py:153-157
+            raise ValueError(
+                f"Krum requires n >= 2f + 3. Got n={n}, f={f}. Need at least {2 * f + 3} clients.")
+        self.distances = ops.pairwise_l2(cm.X, self.pairwise_method)
+        self.scores_device, self.order_device = ops.krum_select(self.distances, f)
+        return self.order_device
+
+    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
+        cm = as_matrix(client_updates)
+        order = self.select(cm)
+        order_host = order.cpu().tolist()
+        self.client_scores = self.scores_device.cpu().tolist()
+        self.selected_clients = order_host[: self.multi_k]
+        self.rejected_clients = order_host[self.multi_k:]
+        if self.multi_k == 1:
+            sel = self.selected_clients[0]
+            if isinstance(client_updates, ClientMatrix):
+                return client_updates.row(sel)
+            return client_updates[sel]
+        flat = ops.rows_mean(cm.X, order[: min(self.multi_k, cm.K)], divisor=self.multi_k)
+        return cm.unflatten(flat, source_device(client_updates))
+
+    def detect_malicious(self, client_updates: Updates, num_examples: List[int]) -> List[int]:
+        if not self.client_scores:
+            self.aggregate(client_updates, num_examples)
+        return self.rejected_clients
+
+    def get_metrics(self) -> Dict[str, Any]:
+        return {
+            "defense_type": "krum",
+            "num_malicious_assumed": self.num_malicious,
+            "multi_k": self.multi_k,
+            "selected_clients": self.selected_clients,
+            "rejected_clients": self.rejected_clients,
+            "client_scores": self.client_scores,
+        }
+
+    def __repr__(self) -> str:
+        return f"KrumDefense(f={self.num_malicious}, k={self.multi_k})"
+
+
+class MultiKrumDefense(KrumDefense):
+    """multi_k defaults to cfg['default_k'] or 3, written back into the config
+    dict as the reference does (krum.py:232-237)."""
+
+    def __init__(self, defense_config: Dict[str, Any]):
+        if "multi_k" not in defense_config:
+            defense_config["multi_k"] = defense_config.get("default_k", 3)
+        super().__init__(defense_config)

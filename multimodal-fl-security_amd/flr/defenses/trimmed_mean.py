@@ -1,0 +1,56 @@
+"""Coordinate-wise trimmed mean and median (mirror of src/defenses/trimmed_mean.py:14-174)."""
+from __future__ import annotations
+
+from typing import Any, Dict, List
+
+import torch
+
+from .. import ops
+from .base_defense import BaseDefense, Updates, as_matrix, source_device
+
+
+class TrimmedMeanDefense(BaseDefense):
+    """t = max(1, int(n * trim_ratio)) per end; median if n - 2t < 1 (trimmed_mean.py:63-72)."""
+
+    def __init__(self, defense_config: Dict[str, Any]):
+        super().__init__(defense_config)
+        self.trim_ratio = defense_config.get("trim_ratio", 0.1)
+        self.num_trimmed_per_end = 0
+
+    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
+        cm = as_matrix(client_updates)
+        n = cm.K
+        self.num_trimmed_per_end = max(1, int(n * self.trim_ratio))
+        if n - 2 * self.num_trimmed_per_end < 1:
+            flat = ops.median_lower(cm.X)
+        else:
+            flat = ops.trimmed_mean(cm.X, self.num_trimmed_per_end)
+        return cm.unflatten(flat, source_device(client_updates))
+
+    def get_metrics(self) -> Dict[str, Any]:
+        return {
+            "defense_type": "trimmed_mean",
+            "trim_ratio": self.trim_ratio,
+            "num_trimmed_per_end": self.num_trimmed_per_end,
+        }
+
+    def __repr__(self) -> str:
+        return f"TrimmedMeanDefense(trim_ratio={self.trim_ratio})"
+
+
+class MedianDefense(BaseDefense):
+    """Lower median per coordinate, torch.median(dim=0)[0] (trimmed_mean.py:141-166)."""
+
+    def __init__(self, defense_config: Dict[str, Any] = None):
+        super().__init__(defense_config or {})
+
+    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
+        cm = as_matrix(client_updates)
+        flat = ops.median_lower(cm.X)
+        return cm.unflatten(flat, source_device(client_updates))
+
+    def get_metrics(self) -> Dict[str, Any]:
+        return {"defense_type": "median"}
+
+    def __repr__(self) -> str:
+        return "MedianDefense()"

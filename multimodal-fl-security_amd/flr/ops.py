@@ -1,0 +1,106 @@
+"""Tensor-level wrappers over the flr C ABI (device tensors in, device tensors out).
+
+Each op validates shapes on the host, allocates outputs / workspace with the
+PyTorch caching allocator on the tensor's device, and enqueues the HIP
+kernels on torch's current stream.  No op has a fallback: a CPU tensor, a
+wrong dtype or a missing library raises.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _capi
+
+CHUNK = 64  # coordinates per pairwise chunk; client matrices pad ldx to this
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _check_matrix(X: torch.Tensor, name: str = "X") -> Tuple[int, int, int]:
+    if not isinstance(X, torch.Tensor) or not X.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA/HIP tensor (the engine has no CPU path)")
+    if X.dtype != torch.float32 or X.dim() != 2 or X.stride(1) != 1 or X.stride(0) < X.shape[1]:
+        raise ValueError(f"{name} must be a row-major float32 [K, P] matrix (got {X.dtype}, "
+                         f"shape {tuple(X.shape)}, strides {X.stride()})")
+    return X.shape[0], X.shape[1], X.stride(0)
+
+
+def pairwise_l2(X: torch.Tensor, method: str = "gram") -> torch.Tensor:
+    """K×K float64 distances, D[i][j] = fp32 ||X_i - X_j|| (krum.py:73-99)."""
+    K, P, ldx = _check_matrix(X)
+    D = torch.empty((K, K), dtype=torch.float64, device=X.device)
+    if method == "gram":
+        ws_fn, fn = "flr_pairwise_l2_workspace", "flr_pairwise_l2"
+    elif method == "direct":
+        ws_fn, fn = "flr_pairwise_l2_direct_workspace", "flr_pairwise_l2_direct"
+    else:
+        raise ValueError(f"unknown pairwise method {method!r}")
+    nbytes = int(getattr(_capi.lib(), ws_fn)(K, P))
+    ws = torch.empty(max(nbytes, 256) + 256, dtype=torch.uint8, device=X.device)
+    off = (-ws.data_ptr()) % 256
+    _capi.call(fn, X.data_ptr(), K, P, ldx, D.data_ptr(), ws.data_ptr() + off, nbytes, _stream(X))
+    return D
+
+
+def krum_select(D: torch.Tensor, f: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(scores fp64 [K], order int32 [K]) — krum.py:101-131, 149-176."""
+    if not D.is_cuda or D.dtype != torch.float64 or D.dim() != 2 or D.shape[0] != D.shape[1]:
+        raise ValueError("D must be a square float64 device matrix")
+    D = D.contiguous()
+    K = D.shape[0]
+    scores = torch.empty(K, dtype=torch.float64, device=D.device)
+    order = torch.empty(K, dtype=torch.int32, device=D.device)
+    _capi.call("flr_krum_select", D.data_ptr(), K, int(f), scores.data_ptr(), order.data_ptr(), _stream(D))
+    return scores, order
+
+
+def rows_mean(X: torch.Tensor, rows: torch.Tensor, divisor: Optional[int] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Ordered fp32 sum of X[rows] divided by `divisor` (krum.py:182-192)."""
+    K, P, ldx = _check_matrix(X)
+    rows = rows.to(device=X.device, dtype=torch.int32).contiguous()
+    m = rows.numel()
+    divisor = m if divisor is None else int(divisor)
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=X.device)
+    _capi.call("flr_rows_mean", X.data_ptr(), K, P, ldx, rows.data_ptr(), m, divisor, out.data_ptr(),
+               _stream(X))
+    return out
+
+
+def fedavg(X: torch.Tensor, num_examples, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Example-weighted average (base_defense.py:80-97)."""
+    K, P, ldx = _check_matrix(X)
+    n = torch.as_tensor(num_examples, dtype=torch.int64).to(X.device).contiguous()
+    if n.numel() != K:
+        raise ValueError(f"num_examples has {n.numel()} entries for {K} clients")
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=X.device)
+    _capi.call("flr_fedavg", X.data_ptr(), K, P, ldx, n.data_ptr(), out.data_ptr(), _stream(X))
+    return out
+
+
+def trimmed_mean(X: torch.Tensor, t: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Coordinate-wise mean of sorted ranks [t, K-t) (trimmed_mean.py:74-88)."""
+    K, P, ldx = _check_matrix(X)
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=X.device)
+    _capi.call("flr_trimmed_mean", X.data_ptr(), K, P, ldx, int(t), out.data_ptr(), _stream(X))
+    return out
+
+
+def median_lower(X: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Coordinate-wise lower median (trimmed_mean.py:101, 163)."""
+    K, P, ldx = _check_matrix(X)
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=X.device)
+    _capi.call("flr_median_lower", X.data_ptr(), K, P, ldx, out.data_ptr(), _stream(X))
+    return out

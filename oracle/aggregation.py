@@ -1,0 +1,149 @@
+"""ORACLE (test infrastructure only) — CPU restatement of the aggregation rules.
+
+Each function follows the cited reference lines with the same torch / numpy
+operations in the same order, so on this image it reproduces the reference's
+numbers.  Inputs are reference-style ``List[List[Tensor]]`` on the CPU.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import numpy as np
+import torch
+
+Update = Sequence[torch.Tensor]
+
+
+def flat(update: Update) -> torch.Tensor:
+    """krum.py:55-57 — one fp32 vector per client."""
+    return torch.cat([p.flatten().float() for p in update])
+
+
+def distance_matrix(updates: Sequence[Update]) -> np.ndarray:
+    """krum.py:73-99 — fp64 matrix of fp32 torch.norm(.).item() per pair."""
+    n = len(updates)
+    vecs = [flat(u) for u in updates]
+    out = np.zeros((n, n))
+    for a in range(n):
+        for b in range(a + 1, n):
+            v = torch.norm(vecs[a] - vecs[b]).item()
+            out[a, b] = v
+            out[b, a] = v
+    return out
+
+
+def krum_scores(dist: np.ndarray, num_neighbors: int) -> List[float]:
+    """krum.py:101-131 and :165-169 — sum of sorted row entries 1..m."""
+    scores = []
+    for a in range(dist.shape[0]):
+        row_sorted = np.sort(dist[a].copy())
+        scores.append(np.sum(row_sorted[1:num_neighbors + 1]))
+    return scores
+
+
+def krum(updates: Sequence[Update], num_malicious: int, multi_k: int):
+    """krum.py:149-192.  Returns (aggregate, scores, selected, rejected, dist)."""
+    n, f = len(updates), num_malicious
+    if n < 2 * f + 3:
+        raise ValueError(f"Krum requires n >= 2f + 3. Got n={n}, f={f}.")
+    dist = distance_matrix(updates)
+    scores = krum_scores(dist, n - f - 2)
+    order = np.argsort(scores)
+    selected = order[:multi_k].tolist()
+    rejected = order[multi_k:].tolist()
+    if multi_k == 1:
+        return list(updates[selected[0]]), scores, selected, rejected, dist
+    chosen = [updates[i] for i in selected]
+    agg = []
+    for pi in range(len(chosen[0])):
+        total = sum(u[pi] for u in chosen)
+        agg.append(total / multi_k)
+    return agg, scores, selected, rejected, dist
+
+
+def fedavg(updates: Sequence[Update], num_examples: Sequence[int]) -> List[torch.Tensor]:
+    """base_defense.py:80-97 (== run_experiments.py:246-254)."""
+    total_examples = sum(num_examples)
+    agg = []
+    for pi in range(len(updates[0])):
+        weighted = sum(num_examples[i] * updates[i][pi] for i in range(len(updates)))
+        agg.append(weighted / total_examples)
+    return agg
+
+
+def median(updates: Sequence[Update]) -> List[torch.Tensor]:
+    """trimmed_mean.py:92-103 / 156-166 — torch.median(dim=0) (lower median)."""
+    agg = []
+    for pi in range(len(updates[0])):
+        stacked = torch.stack([u[pi].float() for u in updates])
+        agg.append(torch.median(stacked, dim=0)[0])
+    return agg
+
+
+def trimmed_mean(updates: Sequence[Update], trim_ratio: float) -> Tuple[List[torch.Tensor], int]:
+    """trimmed_mean.py:63-90.  Returns (aggregate, num_trimmed_per_end)."""
+    n = len(updates)
+    t = max(1, int(n * trim_ratio))
+    if n - 2 * t < 1:
+        return median(updates), t
+    agg = []
+    for pi in range(len(updates[0])):
+        stacked = torch.stack([u[pi].float() for u in updates])
+        sorted_vals, _ = torch.sort(stacked, dim=0)
+        agg.append(sorted_vals[t:n - t].mean(dim=0))
+    return agg, t
+
+
+def sign_flip(update: Update) -> List[torch.Tensor]:
+    """model_poisoning.py:274-276 — IPM without a benign mean negates the update."""
+    return [-p for p in update]
+
+
+# ---- op-level semantics the kernels restate (pinned in tests/test_oracle.py) ----
+
+def numpy_pairwise_sum(a: np.ndarray) -> float:
+    """numpy's float64 pairwise summation (what np.sum does on a contiguous slice)."""
+    n = len(a)
+    if n < 8:
+        res = 0.0
+        for i in range(n):
+            res += a[i]
+        return res
+    if n <= 128:
+        r = [a[j] for j in range(8)]
+        i = 8
+        while i < n - (n % 8):
+            for j in range(8):
+                r[j] += a[i + j]
+            i += 8
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+        while i < n:
+            res += a[i]
+            i += 1
+        return res
+    n2 = n // 2
+    n2 -= n2 % 8
+    return numpy_pairwise_sum(a[:n2]) + numpy_pairwise_sum(a[n2:])
+
+
+def torch_outer_sum(rows: torch.Tensor) -> torch.Tensor:
+    """torch's CPU vectorised outer reduction (cascade_sum / multi_row_sum):
+    16-row blocks accumulated from zero, folded through 4 levels."""
+    R = rows.shape[0]
+    acc = [torch.zeros(rows.shape[1:], dtype=rows.dtype) for _ in range(4)]
+    i = 0
+    while i + 16 <= R:
+        for _ in range(16):
+            acc[0] = acc[0] + rows[i]
+            i += 1
+        for j in range(1, 4):
+            acc[j] = acc[j] + acc[j - 1]
+            acc[j - 1] = torch.zeros_like(acc[0])
+            if i & (15 << (4 * j)):
+                break
+    while i < R:
+        acc[0] = acc[0] + rows[i]
+        i += 1
+    for j in range(1, 4):
+        acc[0] = acc[0] + acc[j]
+    return acc[0]

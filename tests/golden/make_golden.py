@@ -1,0 +1,99 @@
+"""Generate the golden fixtures in tests/golden/ from the oracle (CPU).
+
+Run from the repo root:  python tests/golden/make_golden.py
+Every fixture records the torch / numpy versions and CPU model that produced
+it (the reference's torch.norm accumulation order is ISA-specific).
+Inputs are stored in the fixture (float32), so the GPU box needs nothing
+but the .npz files.
+"""
+from __future__ import annotations
+
+import os
+import platform
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "multimodal-fl-security_amd"))
+
+from oracle import aggregation as orc  # noqa: E402
+from flr.workload import update_matrix, split_rows  # noqa: E402
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+META = dict(torch=torch.__version__, numpy=np.__version__, cpu=cpu_model())
+
+
+def margin(scores, multi_k):
+    s = np.sort(np.asarray(scores))
+    if multi_k >= len(s):
+        return float("inf")
+    return float((s[multi_k] - s[multi_k - 1]) / max(abs(s[multi_k]), 1e-300))
+
+
+def krum_case(name, X, shapes, f, multi_k):
+    ups = split_rows(X, sum(int(np.prod(s)) for s in shapes), shapes)
+    agg, scores, sel, rej, dist = orc.krum(ups, f, multi_k)
+    flat_agg = torch.cat([a.reshape(-1) for a in agg]).numpy()
+    np.savez_compressed(
+        os.path.join(HERE, f"krum_{name}.npz"), X=X.numpy(), shapes=np.array([list(s) + [0] * (4 - len(s)) for s in shapes]),
+        ndims=np.array([len(s) for s in shapes]), f=f, multi_k=multi_k, dist=dist, scores=np.array(scores),
+        selected=np.array(sel), rejected=np.array(rej), agg=flat_agg, margin=margin(scores, multi_k), **META)
+
+
+def stat_case(name, X, shapes, trim_ratio, num_examples):
+    P = sum(int(np.prod(s)) for s in shapes)
+    ups = split_rows(X, P, shapes)
+    tm, t = orc.trimmed_mean(ups, trim_ratio)
+    med = orc.median(ups)
+    fa = orc.fedavg(ups, num_examples)
+    cat = lambda lst: torch.cat([a.reshape(-1) for a in lst]).numpy()  # noqa: E731
+    np.savez_compressed(
+        os.path.join(HERE, f"stat_{name}.npz"), X=X.numpy(), shapes=np.array([list(s) + [0] * (4 - len(s)) for s in shapes]),
+        ndims=np.array([len(s) for s in shapes]), trim_ratio=trim_ratio, t=t, trimmed=cat(tm), median=cat(med),
+        num_examples=np.array(num_examples, dtype=np.int64), fedavg=cat(fa), **META)
+
+
+def main():
+    torch.manual_seed(0)
+    # reference demo construction (krum.py:244-263): 5 benign base+0.1N, 2 malicious 10*base+5N
+    g = torch.Generator().manual_seed(42)
+    base = [torch.randn(10, 10, generator=g), torch.randn(10, generator=g)]
+    ups = [[b + torch.randn(b.shape, generator=g) * 0.1 for b in base] for _ in range(5)]
+    ups += [[b * 10 + torch.randn(b.shape, generator=g) * 5 for b in base] for _ in range(2)]
+    X = torch.stack([torch.cat([t.reshape(-1) for t in u]) for u in ups])
+    krum_case("demo_k1", X, [(10, 10), (10,)], 2, 1)
+    krum_case("demo_k3", X, [(10, 10), (10,)], 2, 3)
+    # workload-shaped cases (SURVEY §8d generator, CPU)
+    for (K, P, f, mk) in [(5, 110, 1, 2), (7, 4099, 2, 3), (16, 4099, 3, 8), (32, 2053, 6, 16),
+                          (40, 1600, 8, 20), (12, 1000, 2, 6)]:
+        X = update_matrix(K, P, f=f, seed=1000 + K, device="cpu")[:, :P].contiguous()
+        krum_case(f"K{K}_P{P}", X, [(P,)], f, mk)
+    # order statistics + fedavg
+    for (K, shapes, ratio) in [(5, [(10, 11)], 0.2), (7, [(4099,)], 0.2), (16, [(3, 7, 7), (2853,)], 0.1),
+                               (33, [(1024,)], 0.1), (50, [(640,)], 0.2), (4, [(64, 3), (100,)], 0.1)]:
+        P = sum(int(np.prod(s)) for s in shapes)
+        gen = torch.Generator().manual_seed(K * 7 + P)
+        X = torch.randn(K, P, generator=gen)
+        X[K // 3] *= 100.0  # an outlier client
+        n_ex = [int(v) for v in torch.randint(10, 5000, (K,), generator=gen)]
+        stat_case(f"K{K}_P{P}", X, shapes, ratio, n_ex)
+    print("fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

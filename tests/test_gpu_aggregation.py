@@ -1,0 +1,192 @@
+"""GPU parity: the HIP aggregation kernels vs the oracle / golden fixtures.
+
+Bars (north_star): Krum/Multi-Krum indices bit-exact; Krum
+scores bit-exact given the same distance matrix; distances within 2e-5
+relative of the reference's fp32 torch.norm (whose own error vs exact is
+~1e-5 at 1e6 and ~3e-4 at 1e7 coordinates); median bit-exact; Multi-Krum
+mean and FedAvg bit-exact; trimmed mean within 1e-5 (bit-exact on the
+coordinates torch sums with its vectorised cascade).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_files, load_golden, shapes_of
+from oracle import aggregation as orc
+from flr import ops
+from flr.defenses import get_defense, KrumDefense
+from flr.matrix import ClientMatrix, padded_ld
+from flr.workload import split_rows, update_matrix
+
+pytestmark = pytest.mark.gpu
+
+
+def to_matrix(X_np, device):
+    K, P = X_np.shape
+    data = torch.zeros((K, padded_ld(P)), dtype=torch.float32, device=device)
+    data[:, :P] = torch.from_numpy(X_np).to(device)
+    return data[:, :P]
+
+
+# ---------------- pairwise distances ----------------
+
+@pytest.mark.parametrize("path", golden_files("krum"), ids=lambda p: p.split("/")[-1])
+@pytest.mark.parametrize("method", ["gram", "direct"])
+def test_pairwise_vs_golden(cuda, path, method):
+    fx = load_golden(path)
+    X = to_matrix(fx["X"], cuda)
+    D = ops.pairwise_l2(X, method).cpu().numpy()
+    ref = fx["dist"]
+    assert np.all(np.diag(D) == 0) and np.array_equal(D, D.T)
+    rel = np.abs(D - ref) / np.maximum(ref, 1e-30)
+    np.fill_diagonal(rel, 0)
+    assert rel.max() < 2e-5, rel.max()
+
+
+@pytest.mark.parametrize("K,P", [(1, 100), (2, 64), (3, 1), (33, 129), (64, 4096), (100, 6400),
+                                 (128, 65536 + 17), (129, 3000), (200, 2048), (300, 1111)])
+def test_pairwise_gram_vs_direct_and_fp64(cuda, K, P):
+    X = update_matrix(K, P, f=K // 5, seed=K + P, device=cuda)[:, :P]
+    Dg = ops.pairwise_l2(X, "gram").cpu().numpy()
+    Dd = ops.pairwise_l2(X, "direct").cpu().numpy()
+    Xd = X.double().cpu()
+    exact = torch.cdist(Xd, Xd).numpy() if K > 1 else np.zeros((1, 1))
+    for D in (Dg, Dd):
+        rel = np.abs(D - exact) / np.maximum(exact, 1e-30)
+        np.fill_diagonal(rel, 0)
+        assert rel.max() < 5e-6, rel.max()
+
+
+def test_pairwise_large_offset_centering(cuda):
+    # a large common component (weights, not deltas) must not cost accuracy
+    K, P = 48, 50000
+    X = update_matrix(K, P, f=0, seed=5, device=cuda)[:, :P] + 3.0
+    D = ops.pairwise_l2(X).cpu().double()
+    Xd = X.double().cpu()
+    exact = torch.cdist(Xd, Xd)
+    rel = ((D - exact).abs() / exact.clamp_min(1e-30)).fill_diagonal_(0)
+    assert rel.max().item() < 5e-6
+
+
+def test_pairwise_unaligned_rows(cuda):
+    K, P = 9, 1001
+    base = torch.randn(K * P + 1, device=cuda)
+    X = base[1:].view(K, P)  # 4-B aligned only, ld = P (odd): the tail path does all of it
+    D = ops.pairwise_l2(X).cpu().double()
+    exact = torch.cdist(X.double().cpu(), X.double().cpu())
+    assert ((D - exact).abs() / exact.clamp_min(1e-30)).fill_diagonal_(0).max().item() < 5e-6
+
+
+# ---------------- selection ----------------
+
+@pytest.mark.parametrize("path", golden_files("krum"), ids=lambda p: p.split("/")[-1])
+def test_krum_select_bitexact_given_distances(cuda, path):
+    fx = load_golden(path)
+    D = torch.from_numpy(fx["dist"]).to(cuda)
+    scores, order = ops.krum_select(D, int(fx["f"]))
+    np.testing.assert_array_equal(scores.cpu().numpy(), fx["scores"])
+    mk = int(fx["multi_k"])
+    assert order.cpu().tolist()[:mk] == fx["selected"].tolist()
+
+
+def test_krum_select_random_rows_bitexact(cuda):
+    rng = np.random.default_rng(1)
+    for K, f in [(5, 1), (50, 10), (128, 25), (257, 50), (512, 100)]:
+        A = rng.random((K, K)) * 10
+        D = np.triu(A, 1) + np.triu(A, 1).T
+        scores = orc.krum_scores(D, K - f - 2)
+        s, o = ops.krum_select(torch.from_numpy(D).to(cuda), f)
+        np.testing.assert_array_equal(s.cpu().numpy(), np.asarray(scores))
+        assert o.cpu().tolist() == np.argsort(scores, kind="stable").tolist()
+
+
+def test_krum_rejects_small_n(cuda):
+    with pytest.raises(ValueError):
+        get_defense("krum", {"num_malicious": 2}).aggregate(
+            [[torch.randn(4, device=cuda)] for _ in range(3)], [1] * 3)
+
+
+# ---------------- end-to-end defenses vs golden ----------------
+
+@pytest.mark.parametrize("path", golden_files("krum"), ids=lambda p: p.split("/")[-1])
+def test_krum_defense_vs_golden(cuda, path):
+    fx = load_golden(path)
+    shapes = shapes_of(fx)
+    X = torch.from_numpy(fx["X"]).to(cuda)
+    ups = split_rows(X, X.shape[1], shapes)
+    d = KrumDefense({"num_malicious": int(fx["f"]), "multi_k": int(fx["multi_k"])})
+    agg = d.aggregate(ups, [100] * len(ups))
+    assert d.selected_clients == fx["selected"].tolist()
+    assert d.rejected_clients == fx["rejected"].tolist()
+    flat = torch.cat([a.reshape(-1) for a in agg]).cpu().numpy()
+    np.testing.assert_array_equal(flat, fx["agg"])  # same rows, same order -> bit-exact
+    if int(fx["multi_k"]) == 1:
+        assert agg is ups[d.selected_clients[0]]  # reference returns the caller's list
+
+
+@pytest.mark.parametrize("path", golden_files("stat"), ids=lambda p: p.split("/")[-1])
+def test_stat_defenses_vs_golden(cuda, path):
+    fx = load_golden(path)
+    shapes = shapes_of(fx)
+    X = torch.from_numpy(fx["X"]).to(cuda)
+    ups = split_rows(X, X.shape[1], shapes)
+    cat = lambda lst: torch.cat([a.reshape(-1) for a in lst]).cpu().numpy()  # noqa: E731
+    med = cat(get_defense("median", {}).aggregate(ups, []))
+    np.testing.assert_array_equal(med, fx["median"])
+    tmd = get_defense("trimmed_mean", {"trim_ratio": float(fx["trim_ratio"])})
+    tm = cat(tmd.aggregate(ups, []))
+    assert tmd.num_trimmed_per_end == int(fx["t"])
+    np.testing.assert_allclose(tm, fx["trimmed"], rtol=1e-5, atol=1e-6)
+    fa = cat(get_defense("fedavg", {}).aggregate(ups, fx["num_examples"].tolist()))
+    np.testing.assert_array_equal(fa, fx["fedavg"])
+
+
+@pytest.mark.parametrize("K", [2, 3, 5, 8, 9, 16, 31, 64, 100, 128])
+def test_order_stats_vs_torch(cuda, K):
+    P = 5003
+    X = torch.randn(K, P, device=cuda)
+    X[0, :10] = float("inf")
+    X[1 % K, 10:20] = -float("inf")
+    ref_sorted = torch.sort(X.cpu(), dim=0)[0]
+    np.testing.assert_array_equal(ops.median_lower(X).cpu().numpy(), torch.median(X.cpu(), dim=0)[0].numpy())
+    t = max(1, int(K * 0.1))
+    if K - 2 * t >= 1:
+        Xf = X.clone()
+        Xf[~torch.isfinite(Xf)] = 0.0
+        ref = torch.sort(Xf.cpu(), dim=0)[0][t:K - t].mean(dim=0)
+        got = ops.trimmed_mean(Xf, t).cpu()
+        torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+        # bit-exact on the vectorised columns (all but the scalar tail)
+        ncol = (P // 64) * 64
+        cas = orc.torch_outer_sum(torch.sort(Xf.cpu(), dim=0)[0][t:K - t]) / (K - 2 * t)
+        assert torch.equal(got[:ncol], cas[:ncol])
+    del ref_sorted
+
+
+def test_trimmed_falls_back_to_median(cuda):
+    ups = [[torch.randn(7, device=cuda)] for _ in range(3)]
+    d = get_defense("trimmed_mean", {"trim_ratio": 0.5})
+    out = d.aggregate(ups, [])
+    ref = orc.median([[u[0].cpu()] for u in ups])[0]
+    assert torch.equal(out[0].cpu(), ref)
+
+
+def test_rows_mean_and_fedavg_bitexact(cuda):
+    K, P = 37, 10007
+    X = torch.randn(K, P, device=cuda)
+    rows = torch.tensor([5, 3, 30, 0, 12], dtype=torch.int32)
+    got = ops.rows_mean(X, rows, divisor=5).cpu()
+    ups = [[X[i].cpu()] for i in range(K)]
+    ref = sum(ups[i][0] for i in rows.tolist()) / 5
+    assert torch.equal(got, ref)
+    n = [int(v) for v in torch.randint(1, 100000, (K,))]
+    assert torch.equal(ops.fedavg(X, n).cpu(), orc.fedavg(ups, n)[0])
+
+
+def test_client_matrix_zero_copy_defense(cuda):
+    K, P = 20, 3000
+    cm = ClientMatrix(update_matrix(K, P, f=4, device=cuda), P, [(P,)])
+    d = get_defense("krum", {"num_malicious": 4, "multi_k": 10})
+    out = d.aggregate(cm, [1] * K)
+    assert out[0].shape == (P,)
+    assert not set(d.selected_clients) & set(range(4))  # sign-flipped clients rejected

@@ -1,0 +1,122 @@
+"""CPU: pin the oracle — reference property tests restated, op semantics, golden vectors."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_files, load_golden, shapes_of
+from oracle import aggregation as orc
+from flr.workload import split_rows
+
+
+def mock_updates(n, shapes=((10, 10), (10,)), seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return [[torch.randn(s, generator=g) for s in shapes] for _ in range(n)]
+
+
+# ---- tests/test_defenses.py of the reference, restated against the oracle ----
+
+def test_ref_single_krum():  # test_defenses.py:40-52
+    ups = mock_updates(5)
+    agg, scores, sel, rej, _ = orc.krum(ups, 1, 1)
+    assert len(agg) == len(ups[0]) and len(sel) == 1
+
+
+def test_ref_multi_krum():  # :54-63
+    agg, _, sel, _, _ = orc.krum(mock_updates(5), 1, 2)
+    assert len(agg) == 2 and len(sel) == 2
+
+
+def test_ref_malicious_detection():  # :65-81
+    g = torch.Generator().manual_seed(3)
+    ups = [[torch.zeros(10, 10) + torch.randn(10, 10, generator=g) * 0.01] for _ in range(4)]
+    ups.append([torch.randn(10, 10, generator=g) * 100])
+    _, _, sel, _, _ = orc.krum(ups, 1, 1)
+    assert 4 not in sel
+
+
+def test_ref_insufficient_clients():  # :83-91
+    with pytest.raises(ValueError):
+        orc.krum(mock_updates(3), 2, 1)
+
+
+def test_ref_trimmed_outliers():  # :112-129
+    base = torch.zeros(10)
+    ups = [[base + 0.1], [base + 0.2], [base], [base + 100], [base - 100]]
+    agg, t = orc.trimmed_mean(ups, 0.2)
+    assert t == 1 and agg[0].abs().mean() < 1.0
+
+
+def test_ref_median_outlier():  # :145-160
+    ups = [[torch.tensor([1.0, 1.0])], [torch.tensor([1.1, 0.9])], [torch.tensor([0.9, 1.1])],
+           [torch.tensor([100.0, 100.0])], [torch.tensor([1.0, 1.0])]]
+    assert torch.allclose(orc.median(ups)[0], torch.tensor([1.0, 1.0]), atol=0.2)
+
+
+def test_ref_lower_median_even():  # torch.median(dim=0) is the lower median
+    ups = [[torch.tensor([float(v)])] for v in (4, 1, 3, 2)]
+    assert orc.median(ups)[0].item() == 2.0
+
+
+def test_sign_flip_negates():  # model_poisoning.py:274-276
+    u = [torch.ones(3), -2 * torch.ones(2)]
+    assert all(torch.equal(a, -b) for a, b in zip(orc.sign_flip(u), u))
+
+
+# ---- op semantics restated by the kernels ----
+
+@pytest.mark.parametrize("n", [0, 1, 5, 7, 8, 9, 63, 64, 101, 127, 128, 129, 200, 255, 511, 1000])
+def test_numpy_pairwise_sum_exact(n):
+    a = np.random.default_rng(n).standard_normal(n) * 10
+    assert orc.numpy_pairwise_sum(a) == np.sum(a) or (n == 0 and np.sum(a) == 0)
+    assert 0.0 + orc.numpy_pairwise_sum(a) == np.sum(a)
+
+
+@pytest.mark.parametrize("R", [1, 5, 15, 16, 17, 33, 104, 206, 300])
+def test_torch_outer_sum_cascade(R):
+    x = torch.randn(R, 4096, generator=torch.Generator().manual_seed(R))
+    got = orc.torch_outer_sum(x)
+    ref = x.sum(dim=0)
+    assert torch.equal(got, ref)
+    assert torch.equal(x.mean(dim=0), ref / R)
+
+
+def test_scalar_division_is_ieee():
+    x = torch.randn(100003)
+    for k in (3, 7, 64, 101):
+        assert torch.equal(x / k, (x.double() / k).float())
+
+
+# ---- golden fixtures reproduce ----
+
+@pytest.mark.parametrize("path", golden_files("krum"), ids=lambda p: p.split("/")[-1])
+def test_golden_krum_reproduces(path):
+    fx = load_golden(path)
+    shapes = shapes_of(fx)
+    X = torch.from_numpy(fx["X"])
+    ups = split_rows(X, X.shape[1], shapes)
+    agg, scores, sel, rej, dist = orc.krum(ups, int(fx["f"]), int(fx["multi_k"]))
+    assert sel == fx["selected"].tolist() and rej == fx["rejected"].tolist()
+    np.testing.assert_array_equal(np.asarray(scores), fx["scores"])
+    np.testing.assert_array_equal(dist, fx["dist"])
+    flat = torch.cat([a.reshape(-1) for a in agg]).numpy()
+    np.testing.assert_array_equal(flat, fx["agg"])
+
+
+@pytest.mark.parametrize("path", golden_files("stat"), ids=lambda p: p.split("/")[-1])
+def test_golden_stats_reproduce(path):
+    fx = load_golden(path)
+    shapes = shapes_of(fx)
+    X = torch.from_numpy(fx["X"])
+    ups = split_rows(X, X.shape[1], shapes)
+    tm, t = orc.trimmed_mean(ups, float(fx["trim_ratio"]))
+    assert t == int(fx["t"])
+    cat = lambda lst: torch.cat([a.reshape(-1) for a in lst]).numpy()  # noqa: E731
+    np.testing.assert_array_equal(cat(tm), fx["trimmed"])
+    np.testing.assert_array_equal(cat(orc.median(ups)), fx["median"])
+    np.testing.assert_array_equal(cat(orc.fedavg(ups, fx["num_examples"].tolist())), fx["fedavg"])
+
+
+def test_golden_krum_margins_recorded():
+    for path in golden_files("krum"):
+        fx = load_golden(path)
+        assert float(fx["margin"]) > 0  # no exact tie at the selection boundary
