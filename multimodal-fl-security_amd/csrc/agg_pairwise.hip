@@ -5,10 +5,12 @@
 //
 // Engine (MFMA path, flr_pairwise_l2):
 //   ||x_i - x_j||^2 = G_ii + G_jj - 2 G_ij with G the Gram matrix of the
-//   per-coordinate CENTRED client matrix y = x - c (c = mean over the group's
-//   rows for that coordinate; distances are translation invariant, so any
-//   per-coordinate constant is exact, and centring removes the cancellation
-//   that makes a raw-weight Gram useless).  y is split into bf16 hi + lo
+//   CENTRED client matrix y = x - x_pivot (distances are translation
+//   invariant, so subtracting any per-coordinate constant is exact; centring
+//   removes the cancellation that makes a raw-weight Gram useless).  The pivot
+//   is the medoid of a strided 2048-coordinate sample (prepass kernels below):
+//   a central client, robust to < 50 % outliers, so benign pairs keep a
+//   cancellation factor (|y_i|^2+|y_j|^2)/|y_i-y_j|^2 of about 2.  y is split into bf16 hi + lo
 //   (y = hi + lo + O(2^-17 |y|)) and G_ij = sum (hi_i+lo_i)(hi_j+lo_j) is
 //   formed by four v_mfma_f32_32x32x16_bf16 products (each bf16*bf16 product is
 //   exact in fp32, accumulation fp32).  The diagonal G_ii comes from the same
@@ -23,6 +25,7 @@
 #include "flr_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace flr {
@@ -80,15 +83,47 @@ __host__ __device__ inline int diag_tile_index(int nl, int a, int b) {
   return t + (b - a);
 }
 
-// Sum over the 32 lanes of each half-wave; every lane ends with the same value
-// (each step pairs lanes symmetrically, so fp addition order is identical).
-__device__ __forceinline__ float half_wave_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // xor 1
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // xor 2
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)); // half mirror
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)); // mirror
-  v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));                     // xor 16
-  return v;
+// LDS fragment reads as ONE asm statement (reads + lgkmcnt(0) together, outputs
+// early-clobber): hipcc cannot see them, so it does not put its conservative
+// vmcnt(0) (for the in-flight LDS-DMA into the other buffer) in front of them.
+// Block b of the image sits at +8192 B * b; a0/a1 are the byte addresses of this
+// lane's two 16-B slots in block 0.
+#define FLR_DSR(n, o) "ds_read_b128 %" #n ", %" #o
+template <int NL>
+__device__ __forceinline__ void lds_read_blocks(uint32_t a0, uint32_t a1, f32x4 (&v)[NL][2]) {
+  if constexpr (NL == 1) {
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(v[0][0]), "=&v"(v[0][1]) : "v"(a0), "v"(a1) : "memory");
+  } else if constexpr (NL == 2) {
+    asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\t"
+                 "ds_read_b128 %2, %4 offset:8192\n\tds_read_b128 %3, %5 offset:8192\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[1][0]), "=&v"(v[1][1]) : "v"(a0), "v"(a1) : "memory");
+  } else if constexpr (NL == 3) {
+    asm volatile("ds_read_b128 %0, %6\n\tds_read_b128 %1, %7\n\t"
+                 "ds_read_b128 %2, %6 offset:8192\n\tds_read_b128 %3, %7 offset:8192\n\t"
+                 "ds_read_b128 %4, %6 offset:16384\n\tds_read_b128 %5, %7 offset:16384\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[2][0]), "=&v"(v[2][1])
+                 : "v"(a0), "v"(a1) : "memory");
+  } else if constexpr (NL == 4) {
+    asm volatile("ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\t"
+                 "ds_read_b128 %2, %8 offset:8192\n\tds_read_b128 %3, %9 offset:8192\n\t"
+                 "ds_read_b128 %4, %8 offset:16384\n\tds_read_b128 %5, %9 offset:16384\n\t"
+                 "ds_read_b128 %6, %8 offset:24576\n\tds_read_b128 %7, %9 offset:24576\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[2][0]), "=&v"(v[2][1]),
+                   "=&v"(v[3][0]), "=&v"(v[3][1])
+                 : "v"(a0), "v"(a1) : "memory");
+  } else {
+    static_assert(NL == 6, "unsupported block count");
+    asm volatile("ds_read_b128 %0, %12\n\tds_read_b128 %1, %13\n\t"
+                 "ds_read_b128 %2, %12 offset:8192\n\tds_read_b128 %3, %13 offset:8192\n\t"
+                 "ds_read_b128 %4, %12 offset:16384\n\tds_read_b128 %5, %13 offset:16384\n\t"
+                 "ds_read_b128 %6, %12 offset:24576\n\tds_read_b128 %7, %13 offset:24576\n\t"
+                 "ds_read_b128 %8, %12 offset:32768\n\tds_read_b128 %9, %13 offset:32768\n\t"
+                 "ds_read_b128 %10, %12 offset:40960\n\tds_read_b128 %11, %13 offset:40960\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[2][0]), "=&v"(v[2][1]),
+                   "=&v"(v[3][0]), "=&v"(v[3][1]), "=&v"(v[4][0]), "=&v"(v[4][1]), "=&v"(v[5][0]), "=&v"(v[5][1])
+                 : "v"(a0), "v"(a1) : "memory");
+  }
 }
 
 struct GroupDesc {
@@ -119,10 +154,10 @@ __device__ __forceinline__ GroupDesc group_desc(int g, int K, bool cross) {
   return d;
 }
 
-template <int NL, bool CROSS>
+template <int NL, bool CROSS, int TERMS, int ABLATE = 0>
 __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
     const float* __restrict__ X, int K, int64_t ldx, int nchunks, int group_base,
-    float* __restrict__ partials, int nseg) {
+    const int* __restrict__ pivot_ptr, float* __restrict__ partials, int nseg) {
   using TS = TileSet<NL, CROSS>;
   constexpr int NT = TS::N;
   constexpr int ROWS = 32 * NL;
@@ -137,8 +172,11 @@ __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
   const int h = lane >> 5, r = lane & 31;
   const GroupDesc gd = group_desc(g, K, CROSS);
 
-  const int c_begin = (int)((int64_t)nchunks * seg / nseg);
-  const int c_end = (int)((int64_t)nchunks * (seg + 1) / nseg);
+  // Round-robin chunks: at any moment the grid reads one contiguous span of
+  // nseg*256 B of every row (DRAM-page friendly), not nseg scattered 256-B runs.
+  const int c_begin = seg;
+  const int c_end = nchunks;
+  const int c_step = nseg;
 
   // Per-lane DMA source rows: instruction q of this wave covers LDS rows
   // 4*inst .. 4*inst+3, inst = wave*2*NL + q; this lane feeds row inst*4+lane/16.
@@ -152,6 +190,19 @@ __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
     const int slot = (lane & 15) ^ (lrow & 15);  // XOR swizzle on the source
     src_row[q] = X + (int64_t)grow * ldx + 4 * slot;
   }
+
+  // centre values for this lane's 8 coordinates of the wave's k-step
+  const int pivot = __builtin_amdgcn_readfirstlane(*pivot_ptr);
+  const float* cen_src = X + (int64_t)pivot * ldx + 16 * wave + 8 * h;
+  auto load_cen = [&](int chunk, float (&c)[8]) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(cen_src + (int64_t)chunk * CW);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(cen_src + (int64_t)chunk * CW + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c[j] = a[j];
+      c[4 + j] = b[j];
+    }
+  };
 
   auto stage = [&](int chunk, float* buf) {
 #pragma unroll
@@ -172,52 +223,60 @@ __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
 #pragma unroll
   for (int b = 0; b < NL; ++b) dsum[b] = 0.f;
 
-  const float inv_rows = 1.0f / (float)ROWS;
   int cur = 0;
-  if (c_begin < c_end) stage(c_begin, lds);
+  float cen[8], cen_next[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cen[j] = cen_next[j] = 0.f;
+  if (c_begin < c_end) {
+    stage(c_begin, lds);
+    load_cen(c_begin, cen);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int c = c_begin; c < c_end; ++c) {
+  for (int c = c_begin; c < c_end; c += c_step) {
     float* buf = lds + cur * BUF;
-    if (c + 1 < c_end) stage(c + 1, lds + (cur ^ 1) * BUF);
+    if (c + c_step < c_end && ABLATE != 2) {
+      stage(c + c_step, lds + (cur ^ 1) * BUF);
+      load_cen(c + c_step, cen_next);
+    }
+    if constexpr (ABLATE == 1) {
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      cur ^= 1;
+      continue;
+    }
 
     // ---- this wave's k-step: coordinates 16*wave + 8h + j of the chunk ----
     float raw[NL][8];
-#pragma unroll
-    for (int b = 0; b < NL; ++b) {
-      const int lrow = 32 * b + r;
+    {
+      // row r of every block has the same swizzle (32*b + r = r mod 16)
       const int s0 = 4 * wave + 2 * h;
-      const int p0 = s0 ^ (lrow & 15), p1 = (s0 + 1) ^ (lrow & 15);
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(buf + lrow * CW + 4 * p0);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(buf + lrow * CW + 4 * p1);
+      const int p0 = s0 ^ (r & 15), p1 = (s0 + 1) ^ (r & 15);
+      const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(buf) + (uint32_t)(r * CW * 4);
+      f32x4 v[NL][2];
+      lds_read_blocks<NL>(base + 16u * p0, base + 16u * p1, v);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        raw[b][j] = v0[j];
-        raw[b][4 + j] = v1[j];
-      }
+      for (int b = 0; b < NL; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          raw[b][j] = v[b][0][j];
+          raw[b][4 + j] = v[b][1][j];
+        }
     }
-    float cen[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float s = raw[0][j];
-#pragma unroll
-      for (int b = 1; b < NL; ++b) s += raw[b][j];
-      cen[j] = half_wave_sum(s) * inv_rows;
-    }
-    bf16x8 hi[NL], lo[NL];
+    bf16x8 hi[NL], lo[NL], lo2[NL];
 #pragma unroll
     for (int b = 0; b < NL; ++b) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float y = raw[b][j] - cen[j];
         const __bf16 hb = (__bf16)y;
-        const float hf = (float)hb;
-        const __bf16 lb = (__bf16)(y - hf);
+        const float r1 = y - (float)hb;
+        const __bf16 lb = (__bf16)r1;
         hi[b][j] = hb;
         lo[b][j] = lb;
-        const float v = hf + (float)lb;
-        dsum[b] = __builtin_fmaf(v, v, dsum[b]);
+        if constexpr (TERMS == 3) lo2[b][j] = (__bf16)(r1 - (float)lb);
+        dsum[b] = __builtin_fmaf(y, y, dsum[b]);
       }
     }
     static_for<0, NT>([&](auto tc) {
@@ -227,11 +286,20 @@ __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
       acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi[a], lo[bb], acc[t], 0, 0, 0);
       acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lo[a], hi[bb], acc[t], 0, 0, 0);
       acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lo[a], lo[bb], acc[t], 0, 0, 0);
+      if constexpr (TERMS == 3) {
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi[a], lo2[bb], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lo2[a], hi[bb], acc[t], 0, 0, 0);
+      }
     });
 
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // next chunk landed (this wave's DMA + centre loads), then every wave is
+    // done reading `cur` before anyone restages it.  sched_barrier keeps the
+    // register-only MFMA/VALU work of this chunk in front of the wait.
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     cur ^= 1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cen[j] = cen_next[j];
   }
 
   // ---- epilogue: reduce the 4 waves in fixed order, write the record ----
@@ -260,24 +328,43 @@ __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
   }
 }
 
-// Sum the per-segment records of every group in fixed order (fp64).
-// Thread (w, lane): entry blockIdx.x*64 + lane, segments s = w (mod 4).
+// Sum the per-segment records of every group in fixed order (fp64), in two
+// stages: stage 1 (grid.z = RSPLIT) sums a contiguous run of segments per
+// split with 4 waves x 4 independent accumulators; stage 2 adds the splits.
+constexpr int RSPLIT = 8;
 __global__ __launch_bounds__(256) void reduce_records_kernel(const float* __restrict__ partials,
-                                                              int nseg, double* __restrict__ gsum) {
+                                                              int nseg, double* __restrict__ stage1) {
   __shared__ double red[4][64];
-  const int g = blockIdx.y;
+  const int g = blockIdx.y, z = blockIdx.z;
   const int e = blockIdx.x * 64 + (threadIdx.x & 63);
   const int w = threadIdx.x >> 6;
-  double s = 0.0;
+  const int s0 = (int)((int64_t)nseg * z / RSPLIT), s1 = (int)((int64_t)nseg * (z + 1) / RSPLIT);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   if (e < REC) {
     const float* p = partials + (int64_t)g * nseg * REC + e;
-    for (int k = w; k < nseg; k += 4) s += (double)p[(int64_t)k * REC];
+    int k = s0 + w;
+    for (; k + 12 < s1; k += 16) {
+      a0 += (double)p[(int64_t)k * REC];
+      a1 += (double)p[(int64_t)(k + 4) * REC];
+      a2 += (double)p[(int64_t)(k + 8) * REC];
+      a3 += (double)p[(int64_t)(k + 12) * REC];
+    }
+    for (; k < s1; k += 4) a0 += (double)p[(int64_t)k * REC];
   }
-  red[w][threadIdx.x & 63] = s;
+  red[w][threadIdx.x & 63] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (w == 0 && e < REC)
-    gsum[(int64_t)g * REC + e] =
+    stage1[((int64_t)g * RSPLIT + z) * REC + e] =
         ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
+__global__ void reduce_splits_kernel(const double* __restrict__ stage1, int ngroups, double* __restrict__ gsum) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)ngroups * REC) return;
+  const int g = (int)(idx / REC), e = (int)(idx % REC);
+  double s = 0.0;
+  for (int z = 0; z < RSPLIT; ++z) s += stage1[((int64_t)g * RSPLIT + z) * REC + e];
+  gsum[idx] = s;
 }
 
 // Exact-difference contribution of the coordinates that do not fill a chunk.
@@ -353,6 +440,50 @@ __global__ void assemble_kernel(const double* __restrict__ gsum, const double* _
   D[idx] = (double)(float)sqrt(d2);
 }
 
+// ---- pivot prepass: medoid of a strided coordinate sample ----
+// Xs[i][s] = X[i][s*stride] (row-major, ld = SAMPLE); the sample's exact
+// distances come from the direct kernel below; pivot = argmin_i sum_j Ds[i][j].
+constexpr int SAMPLE = 2048;
+constexpr int MAXK_PIVOT = 1024;
+constexpr int SAMPLE_NSEG = 8;
+
+__global__ void sample_gather_kernel(const float* __restrict__ X, int K, int64_t ldx, int S, int64_t stride,
+                                     float* __restrict__ Xs) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)K * S) return;
+  const int i = (int)(idx / S), s = (int)(idx % S);
+  Xs[idx] = X[(int64_t)i * ldx + (int64_t)s * stride];
+}
+
+// One workgroup: rowsum_i = sum_j Ds[i][j] (fp64, j order), then argmin
+// (lowest index on ties).
+__global__ __launch_bounds__(256) void pivot_kernel(const double* __restrict__ Ds, int K, int* __restrict__ pivot) {
+  __shared__ double bv[256];
+  __shared__ int bi[256];
+  double v = __builtin_huge_val();
+  int ix = 0x7fffffff;
+  for (int i = threadIdx.x; i < K; i += 256) {
+    double r = 0.0;
+    for (int j = 0; j < K; ++j) r += Ds[(int64_t)i * K + j];
+    if (r < v) { v = r; ix = i; }
+  }
+  bv[threadIdx.x] = v;
+  bi[threadIdx.x] = ix;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const double v2 = bv[threadIdx.x + o];
+      const int i2 = bi[threadIdx.x + o];
+      if (v2 < bv[threadIdx.x] || (v2 == bv[threadIdx.x] && i2 < bi[threadIdx.x])) {
+        bv[threadIdx.x] = v2;
+        bi[threadIdx.x] = i2;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *pivot = bi[0] == 0x7fffffff ? 0 : bi[0];
+}
+
 struct Plan {
   int nchunks;       // full 64-coordinate chunks
   int nseg;          // segments per group
@@ -380,16 +511,74 @@ inline Plan make_plan(int64_t K, int64_t P) {
   return p;
 }
 
-inline size_t ws_partials(const Plan& p) { return (size_t)p.ngroups() * p.nseg * REC * sizeof(float); }
-inline size_t ws_gsum(const Plan& p) { return (size_t)p.ngroups() * REC * sizeof(double); }
+inline int direct_npairs(int64_t K) {
+  const int nb = cdiv((int)K, 32);
+  return nb * (nb + 1) / 2;
+}
+
+// Workspace carve-up (every piece 256-B aligned).
+struct Layout {
+  size_t partials, stage1, gsum, tail, xs, spart, ds, pivot, total;
+};
+inline Layout layout(int64_t K, int64_t P) {
+  const Plan p = make_plan(K, P);
+  Layout l;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off += align_up(bytes, 256); return o; };
+  l.partials = take((size_t)p.ngroups() * p.nseg * REC * sizeof(float));
+  l.stage1 = take((size_t)p.ngroups() * RSPLIT * REC * sizeof(double));
+  l.gsum = take((size_t)p.ngroups() * REC * sizeof(double));
+  l.tail = take((size_t)K * K * sizeof(double));
+  l.xs = take((size_t)K * SAMPLE * sizeof(float));
+  l.spart = take((size_t)direct_npairs(K) * SAMPLE_NSEG * 1024 * sizeof(float));
+  l.ds = take((size_t)K * K * sizeof(double));
+  l.pivot = take(sizeof(int));
+  l.total = off;
+  return l;
+}
+
+inline int gram_ablate() {
+  static const int a = [] {
+    const char* e = getenv("FLR_GRAM_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  return a;
+}
+
+// bf16 terms per value: 3 (hi+mid+lo, 6 MFMA products) removes the split's
+// representation error, which dominates below ~1M coordinates; above that the
+// fp32 accumulation dominates and 2 terms (4 products) measure the same error
+// at 2/3 of the kernel time.  FLR_GRAM_TERMS=2|3 overrides.
+inline int gram_terms(int64_t P) {
+  const char* e = getenv("FLR_GRAM_TERMS");
+  if (e && (e[0] == '2' || e[0] == '3')) return e[0] - '0';
+  return P < (int64_t(1) << 20) ? 3 : 2;
+}
 
 template <int NL, bool CROSS>
-int launch_gram(const float* X, int K, int64_t ldx, const Plan& p, int group_base, int ngroups,
-                float* partials, hipStream_t st) {
+int launch_gram(const float* X, int K, int64_t ldx, int64_t P, const Plan& p, int group_base, int ngroups,
+                const int* pivot, float* partials, hipStream_t st) {
   const size_t lds = (size_t)2 * 32 * NL * CW * sizeof(float);
   dim3 grid(p.nseg, ngroups);
-  hipLaunchKernelGGL((gram_partials_kernel<NL, CROSS>), grid, dim3(THREADS), lds, st, X, K, ldx,
-                     p.nchunks, group_base, partials + (size_t)group_base * p.nseg * REC, p.nseg);
+  if (gram_terms(P) == 3) {
+    hipLaunchKernelGGL((gram_partials_kernel<NL, CROSS, 3>), grid, dim3(THREADS), lds, st, X, K, ldx,
+                       p.nchunks, group_base, pivot, partials + (size_t)group_base * p.nseg * REC, p.nseg);
+    return launch_status("gram_partials_kernel");
+  }
+  if constexpr (NL == 4 && !CROSS) {
+    if (gram_ablate() == 1) {
+      hipLaunchKernelGGL((gram_partials_kernel<4, false, 2, 1>), grid, dim3(THREADS), lds, st, X, K, ldx,
+                         p.nchunks, group_base, pivot, partials + (size_t)group_base * p.nseg * REC, p.nseg);
+      return launch_status("gram_partials_kernel");
+    }
+    if (gram_ablate() == 2) {
+      hipLaunchKernelGGL((gram_partials_kernel<4, false, 2, 2>), grid, dim3(THREADS), lds, st, X, K, ldx,
+                         p.nchunks, group_base, pivot, partials + (size_t)group_base * p.nseg * REC, p.nseg);
+      return launch_status("gram_partials_kernel");
+    }
+  }
+  hipLaunchKernelGGL((gram_partials_kernel<NL, CROSS, 2>), grid, dim3(THREADS), lds, st, X, K, ldx,
+                     p.nchunks, group_base, pivot, partials + (size_t)group_base * p.nseg * REC, p.nseg);
   return launch_status("gram_partials_kernel");
 }
 
@@ -480,52 +669,74 @@ using namespace flr::pw;
 
 extern "C" size_t flr_pairwise_l2_workspace(int64_t K, int64_t P) {
   if (K < 1 || P < 0) return 0;
-  const Plan p = make_plan(K, P);
-  return align_up(ws_partials(p), 256) + align_up(ws_gsum(p), 256) +
-         align_up((size_t)K * K * sizeof(double), 256);
+  return layout(K, P).total;
 }
 
 extern "C" int flr_pairwise_l2(const float* X, int64_t K, int64_t P, int64_t ldx, double* D,
                                void* workspace, size_t workspace_bytes, void* stream) {
   if (K < 1 || P < 0 || ldx < P || !D || (K > 1 && P > 0 && !X)) return FLR_ERR_ARG;
-  if (K > (1 << 16)) return FLR_ERR_UNSUPPORTED;
-  const size_t need = flr_pairwise_l2_workspace(K, P);
-  if (!workspace || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 255))
+  if (K > MAXK_PIVOT) return FLR_ERR_UNSUPPORTED;
+  const Layout L = layout(K, P);
+  if (!workspace || workspace_bytes < L.total || (reinterpret_cast<uintptr_t>(workspace) & 255))
     return FLR_ERR_WORKSPACE;
   hipStream_t st = as_stream(stream);
   const Plan p = make_plan(K, P);
   char* w = static_cast<char*>(workspace);
-  float* partials = reinterpret_cast<float*>(w);
-  double* gsum = reinterpret_cast<double*>(w + align_up(ws_partials(p), 256));
-  double* tail = reinterpret_cast<double*>(w + align_up(ws_partials(p), 256) + align_up(ws_gsum(p), 256));
+  float* partials = reinterpret_cast<float*>(w + L.partials);
+  double* stage1 = reinterpret_cast<double*>(w + L.stage1);
+  double* gsum = reinterpret_cast<double*>(w + L.gsum);
+  double* tail = reinterpret_cast<double*>(w + L.tail);
+  float* Xs = reinterpret_cast<float*>(w + L.xs);
+  float* spart = reinterpret_cast<float*>(w + L.spart);
+  double* Ds = reinterpret_cast<double*>(w + L.ds);
+  int* pivot = reinterpret_cast<int*>(w + L.pivot);
 
-  // The DMA path reads 16-B pieces: needs 16-B aligned rows.
+  // The DMA path reads 16-B pieces: it needs 16-B aligned rows.
   const bool aligned = ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && (ldx % 4 == 0);
   const int64_t p_main = aligned ? (int64_t)p.nchunks * CW : 0;
   const int K32 = (int)K;
+  const int nblk = (int)((K * K + 255) / 256);
   int rc = FLR_OK;
   if (p_main > 0) {
+    // 1. pivot: medoid of a strided sample of the main region (exact differences)
+    const int S = (int)std::min<int64_t>(SAMPLE, p_main);
+    const int64_t stride = p_main / S;
+    hipLaunchKernelGGL(sample_gather_kernel, dim3((unsigned)cdiv(K32 * S, 256)), dim3(256), 0, st, X, K32, ldx,
+                       S, stride, Xs);
+    if ((rc = launch_status("sample_gather_kernel")) != FLR_OK) return rc;
+    const int snseg = std::min(SAMPLE_NSEG, cdiv(S, DCW));
+    hipLaunchKernelGGL(direct_partials_kernel, dim3(snseg, direct_npairs(K)), dim3(256), 0, st, Xs, K32,
+                       (int64_t)S, (int64_t)S, snseg, spart);
+    if ((rc = launch_status("direct_partials_kernel(sample)")) != FLR_OK) return rc;
+    hipLaunchKernelGGL(direct_assemble_kernel, dim3(nblk), dim3(256), 0, st, spart, K32, snseg, Ds);
+    if ((rc = launch_status("direct_assemble_kernel(sample)")) != FLR_OK) return rc;
+    hipLaunchKernelGGL(pivot_kernel, dim3(1), dim3(256), 0, st, Ds, K32, pivot);
+    if ((rc = launch_status("pivot_kernel")) != FLR_OK) return rc;
+    // 2. centred Gram partials over every full chunk
     if (K <= SUPER) {
       switch (p.nl_diag) {
-        case 1: rc = launch_gram<1, false>(X, K32, ldx, p, 0, 1, partials, st); break;
-        case 2: rc = launch_gram<2, false>(X, K32, ldx, p, 0, 1, partials, st); break;
-        case 3: rc = launch_gram<3, false>(X, K32, ldx, p, 0, 1, partials, st); break;
-        default: rc = launch_gram<4, false>(X, K32, ldx, p, 0, 1, partials, st); break;
+        case 1: rc = launch_gram<1, false>(X, K32, ldx, P, p, 0, 1, pivot, partials, st); break;
+        case 2: rc = launch_gram<2, false>(X, K32, ldx, P, p, 0, 1, pivot, partials, st); break;
+        case 3: rc = launch_gram<3, false>(X, K32, ldx, P, p, 0, 1, pivot, partials, st); break;
+        default: rc = launch_gram<4, false>(X, K32, ldx, P, p, 0, 1, pivot, partials, st); break;
       }
     } else {
-      rc = launch_gram<4, false>(X, K32, ldx, p, 0, p.ngroups_diag, partials, st);
+      rc = launch_gram<4, false>(X, K32, ldx, P, p, 0, p.ngroups_diag, pivot, partials, st);
       if (rc == FLR_OK)
-        rc = launch_gram<6, true>(X, K32, ldx, p, p.ngroups_diag, p.ngroups_cross, partials, st);
+        rc = launch_gram<6, true>(X, K32, ldx, P, p, p.ngroups_diag, p.ngroups_cross, pivot, partials, st);
     }
     if (rc != FLR_OK) return rc;
-    dim3 rgrid(cdiv(REC, 64), p.ngroups());
-    hipLaunchKernelGGL(reduce_records_kernel, rgrid, dim3(256), 0, st, partials, p.nseg, gsum);
+    // 3. fixed-order fp64 reduction of the per-segment records
+    hipLaunchKernelGGL(reduce_records_kernel, dim3(cdiv(REC, 64), p.ngroups(), RSPLIT), dim3(256), 0, st, partials,
+                       p.nseg, stage1);
     if ((rc = launch_status("reduce_records_kernel")) != FLR_OK) return rc;
+    hipLaunchKernelGGL(reduce_splits_kernel, dim3(cdiv(p.ngroups() * REC, 256)), dim3(256), 0, st, stage1,
+                       p.ngroups(), gsum);
+    if ((rc = launch_status("reduce_splits_kernel")) != FLR_OK) return rc;
   } else {
-    if (hipMemsetAsync(gsum, 0, ws_gsum(p), st) != hipSuccess) return FLR_ERR_HIP;
+    if (hipMemsetAsync(gsum, 0, (size_t)p.ngroups() * REC * sizeof(double), st) != hipSuccess) return FLR_ERR_HIP;
   }
-  const int64_t kk = K * K;
-  const int nblk = (int)((kk + 255) / 256);
+  // 4. exact contribution of the trailing partial chunk, then D
   hipLaunchKernelGGL(tail_d2_kernel, dim3(nblk), dim3(256), 0, st, X, K32, ldx, p_main, P, tail);
   if ((rc = launch_status("tail_d2_kernel")) != FLR_OK) return rc;
   hipLaunchKernelGGL(assemble_kernel, dim3(nblk), dim3(256), 0, st, gsum, tail, K32, D);
@@ -534,9 +745,7 @@ extern "C" int flr_pairwise_l2(const float* X, int64_t K, int64_t P, int64_t ldx
 
 extern "C" size_t flr_pairwise_l2_direct_workspace(int64_t K, int64_t P) {
   if (K < 1 || P < 0) return 0;
-  const int nb = cdiv((int)K, 32);
-  const int npairs = nb * (nb + 1) / 2;
-  return (size_t)npairs * direct_nseg(K, P) * 1024 * sizeof(float);
+  return (size_t)direct_npairs(K) * direct_nseg(K, P) * 1024 * sizeof(float);
 }
 
 extern "C" int flr_pairwise_l2_direct(const float* X, int64_t K, int64_t P, int64_t ldx, double* D,

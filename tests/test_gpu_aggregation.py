@@ -46,15 +46,24 @@ def test_pairwise_vs_golden(cuda, path, method):
 @pytest.mark.parametrize("K,P", [(1, 100), (2, 64), (3, 1), (33, 129), (64, 4096), (100, 6400),
                                  (128, 65536 + 17), (129, 3000), (200, 2048), (300, 1111)])
 def test_pairwise_gram_vs_direct_and_fp64(cuda, K, P):
-    X = update_matrix(K, P, f=K // 5, seed=K + P, device=cuda)[:, :P]
+    """Error model of the Gram path: relative error on a pair's
+    distance scales with its cancellation factor w.r.t. the medoid pivot —
+    ~1e-7 for pairs near the bulk, up to ~1e-5 for pairs inside a far outlier
+    cluster (here the f = K/5 sign-flipped clients).  The direct path has no
+    cancellation."""
+    f = K // 5
+    X = update_matrix(K, P, f=f, seed=K + P, device=cuda)[:, :P]
     Dg = ops.pairwise_l2(X, "gram").cpu().numpy()
     Dd = ops.pairwise_l2(X, "direct").cpu().numpy()
     Xd = X.double().cpu()
     exact = torch.cdist(Xd, Xd).numpy() if K > 1 else np.zeros((1, 1))
-    for D in (Dg, Dd):
+    benign = np.arange(K) >= f
+    for D, tol_bulk, tol_all in ((Dg, 2e-6, 2e-5), (Dd, 2e-6, 2e-6)):
         rel = np.abs(D - exact) / np.maximum(exact, 1e-30)
         np.fill_diagonal(rel, 0)
-        assert rel.max() < 5e-6, rel.max()
+        assert rel.max() < tol_all, rel.max()
+        assert rel[np.ix_(benign, np.ones(K, bool))].max() < tol_bulk
+        assert np.all(np.diag(D) == 0) and np.array_equal(D, D.T)
 
 
 def test_pairwise_large_offset_centering(cuda):
