@@ -49,6 +49,12 @@ int flr_pairwise_l2(const float* X, int64_t K, int64_t P, int64_t ldx,
                     double* D, void* workspace, size_t workspace_bytes,
                     void* stream);
 
+/* Same, recording two caller-created hipEvent_t around the main MFMA kernel
+ * launch(es) on `stream` (for live per-kernel timing); either may be NULL. */
+int flr_pairwise_l2_ex(const float* X, int64_t K, int64_t P, int64_t ldx,
+                       double* D, void* workspace, size_t workspace_bytes,
+                       void* stream, void* ev_begin, void* ev_end);
+
 /* Direct-difference VALU variant (same contract, exact fp32 differences);
  * a slower second implementation used to cross-check the MFMA path. */
 size_t flr_pairwise_l2_direct_workspace(int64_t K, int64_t P);
@@ -102,6 +108,36 @@ int flr_trimmed_mean(const float* X, int64_t K, int64_t P, int64_t ldx,
  */
 int flr_median_lower(const float* X, int64_t K, int64_t P, int64_t ldx,
                      float* out, void* stream);
+
+/* ---- a6 + a7: fused gradient clip + SGD-momentum step -----------------
+ * Replaces, for every client row at once, clip_grad_norm_(params, max_norm)
+ * + torch.optim.SGD(lr, momentum, weight_decay).step()
+ * (experiments/run_experiments.py:206-211, 234-235; fl_client.py:123-141):
+ *   coef_k = min(1, max_norm / (||G_k|| + 1e-6))   (skipped if max_norm <= 0)
+ *   g = coef_k*G_k + wd*X_k;  M_k = first ? g : momentum*M_k + g;  X_k -= lr*M_k
+ * X, G, M: device fp32 K×P (row stride ld), updated in place.  norms_out:
+ * optional device fp32 [K] (pre-clip gradient norms).
+ */
+size_t flr_clip_sgd_workspace(int64_t K);
+int flr_clip_sgd_step(float* X, const float* G, float* M, int64_t K, int64_t P,
+                      int64_t ld, float lr, float momentum, float weight_decay,
+                      float max_norm, int first_step, float* norms_out,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- a5: cross-entropy forward + backward ------------------------------
+ * Replaces nn.CrossEntropyLoss() (mean over each client's batch;
+ * run_experiments.py:186, 232) for K clients × B rows × C classes:
+ *   loss[k] = mean_b (logsumexp(z_kb) - z_kb[y_kb]);
+ *   dlogits = (softmax(z) - onehot(y)) / B.
+ * logits/dlogits: device fp32 [K*B, C]; labels: device int64 [K*B];
+ * loss: device fp32 [K]; loss_rows: device fp32 [K*B] scratch.
+ */
+int flr_cross_entropy(const float* logits, const int64_t* labels, int64_t K,
+                      int64_t B, int64_t C, float* loss, float* dlogits,
+                      float* loss_rows, void* stream);
+/* d[k, b, c] *= gk[k]  (chain rule for a per-client upstream gradient). */
+int flr_scale_client_rows(float* d, const float* gk, int64_t K, int64_t B,
+                          int64_t C, void* stream);
 
 #ifdef __cplusplus
 }

@@ -674,6 +674,12 @@ extern "C" size_t flr_pairwise_l2_workspace(int64_t K, int64_t P) {
 
 extern "C" int flr_pairwise_l2(const float* X, int64_t K, int64_t P, int64_t ldx, double* D,
                                void* workspace, size_t workspace_bytes, void* stream) {
+  return flr_pairwise_l2_ex(X, K, P, ldx, D, workspace, workspace_bytes, stream, nullptr, nullptr);
+}
+
+extern "C" int flr_pairwise_l2_ex(const float* X, int64_t K, int64_t P, int64_t ldx, double* D,
+                                  void* workspace, size_t workspace_bytes, void* stream, void* ev_begin,
+                                  void* ev_end) {
   if (K < 1 || P < 0 || ldx < P || !D || (K > 1 && P > 0 && !X)) return FLR_ERR_ARG;
   if (K > MAXK_PIVOT) return FLR_ERR_UNSUPPORTED;
   const Layout L = layout(K, P);
@@ -713,6 +719,7 @@ extern "C" int flr_pairwise_l2(const float* X, int64_t K, int64_t P, int64_t ldx
     hipLaunchKernelGGL(pivot_kernel, dim3(1), dim3(256), 0, st, Ds, K32, pivot);
     if ((rc = launch_status("pivot_kernel")) != FLR_OK) return rc;
     // 2. centred Gram partials over every full chunk
+    if (ev_begin && hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), st) != hipSuccess) return FLR_ERR_HIP;
     if (K <= SUPER) {
       switch (p.nl_diag) {
         case 1: rc = launch_gram<1, false>(X, K32, ldx, P, p, 0, 1, pivot, partials, st); break;
@@ -726,6 +733,7 @@ extern "C" int flr_pairwise_l2(const float* X, int64_t K, int64_t P, int64_t ldx
         rc = launch_gram<6, true>(X, K32, ldx, P, p, p.ngroups_diag, p.ngroups_cross, pivot, partials, st);
     }
     if (rc != FLR_OK) return rc;
+    if (ev_end && hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), st) != hipSuccess) return FLR_ERR_HIP;
     // 3. fixed-order fp64 reduction of the per-segment records
     hipLaunchKernelGGL(reduce_records_kernel, dim3(cdiv(REC, 64), p.ngroups(), RSPLIT), dim3(256), 0, st, partials,
                        p.nseg, stage1);

@@ -1,0 +1,178 @@
+// a5 / a6 / a7 — cross-entropy and the fused clip + SGD-momentum step, for all
+// clients of a GPU at once (client matrix layout, one row per client).
+//
+// Reference (per client, experiments/run_experiments.py:206-235):
+//   loss = CrossEntropyLoss()(model(x), y)                        (mean over batch)
+//   loss.backward(); clip_grad_norm_(params, 1.0); optimizer.step()
+//   optimizer = SGD(lr, momentum=0.9, weight_decay=wd), re-created per client
+//   per round, so the momentum buffer starts as a copy of the first gradient.
+// torch.optim.SGD (single-tensor path): g += wd*p; buf = g (first step) else
+// buf = momentum*buf + g; p += -lr*buf.  clip_grad_norm_: total = ||grads||_2,
+// coef = min(1, max_norm / (total + 1e-6)), g *= coef.
+#include "flr_common.h"
+
+namespace flr {
+namespace train {
+
+constexpr int THREADS = 256;
+constexpr int NBLK = 128;  // norm partial blocks per client row
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// partial[k][b] = sum of g^2 over block b of row k (fp64 for a stable norm).
+__global__ __launch_bounds__(THREADS) void sumsq_kernel(const float* __restrict__ G, int64_t P, int64_t ldg,
+                                                        double* __restrict__ partial) {
+  __shared__ double red[THREADS / 64];
+  const int k = blockIdx.y, b = blockIdx.x;
+  const float* g = G + (int64_t)k * ldg;
+  const int64_t p0 = P * b / NBLK, p1 = P * (b + 1) / NBLK;
+  double acc = 0.0;
+  for (int64_t p = p0 + threadIdx.x; p < p1; p += THREADS) {
+    const double v = (double)g[p];
+    acc += v * v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int w = 0; w < THREADS / 64; ++w) s += red[w];
+    partial[(int64_t)k * NBLK + b] = s;
+  }
+}
+
+// coef[k] = min(1, max_norm / (||g_k|| + 1e-6)) in fp32 (torch computes it in
+// the gradient dtype); norms_out[k] = ||g_k||.
+__global__ void clip_coef_kernel(const double* __restrict__ partial, int K, float max_norm,
+                                 float* __restrict__ coef, float* __restrict__ norms_out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  double s = 0.0;
+  for (int b = 0; b < NBLK; ++b) s += partial[(int64_t)k * NBLK + b];
+  const float total = (float)sqrt(s);
+  float c = __fdiv_rn(max_norm, __fadd_rn(total, 1e-6f));
+  coef[k] = c < 1.0f ? c : 1.0f;
+  if (norms_out) norms_out[k] = total;
+}
+
+// The whole optimizer step, one pass: g' = coef*g (+wd*p); buf; p.
+__global__ __launch_bounds__(THREADS) void sgd_kernel(float* __restrict__ X, const float* __restrict__ G,
+                                                      float* __restrict__ M, int64_t P, int64_t ld,
+                                                      const float* __restrict__ coef, float lr, float mom,
+                                                      float wd, int first) {
+  const int k = blockIdx.y;
+  const float c = coef ? coef[k] : 1.0f;
+  float* x = X + (int64_t)k * ld;
+  const float* g = G + (int64_t)k * ld;
+  float* m = M + (int64_t)k * ld;
+  const float nlr = -lr;
+  for (int64_t p = (int64_t)blockIdx.x * THREADS + threadIdx.x; p < P; p += (int64_t)gridDim.x * THREADS) {
+    const float xp = x[p];
+    float gp = g[p] * c;
+    if (wd != 0.0f) gp = __builtin_fmaf(wd, xp, gp);
+    const float b = first ? gp : m[p] * mom + gp;  // buf.mul_(mom).add_(g): two roundings
+    m[p] = b;
+    x[p] = __builtin_fmaf(nlr, b, xp);
+  }
+}
+
+// Cross-entropy over rows of logits [R, C] (R = K*B), labels int64 [R].
+// loss_row[r] = logsumexp - logit[label]; dlogits = (softmax - onehot) * scale
+// with scale = 1/B (mean over each client's batch).  One wave per row.
+__global__ __launch_bounds__(THREADS) void ce_kernel(const float* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                     int R, int C, float scale, float* __restrict__ loss_row,
+                                                     float* __restrict__ dlogits) {
+  const int r = blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const float* z = logits + (int64_t)r * C;
+  float mx = -__builtin_huge_valf();
+  for (int c = lane; c < C; c += 64) mx = fmaxf(mx, z[c]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float se = 0.f;
+  for (int c = lane; c < C; c += 64) se += expf(z[c] - mx);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+  const float lse = mx + logf(se);
+  const int64_t y = labels[r];
+  if (lane == 0) loss_row[r] = lse - z[y];
+  float* dz = dlogits + (int64_t)r * C;
+  for (int c = lane; c < C; c += 64) {
+    const float sm = expf(z[c] - lse);
+    dz[c] = (sm - (c == y ? 1.0f : 0.0f)) * scale;
+  }
+}
+
+// loss[k] = mean over the client's B rows (sequential, fp32).
+__global__ void ce_mean_kernel(const float* __restrict__ loss_row, int K, int B, float* __restrict__ loss) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += loss_row[(int64_t)k * B + b];
+  loss[k] = s / (float)B;
+}
+
+__global__ void scale_rows_kernel(float* __restrict__ d, const float* __restrict__ gk, int K, int B, int C) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)K * B * C) return;
+  d[i] *= gk[i / ((int64_t)B * C)];
+}
+
+}  // namespace train
+}  // namespace flr
+
+using namespace flr;
+
+extern "C" size_t flr_clip_sgd_workspace(int64_t K) {
+  return align_up((size_t)K * train::NBLK * sizeof(double), 256) + align_up((size_t)K * sizeof(float), 256);
+}
+
+extern "C" int flr_clip_sgd_step(float* X, const float* G, float* M, int64_t K, int64_t P, int64_t ld, float lr,
+                                 float momentum, float weight_decay, float max_norm, int first_step,
+                                 float* norms_out, void* workspace, size_t workspace_bytes, void* stream) {
+  if (K < 1 || P < 0 || ld < P || !X || !G || !M) return FLR_ERR_ARG;
+  if (max_norm > 0 && (!workspace || workspace_bytes < flr_clip_sgd_workspace(K))) return FLR_ERR_WORKSPACE;
+  if (P == 0) return FLR_OK;
+  hipStream_t st = as_stream(stream);
+  float* coef = nullptr;
+  int rc;
+  if (max_norm > 0) {
+    double* partial = static_cast<double*>(workspace);
+    coef = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                    align_up((size_t)K * train::NBLK * sizeof(double), 256));
+    hipLaunchKernelGGL(train::sumsq_kernel, dim3(train::NBLK, (unsigned)K), dim3(train::THREADS), 0, st, G, P, ld,
+                       partial);
+    if ((rc = launch_status("sumsq_kernel")) != FLR_OK) return rc;
+    hipLaunchKernelGGL(train::clip_coef_kernel, dim3(cdiv((int)K, 64)), dim3(64), 0, st, partial, (int)K, max_norm,
+                       coef, norms_out);
+    if ((rc = launch_status("clip_coef_kernel")) != FLR_OK) return rc;
+  }
+  const int64_t per_row = (P + train::THREADS - 1) / train::THREADS;
+  const unsigned gx = (unsigned)(per_row < 1024 ? per_row : 1024);
+  hipLaunchKernelGGL(train::sgd_kernel, dim3(gx, (unsigned)K), dim3(train::THREADS), 0, st, X, G, M, P, ld, coef, lr,
+                     momentum, weight_decay, first_step);
+  return launch_status("sgd_kernel");
+}
+
+extern "C" int flr_cross_entropy(const float* logits, const int64_t* labels, int64_t K, int64_t B, int64_t C,
+                                 float* loss, float* dlogits, float* loss_rows, void* stream) {
+  if (K < 1 || B < 1 || C < 1 || !logits || !labels || !loss || !dlogits || !loss_rows) return FLR_ERR_ARG;
+  hipStream_t st = as_stream(stream);
+  const int R = (int)(K * B);
+  hipLaunchKernelGGL(train::ce_kernel, dim3(cdiv(R, train::THREADS / 64)), dim3(train::THREADS), 0, st, logits,
+                     labels, R, (int)C, 1.0f / (float)B, loss_rows, dlogits);
+  int rc = launch_status("ce_kernel");
+  if (rc != FLR_OK) return rc;
+  hipLaunchKernelGGL(train::ce_mean_kernel, dim3(cdiv((int)K, 64)), dim3(64), 0, st, loss_rows, (int)K, (int)B, loss);
+  return launch_status("ce_mean_kernel");
+}
+
+extern "C" int flr_scale_client_rows(float* d, const float* gk, int64_t K, int64_t B, int64_t C, void* stream) {
+  if (K < 1 || B < 1 || C < 1 || !d || !gk) return FLR_ERR_ARG;
+  const int64_t n = K * B * C;
+  hipLaunchKernelGGL(train::scale_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), d,
+                     gk, (int)K, (int)B, (int)C);
+  return launch_status("scale_rows_kernel");
+}

@@ -33,6 +33,8 @@ SIGNATURES = {
     "flr_last_error": (ctypes.c_char_p, []),
     "flr_pairwise_l2_workspace": (_size_t, [_i64, _i64]),
     "flr_pairwise_l2": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "flr_pairwise_l2_ex": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p, _c_void_p,
+                                  _c_void_p]),
     "flr_pairwise_l2_direct_workspace": (_size_t, [_i64, _i64]),
     "flr_pairwise_l2_direct": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "flr_krum_select": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),
@@ -40,6 +42,11 @@ SIGNATURES = {
     "flr_fedavg": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),
     "flr_trimmed_mean": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p]),
     "flr_median_lower": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p]),
+    "flr_clip_sgd_workspace": (_size_t, [_i64]),
+    "flr_clip_sgd_step": (_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64, ctypes.c_float, ctypes.c_float,
+                                 ctypes.c_float, ctypes.c_float, _int, _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "flr_cross_entropy": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "flr_scale_client_rows": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p]),
 }
 
 _lock = threading.Lock()

@@ -32,15 +32,24 @@ def source_device(client_updates: Updates) -> torch.device:
 
 
 class BaseDefense(ABC):
-    """Abstract defense (base_defense.py:13-71)."""
+    """Abstract defense (base_defense.py:13-71).
+
+    Subclasses implement ``aggregate_flat(cm, num_examples) -> [P] tensor``
+    on a device client matrix; ``aggregate`` adapts the reference signature.
+    """
 
     def __init__(self, defense_config: Dict[str, Any]):
         self.config = defense_config
         self.name = self.__class__.__name__
 
     @abstractmethod
-    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
+    def aggregate_flat(self, cm: ClientMatrix, num_examples: List[int]) -> torch.Tensor:
         ...
+
+    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
+        cm = as_matrix(client_updates)
+        flat = self.aggregate_flat(cm, num_examples)
+        return cm.unflatten(flat, source_device(client_updates))
 
     def detect_malicious(self, client_updates: Updates, num_examples: List[int]) -> List[int]:
         return []
@@ -58,7 +67,5 @@ class NoDefense(BaseDefense):
     def __init__(self, defense_config: Dict[str, Any] = None):
         super().__init__(defense_config or {})
 
-    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
-        cm = as_matrix(client_updates)
-        flat = ops.fedavg(cm.X, list(num_examples))
-        return cm.unflatten(flat, source_device(client_updates))
+    def aggregate_flat(self, cm: ClientMatrix, num_examples: List[int]) -> torch.Tensor:
+        return ops.fedavg(cm.X, list(num_examples))

@@ -42,19 +42,31 @@ class KrumDefense(BaseDefense):
         self.scores_device, self.order_device = ops.krum_select(self.distances, f)
         return self.order_device
 
-    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
-        cm = as_matrix(client_updates)
+    def aggregate_flat(self, cm: ClientMatrix, num_examples: List[int], publish: bool = True) -> torch.Tensor:
+        """Device pipeline; with publish=False the host copies of the scores
+        and indices are skipped (no device sync) — call publish() later."""
         order = self.select(cm)
-        order_host = order.cpu().tolist()
+        if publish:
+            self.publish()
+        if self.multi_k == 1:
+            return cm.data[int(order[0].item()), : cm.P]
+        return ops.rows_mean(cm.X, order[: min(self.multi_k, cm.K)], divisor=self.multi_k)
+
+    def publish(self) -> None:
+        """Host copies of scores / selected / rejected (krum.py:171-176)."""
+        order_host = self.order_device.cpu().tolist()
         self.client_scores = self.scores_device.cpu().tolist()
         self.selected_clients = order_host[: self.multi_k]
         self.rejected_clients = order_host[self.multi_k:]
-        if self.multi_k == 1:
+
+    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
+        cm = as_matrix(client_updates)
+        if self.multi_k == 1:  # single Krum returns the caller's own list (krum.py:178-181)
+            self.select(cm)
+            self.publish()
             sel = self.selected_clients[0]
-            if isinstance(client_updates, ClientMatrix):
-                return client_updates.row(sel)
-            return client_updates[sel]
-        flat = ops.rows_mean(cm.X, order[: min(self.multi_k, cm.K)], divisor=self.multi_k)
+            return cm.row(sel) if isinstance(client_updates, ClientMatrix) else client_updates[sel]
+        flat = self.aggregate_flat(cm, num_examples)
         return cm.unflatten(flat, source_device(client_updates))
 
     def detect_malicious(self, client_updates: Updates, num_examples: List[int]) -> List[int]:

@@ -6,7 +6,8 @@ from typing import Any, Dict, List
 import torch
 
 from .. import ops
-from .base_defense import BaseDefense, Updates, as_matrix, source_device
+from ..matrix import ClientMatrix
+from .base_defense import BaseDefense
 
 
 class TrimmedMeanDefense(BaseDefense):
@@ -17,15 +18,12 @@ class TrimmedMeanDefense(BaseDefense):
         self.trim_ratio = defense_config.get("trim_ratio", 0.1)
         self.num_trimmed_per_end = 0
 
-    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
-        cm = as_matrix(client_updates)
+    def aggregate_flat(self, cm: ClientMatrix, num_examples: List[int]) -> torch.Tensor:
         n = cm.K
         self.num_trimmed_per_end = max(1, int(n * self.trim_ratio))
         if n - 2 * self.num_trimmed_per_end < 1:
-            flat = ops.median_lower(cm.X)
-        else:
-            flat = ops.trimmed_mean(cm.X, self.num_trimmed_per_end)
-        return cm.unflatten(flat, source_device(client_updates))
+            return ops.median_lower(cm.X)
+        return ops.trimmed_mean(cm.X, self.num_trimmed_per_end)
 
     def get_metrics(self) -> Dict[str, Any]:
         return {
@@ -44,10 +42,8 @@ class MedianDefense(BaseDefense):
     def __init__(self, defense_config: Dict[str, Any] = None):
         super().__init__(defense_config or {})
 
-    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
-        cm = as_matrix(client_updates)
-        flat = ops.median_lower(cm.X)
-        return cm.unflatten(flat, source_device(client_updates))
+    def aggregate_flat(self, cm: ClientMatrix, num_examples: List[int]) -> torch.Tensor:
+        return ops.median_lower(cm.X)
 
     def get_metrics(self) -> Dict[str, Any]:
         return {"defense_type": "median"}

@@ -1,0 +1,194 @@
+"""The multimodal client model: ResNet-18 image trunk + 1-layer GRU text
+encoder + late-fusion MLP (BASELINE.json configs C2/C3).
+
+The reference's only multimodal model is CUB200MultimodalCNN
+(src/models/cub200_cnn.py:57-118): conv image branch, a second modality
+branch, concat late fusion, Linear -> ReLU -> Dropout -> Linear head.  The
+BASELINE configs name ResNet-18 for the image and a 1-layer GRU for the text,
+which the reference does not contain; this module keeps the reference's
+fusion-head structure (cub200_cnn.py:88-93, 109-117) and uses the standard
+ResNet-18 (BasicBlock [2,2,2,2], 7x7/2 stem + 3x3/2 max-pool) and torch GRU
+definitions for the branches.
+
+Two forms of the same network:
+* ``MultimodalNet`` — a plain ``nn.Module`` for ONE client; its
+  ``parameters()`` order defines the client-matrix row layout.  The oracle
+  trains it with the reference's loop.
+* ``batched_forward`` — the engine's client-batched form: every weight is a
+  [K, ...] tensor (a view of the client matrix), activations for all K
+  clients travel together (convolutions as grouped convolutions, GRU / MLP as
+  batched matmuls), so one launch serves every client of a GPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass(frozen=True)
+class ModelSpec:
+    num_classes: int = 10
+    image_size: int = 32
+    in_channels: int = 3
+    widths: Tuple[int, ...] = (64, 128, 256, 512)
+    blocks: Tuple[int, ...] = (2, 2, 2, 2)
+    vocab: int = 1000
+    seq_len: int = 16
+    embed: int = 128
+    hidden: int = 256
+    fusion: int = 256
+    dropout: float = 0.5
+
+    @property
+    def name(self) -> str:
+        return "resnet18-img+gru1-text late-fusion"
+
+
+TINY = ModelSpec(widths=(8, 16, 16, 32), blocks=(1, 1, 1, 1), vocab=50, embed=8, hidden=16, fusion=16,
+                 dropout=0.0)
+
+
+class BasicBlock(nn.Module):
+    def __init__(self, cin: int, cout: int, stride: int):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        y = F.relu(self.bn1(self.conv1(x)))
+        y = self.bn2(self.conv2(y))
+        return F.relu(y + idt)
+
+
+class MultimodalNet(nn.Module):
+    def __init__(self, spec: ModelSpec = ModelSpec()):
+        super().__init__()
+        self.spec = spec
+        w = spec.widths
+        self.conv1 = nn.Conv2d(spec.in_channels, w[0], 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(w[0])
+        layers = []
+        cin = w[0]
+        for i, (cout, n) in enumerate(zip(w, spec.blocks)):
+            blocks = []
+            for b in range(n):
+                blocks.append(BasicBlock(cin, cout, 2 if (b == 0 and i > 0) else 1))
+                cin = cout
+            layers.append(nn.Sequential(*blocks))
+        self.layers = nn.Sequential(*layers)
+        self.embedding = nn.Embedding(spec.vocab, spec.embed)
+        self.gru = nn.GRU(spec.embed, spec.hidden, num_layers=1, batch_first=True)
+        self.fc1 = nn.Linear(w[-1] + spec.hidden, spec.fusion)
+        self.dropout = nn.Dropout(spec.dropout)
+        self.fc2 = nn.Linear(spec.fusion, spec.num_classes)
+
+    def forward(self, images: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
+        x = F.relu(self.bn1(self.conv1(images)))
+        x = F.max_pool2d(x, 3, 2, 1)
+        x = self.layers(x)
+        img = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        _, h = self.gru(self.embedding(tokens))
+        txt = h[-1]
+        z = torch.cat([img, txt], dim=1)
+        z = self.dropout(F.relu(self.fc1(z)))
+        return self.fc2(z)
+
+
+def param_layout(spec: ModelSpec) -> List[Tuple[str, torch.Size]]:
+    """(name, shape) in parameters() order — the client-matrix row layout."""
+    with torch.device("meta"):
+        m = MultimodalNet(spec)
+    return [(n, p.shape) for n, p in m.named_parameters()]
+
+
+def num_params(spec: ModelSpec) -> int:
+    return sum(int(s.numel()) for _, s in param_layout(spec))
+
+
+# ---------------------------------------------------------------------------
+# client-batched form
+# ---------------------------------------------------------------------------
+
+def split_params(X: torch.Tensor, spec: ModelSpec) -> Dict[str, torch.Tensor]:
+    """Views [K, *shape] of the client matrix X [K, >=P] per parameter."""
+    out, off = {}, 0
+    K = X.shape[0]
+    for name, shape in param_layout(spec):
+        n = int(shape.numel())
+        out[name] = X[:, off:off + n].view(K, *shape)
+        off += n
+    return out
+
+
+def _gconv(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
+    """x [B, K*Cin, H, W], w [K, Cout, Cin, kh, kw] -> [B, K*Cout, H', W']."""
+    K, cout = w.shape[0], w.shape[1]
+    return F.conv2d(x, w.reshape(K * cout, *w.shape[2:]), stride=stride, padding=pad, groups=K)
+
+
+def _gbn(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Per-client BatchNorm in train mode (batch statistics); running stats are
+    not part of parameters() and never aggregated (run_experiments.py:238,258)."""
+    return F.batch_norm(x, None, None, g.reshape(-1), b.reshape(-1), training=True, momentum=0.0, eps=1e-5)
+
+
+def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: torch.Tensor, spec: ModelSpec,
+                    dropout_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """images [K, B, C, H, W], tokens [K, B, T] -> logits [K, B, num_classes].
+
+    dropout_mask: optional [K, B, fusion] tensor of {0, 1/(1-p)} (explicit masks
+    make the step reproducible); None applies no dropout.
+    """
+    K, B = images.shape[:2]
+    x = images.transpose(0, 1).reshape(B, K * spec.in_channels, *images.shape[3:])
+    x = F.relu(_gbn(_gconv(x, p["conv1.weight"], 2, 3), p["bn1.weight"], p["bn1.bias"]))
+    x = F.max_pool2d(x, 3, 2, 1)
+    w = spec.widths
+    for li, nblk in enumerate(spec.blocks):
+        for bi in range(nblk):
+            pre = f"layers.{li}.{bi}."
+            stride = 2 if (bi == 0 and li > 0) else 1
+            idt = x
+            if (pre + "downsample.0.weight") in p:
+                idt = _gbn(_gconv(x, p[pre + "downsample.0.weight"], stride, 0), p[pre + "downsample.1.weight"],
+                           p[pre + "downsample.1.bias"])
+            y = F.relu(_gbn(_gconv(x, p[pre + "conv1.weight"], stride, 1), p[pre + "bn1.weight"], p[pre + "bn1.bias"]))
+            y = _gbn(_gconv(y, p[pre + "conv2.weight"], 1, 1), p[pre + "bn2.weight"], p[pre + "bn2.bias"])
+            x = F.relu(y + idt)
+    img = x.mean(dim=(2, 3)).view(B, K, w[-1]).transpose(0, 1)  # [K, B, 512]
+
+    # text: embedding gather + GRU with per-client weights (gate order r, z, n)
+    V, E, H = spec.vocab, spec.embed, spec.hidden
+    table = p["embedding.weight"]  # [K, V, E]
+    T = tokens.shape[2]
+    kofs = (torch.arange(K, device=tokens.device) * V).view(K, 1, 1)
+    emb = table.reshape(K * V, E)[(tokens + kofs).reshape(-1)].view(K, B * T, E)
+    gi = torch.baddbmm(p["gru.bias_ih_l0"].unsqueeze(1), emb, p["gru.weight_ih_l0"].transpose(1, 2))
+    gi = gi.view(K, B, T, 3 * H)
+    whh_t = p["gru.weight_hh_l0"].transpose(1, 2)
+    bhh = p["gru.bias_hh_l0"].unsqueeze(1)
+    h = torch.zeros(K, B, H, device=images.device, dtype=images.dtype)
+    for t in range(T):
+        gh = torch.baddbmm(bhh, h, whh_t)
+        i_r, i_z, i_n = gi[:, :, t].chunk(3, dim=-1)
+        h_r, h_z, h_n = gh.chunk(3, dim=-1)
+        r = torch.sigmoid(i_r + h_r)
+        z = torch.sigmoid(i_z + h_z)
+        n = torch.tanh(i_n + r * h_n)
+        h = (1 - z) * n + z * h
+
+    f = torch.cat([img, h], dim=2)  # [K, B, 512 + H]
+    f = F.relu(torch.baddbmm(p["fc1.bias"].unsqueeze(1), f, p["fc1.weight"].transpose(1, 2)))
+    if dropout_mask is not None:
+        f = f * dropout_mask
+    return torch.baddbmm(p["fc2.bias"].unsqueeze(1), f, p["fc2.weight"].transpose(1, 2))

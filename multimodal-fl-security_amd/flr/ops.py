@@ -33,8 +33,11 @@ def _check_matrix(X: torch.Tensor, name: str = "X") -> Tuple[int, int, int]:
     return X.shape[0], X.shape[1], X.stride(0)
 
 
-def pairwise_l2(X: torch.Tensor, method: str = "gram") -> torch.Tensor:
-    """K×K float64 distances, D[i][j] = fp32 ||X_i - X_j|| (krum.py:73-99)."""
+def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None) -> torch.Tensor:
+    """K×K float64 distances, D[i][j] = fp32 ||X_i - X_j|| (krum.py:73-99).
+
+    events: optional (begin, end) raw hipEvent_t handles recorded around the
+    main MFMA kernel (flr.timing.HipEventPair)."""
     K, P, ldx = _check_matrix(X)
     D = torch.empty((K, K), dtype=torch.float64, device=X.device)
     if method == "gram":
@@ -46,7 +49,11 @@ def pairwise_l2(X: torch.Tensor, method: str = "gram") -> torch.Tensor:
     nbytes = int(getattr(_capi.lib(), ws_fn)(K, P))
     ws = torch.empty(max(nbytes, 256) + 256, dtype=torch.uint8, device=X.device)
     off = (-ws.data_ptr()) % 256
-    _capi.call(fn, X.data_ptr(), K, P, ldx, D.data_ptr(), ws.data_ptr() + off, nbytes, _stream(X))
+    if events is not None and method == "gram":
+        _capi.call("flr_pairwise_l2_ex", X.data_ptr(), K, P, ldx, D.data_ptr(), ws.data_ptr() + off, nbytes,
+                   _stream(X), events[0], events[1])
+    else:
+        _capi.call(fn, X.data_ptr(), K, P, ldx, D.data_ptr(), ws.data_ptr() + off, nbytes, _stream(X))
     return D
 
 

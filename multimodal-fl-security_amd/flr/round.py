@@ -1,0 +1,83 @@
+"""One federated round on the engine (the body of ExperimentRunner.run_simulation,
+experiments/run_experiments.py:188-259, minus evaluation and checkpointing).
+
+  for each client: fresh model <- global; local SGD                (:193-240)
+  malicious clients submit a poisoned update                       (malicious_client.py:103-115)
+  aggregated = defense.aggregate(client_updates, num_examples)     (:243-254)
+  global params <- aggregated                                      (:257-259)
+
+The K clients are sharded over the GPUs (flr.dist); each GPU trains its rows
+of the client matrix together, one all-gather assembles the K×P matrix, and
+the aggregation kernels read it in place.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import torch
+
+from . import dist as fdist
+from .defenses import get_defense
+from .matrix import ClientMatrix
+from .models.multimodal import ModelSpec, MultimodalNet, param_layout
+from .train import ClientBatchTrainer, TrainConfig, make_dropout_masks, synthetic_batches
+
+
+@dataclass
+class RoundConfig:
+    num_clients: int = 128
+    batch: int = 32                      # run_experiments.py:40
+    defense: str = "krum"
+    defense_cfg: Dict = field(default_factory=dict)
+    attack: str = "sign_flip"            # IPM without a benign mean (model_poisoning.py:274-276)
+    num_attackers: int = 25              # f = int(0.2 K), clients 0..f-1 (experiment_matrix.py:67-68)
+    seed: int = 42                       # run_experiments.py:43
+
+
+def initial_global(spec: ModelSpec, seed: int, device) -> torch.Tensor:
+    """Global model init: the torch default init of MultimodalNet under seed."""
+    torch.manual_seed(seed)
+    m = MultimodalNet(spec)
+    return torch.cat([p.detach().reshape(-1) for p in m.parameters()]).to(device)
+
+
+class RoundEngine:
+    def __init__(self, spec: ModelSpec, rcfg: RoundConfig, tcfg: TrainConfig = TrainConfig(), device="cuda",
+                 rank: int = 0, world: int = 1):
+        self.spec, self.rcfg, self.tcfg = spec, rcfg, tcfg
+        self.device = torch.device(device)
+        self.rank, self.world = rank, world
+        K = rcfg.num_clients
+        self.lo, self.hi = fdist.shard(K, world, rank)
+        shapes = [s for _, s in param_layout(spec)]
+        self.trainer = ClientBatchTrainer(spec, self.hi - self.lo, self.device, tcfg)
+        self.full = self.trainer.X if world == 1 else ClientMatrix.empty(K, shapes, self.device)
+        cfg = dict(rcfg.defense_cfg)
+        if rcfg.defense in ("krum", "multi_krum"):  # run_experiments.py:155-162
+            cfg.setdefault("num_malicious", rcfg.num_attackers)
+            cfg.setdefault("multi_k", max(1, K // 2))
+        self.defense = get_defense(rcfg.defense, cfg)
+        self.global_flat = initial_global(spec, rcfg.seed, self.device)
+        steps = tcfg.local_steps
+        self.batches = synthetic_batches(spec, steps, range(self.lo, self.hi), rcfg.batch, self.device)
+        self.masks = make_dropout_masks(spec, steps, self.hi - self.lo, rcfg.batch, self.device,
+                                        seed=rcfg.seed + 7919 * (rank + 1))
+        self.num_examples = [steps * rcfg.batch] * K  # len(client dataset) (run_experiments.py:240)
+        self.losses: Optional[torch.Tensor] = None
+
+    def _poison(self) -> None:
+        f = self.rcfg.num_attackers if self.rcfg.attack == "sign_flip" else 0
+        lo, hi = self.lo, min(self.hi, f)
+        if hi > lo:  # malicious rows submit -update (weights, as the reference negates)
+            self.trainer.X.data[: hi - lo, : self.trainer.P].neg_()
+
+    def run_round(self) -> torch.Tensor:
+        self.trainer.load_global(self.global_flat)
+        self.losses = self.trainer.local_update(self.batches, self.masks)
+        self._poison()
+        fdist.allgather_rows(self.trainer.X.data, self.full.data)
+        agg = self.defense.aggregate_flat(self.full, self.num_examples, **(
+            {"publish": False} if hasattr(self.defense, "publish") else {}))
+        self.global_flat.copy_(agg)
+        return self.global_flat

@@ -1,0 +1,153 @@
+"""Client-batched local training: every client of a GPU steps together.
+
+Reference semantics (experiments/run_experiments.py:193-240, the fp32 branch
+:230-235; contract FLClient.fit / _train, src/client/fl_client.py:76-149):
+each client starts from the global model (:203), builds a fresh
+SGD(lr, momentum=0.9, wd) (:206-211), and for every batch runs forward, mean
+cross-entropy, backward, clip_grad_norm_(1.0) and optimizer.step(); its update
+is the parameter list afterwards (:238) and its reported loss the mean of the
+per-batch losses (fl_client.py:143-149).
+
+Engine: the K_local clients' parameters are the rows of one client matrix X
+([K, P] fp32 in HBM, `model.parameters()` order).  The forward/backward runs
+for all rows at once (flr.models.multimodal.batched_forward: grouped
+convolutions / batched matmuls); the loss is the HIP cross-entropy kernel; the
+gradient rows land in a K×P matrix G and ONE fused HIP kernel applies the
+per-client clip and the SGD-momentum update to X in place.  The trained X is
+the round's update matrix, handed to the server with no flatten/stack copy.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from . import _capi
+from .matrix import ClientMatrix
+from .models.multimodal import ModelSpec, batched_forward, param_layout
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+class CrossEntropy(torch.autograd.Function):
+    """Per-client mean cross-entropy on the flr_cross_entropy HIP kernel.
+    logits [K, B, C] fp32, labels [K, B] int64 -> loss [K]."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        K, B, C = logits.shape
+        z = logits.contiguous()
+        y = labels.contiguous()
+        loss = torch.empty(K, dtype=torch.float32, device=z.device)
+        dz = torch.empty_like(z)
+        rows = torch.empty(K * B, dtype=torch.float32, device=z.device)
+        _capi.call("flr_cross_entropy", z.data_ptr(), y.data_ptr(), K, B, C, loss.data_ptr(), dz.data_ptr(),
+                   rows.data_ptr(), _stream(z))
+        ctx.save_for_backward(dz)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gk):
+        (dz,) = ctx.saved_tensors
+        K, B, C = dz.shape
+        d = dz.clone()
+        gk = gk.contiguous().float()
+        _capi.call("flr_scale_client_rows", d.data_ptr(), gk.data_ptr(), K, B, C, _stream(d))
+        return d, None
+
+
+@dataclass
+class TrainConfig:
+    lr: float = 0.01             # run_experiments.py:41
+    momentum: float = 0.9        # :209
+    weight_decay: float = 0.0    # :210 (1e-4 only for cub200)
+    clip: float = 1.0            # :227, :234
+    local_steps: int = 5
+
+
+class ClientBatchTrainer:
+    """Trains the rows of a client matrix; one instance per GPU."""
+
+    def __init__(self, spec: ModelSpec, num_clients: int, device, cfg: TrainConfig = TrainConfig(),
+                 matrix: Optional[ClientMatrix] = None):
+        self.spec = spec
+        self.cfg = cfg
+        self.device = torch.device(device)
+        layout = param_layout(spec)
+        self.names = [n for n, _ in layout]
+        self.shapes = [s for _, s in layout]
+        self.X = matrix if matrix is not None else ClientMatrix.empty(num_clients, self.shapes, self.device)
+        self.K = self.X.K
+        self.P = self.X.P
+        self.G = torch.zeros_like(self.X.data)
+        self.M = torch.zeros_like(self.X.data)
+        nbytes = int(_capi.lib().flr_clip_sgd_workspace(self.K))
+        self._ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
+        self._ws_off = (-self._ws.data_ptr()) % 256
+        self._ws_bytes = nbytes
+        self.norms = torch.zeros(self.K, dtype=torch.float32, device=self.device)
+
+    # ---- parameter views -------------------------------------------------
+    def _leaves(self) -> List[torch.Tensor]:
+        out = []
+        for off, n, shape in zip(self.X.offsets, self.X.numels, self.shapes):
+            out.append(self.X.data[:, off:off + n].view(self.K, *shape).detach().requires_grad_(True))
+        return out
+
+    def load_global(self, global_flat: torch.Tensor) -> None:
+        """Every client starts from the global model (run_experiments.py:203)."""
+        self.X.data[:, : self.P].copy_(global_flat.to(self.X.data.device).view(1, -1).expand(self.K, -1))
+
+    # ---- one optimizer step for every client -----------------------------
+    def step(self, images, tokens, labels, first: bool, dropout_mask=None) -> torch.Tensor:
+        leaves = self._leaves()
+        params: Dict[str, torch.Tensor] = dict(zip(self.names, leaves))
+        logits = batched_forward(params, images, tokens, self.spec, dropout_mask)
+        loss_k = CrossEntropy.apply(logits, labels)
+        grads = torch.autograd.grad(loss_k.sum(), leaves)
+        for off, n, g in zip(self.X.offsets, self.X.numels, grads):
+            self.G[:, off:off + n].copy_(g.reshape(self.K, n))
+        c = self.cfg
+        _capi.call("flr_clip_sgd_step", self.X.data.data_ptr(), self.G.data_ptr(), self.M.data_ptr(), self.K, self.P,
+                   self.X.data.stride(0), c.lr, c.momentum, c.weight_decay, c.clip, int(first),
+                   self.norms.data_ptr(), self._ws.data_ptr() + self._ws_off, self._ws_bytes, _stream(self.G))
+        return loss_k.detach()
+
+    def local_update(self, batches: Sequence, dropout_masks: Optional[Sequence] = None) -> torch.Tensor:
+        """Runs len(batches) steps; returns each client's mean loss [K]."""
+        total = torch.zeros(self.K, dtype=torch.float32, device=self.device)
+        for s, (images, tokens, labels) in enumerate(batches):
+            mask = None if dropout_masks is None else dropout_masks[s]
+            total += self.step(images, tokens, labels, first=(s == 0), dropout_mask=mask)
+        return total / max(1, len(batches))
+
+
+def make_dropout_masks(spec: ModelSpec, steps: int, K: int, B: int, device, seed: int) -> Optional[List[torch.Tensor]]:
+    """Explicit inverted-dropout masks {0, 1/(1-p)} per step (reproducible)."""
+    if spec.dropout <= 0:
+        return None
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    keep = 1.0 - spec.dropout
+    return [(torch.rand(K, B, spec.fusion, generator=g, device=device) < keep).float() / keep for _ in range(steps)]
+
+
+def synthetic_batches(spec: ModelSpec, steps: int, client_ids: Sequence[int], batch: int, device,
+                      seed_base: int = 1000):
+    """SURVEY §8d inputs: images N(0,1) [B,3,32,32], tokens U{0..V-1} [B,T],
+    labels U{0..C-1}; client c's stream seeded 1000 + c (independent of how
+    clients are sharded over GPUs)."""
+    K = len(client_ids)
+    imgs = torch.empty(steps, K, batch, spec.in_channels, spec.image_size, spec.image_size, device=device)
+    toks = torch.empty(steps, K, batch, spec.seq_len, dtype=torch.int64, device=device)
+    labs = torch.empty(steps, K, batch, dtype=torch.int64, device=device)
+    for j, c in enumerate(client_ids):
+        g = torch.Generator(device="cpu")
+        g.manual_seed(seed_base + int(c))
+        imgs[:, j] = torch.randn(steps, batch, spec.in_channels, spec.image_size, spec.image_size, generator=g).to(device)
+        toks[:, j] = torch.randint(0, spec.vocab, (steps, batch, spec.seq_len), generator=g).to(device)
+        labs[:, j] = torch.randint(0, spec.num_classes, (steps, batch), generator=g).to(device)
+    return [(imgs[s], toks[s], labs[s]) for s in range(steps)]

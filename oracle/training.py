@@ -1,0 +1,57 @@
+"""ORACLE (test infrastructure only) — the reference's local-training loop on CPU.
+
+Restates experiments/run_experiments.py:195-240 (the fp32 CPU branch
+:230-235) and the loss averaging of src/client/fl_client.py:129-149, for one
+client at a time, on flr's MultimodalNet (the reference has no ResNet-18+GRU
+model; its fusion-head structure is cub200_cnn.py:88-93).  Two deviations are
+required for a deterministic comparison and are made explicit: fixed batches
+instead of a shuffling DataLoader, and dropout applied through an explicit mask
+(or p = 0) instead of torch's RNG stream.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+
+class _MaskDropout(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.mask = None
+
+    def forward(self, x):
+        return x if self.mask is None else x * self.mask
+
+
+def local_update(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, lr: float = 0.01,
+                 momentum: float = 0.9, weight_decay: float = 0.0, max_norm: float = 1.0,
+                 masks: Optional[Sequence[torch.Tensor]] = None, threads: Optional[int] = None
+                 ) -> Tuple[List[torch.Tensor], float]:
+    """One client's local update.  Returns (params after training, mean loss)."""
+    if threads:
+        torch.set_num_threads(threads)
+    model = model_cls(spec)
+    off = 0
+    with torch.no_grad():
+        for p in model.parameters():  # load_state_dict(global) for parameters() (:203)
+            n = p.numel()
+            p.copy_(global_flat[off:off + n].view(p.shape))
+            off += n
+    model.dropout = _MaskDropout()
+    optimizer = torch.optim.SGD(model.parameters(), lr=lr, momentum=momentum, weight_decay=weight_decay)  # :206-211
+    criterion = nn.CrossEntropyLoss()
+    model.train()
+    losses = []
+    for s, (images, tokens, labels) in enumerate(batches):
+        model.dropout.mask = None if masks is None else masks[s]
+        optimizer.zero_grad()
+        outputs = model(images, tokens)
+        loss = criterion(outputs, labels)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)  # :234
+        optimizer.step()
+        losses.append(loss.item())
+    update = [p.data.clone() for p in model.parameters()]  # :238
+    return update, sum(losses) / len(losses)

@@ -1,0 +1,70 @@
+"""GPU parity of local training: the client-batched engine vs the oracle's
+per-client reference loop (run_experiments.py:195-240), training loss and
+trained parameters within 1e-5 (north_star)."""
+import pytest
+import torch
+
+from oracle import training as otrain
+from flr.client import Client
+from flr.models.multimodal import TINY, ModelSpec, MultimodalNet, num_params
+from flr.round import initial_global
+from flr.train import ClientBatchTrainer, TrainConfig, make_dropout_masks, synthetic_batches
+
+pytestmark = pytest.mark.gpu
+
+SPEC = TINY
+SPEC_DROP = ModelSpec(widths=(8, 16, 16, 32), blocks=(1, 1, 1, 1), vocab=50, embed=8, hidden=16, fusion=16,
+                      dropout=0.5)
+
+
+def _rel(a, b):
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("spec", [SPEC, SPEC_DROP], ids=["p0", "dropout-masks"])
+def test_batched_training_matches_reference_loop(cuda, spec):
+    K, B, steps = 3, 8, 3
+    glob = initial_global(spec, 42, cuda)
+    tr = ClientBatchTrainer(spec, K, cuda, TrainConfig(local_steps=steps))
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    masks = make_dropout_masks(spec, steps, K, B, cuda, seed=3)
+    tr.load_global(glob)
+    loss = tr.local_update(batches, masks).cpu()
+    for k in range(K):
+        cb = [(im[k].cpu(), tk[k].cpu(), lb[k].cpu()) for im, tk, lb in batches]
+        cm = None if masks is None else [m[k].cpu() for m in masks]
+        upd, ref_loss = otrain.local_update(MultimodalNet, spec, glob.cpu(), cb, masks=cm)
+        ref = torch.cat([u.reshape(-1) for u in upd])
+        got = tr.X.data[k, : tr.P].cpu()
+        assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+        assert _rel(got, ref) < 1e-5, _rel(got, ref)
+
+
+def test_client_api_mirror(cuda):
+    spec = SPEC
+    glob = initial_global(spec, 42, cuda)
+    batches = [(im[0], tk[0], lb[0]) for im, tk, lb in synthetic_batches(spec, 2, [7], 8, cuda)]
+    c = Client(7, batches, spec, cuda)
+    shapes = [p.shape for p in MultimodalNet(spec).parameters()]
+    parts, off = [], 0
+    for s in shapes:
+        n = int(torch.Size(s).numel())
+        parts.append(glob[off:off + n].view(s))
+        off += n
+    params, n, metrics = c.local_update(parts, {"local_epochs": 1, "learning_rate": 0.01})
+    assert n == 16 and metrics["client_id"] == 7 and isinstance(metrics["loss"], float)
+    assert [p.shape for p in params] == shapes
+    upd, ref_loss = otrain.local_update(MultimodalNet, spec, glob.cpu(), [(a.cpu(), b.cpu(), y.cpu()) for a, b, y in batches])
+    assert abs(metrics["loss"] - ref_loss) < 1e-5
+    nd, _, _ = c.fit([p.cpu().numpy() for p in parts], {})
+    assert len(nd) == len(shapes)
+
+
+def test_full_model_single_step_runs(cuda):
+    spec = ModelSpec()
+    assert num_params(spec) == 11_800_394
+    tr = ClientBatchTrainer(spec, 2, cuda, TrainConfig(local_steps=1))
+    tr.load_global(initial_global(spec, 42, cuda))
+    b = synthetic_batches(spec, 1, [0, 1], 4, cuda)
+    loss = tr.local_update(b, make_dropout_masks(spec, 1, 2, 4, cuda, 1))
+    assert torch.isfinite(loss).all()
