@@ -124,6 +124,17 @@ int flr_clip_sgd_step(float* X, const float* G, float* M, int64_t K, int64_t P,
                       float max_norm, int first_step, float* norms_out,
                       void* workspace, size_t workspace_bytes, void* stream);
 
+/* Same step on the parameter-major training layout: parameter j of all K
+ * clients is one contiguous block [K][block_numel[j]]; x/g/m_blocks are host
+ * arrays of nblocks device pointers (nblocks <= 96).  Client k's flattened
+ * parameter e (parameters() order) is block j's element k*n_j + e - pre_j. */
+int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* const* g_blocks,
+                              float* const* m_blocks, const int64_t* block_numel,
+                              int64_t nblocks, int64_t K, float lr, float momentum,
+                              float weight_decay, float max_norm, int first_step,
+                              float* norms_out, void* workspace,
+                              size_t workspace_bytes, void* stream);
+
 /* ---- a5: cross-entropy forward + backward ------------------------------
  * Replaces nn.CrossEntropyLoss() (mean over each client's batch;
  * run_experiments.py:186, 232) for K clients × B rows × C classes:

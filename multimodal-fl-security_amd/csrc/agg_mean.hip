@@ -40,6 +40,12 @@ __global__ __launch_bounds__(THREADS) void rows_mean_kernel(const float* __restr
       for (int e = 0; e < 4; ++e) o[e] = div_rn(acc[e], fm);
       *reinterpret_cast<f32x4*>(out + 4 * v) = o;
     }
+    if (blockIdx.x == 0 && threadIdx.x < (P & 3)) {  // scalar tail
+      const int64_t p = nv * 4 + threadIdx.x;
+      float acc = 0.f;
+      for (int t = 0; t < m; ++t) acc = add_rn(acc, X[(int64_t)rs[t] * ldx + p]);
+      out[p] = div_rn(acc, fm);
+    }
   } else {
     for (int64_t p = (int64_t)blockIdx.x * THREADS + threadIdx.x; p < P; p += (int64_t)gridDim.x * THREADS) {
       float acc = 0.f;
@@ -78,6 +84,12 @@ __global__ __launch_bounds__(THREADS) void fedavg_kernel(const float* __restrict
       for (int e = 0; e < 4; ++e) o[e] = div_rn(acc[e], tf);
       *reinterpret_cast<f32x4*>(out + 4 * v) = o;
     }
+    if (blockIdx.x == 0 && threadIdx.x < (P & 3)) {  // scalar tail
+      const int64_t p = nv * 4 + threadIdx.x;
+      float acc = 0.f;
+      for (int i = 0; i < K; ++i) acc = add_rn(acc, mul_rn(wts[i], X[(int64_t)i * ldx + p]));
+      out[p] = div_rn(acc, tf);
+    }
   } else {
     for (int64_t p = (int64_t)blockIdx.x * THREADS + threadIdx.x; p < P; p += (int64_t)gridDim.x * THREADS) {
       float acc = 0.f;
@@ -94,8 +106,7 @@ inline int grid_for(int64_t work) {
 }
 
 inline bool vec_ok(const void* X, int64_t ldx, int64_t P, const void* out) {
-  return ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(out)) & 15) == 0 && ldx % 4 == 0 &&
-         P % 4 == 0;
+  return ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(out)) & 15) == 0 && ldx % 4 == 0;
 }
 
 }  // namespace mean

@@ -54,7 +54,9 @@ __device__ __forceinline__ void oem_sort(float* v) {
 
 // MODE 0: trimmed mean over ranks [t, K-t); MODE 1: lower median.
 template <int NP, int MODE>
-__global__ __launch_bounds__(THREADS) void orderstat_kernel(const float* __restrict__ X, int K, int64_t P,
+// 3 waves/SIMD: the NP=128 network needs ~150 VGPRs; the bound stops the
+// trimmed sum from pushing the kernel over the 168-VGPR occupancy step.
+__global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __restrict__ X, int K, int64_t P,
                                                             int64_t ldx, int t, float* __restrict__ out) {
   const int64_t p = (int64_t)blockIdx.x * THREADS + threadIdx.x;
   if (p >= P) return;
@@ -62,6 +64,7 @@ __global__ __launch_bounds__(THREADS) void orderstat_kernel(const float* __restr
 #pragma unroll
   for (int k = 0; k < NP; ++k) v[k] = k < K ? X[(int64_t)k * ldx + p] : __builtin_huge_valf();
   oem_sort<0, NP>(v);
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (MODE == 1) {
     const int med = (K - 1) / 2;
     float r = v[0];
@@ -75,22 +78,23 @@ __global__ __launch_bounds__(THREADS) void orderstat_kernel(const float* __restr
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       const int pos = k - t;
-      if (pos >= 0 && pos < R) {
-        a0 = add_rn(a0, v[k]);
-        if (pos < nfull && ((pos + 1) & 15) == 0) {
-          const int i = pos + 1;
-          a1 = add_rn(a1, a0);
-          a0 = 0.f;
-          if ((i & 0xF0) == 0) {
-            a2 = add_rn(a2, a1);
-            a1 = 0.f;
-            if ((i & 0xF00) == 0) {
-              a3 = add_rn(a3, a2);
-              a2 = 0.f;
-            }
-          }
-        }
-      }
+      // branch-free (selects keep the live ranges short; t, R are wave-uniform)
+      const bool in = (unsigned)pos < (unsigned)R;
+      const float n0 = add_rn(a0, v[k]);
+      a0 = in ? n0 : a0;
+      const bool blk = in && pos < nfull && ((pos + 1) & 15) == 0;
+      const int i = pos + 1;
+      const bool l2 = blk && (i & 0xF0) == 0;
+      const bool l3 = l2 && (i & 0xF00) == 0;
+      const float n1 = add_rn(a1, a0);
+      a1 = blk ? n1 : a1;
+      a0 = blk ? 0.f : a0;
+      const float n2 = add_rn(a2, a1);
+      a2 = l2 ? n2 : a2;
+      a1 = l2 ? 0.f : a1;
+      const float n3 = add_rn(a3, a2);
+      a3 = l3 ? n3 : a3;
+      a2 = l3 ? 0.f : a2;
     }
     a0 = add_rn(a0, a1);
     a0 = add_rn(a0, a2);

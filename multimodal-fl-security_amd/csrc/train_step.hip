@@ -120,6 +120,88 @@ __global__ void scale_rows_kernel(float* __restrict__ d, const float* __restrict
   d[i] *= gk[i / ((int64_t)B * C)];
 }
 
+
+// ---- parameter-major ("blocked") variants -------------------------------
+// Training keeps each parameter as its own contiguous [K][n_j] block (so a
+// grouped convolution's weight view is free and autograd's gradient tensors
+// are used in place).  A client's flattened index e in [0, P) lives in block
+// j with pre[j] <= e < pre[j+1], at x[j] + k*n[j] + (e - pre[j]).
+constexpr int MAXB = 96;
+struct BlockTable {
+  float* x[MAXB];
+  const float* g[MAXB];
+  float* m[MAXB];
+  int64_t pre[MAXB + 1];
+  int nb;
+};
+
+__global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable tb, int64_t P,
+                                                                double* __restrict__ partial) {
+  __shared__ double red[THREADS / 64];
+  const int k = blockIdx.y, b = blockIdx.x;
+  const int64_t p0 = P * b / NBLK, p1 = P * (b + 1) / NBLK;
+  double acc = 0.0;
+  for (int j = 0; j < tb.nb; ++j) {
+    const int64_t lo = p0 > tb.pre[j] ? p0 : tb.pre[j];
+    const int64_t hi = p1 < tb.pre[j + 1] ? p1 : tb.pre[j + 1];
+    if (lo >= hi) continue;
+    const int64_t n = tb.pre[j + 1] - tb.pre[j];
+    const float* g = tb.g[j] + (int64_t)k * n - tb.pre[j];
+    for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) {
+      const double v = (double)g[e];
+      acc += v * v;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int w = 0; w < THREADS / 64; ++w) s += red[w];
+    partial[(int64_t)k * NBLK + b] = s;
+  }
+}
+
+// grid (NSGD, K): workgroup b of client k updates flattened range [P*b/NSGD, P*(b+1)/NSGD).
+constexpr int NSGD = 256;
+__global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable tb, int64_t P,
+                                                              const float* __restrict__ coef, float lr, float mom,
+                                                              float wd, int first) {
+  const int k = blockIdx.y, b = blockIdx.x;
+  const float c = coef ? coef[k] : 1.0f;
+  const float nlr = -lr;
+  const int64_t p0 = P * b / NSGD, p1 = P * (b + 1) / NSGD;
+  for (int j = 0; j < tb.nb; ++j) {
+    const int64_t lo = p0 > tb.pre[j] ? p0 : tb.pre[j];
+    const int64_t hi = p1 < tb.pre[j + 1] ? p1 : tb.pre[j + 1];
+    if (lo >= hi) continue;
+    const int64_t n = tb.pre[j + 1] - tb.pre[j];
+    const int64_t base = (int64_t)k * n - tb.pre[j];
+    float* x = tb.x[j] + base;
+    const float* g = tb.g[j] + base;
+    float* m = tb.m[j] + base;
+    if (first) {
+      for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) {
+        const float xp = x[e];
+        float gp = g[e] * c;
+        if (wd != 0.0f) gp = __builtin_fmaf(wd, xp, gp);
+        m[e] = gp;
+        x[e] = __builtin_fmaf(nlr, gp, xp);
+      }
+    } else {
+      for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) {
+        const float xp = x[e];
+        float gp = g[e] * c;
+        if (wd != 0.0f) gp = __builtin_fmaf(wd, xp, gp);
+        const float bb = m[e] * mom + gp;
+        m[e] = bb;
+        x[e] = __builtin_fmaf(nlr, bb, xp);
+      }
+    }
+  }
+}
+
 }  // namespace train
 }  // namespace flr
 
@@ -175,4 +257,42 @@ extern "C" int flr_scale_client_rows(float* d, const float* gk, int64_t K, int64
   hipLaunchKernelGGL(train::scale_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), d,
                      gk, (int)K, (int)B, (int)C);
   return launch_status("scale_rows_kernel");
+}
+
+extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* const* g_blocks, float* const* m_blocks,
+                                         const int64_t* block_numel, int64_t nblocks, int64_t K, float lr,
+                                         float momentum, float weight_decay, float max_norm, int first_step,
+                                         float* norms_out, void* workspace, size_t workspace_bytes, void* stream) {
+  if (K < 1 || nblocks < 1 || nblocks > train::MAXB || !x_blocks || !g_blocks || !m_blocks || !block_numel)
+    return FLR_ERR_ARG;
+  if (max_norm > 0 && (!workspace || workspace_bytes < flr_clip_sgd_workspace(K))) return FLR_ERR_WORKSPACE;
+  train::BlockTable tb;
+  tb.nb = (int)nblocks;
+  tb.pre[0] = 0;
+  for (int j = 0; j < tb.nb; ++j) {
+    if (!x_blocks[j] || !g_blocks[j] || !m_blocks[j] || block_numel[j] < 0) return FLR_ERR_ARG;
+    tb.x[j] = x_blocks[j];
+    tb.g[j] = g_blocks[j];
+    tb.m[j] = m_blocks[j];
+    tb.pre[j + 1] = tb.pre[j] + block_numel[j];
+  }
+  const int64_t P = tb.pre[tb.nb];
+  if (P == 0) return FLR_OK;
+  hipStream_t st = as_stream(stream);
+  float* coef = nullptr;
+  int rc;
+  if (max_norm > 0) {
+    double* partial = static_cast<double*>(workspace);
+    coef = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                    align_up((size_t)K * train::NBLK * sizeof(double), 256));
+    hipLaunchKernelGGL(train::sumsq_blocked_kernel, dim3(train::NBLK, (unsigned)K), dim3(train::THREADS), 0, st, tb,
+                       P, partial);
+    if ((rc = launch_status("sumsq_blocked_kernel")) != FLR_OK) return rc;
+    hipLaunchKernelGGL(train::clip_coef_kernel, dim3(cdiv((int)K, 64)), dim3(64), 0, st, partial, (int)K, max_norm,
+                       coef, norms_out);
+    if ((rc = launch_status("clip_coef_kernel")) != FLR_OK) return rc;
+  }
+  hipLaunchKernelGGL(train::sgd_blocked_kernel, dim3(train::NSGD, (unsigned)K), dim3(train::THREADS), 0, st, tb, P,
+                     coef, lr, momentum, weight_decay, first_step);
+  return launch_status("sgd_blocked_kernel");
 }

@@ -12,12 +12,15 @@ Engine: the K_local clients' parameters are the rows of one client matrix X
 ([K, P] fp32 in HBM, `model.parameters()` order).  The forward/backward runs
 for all rows at once (flr.models.multimodal.batched_forward: grouped
 convolutions / batched matmuls); the loss is the HIP cross-entropy kernel; the
-gradient rows land in a K×P matrix G and ONE fused HIP kernel applies the
-per-client clip and the SGD-momentum update to X in place.  The trained X is
-the round's update matrix, handed to the server with no flatten/stack copy.
+training state is parameter-major (one contiguous [K, *shape] block per
+parameter), autograd's gradient blocks feed ONE fused HIP kernel that applies
+the per-client clip and the SGD-momentum update in place, and the trained
+blocks are written once per round into the client-major matrix X the server
+aggregates.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -69,7 +72,16 @@ class TrainConfig:
 
 
 class ClientBatchTrainer:
-    """Trains the rows of a client matrix; one instance per GPU."""
+    """Trains K clients of one GPU together.
+
+    Training state is PARAMETER-MAJOR: parameter j of all K clients is one
+    contiguous [K, *shape_j] block (W, and momentum Mb alike), so grouped
+    convolutions see their weights as free [K*Cout, Cin, kh, kw] views and
+    autograd's per-parameter gradients feed the fused clip+SGD kernel with no
+    copy.  After the local steps, `export()` writes the client-major client
+    matrix X (row k = client k's parameters() vector) once per round for the
+    aggregation kernels.
+    """
 
     def __init__(self, spec: ModelSpec, num_clients: int, device, cfg: TrainConfig = TrainConfig(),
                  matrix: Optional[ClientMatrix] = None):
@@ -82,46 +94,62 @@ class ClientBatchTrainer:
         self.X = matrix if matrix is not None else ClientMatrix.empty(num_clients, self.shapes, self.device)
         self.K = self.X.K
         self.P = self.X.P
-        self.G = torch.zeros_like(self.X.data)
-        self.M = torch.zeros_like(self.X.data)
+        self.numels = list(self.X.numels)
+        self.offsets = list(self.X.offsets)
+        # one buffer per state, each block 256-B aligned
+        self._boffs, tot = [], 0
+        for n in self.numels:
+            self._boffs.append(tot)
+            tot += (self.K * n + 63) // 64 * 64
+        self._wbuf = torch.zeros(tot, dtype=torch.float32, device=self.device)
+        self._mbuf = torch.zeros(tot, dtype=torch.float32, device=self.device)
+        self.W = [self._wbuf[o:o + self.K * n].view(self.K, *s) for o, n, s in zip(self._boffs, self.numels, self.shapes)]
+        self.Mb = [self._mbuf[o:o + self.K * n].view(self.K, *s) for o, n, s in zip(self._boffs, self.numels, self.shapes)]
         nbytes = int(_capi.lib().flr_clip_sgd_workspace(self.K))
         self._ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
         self._ws_off = (-self._ws.data_ptr()) % 256
         self._ws_bytes = nbytes
         self.norms = torch.zeros(self.K, dtype=torch.float32, device=self.device)
-
-    # ---- parameter views -------------------------------------------------
-    def _leaves(self) -> List[torch.Tensor]:
-        out = []
-        for off, n, shape in zip(self.X.offsets, self.X.numels, self.shapes):
-            out.append(self.X.data[:, off:off + n].view(self.K, *shape).detach().requires_grad_(True))
-        return out
+        nb = len(self.W)
+        self._xp = (ctypes.c_void_p * nb)(*[w.data_ptr() for w in self.W])
+        self._mp = (ctypes.c_void_p * nb)(*[m.data_ptr() for m in self.Mb])
+        self._np = (ctypes.c_int64 * nb)(*self.numels)
 
     def load_global(self, global_flat: torch.Tensor) -> None:
         """Every client starts from the global model (run_experiments.py:203)."""
-        self.X.data[:, : self.P].copy_(global_flat.to(self.X.data.device).view(1, -1).expand(self.K, -1))
+        g = global_flat.to(self.device)
+        for w, off, n in zip(self.W, self.offsets, self.numels):
+            w.view(self.K, n).copy_(g[off:off + n].view(1, n).expand(self.K, n))
+
+    def export(self) -> ClientMatrix:
+        """Client-major client matrix for the server (row k = client k)."""
+        for w, off, n in zip(self.W, self.offsets, self.numels):
+            self.X.data[:, off:off + n].copy_(w.view(self.K, n))
+        return self.X
 
     # ---- one optimizer step for every client -----------------------------
     def step(self, images, tokens, labels, first: bool, dropout_mask=None) -> torch.Tensor:
-        leaves = self._leaves()
+        leaves = [w.detach().requires_grad_(True) for w in self.W]
         params: Dict[str, torch.Tensor] = dict(zip(self.names, leaves))
         logits = batched_forward(params, images, tokens, self.spec, dropout_mask)
         loss_k = CrossEntropy.apply(logits, labels)
-        grads = torch.autograd.grad(loss_k.sum(), leaves)
-        for off, n, g in zip(self.X.offsets, self.X.numels, grads):
-            self.G[:, off:off + n].copy_(g.reshape(self.K, n))
+        grads = [g.contiguous() for g in torch.autograd.grad(loss_k.sum(), leaves)]
+        gp = (ctypes.c_void_p * len(grads))(*[g.data_ptr() for g in grads])
         c = self.cfg
-        _capi.call("flr_clip_sgd_step", self.X.data.data_ptr(), self.G.data_ptr(), self.M.data_ptr(), self.K, self.P,
-                   self.X.data.stride(0), c.lr, c.momentum, c.weight_decay, c.clip, int(first),
-                   self.norms.data_ptr(), self._ws.data_ptr() + self._ws_off, self._ws_bytes, _stream(self.G))
+        _capi.call("flr_clip_sgd_step_blocked", self._xp, gp, self._mp, self._np, len(grads), self.K, c.lr,
+                   c.momentum, c.weight_decay, c.clip, int(first), self.norms.data_ptr(),
+                   self._ws.data_ptr() + self._ws_off, self._ws_bytes, _stream(self._wbuf))
         return loss_k.detach()
 
-    def local_update(self, batches: Sequence, dropout_masks: Optional[Sequence] = None) -> torch.Tensor:
+    def local_update(self, batches: Sequence, dropout_masks: Optional[Sequence] = None,
+                     export: bool = True) -> torch.Tensor:
         """Runs len(batches) steps; returns each client's mean loss [K]."""
         total = torch.zeros(self.K, dtype=torch.float32, device=self.device)
         for s, (images, tokens, labels) in enumerate(batches):
             mask = None if dropout_masks is None else dropout_masks[s]
             total += self.step(images, tokens, labels, first=(s == 0), dropout_mask=mask)
+        if export:
+            self.export()
         return total / max(1, len(batches))
 
 

@@ -192,6 +192,19 @@ def test_rows_mean_and_fedavg_bitexact(cuda):
     assert torch.equal(ops.fedavg(X, n).cpu(), orc.fedavg(ups, n)[0])
 
 
+@pytest.mark.parametrize("P", [4097, 4098, 4099, 11_800_394 // 100])
+def test_rows_mean_fedavg_vector_path_with_tail(cuda, P):
+    K = 9
+    data = torch.zeros((K, padded_ld(P)), device=cuda)
+    data[:, :P] = torch.randn(K, P, device=cuda)
+    X = data[:, :P]
+    rows = torch.tensor([4, 0, 7], dtype=torch.int32)
+    ref = (0 + X[4].cpu() + X[0].cpu() + X[7].cpu()) / 3
+    assert torch.equal(ops.rows_mean(X, rows).cpu(), ref)
+    n = list(range(1, K + 1))
+    assert torch.equal(ops.fedavg(X, n).cpu(), orc.fedavg([[X[i].cpu()] for i in range(K)], n)[0])
+
+
 def test_client_matrix_zero_copy_defense(cuda):
     K, P = 20, 3000
     cm = ClientMatrix(update_matrix(K, P, f=4, device=cuda), P, [(P,)])
