@@ -103,6 +103,112 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
   }
 }
 
+
+// ---- K > 128: one coordinate spread over L = 2 or 4 adjacent lanes ------------
+// Lane g of the group holds clients [128g, 128g+128) (padding +inf) and the
+// group runs a full bitonic sort over N = 128 L elements, element e = 128g + i
+// in register i of lane g: stages with j < 128 compare registers of one lane
+// (direction known at compile time while k <= 128, per lane above), stages with
+// j >= 128 exchange register i with lane g ^ (j/128).  Rank e then sits in lane
+// e/128, register e%128.  Trimmed sums are per-lane sequential in rank order,
+// combined in lane order (deterministic; 1e-5 vs torch, not bit-exact).
+template <int K2, int J>
+__device__ __forceinline__ void bitonic_reg_stage(float* v, bool asc_lane) {
+  // k = K2, j = J < 128: pairs (i, i ^ J) inside the lane
+#pragma unroll
+  for (int i = 0; i < 128; ++i) {
+    const int p = i ^ J;
+    if (p > i) {
+      const float a = v[i], b = v[p];
+      const float lo = fminf(a, b), hi = fmaxf(a, b);
+      bool asc;
+      if constexpr (K2 < 128) asc = (i & K2) == 0;  // (128g + i) & K2 == i & K2
+      else asc = asc_lane;                          // K2 >= 128: set by the lane index
+      v[i] = asc ? lo : hi;
+      v[p] = asc ? hi : lo;
+    }
+  }
+}
+
+template <int K2, int J>
+__device__ __forceinline__ void bitonic_lane_stage(float* v, int g) {
+  constexpr int JL = J / 128;
+  const bool lower = (g & JL) == 0;
+  const bool asc = ((g * 128) & K2) == 0;
+  const bool keep_min = lower == asc;
+  // partner lane = lane ^ JL (JL = 1 or 2): a DPP quad permutation, so the
+  // exchange is one VALU op per register (no LDS round trip, short live range)
+  constexpr int CTRL = JL == 1 ? 0xB1 : 0x4E;
+#pragma unroll
+  for (int i = 0; i < 128; ++i) {
+    const float w = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[i]), CTRL, 0xF, 0xF, false));
+    v[i] = keep_min ? fminf(v[i], w) : fmaxf(v[i], w);
+  }
+}
+
+template <int K2, int J, int N>
+__device__ __forceinline__ void bitonic_stages_j(float* v, int g) {
+  if constexpr (J >= 1) {
+    if constexpr (J >= 128) bitonic_lane_stage<K2, J>(v, g);
+    else bitonic_reg_stage<K2, J>(v, ((g * 128) & K2) == 0);
+    bitonic_stages_j<K2, J / 2, N>(v, g);
+  }
+}
+
+template <int K2, int N>
+__device__ __forceinline__ void bitonic_sort_all(float* v, int g) {
+  if constexpr (K2 <= N) {
+    bitonic_stages_j<K2, K2 / 2, N>(v, g);
+    bitonic_sort_all<K2 * 2, N>(v, g);
+  }
+}
+
+template <int L, int MODE>
+__global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const float* __restrict__ X, int K,
+                                                                         int64_t P, int64_t ldx, int t,
+                                                                         float* __restrict__ out) {
+  const int64_t gidx = (int64_t)blockIdx.x * THREADS + threadIdx.x;
+  const int64_t p = gidx / L;
+  const int g = (int)(gidx % L);
+  const bool active = p < P;  // inactive lanes still join the shuffles
+  const int64_t pc = active ? p : 0;
+  float v[128];
+#pragma unroll
+  for (int i = 0; i < 128; ++i) {
+    const int k = 128 * g + i;
+    v[i] = k < K ? X[(int64_t)k * ldx + pc] : __builtin_huge_valf();
+  }
+  bitonic_sort_all<2, 128 * L>(v, g);
+  __builtin_amdgcn_sched_barrier(0);
+  float r = 0.f;
+  if constexpr (MODE == 1) {
+    const int med = (K - 1) / 2;
+    const int loc = med - 128 * g;
+#pragma unroll
+    for (int i = 0; i < 128; ++i) r = (i == loc) ? v[i] : r;
+    if (active && g == med / 128) out[p] = r;  // the lane that owns rank med
+  } else {
+    const int lo = t, hi = K - t;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 128; ++i) {
+      const int e = 128 * g + i;
+      acc = (e >= lo && e < hi) ? add_rn(acc, v[i]) : acc;
+    }
+    // combine lanes in order 0..L-1 (lane 0 ends with the total)
+    float tot = acc;
+    if constexpr (L >= 2) {
+      const float a1 = __shfl_down(acc, 1, 64);
+      tot = add_rn(acc, a1);  // lanes 0: acc0 + acc1 ; lane 2: acc2 + acc3
+      if constexpr (L == 4) {
+        const float t2 = __shfl_down(tot, 2, 64);
+        tot = add_rn(tot, t2);
+      }
+    }
+    if (active && g == 0) out[p] = div_rn(tot, (float)(K - 2 * t));
+  }
+}
+
 template <int MODE>
 int launch(const float* X, int K, int64_t P, int64_t ldx, int t, float* out, hipStream_t st) {
   const dim3 grid((unsigned)((P + THREADS - 1) / THREADS));
@@ -116,6 +222,12 @@ int launch(const float* X, int K, int64_t P, int64_t ldx, int t, float* out, hip
     hipLaunchKernelGGL((orderstat_kernel<64, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out);
   else if (K <= 128)
     hipLaunchKernelGGL((orderstat_kernel<128, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out);
+  else if (K <= 256)
+    hipLaunchKernelGGL((orderstat_multilane_kernel<2, MODE>), dim3((unsigned)((2 * P + THREADS - 1) / THREADS)),
+                       dim3(THREADS), 0, st, X, K, P, ldx, t, out);
+  else if (K <= 512)
+    hipLaunchKernelGGL((orderstat_multilane_kernel<4, MODE>), dim3((unsigned)((4 * P + THREADS - 1) / THREADS)),
+                       dim3(THREADS), 0, st, X, K, P, ldx, t, out);
   else
     return FLR_ERR_UNSUPPORTED;
   return launch_status("orderstat_kernel");

@@ -18,6 +18,7 @@ from typing import Dict, Optional
 import torch
 
 from . import dist as fdist
+from .attacks import Backdoor, poison_batches_
 from .defenses import get_defense
 from .matrix import ClientMatrix
 from .models.multimodal import ModelSpec, MultimodalNet, param_layout
@@ -30,7 +31,7 @@ class RoundConfig:
     batch: int = 32                      # run_experiments.py:40
     defense: str = "krum"
     defense_cfg: Dict = field(default_factory=dict)
-    attack: str = "sign_flip"            # IPM without a benign mean (model_poisoning.py:274-276)
+    attack: str = "sign_flip"            # "sign_flip" (model_poisoning.py:274-276) | "backdoor" | "none"
     num_attackers: int = 25              # f = int(0.2 K), clients 0..f-1 (experiment_matrix.py:67-68)
     seed: int = 42                       # run_experiments.py:43
 
@@ -63,6 +64,9 @@ class RoundEngine:
         self.batches = synthetic_batches(spec, steps, range(self.lo, self.hi), rcfg.batch, self.device)
         self.masks = make_dropout_masks(spec, steps, self.hi - self.lo, rcfg.batch, self.device,
                                         seed=rcfg.seed + 7919 * (rank + 1))
+        if rcfg.attack == "backdoor":  # data poisoning of the malicious clients (run_experiments.py:173-175)
+            cols = [c - self.lo for c in range(self.lo, min(self.hi, rcfg.num_attackers))]
+            poison_batches_(self.batches, cols, Backdoor(image_size=(spec.image_size, spec.image_size)))
         self.num_examples = [steps * rcfg.batch] * K  # len(client dataset) (run_experiments.py:240)
         self.losses: Optional[torch.Tensor] = None
 

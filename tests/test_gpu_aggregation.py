@@ -150,7 +150,7 @@ def test_stat_defenses_vs_golden(cuda, path):
     np.testing.assert_array_equal(fa, fx["fedavg"])
 
 
-@pytest.mark.parametrize("K", [2, 3, 5, 8, 9, 16, 31, 64, 100, 128])
+@pytest.mark.parametrize("K", [2, 3, 5, 8, 9, 16, 31, 64, 100, 128, 129, 200, 256, 300, 512])
 def test_order_stats_vs_torch(cuda, K):
     P = 5003
     X = torch.randn(K, P, device=cuda)
@@ -165,6 +165,8 @@ def test_order_stats_vs_torch(cuda, K):
         ref = torch.sort(Xf.cpu(), dim=0)[0][t:K - t].mean(dim=0)
         got = ops.trimmed_mean(Xf, t).cpu()
         torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+        if K > 128:  # multi-lane path: per-lane sums, not torch's cascade order
+            return
         # bit-exact on the vectorised columns (all but the scalar tail)
         ncol = (P // 64) * 64
         cas = orc.torch_outer_sum(torch.sort(Xf.cpu(), dim=0)[0][t:K - t]) / (K - 2 * t)

@@ -31,3 +31,10 @@ D = ops.pairwise_l2(X, "gram"); D2 = ops.pairwise_l2(X, "direct")
 print("gram vs direct max rel", ((D - D2).abs() / D2.clamp_min(1e-30)).max().item())
 s, o = ops.krum_select(D, f)
 print("selected attackers:", sorted(set(o[:K//2].tolist()) & set(range(f))))
+for K2 in (256, 512):
+    P2 = 2_000_000
+    X2 = update_matrix(K2, P2, f=K2 // 5, device="cuda")[:, :P2]
+    for name, fn in [("median", lambda: ops.median_lower(X2)), ("trimmed", lambda: ops.trimmed_mean(X2, int(0.1 * K2))),
+                     ("pairwise", lambda: ops.pairwise_l2(X2))]:
+        ms = timeit(fn, 5)
+        print(f"K={K2} {name:10s} {ms:8.3f} ms  {4*K2*P2/1e9/ms*1e3:8.1f} GB/s", flush=True)
