@@ -135,6 +135,34 @@ int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* const* g_bloc
                               float* norms_out, void* workspace,
                               size_t workspace_bytes, void* stream);
 
+/* ---- a2: client-batched 2-D convolution (bias-free, as in the conv blocks)
+ * Replaces nn.Conv2d forward/backward for every client of a GPU at once
+ * (image branch, src/models/cub200_cnn.py:71-77 template).  Layouts:
+ *   x  [B][K*Cin][H][W]    (grouped: client k owns channels k*Cin .. k*Cin+Cin-1)
+ *   w  [K][Cout][Cin][KH][KW]
+ *   y  [B][K*Cout][Ho][Wo], Ho = (H + 2 pad - KH) / stride + 1
+ * fp32 in, fp32 accumulate (exact-fp32 MFMA).  bwd_data writes dx, bwd_weight
+ * writes dw (both overwrite).  Kernel taps that only read zero padding are
+ * skipped (their dw is written as exact zeros).  The workspace (optional,
+ * size from flr_conv2d_workspace) enables deterministic split-K for long
+ * reductions; without it the kernels run unsplit. */
+size_t flr_conv2d_workspace(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W,
+                            int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                            int64_t pad);
+int flr_conv2d_fwd(const float* x, const float* w, float* y, int64_t K, int64_t B,
+                   int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH,
+                   int64_t KW, int64_t stride, int64_t pad, void* workspace,
+                   size_t workspace_bytes, void* stream);
+int flr_conv2d_bwd_data(const float* dy, const float* w, float* dx, int64_t K,
+                        int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
+                        int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+                        void* workspace, size_t workspace_bytes, void* stream);
+int flr_conv2d_bwd_weight(const float* x, const float* dy, float* dw, int64_t K,
+                          int64_t B, int64_t Cin, int64_t H, int64_t W,
+                          int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                          int64_t pad, void* workspace, size_t workspace_bytes,
+                          void* stream);
+
 /* ---- a5: cross-entropy forward + backward ------------------------------
  * Replaces nn.CrossEntropyLoss() (mean over each client's batch;
  * run_experiments.py:186, 232) for K clients × B rows × C classes:

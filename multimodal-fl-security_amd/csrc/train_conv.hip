@@ -1,0 +1,365 @@
+// a2 — client-batched convolution (forward, backward-data, backward-weight)
+// for the image encoder, on exact-fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Reference layer: nn.Conv2d(bias=False) inside the conv blocks
+// (src/models/cub200_cnn.py:71-77 template; ResNet-18 BasicBlock here),
+// trained per client in run_experiments.py:216-235.  The engine runs every
+// client of a GPU in one launch: grid.z = client, each client with its own
+// weights [Cout][Cin][KH][KW] (a block of the parameter-major training state)
+// and activations in the grouped layout x[b][k*Cin + c][h][w] (client k's
+// channels are contiguous; torch's grouped-conv layout, so BatchNorm/ReLU/
+// pooling kernels see per-(client, channel) planes).
+//
+// All three products are one implicit-GEMM template: C_k[M][N] = sum_r
+// A_k(m, r) B_k(n, r).  Operand elements are gathered straight from the
+// activation / weight tensors (im2col is never materialised); tiles of
+// 64(M) x 64(N) x 32(R) are staged through LDS as [r][m] / [r][n] images
+// (row stride 65 floats: conflict-free for both the transposing stores and
+// the MFMA operand reads), register-staged one tile ahead.  Each of the 4
+// waves owns a 32x32 output block: 16 MFMAs per tile, lane half h feeding
+// reduction index 16h + q to MFMA q.  fp32 in, fp32 accumulate, one
+// rounding per product (a k-ordered fmaf chain) — fp32 numerics, as the
+// reference's CPU conv.
+#include "flr_common.h"
+
+#include <algorithm>
+
+namespace flr {
+namespace conv {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 64, BN = 64, BK = 32, THREADS = 256;
+constexpr int LDS_STRIDE = 65;
+
+struct FastDiv {  // n / d for 0 <= n < 2^31 via mul-hi (Granlund-Montgomery)
+  uint32_t d, m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  const uint32_t t = __umulhi(n, f.m);
+  return (t + ((n - t) >> 1)) >> (f.s ? f.s - 1 : 0);
+}
+// d == 1 needs s = 0: (t + ((n - t) >> 1)) >> 0 with m = 1 gives n/2 ... handle explicitly
+__device__ __forceinline__ uint32_t udiv(uint32_t n, const FastDiv& f) { return f.d == 1 ? n : fdiv(n, f); }
+
+constexpr int MAXTAPS = 49;
+
+struct Geom {
+  int Kc, B, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo;
+  int64_t xbs, ybs;  // batch strides of x ([B][K*Cin][H][W]) and y ([B][K*Cout][Ho][Wo])
+  FastDiv d_howo, d_wo, d_hw, d_w, d_cin, d_cout;
+  // Kernel taps that read at least one non-padding input pixel.  A tap that
+  // only ever reads the zero padding contributes exact zeros to y, dx and dw,
+  // so the reduction runs over (valid tap, channel) only: r = slot * C + c.
+  int ntaps;
+  int8_t tap_kh[MAXTAPS], tap_kw[MAXTAPS];
+};
+
+// ---- problem accessors -----------------------------------------------------
+// A(m, r) and B(n, r); FAST_*: the dimension consecutive threads walk when
+// loading a tile (true = m / n, false = r), chosen for contiguous addresses.
+
+struct Fwd {  // y = conv(x, w): M = Cout, N = B*Ho*Wo, R = Cin*KH*KW
+  Geom g;
+  const float* x;
+  const float* w;
+  float* y;
+  static constexpr bool FAST_A_M = false, FAST_B_N = true;
+  __host__ __device__ int M() const { return g.Cout; }
+  __host__ __device__ int N() const { return g.B * g.Ho * g.Wo; }
+  __host__ __device__ int R() const { return g.ntaps * g.Cin; }
+  __device__ float a(int k, int m, int r) const {
+    const uint32_t slot = udiv(r, g.d_cin), ci = r - slot * g.Cin;
+    return w[(((int64_t)k * g.Cout + m) * g.Cin + ci) * (g.KH * g.KW) + g.tap_kh[slot] * g.KW + g.tap_kw[slot]];
+  }
+  __device__ float b(int k, int n, int r) const {
+    const uint32_t slot = udiv(r, g.d_cin), ci = r - slot * g.Cin;
+    const int kh = g.tap_kh[slot], kw = g.tap_kw[slot];
+    const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
+    const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+    const int ih = (int)(oh * g.stride + kh) - g.pad, iw = (int)(ow * g.stride + kw) - g.pad;
+    if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return 0.f;
+    return x[bb * g.xbs + ((int64_t)k * g.Cin + ci) * g.H * g.W + ih * g.W + iw];
+  }
+  __device__ void store(int k, int m, int n, float v) const {
+    const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
+    y[bb * g.ybs + ((int64_t)k * g.Cout + m) * g.Ho * g.Wo + p] = v;
+  }
+};
+
+struct Wgt {  // dw = sum_q dy(co, q) im(r, q): M = Cout, N = R, reduction over q = B*Ho*Wo
+  Geom g;
+  const float* x;
+  const float* dy;
+  float* dw;
+  static constexpr bool FAST_A_M = false, FAST_B_N = false;
+  __host__ __device__ int M() const { return g.Cout; }
+  __host__ __device__ int N() const { return g.ntaps * g.Cin; }
+  __host__ __device__ int R() const { return g.B * g.Ho * g.Wo; }
+  __device__ float a(int k, int m, int q) const {
+    const uint32_t bb = udiv(q, g.d_howo), p = q - bb * g.Ho * g.Wo;
+    return dy[bb * g.ybs + ((int64_t)k * g.Cout + m) * g.Ho * g.Wo + p];
+  }
+  __device__ float b(int k, int r, int q) const {
+    const uint32_t slot = udiv(r, g.d_cin), ci = r - slot * g.Cin;
+    const int kh = g.tap_kh[slot], kw = g.tap_kw[slot];
+    const uint32_t bb = udiv(q, g.d_howo), p = q - bb * g.Ho * g.Wo;
+    const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+    const int ih = (int)(oh * g.stride + kh) - g.pad, iw = (int)(ow * g.stride + kw) - g.pad;
+    if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return 0.f;
+    return x[bb * g.xbs + ((int64_t)k * g.Cin + ci) * g.H * g.W + ih * g.W + iw];
+  }
+  __device__ void store(int k, int m, int n, float v) const {
+    const uint32_t slot = udiv(n, g.d_cin), ci = n - slot * g.Cin;
+    dw[(((int64_t)k * g.Cout + m) * g.Cin + ci) * (g.KH * g.KW) + g.tap_kh[slot] * g.KW + g.tap_kw[slot]] = v;
+  }
+};
+
+struct Dgrad {  // dx = conv^T(dy, w): M = Cin, N = B*H*W, R = Cout*KH*KW
+  Geom g;
+  const float* dy;
+  const float* w;
+  float* dx;
+  static constexpr bool FAST_A_M = false, FAST_B_N = true;
+  __host__ __device__ int M() const { return g.Cin; }
+  __host__ __device__ int N() const { return g.B * g.H * g.W; }
+  __host__ __device__ int R() const { return g.ntaps * g.Cout; }
+  __device__ float a(int k, int m, int r) const {
+    const uint32_t slot = udiv(r, g.d_cout), co = r - slot * g.Cout;
+    return w[(((int64_t)k * g.Cout + co) * g.Cin + m) * (g.KH * g.KW) + g.tap_kh[slot] * g.KW + g.tap_kw[slot]];
+  }
+  __device__ float b(int k, int n, int r) const {
+    const uint32_t slot = udiv(r, g.d_cout), co = r - slot * g.Cout;
+    const int kh = g.tap_kh[slot], kw = g.tap_kw[slot];
+    const uint32_t bb = udiv(n, g.d_hw), p = n - bb * g.H * g.W;
+    const uint32_t ih = udiv(p, g.d_w), iw = p - ih * g.W;
+    const int nh = (int)ih + g.pad - kh, nw = (int)iw + g.pad - kw;
+    if (nh < 0 || nw < 0) return 0.f;
+    const int oh = nh / g.stride, ow = nw / g.stride;
+    if (oh * g.stride != nh || ow * g.stride != nw || oh >= g.Ho || ow >= g.Wo) return 0.f;
+    return dy[bb * g.ybs + ((int64_t)k * g.Cout + co) * g.Ho * g.Wo + oh * g.Wo + ow];
+  }
+  __device__ void store(int k, int m, int n, float v) const {
+    const uint32_t bb = udiv(n, g.d_hw), p = n - bb * g.H * g.W;
+    dx[bb * g.xbs + ((int64_t)k * g.Cin + m) * g.H * g.W + p] = v;
+  }
+};
+
+// ---- the implicit-GEMM kernel ---------------------------------------------
+// Split-K: blockIdx.z = client * S + split; split s reduces the BK-aligned
+// range [rb, re) and, when S > 1, writes its tile to part[(s*K + k)][M][N];
+// cgemm_reduce then adds the S partials in split order (deterministic).
+template <class Prob>
+__global__ __launch_bounds__(THREADS, 2) void cgemm_kernel(const Prob pb, int S, float* __restrict__ part) {
+  __shared__ float As[2][BK * LDS_STRIDE];
+  __shared__ float Bs[2][BK * LDS_STRIDE];
+  const int k = blockIdx.z / S, split = blockIdx.z % S;
+  const int M = pb.M(), N = pb.N(), R = pb.R();
+  const int ktiles = cdiv(R, BK);
+  const int rb = (int)((int64_t)ktiles * split / S) * BK, re = min(R, (int)((int64_t)ktiles * (split + 1) / S) * BK);
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, l32 = lane & 31;
+
+  // this thread's 8 A and 8 B tile slots: (mm, kk) / (nn, kk)
+  int am[8], ak[8], bn[8], bk[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = tid + THREADS * i;
+    if (Prob::FAST_A_M) { am[i] = e % BM; ak[i] = e / BM; } else { ak[i] = e % BK; am[i] = e / BK; }
+    if (Prob::FAST_B_N) { bn[i] = e % BN; bk[i] = e / BN; } else { bk[i] = e % BK; bn[i] = e / BK; }
+  }
+  float ra[8], rb_[8];
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      As[buf][ak[i] * LDS_STRIDE + am[i]] = ra[i];
+      Bs[buf][bk[i] * LDS_STRIDE + bn[i]] = rb_[i];
+    }
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  auto loadr = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + am[i], r = r0 + ak[i];
+      ra[i] = (m < M && r < re) ? pb.a(k, m, r) : 0.f;
+      const int n = n0 + bn[i], rr = r0 + bk[i];
+      rb_[i] = (n < N && rr < re) ? pb.b(k, n, rr) : 0.f;
+    }
+  };
+  loadr(rb);
+  stash(0);
+  __syncthreads();
+  int cur = 0;
+  for (int r0 = rb; r0 < re; r0 += BK) {
+    const bool more = r0 + BK < re;
+    if (more) loadr(r0 + BK);  // in flight during the MFMAs below
+    const float* Ab = As[cur] + 32 * wm + l32;
+    const float* Bb = Bs[cur] + 32 * wn + l32;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int kk = 16 * h + q;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ab[kk * LDS_STRIDE], Bb[kk * LDS_STRIDE], acc, 0, 0, 0);
+    }
+    if (more) stash(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // C/D map of 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int m = m0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+    const int n = n0 + 32 * wn + l32;
+    if (m < M && n < N) {
+      if (S == 1) pb.store(k, m, n, acc[e]);
+      else part[(((int64_t)split * pb.g.Kc + k) * M + m) * N + n] = acc[e];
+    }
+  }
+}
+
+template <class Prob>
+__global__ void cgemm_reduce(const Prob pb, int S, const float* __restrict__ part) {
+  const int M = pb.M(), N = pb.N(), K = pb.g.Kc;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t MN = (int64_t)M * N;
+  if (idx >= MN * K) return;
+  const int k = (int)(idx / MN);
+  const int m = (int)((idx % MN) / N), n = (int)(idx % N);
+  float v = part[idx];
+  for (int s = 1; s < S; ++s) v += part[(int64_t)s * MN * K + idx];
+  pb.store(k, m, n, v);
+}
+
+inline Geom make_geom(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH,
+                      int64_t KW, int64_t stride, int64_t pad) {
+  Geom g;
+  g.Kc = (int)K; g.B = (int)B; g.Cin = (int)Cin; g.H = (int)H; g.W = (int)W; g.Cout = (int)Cout;
+  g.KH = (int)KH; g.KW = (int)KW; g.stride = (int)stride; g.pad = (int)pad;
+  g.Ho = (int)((H + 2 * pad - KH) / stride + 1);
+  g.Wo = (int)((W + 2 * pad - KW) / stride + 1);
+  g.xbs = K * Cin * H * W;
+  g.ybs = K * Cout * g.Ho * g.Wo;
+  g.d_howo = make_fastdiv((uint32_t)(g.Ho * g.Wo));
+  g.d_wo = make_fastdiv((uint32_t)g.Wo);
+  g.d_hw = make_fastdiv((uint32_t)(H * W));
+  g.d_w = make_fastdiv((uint32_t)W);
+  g.d_cin = make_fastdiv((uint32_t)Cin);
+  g.d_cout = make_fastdiv((uint32_t)Cout);
+  g.ntaps = 0;
+  for (int kh = 0; kh < KH; ++kh) {
+    bool hv = false;
+    for (int oh = 0; oh < g.Ho && !hv; ++oh) { const int ih = oh * (int)stride - (int)pad + kh; hv = ih >= 0 && ih < H; }
+    for (int kw = 0; kw < KW; ++kw) {
+      bool wv = false;
+      for (int ow = 0; ow < g.Wo && !wv; ++ow) { const int iw = ow * (int)stride - (int)pad + kw; wv = iw >= 0 && iw < W; }
+      if (hv && wv) { g.tap_kh[g.ntaps] = (int8_t)kh; g.tap_kw[g.ntaps] = (int8_t)kw; ++g.ntaps; }
+    }
+  }
+  return g;
+}
+
+inline bool geom_ok(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+                    int64_t stride, int64_t pad) {
+  if (K < 1 || B < 1 || Cin < 1 || H < 1 || W < 1 || Cout < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0)
+    return false;
+  if (H + 2 * pad < KH || W + 2 * pad < KW || KH * KW > MAXTAPS) return false;
+  // 32-bit index space per client for the GEMM dims and offsets
+  return K * Cin * H * W * B < (int64_t(1) << 31) && K * Cout * H * W * B < (int64_t(1) << 31) &&
+         K <= 65535;
+}
+
+// Splits so that a launch has >= ~2048 workgroups while each split keeps >= 8 K-tiles.
+inline int choose_splits(int M, int N, int R, int K) {
+  const int tiles = cdiv(M, BM) * cdiv(N, BN) * K;
+  const int ktiles = cdiv(R, BK);
+  int S = 1;
+  while (S < 16 && tiles * S < 2048 && ktiles / (2 * S) >= 8) S *= 2;
+  return S;
+}
+
+template <class Prob>
+size_t splits_workspace(const Prob& pb) {
+  const int S = choose_splits(pb.M(), pb.N(), pb.R(), pb.g.Kc);
+  return S > 1 ? (size_t)S * pb.g.Kc * pb.M() * pb.N() * sizeof(float) : 0;
+}
+
+template <class Prob>
+int launch(const Prob& pb, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
+  const int M = pb.M(), N = pb.N(), R = pb.R(), K = pb.g.Kc;
+  if (R == 0) return FLR_OK;
+  int S = choose_splits(M, N, R, K);
+  if (S > 1 && (!ws || ws_bytes < splits_workspace(pb))) S = 1;  // no workspace: single split
+  dim3 grid((unsigned)cdiv(N, BN), (unsigned)cdiv(M, BM), (unsigned)(K * S));
+  hipLaunchKernelGGL(cgemm_kernel<Prob>, grid, dim3(THREADS), 0, st, pb, S, static_cast<float*>(ws));
+  int rc = launch_status(name);
+  if (rc != FLR_OK || S == 1) return rc;
+  const int64_t total = (int64_t)M * N * K;
+  hipLaunchKernelGGL(cgemm_reduce<Prob>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, pb, S,
+                     static_cast<const float*>(ws));
+  return launch_status(name);
+}
+
+}  // namespace conv
+}  // namespace flr
+
+using namespace flr;
+using namespace flr::conv;
+
+extern "C" size_t flr_conv2d_workspace(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
+                                       int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
+  if (!geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return 0;
+  const Geom g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  Fwd f; f.g = g; Dgrad d; d.g = g; Wgt w; w.g = g;
+  size_t m = splits_workspace(f);
+  m = std::max(m, splits_workspace(d));
+  m = std::max(m, splits_workspace(w));
+  return m;
+}
+
+extern "C" int flr_conv2d_fwd(const float* x, const float* w, float* y, int64_t K, int64_t B, int64_t Cin, int64_t H,
+                              int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+                              void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !w || !y || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
+  Fwd pb;
+  pb.g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  pb.x = x; pb.w = w; pb.y = y;
+  return launch(pb, ws, ws_bytes, as_stream(stream), "conv fwd");
+}
+
+extern "C" int flr_conv2d_bwd_data(const float* dy, const float* w, float* dx, int64_t K, int64_t B, int64_t Cin,
+                                   int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                                   int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+  if (!dy || !w || !dx || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
+  Dgrad pb;
+  pb.g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  pb.dy = dy; pb.w = w; pb.dx = dx;
+  return launch(pb, ws, ws_bytes, as_stream(stream), "conv bwd data");
+}
+
+extern "C" int flr_conv2d_bwd_weight(const float* x, const float* dy, float* dw, int64_t K, int64_t B, int64_t Cin,
+                                     int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                                     int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !dy || !dw || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
+  Wgt pb;
+  pb.g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  pb.x = x; pb.dy = dy; pb.dw = dw;
+  hipStream_t st = as_stream(stream);
+  if (pb.g.ntaps < KH * KW &&  // dead taps get exact-zero gradients
+      hipMemsetAsync(dw, 0, (size_t)K * Cout * Cin * KH * KW * sizeof(float), st) != hipSuccess)
+    return FLR_ERR_HIP;
+  return launch(pb, ws, ws_bytes, st, "conv bwd weight");
+}

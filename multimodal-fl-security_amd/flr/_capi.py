@@ -48,6 +48,10 @@ SIGNATURES = {
     "flr_clip_sgd_step_blocked": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64, ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_float, _int, _c_void_p, _c_void_p,
                                          _size_t, _c_void_p]),
+    "flr_conv2d_workspace": (_size_t, [_i64] * 10),
+    "flr_conv2d_fwd": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
+    "flr_conv2d_bwd_data": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
+    "flr_conv2d_bwd_weight": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_cross_entropy": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "flr_scale_client_rows": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p]),
 }

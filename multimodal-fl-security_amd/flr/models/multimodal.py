@@ -21,6 +21,7 @@ Two forms of the same network:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -130,8 +131,16 @@ def split_params(X: torch.Tensor, spec: ModelSpec) -> Dict[str, torch.Tensor]:
     return out
 
 
-def _gconv(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
+# "native": the flr HIP conv kernels (default on a GPU); "torch": grouped
+# F.conv2d (MIOpen) — the CPU-side model-equivalence tests use it.
+_CONV = os.environ.get("FLR_CONV", "native")
+
+
+def _gconv(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, need_dx: bool = True) -> torch.Tensor:
     """x [B, K*Cin, H, W], w [K, Cout, Cin, kh, kw] -> [B, K*Cout, H', W']."""
+    if _CONV == "native" and x.is_cuda:
+        from ..nn import client_conv2d
+        return client_conv2d(x, w, stride, pad, need_dx)
     K, cout = w.shape[0], w.shape[1]
     return F.conv2d(x, w.reshape(K * cout, *w.shape[2:]), stride=stride, padding=pad, groups=K)
 
@@ -151,7 +160,7 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     """
     K, B = images.shape[:2]
     x = images.transpose(0, 1).reshape(B, K * spec.in_channels, *images.shape[3:])
-    x = F.relu(_gbn(_gconv(x, p["conv1.weight"], 2, 3), p["bn1.weight"], p["bn1.bias"]))
+    x = F.relu(_gbn(_gconv(x, p["conv1.weight"], 2, 3, need_dx=False), p["bn1.weight"], p["bn1.bias"]))
     x = F.max_pool2d(x, 3, 2, 1)
     w = spec.widths
     for li, nblk in enumerate(spec.blocks):

@@ -1,0 +1,43 @@
+"""GPU: the client-batched conv kernels vs fp64 grouped convolution (torch CPU)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from flr.nn import client_conv2d
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # (K, B, Cin, H, W, Cout, KH, stride, pad)
+    (3, 4, 3, 32, 32, 8, 7, 2, 3),     # stem 7x7/2
+    (3, 4, 8, 8, 8, 8, 3, 1, 1),       # layer1 3x3
+    (2, 4, 8, 8, 8, 16, 3, 2, 1),      # layer2 first conv, stride 2
+    (2, 4, 8, 8, 8, 16, 1, 2, 0),      # downsample 1x1/2
+    (2, 3, 16, 2, 2, 24, 3, 1, 1),     # tiny spatial
+    (2, 5, 16, 1, 1, 70, 3, 1, 1),     # 1x1 spatial, ragged Cout
+    (1, 2, 5, 7, 9, 3, 3, 2, 1),       # odd everything
+    (4, 32, 64, 8, 8, 64, 3, 1, 1),    # real layer1 shape, 4 clients
+    (8, 32, 256, 4, 4, 256, 3, 1, 1),  # layer3 conv2: split-K path
+    (4, 32, 512, 1, 1, 512, 3, 1, 1),  # layer4 at 1x1: 8 of 9 taps dead, split-K
+    (4, 32, 256, 2, 2, 512, 3, 2, 1),  # layer4 first conv: 2x2 -> 1x1, 4 taps live
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+def test_conv_fwd_bwd_vs_fp64(cuda, shape):
+    K, B, Cin, H, W, Cout, KS, stride, pad = shape
+    g = torch.Generator(device="cpu").manual_seed(sum(shape))
+    x = torch.randn(B, K * Cin, H, W, generator=g)
+    w = torch.randn(K, Cout, Cin, KS, KS, generator=g) * 0.1
+    xg = x.to(cuda).requires_grad_(True)
+    wg = w.to(cuda).requires_grad_(True)
+    y = client_conv2d(xg, wg, stride, pad)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy.to(cuda))
+    xd = x.double().requires_grad_(True)
+    wd = w.double().requires_grad_(True)
+    yr = F.conv2d(xd, wd.reshape(K * Cout, Cin, KS, KS), stride=stride, padding=pad, groups=K)
+    yr.backward(dy.double())
+    for got, ref in ((y, yr), (xg.grad, xd.grad), (wg.grad, wd.grad)):
+        err = (got.detach().cpu().double() - ref.detach()).abs().max().item()
+        scale = ref.detach().abs().max().item()
+        assert err <= 2e-6 * max(scale, 1.0), (err, scale)
