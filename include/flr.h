@@ -178,6 +178,38 @@ int flr_cross_entropy(const float* logits, const int64_t* labels, int64_t K,
 int flr_scale_client_rows(float* d, const float* gk, int64_t K, int64_t B,
                           int64_t C, void* stream);
 
+/* ---- a3: GRU recurrence, pointwise gate math per time step ----------------
+ * Replaces the per-step cell of nn.GRU (torch gate order r, z, n;
+ * h' = (h - n) * z + n), used by the text branch of the multimodal model.
+ * Layouts: gi [K][B][T][3H], gh [K][B][3H] (= h_t W_hh^T + b_hh),
+ * hseq [K][T+1][B][H], gates [K][T][B][4][H] (r, z, n, h_n),
+ * dgh [K][T][B][3H], dgi [K][B][T][3H], dh / dh_direct [K][B][H].
+ * fwd_step reads hseq[:, t] and writes hseq[:, t+1] and gates[:, t];
+ * bwd_step takes dh = dL/dh_{t+1} and writes dgh[:, t], dgi[:, :, t] and
+ * dh_direct (the z-gate path of dL/dh_t; the caller adds dgh[:, t] W_hh). */
+int flr_gru_fwd_step(const float* gi, const float* gh, float* hseq, float* gates,
+                     int64_t K, int64_t B, int64_t T, int64_t H, int64_t t,
+                     void* stream);
+int flr_gru_bwd_step(const float* dh, const float* gates, const float* hseq,
+                     float* dgh, float* dgi, float* dh_direct, int64_t K,
+                     int64_t B, int64_t T, int64_t H, int64_t t, void* stream);
+
+/* ---- a2: per-client BatchNorm (train mode) + fused residual add / ReLU ----
+ * Replaces nn.BatchNorm2d(train) [+ identity add] [+ ReLU] of the conv blocks.
+ * x, y, residual: [B][KC][HW] (kc = client*C + channel), gamma/beta/mean/
+ * invstd: [KC].  fwd: y = act(x*alpha + (beta - mean*alpha) [+ residual]),
+ * alpha = gamma/sqrt(var + eps), batch statistics over B*HW, act = ReLU if
+ * relu != 0.  bwd: g = dy * (y > 0) if relu else dy; writes dx, dgamma,
+ * dbeta, and dresidual = g when dresidual != NULL. */
+int flr_batchnorm_fwd(const float* x, const float* gamma, const float* beta,
+                      const float* residual, float* y, float* mean, float* invstd,
+                      int64_t B, int64_t KC, int64_t HW, float eps, int relu,
+                      void* stream);
+int flr_batchnorm_bwd(const float* dy, const float* x, const float* y,
+                      const float* gamma, const float* mean, const float* invstd,
+                      float* dx, float* dgamma, float* dbeta, float* dresidual,
+                      int64_t B, int64_t KC, int64_t HW, int relu, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -131,14 +131,14 @@ def split_params(X: torch.Tensor, spec: ModelSpec) -> Dict[str, torch.Tensor]:
     return out
 
 
-# "native": the flr HIP conv kernels (default on a GPU); "torch": grouped
-# F.conv2d (MIOpen) — the CPU-side model-equivalence tests use it.
-_CONV = os.environ.get("FLR_CONV", "native")
+# "native": the flr HIP layer kernels (conv, GRU gates; default on a GPU);
+# "torch": torch ops (MIOpen grouped conv etc.) — the CPU path and A/B timing.
+_LAYERS = os.environ.get("FLR_LAYERS", "native")
 
 
 def _gconv(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, need_dx: bool = True) -> torch.Tensor:
     """x [B, K*Cin, H, W], w [K, Cout, Cin, kh, kw] -> [B, K*Cout, H', W']."""
-    if _CONV == "native" and x.is_cuda:
+    if _LAYERS == "native" and x.is_cuda:
         from ..nn import client_conv2d
         return client_conv2d(x, w, stride, pad, need_dx)
     K, cout = w.shape[0], w.shape[1]
@@ -151,6 +151,37 @@ def _gbn(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return F.batch_norm(x, None, None, g.reshape(-1), b.reshape(-1), training=True, momentum=0.0, eps=1e-5)
 
 
+def _gru_torch(gi: torch.Tensor, whh: torch.Tensor, bhh: torch.Tensor) -> torch.Tensor:
+    """The GRU recurrence in torch ops (torch's cell: h' = (h - n) * z + n)."""
+    K, B, T, H3 = gi.shape
+    H = H3 // 3
+    whh_t = whh.transpose(1, 2)
+    bias = bhh.unsqueeze(1)
+    h = torch.zeros(K, B, H, device=gi.device, dtype=gi.dtype)
+    for t in range(T):
+        gh = torch.baddbmm(bias, h, whh_t)
+        i_r, i_z, i_n = gi[:, :, t].chunk(3, dim=-1)
+        h_r, h_z, h_n = gh.chunk(3, dim=-1)
+        r = torch.sigmoid(i_r + h_r)
+        z = torch.sigmoid(i_z + h_z)
+        n = torch.tanh(i_n + r * h_n)
+        h = (h - n) * z + n
+    return h
+
+
+def _bn_act(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, residual: Optional[torch.Tensor] = None,
+            relu: bool = True) -> torch.Tensor:
+    """act(BN(x) [+ residual]) — the block's BN, shortcut add and ReLU, fused
+    into one HIP kernel each way on the native path."""
+    if _LAYERS == "native" and x.is_cuda:
+        from ..nn import client_batchnorm
+        return client_batchnorm(x, g, b, residual, relu)
+    y = _gbn(x, g, b)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
 def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: torch.Tensor, spec: ModelSpec,
                     dropout_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
     """images [K, B, C, H, W], tokens [K, B, T] -> logits [K, B, num_classes].
@@ -160,7 +191,7 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     """
     K, B = images.shape[:2]
     x = images.transpose(0, 1).reshape(B, K * spec.in_channels, *images.shape[3:])
-    x = F.relu(_gbn(_gconv(x, p["conv1.weight"], 2, 3, need_dx=False), p["bn1.weight"], p["bn1.bias"]))
+    x = _bn_act(_gconv(x, p["conv1.weight"], 2, 3, need_dx=False), p["bn1.weight"], p["bn1.bias"])
     x = F.max_pool2d(x, 3, 2, 1)
     w = spec.widths
     for li, nblk in enumerate(spec.blocks):
@@ -169,11 +200,11 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
             stride = 2 if (bi == 0 and li > 0) else 1
             idt = x
             if (pre + "downsample.0.weight") in p:
-                idt = _gbn(_gconv(x, p[pre + "downsample.0.weight"], stride, 0), p[pre + "downsample.1.weight"],
-                           p[pre + "downsample.1.bias"])
-            y = F.relu(_gbn(_gconv(x, p[pre + "conv1.weight"], stride, 1), p[pre + "bn1.weight"], p[pre + "bn1.bias"]))
-            y = _gbn(_gconv(y, p[pre + "conv2.weight"], 1, 1), p[pre + "bn2.weight"], p[pre + "bn2.bias"])
-            x = F.relu(y + idt)
+                idt = _bn_act(_gconv(x, p[pre + "downsample.0.weight"], stride, 0), p[pre + "downsample.1.weight"],
+                              p[pre + "downsample.1.bias"], relu=False)
+            y = _bn_act(_gconv(x, p[pre + "conv1.weight"], stride, 1), p[pre + "bn1.weight"], p[pre + "bn1.bias"])
+            x = _bn_act(_gconv(y, p[pre + "conv2.weight"], 1, 1), p[pre + "bn2.weight"], p[pre + "bn2.bias"],
+                        residual=idt)
     img = x.mean(dim=(2, 3)).view(B, K, w[-1]).transpose(0, 1)  # [K, B, 512]
 
     # text: embedding gather + GRU with per-client weights (gate order r, z, n)
@@ -184,17 +215,11 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     emb = table.reshape(K * V, E)[(tokens + kofs).reshape(-1)].view(K, B * T, E)
     gi = torch.baddbmm(p["gru.bias_ih_l0"].unsqueeze(1), emb, p["gru.weight_ih_l0"].transpose(1, 2))
     gi = gi.view(K, B, T, 3 * H)
-    whh_t = p["gru.weight_hh_l0"].transpose(1, 2)
-    bhh = p["gru.bias_hh_l0"].unsqueeze(1)
-    h = torch.zeros(K, B, H, device=images.device, dtype=images.dtype)
-    for t in range(T):
-        gh = torch.baddbmm(bhh, h, whh_t)
-        i_r, i_z, i_n = gi[:, :, t].chunk(3, dim=-1)
-        h_r, h_z, h_n = gh.chunk(3, dim=-1)
-        r = torch.sigmoid(i_r + h_r)
-        z = torch.sigmoid(i_z + h_z)
-        n = torch.tanh(i_n + r * h_n)
-        h = (1 - z) * n + z * h
+    if _LAYERS == "native" and gi.is_cuda:  # flr HIP gate kernels (one launch per step)
+        from ..nn import client_gru
+        h = client_gru(gi, p["gru.weight_hh_l0"], p["gru.bias_hh_l0"])
+    else:
+        h = _gru_torch(gi, p["gru.weight_hh_l0"], p["gru.bias_hh_l0"])
 
     f = torch.cat([img, h], dim=2)  # [K, B, 512 + H]
     f = F.relu(torch.baddbmm(p["fc1.bias"].unsqueeze(1), f, p["fc1.weight"].transpose(1, 2)))

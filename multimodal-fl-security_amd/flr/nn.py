@@ -61,3 +61,104 @@ class ClientConv2d(torch.autograd.Function):
 
 def client_conv2d(x, w, stride: int, pad: int, need_dx: bool = True):
     return ClientConv2d.apply(x, w, stride, pad, need_dx)
+
+
+class ClientGRU(torch.autograd.Function):
+    """Final hidden state of a 1-layer GRU (h_0 = 0) for K clients at once.
+
+    gi [K, B, T, 3H] = x W_ih^T + b_ih (computed by the caller, so autograd
+    handles W_ih, b_ih and the embedding), whh [K, 3H, H], bhh [K, 3H] ->
+    h_T [K, B, H].  Per step: one batched GEMM (h W_hh^T + b_hh) and one
+    flr_gru_fwd_step launch; backward: one flr_gru_bwd_step and one GEMM per
+    step, then dW_hh / db_hh over all steps at once.
+    """
+
+    @staticmethod
+    def forward(ctx, gi, whh, bhh):
+        gi = gi.contiguous()
+        K, B, T, H3 = gi.shape
+        H = H3 // 3
+        dev = gi.device
+        hseq = torch.empty(K, T + 1, B, H, dtype=gi.dtype, device=dev)
+        hseq[:, 0].zero_()
+        gates = torch.empty(K, T, B, 4, H, dtype=gi.dtype, device=dev)
+        whh_t = whh.transpose(1, 2)
+        bias = bhh.unsqueeze(1)
+        st = _stream(gi)
+        for t in range(T):
+            gh = torch.baddbmm(bias, hseq[:, t], whh_t)
+            _capi.call("flr_gru_fwd_step", gi.data_ptr(), gh.data_ptr(), hseq.data_ptr(), gates.data_ptr(),
+                       K, B, T, H, t, st)
+        ctx.save_for_backward(whh, hseq, gates)
+        return hseq[:, T].contiguous()
+
+    @staticmethod
+    def backward(ctx, dhT):
+        whh, hseq, gates = ctx.saved_tensors
+        K, T, B, _, H = gates.shape
+        dev = dhT.device
+        dgh = torch.empty(K, T, B, 3 * H, dtype=dhT.dtype, device=dev)
+        dgi = torch.empty(K, B, T, 3 * H, dtype=dhT.dtype, device=dev)
+        dh = dhT.contiguous()
+        dh_direct = torch.empty(K, B, H, dtype=dhT.dtype, device=dev)
+        st = _stream(dh)
+        for t in range(T - 1, -1, -1):
+            _capi.call("flr_gru_bwd_step", dh.data_ptr(), gates.data_ptr(), hseq.data_ptr(), dgh.data_ptr(),
+                       dgi.data_ptr(), dh_direct.data_ptr(), K, B, T, H, t, st)
+            if t > 0:  # dL/dh_t = z-path + dgh_t W_hh   (dL/dh_0 is not needed)
+                dh = torch.baddbmm(dh_direct, dgh[:, t], whh)
+        dgh2 = dgh.view(K, T * B, 3 * H)
+        dwhh = torch.bmm(dgh2.transpose(1, 2), hseq[:, :T].reshape(K, T * B, H))
+        dbhh = dgh2.sum(dim=1)
+        return dgi, dwhh, dbhh
+
+
+def client_gru(gi: torch.Tensor, whh: torch.Tensor, bhh: torch.Tensor) -> torch.Tensor:
+    return ClientGRU.apply(gi, whh, bhh)
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+class ClientBatchNorm(torch.autograd.Function):
+    """out = act(BN_train(x) [+ residual]) per (client, channel) plane of the
+    grouped layout x[B, K*C, H, W]; gamma/beta [K, C] (flr_batchnorm_fwd/_bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, relu: bool, eps: float):
+        x = x.contiguous()
+        B, KC = x.shape[:2]
+        HW = x[0, 0].numel()
+        g = gamma.contiguous()
+        b = beta.contiguous()
+        assert g.numel() == KC and b.numel() == KC, (x.shape, gamma.shape)
+        res = None if residual is None else residual.contiguous()
+        y = torch.empty_like(x)
+        mean = torch.empty(KC, dtype=x.dtype, device=x.device)
+        invstd = torch.empty_like(mean)
+        _capi.call("flr_batchnorm_fwd", x.data_ptr(), g.data_ptr(), b.data_ptr(), _ptr(res), y.data_ptr(),
+                   mean.data_ptr(), invstd.data_ptr(), B, KC, HW, eps, int(relu), _stream(x))
+        ctx.save_for_backward(x, y if relu else None, g, mean, invstd)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, g, mean, invstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        B, KC = x.shape[:2]
+        HW = x[0, 0].numel()
+        dx = torch.empty_like(x)
+        dg = torch.empty_like(g)
+        db = torch.empty_like(g)
+        dres = torch.empty_like(x) if ctx.has_res and ctx.needs_input_grad[3] else None
+        _capi.call("flr_batchnorm_bwd", dy.data_ptr(), x.data_ptr(), _ptr(y), g.data_ptr(), mean.data_ptr(),
+                   invstd.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _ptr(dres), B, KC, HW,
+                   int(ctx.relu), _stream(dy))
+        return dx, dg, db, dres, None, None
+
+
+def client_batchnorm(x, gamma, beta, residual=None, relu: bool = True, eps: float = 1e-5):
+    return ClientBatchNorm.apply(x, gamma, beta, residual, relu, eps)
