@@ -178,6 +178,25 @@ int flr_cross_entropy(const float* logits, const int64_t* labels, int64_t K,
 int flr_scale_client_rows(float* d, const float* gk, int64_t K, int64_t B,
                           int64_t C, void* stream);
 
+/* ---- §8(f): per-client norms and weighted row combinations ---------------
+ * Building blocks of GradientClippingDefense / NormBoundingDefense /
+ * DPSGDDefense (src/defenses/differential_privacy.py:74-164, 223-334) and
+ * GeometricMedianDefense (src/defenses/trimmed_mean.py:177-265).
+ * flr_row_norms: out[i] = ||X_i - center||_2 (type 0) or ||.||_inf (type 1),
+ * center optional [P]; differences rounded to fp32, squares summed in fp64 in
+ * a fixed order.  Workspace: flr_row_norms_workspace(K) bytes.
+ * flr_weighted_rows: out = (sum_j fl(fl(X[rows[j]] * scales[j]) * weights[j]))
+ * / divisor, sequential in j (rows NULL = all K rows in order, m = K; scales
+ * NULL = 1).  weights/scales are device float arrays of length m. */
+size_t flr_row_norms_workspace(int64_t K);
+int flr_row_norms(const float* X, int64_t K, int64_t P, int64_t ldx,
+                  const float* center, int type, double* out, void* workspace,
+                  size_t workspace_bytes, void* stream);
+int flr_weighted_rows(const float* X, int64_t K, int64_t P, int64_t ldx,
+                      const int32_t* rows, int64_t m, const float* weights,
+                      const float* scales, float divisor, float* out,
+                      void* stream);
+
 /* ---- a3: GRU recurrence, pointwise gate math per time step ----------------
  * Replaces the per-step cell of nn.GRU (torch gate order r, z, n;
  * h' = (h - n) * z + n), used by the text branch of the multimodal model.

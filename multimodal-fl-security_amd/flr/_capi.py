@@ -54,6 +54,11 @@ SIGNATURES = {
     "flr_conv2d_bwd_weight": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_cross_entropy": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "flr_scale_client_rows": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p]),
+    "flr_row_norms_workspace": (_size_t, [_i64]),
+    "flr_row_norms": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _int, _c_void_p, _c_void_p, _size_t,
+                             _c_void_p]),
+    "flr_weighted_rows": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                 ctypes.c_float, _c_void_p, _c_void_p]),
     "flr_batchnorm_fwd": (_int, [_c_void_p] * 7 + [_i64] * 3 + [ctypes.c_float, _int, _c_void_p]),
     "flr_batchnorm_bwd": (_int, [_c_void_p] * 10 + [_i64] * 3 + [_int, _c_void_p]),
     "flr_gru_fwd_step": (_int, [_c_void_p] * 4 + [_i64] * 5 + [_c_void_p]),

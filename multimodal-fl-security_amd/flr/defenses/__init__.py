@@ -1,20 +1,23 @@
 """Defense registry (mirror of src/defenses/__init__.py:28-59).
 
-The names of the reference factory are all registered.  The five on the
-north-star hot path run on the HIP kernels; the others are outside this
-engine's scope (SURVEY.md §2 rows 2b, 5, 6 — "next" rows in §8f) and raise
-NotImplementedError instead of silently doing something else.
+The names of the reference factory are all registered and run on the HIP
+kernels, except FLTrust (needs server-side root-set
+training), which raises NotImplementedError instead of silently doing
+something else.
 """
 from .base_defense import BaseDefense, NoDefense
 from .krum import KrumDefense, MultiKrumDefense
+from .geometric_median import GeometricMedianDefense
+from .norm_based import DPSGDDefense, GradientClippingDefense, NormBoundingDefense
 from .trimmed_mean import MedianDefense, TrimmedMeanDefense
 
 __all__ = [
     "BaseDefense", "NoDefense", "KrumDefense", "MultiKrumDefense",
-    "TrimmedMeanDefense", "MedianDefense", "get_defense",
+    "TrimmedMeanDefense", "MedianDefense", "GeometricMedianDefense",
+    "GradientClippingDefense", "NormBoundingDefense", "DPSGDDefense", "get_defense",
 ]
 
-_NOT_IN_SCOPE = ("geometric_median", "fltrust", "dp_sgd", "gradient_clipping", "norm_bounding")
+_NOT_IN_SCOPE = ("fltrust",)
 
 
 def _out_of_scope(name):
@@ -31,6 +34,10 @@ _DEFENSES = {
     "multi_krum": MultiKrumDefense,
     "trimmed_mean": TrimmedMeanDefense,
     "median": MedianDefense,
+    "geometric_median": GeometricMedianDefense,
+    "dp_sgd": DPSGDDefense,
+    "gradient_clipping": GradientClippingDefense,
+    "norm_bounding": NormBoundingDefense,
 }
 _DEFENSES.update({n: _out_of_scope(n) for n in _NOT_IN_SCOPE})
 

@@ -111,3 +111,49 @@ def median_lower(X: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.T
         out = torch.empty(P, dtype=torch.float32, device=X.device)
     _capi.call("flr_median_lower", X.data_ptr(), K, P, ldx, out.data_ptr(), _stream(X))
     return out
+
+
+def row_norms(X: torch.Tensor, center: Optional[torch.Tensor] = None, kind: str = "l2") -> torch.Tensor:
+    """float64 [K]: ||X_i - center|| per row (l2 or linf); fp32 differences,
+    fp64 accumulation in a fixed order (differential_privacy.py:223-236,
+    trimmed_mean.py:234)."""
+    K, P, ldx = _check_matrix(X)
+    if kind not in ("l2", "linf"):
+        raise ValueError(f"unknown norm kind {kind!r}")
+    if center is not None:
+        if not center.is_cuda or center.dtype != torch.float32 or center.numel() != P:
+            raise ValueError("center must be a float32 device vector of length P")
+        center = center.contiguous()
+    out = torch.empty(K, dtype=torch.float64, device=X.device)
+    nbytes = int(_capi.lib().flr_row_norms_workspace(K))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=X.device)
+    _capi.call("flr_row_norms", X.data_ptr(), K, P, ldx, _ptr(center), 0 if kind == "l2" else 1, out.data_ptr(),
+               ws.data_ptr(), nbytes, _stream(X))
+    return out
+
+
+def weighted_rows(X: torch.Tensor, weights, divisor: float, rows=None, scales=None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = (sum_j fl(fl(X[rows[j]] * scales[j]) * weights[j])) / divisor, in j order
+    (the Python-sum weighted averages of differential_privacy.py:141-148, 268-276,
+    323-330 and trimmed_mean.py:240)."""
+    K, P, ldx = _check_matrix(X)
+    w = torch.as_tensor(weights, dtype=torch.float32).to(X.device).contiguous()
+    m = w.numel()
+    r = None
+    if rows is not None:
+        r = torch.as_tensor(rows, dtype=torch.int32).to(X.device).contiguous()
+        if r.numel() != m:
+            raise ValueError("rows and weights differ in length")
+    elif m != K:
+        raise ValueError(f"{m} weights for {K} rows")
+    s = None
+    if scales is not None:
+        s = torch.as_tensor(scales, dtype=torch.float32).to(X.device).contiguous()
+        if s.numel() != m:
+            raise ValueError("scales and weights differ in length")
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=X.device)
+    _capi.call("flr_weighted_rows", X.data_ptr(), K, P, ldx, _ptr(r), m, w.data_ptr(), _ptr(s), float(divisor),
+               out.data_ptr(), _stream(X))
+    return out

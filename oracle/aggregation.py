@@ -94,6 +94,82 @@ def trimmed_mean(updates: Sequence[Update], trim_ratio: float) -> Tuple[List[tor
     return agg, t
 
 
+def _weighted_avg(updates: Sequence[Update], num_examples: Sequence[int]) -> List[torch.Tensor]:
+    total_examples = sum(num_examples)
+    agg = []
+    for pi in range(len(updates[0])):
+        weighted = sum(num_examples[i] * updates[i][pi] for i in range(len(updates)))
+        agg.append(weighted / total_examples)
+    return agg
+
+
+def gradient_clipping(updates: Sequence[Update], num_examples: Sequence[int], clip_norm: float = 1.0,
+                      clip_type: str = "l2"):
+    """differential_privacy.py:223-283.  Returns (aggregate, original_norms, clipped_count)."""
+    norms, clipped, count = [], [], 0
+    for u in updates:
+        f = torch.cat([t.flatten().float() for t in u])
+        norm = torch.max(torch.abs(f)).item() if clip_type == "linf" else torch.norm(f).item()
+        norms.append(norm)
+        if norm > clip_norm:
+            scale = clip_norm / norm
+            count += 1
+            clipped.append([t * scale for t in u])
+        else:
+            clipped.append(list(u))
+    return _weighted_avg(clipped, num_examples), norms, count
+
+
+def norm_bounding(updates: Sequence[Update], num_examples: Sequence[int], max_norm: float = 10.0,
+                  min_norm: float = 0.0):
+    """differential_privacy.py:299-334.  Returns (aggregate, rejected_clients)."""
+    rejected, valid, valid_n = [], [], []
+    for i, u in enumerate(updates):
+        norm = torch.norm(torch.cat([t.flatten() for t in u])).item()
+        if min_norm <= norm <= max_norm:
+            valid.append(u)
+            valid_n.append(num_examples[i])
+        else:
+            rejected.append(i)
+    if not valid:
+        valid, valid_n = list(updates), list(num_examples)
+    return _weighted_avg(valid, valid_n), rejected
+
+
+def dp_sgd_clipped_mean(updates: Sequence[Update], num_examples: Sequence[int], clip_norm: float = 10.0):
+    """differential_privacy.py:74-96, 127-152 without the noise (steps 1-2).
+    Returns (aggregate before noise, norms)."""
+    clipped, norms = [], []
+    for u in updates:
+        f = torch.cat([t.flatten().float() for t in u])
+        norm = torch.norm(f)
+        if norm > clip_norm:
+            scale = clip_norm / norm
+            clipped.append([t * scale for t in u])
+        else:
+            clipped.append(list(u))
+        norms.append(norm.item())
+    return _weighted_avg(clipped, num_examples), norms
+
+
+def geometric_median(updates: Sequence[Update], max_iters: int = 100, tolerance: float = 1e-5):
+    """trimmed_mean.py:216-251 (Weiszfeld from the coordinate median).
+    Returns (flat aggregate, num_iters)."""
+    U = torch.stack([torch.cat([p.flatten().float() for p in u]) for u in updates])
+    current = torch.median(U, dim=0)[0]
+    num_iters = max_iters
+    for it in range(max_iters):
+        d = torch.clamp(torch.norm(U - current, dim=1), min=1e-10)
+        w = 1.0 / d
+        new = (w.unsqueeze(1) * U).sum(dim=0) / w.sum()
+        change = torch.norm(new - current)
+        current = new
+        if change < tolerance:
+            num_iters = it + 1
+            break
+    return current, num_iters
+
+
 def sign_flip(update: Update) -> List[torch.Tensor]:
     """model_poisoning.py:274-276 — IPM without a benign mean negates the update."""
     return [-p for p in update]
