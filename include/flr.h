@@ -192,6 +192,10 @@ size_t flr_row_norms_workspace(int64_t K);
 int flr_row_norms(const float* X, int64_t K, int64_t P, int64_t ldx,
                   const float* center, int type, double* out, void* workspace,
                   size_t workspace_bytes, void* stream);
+/* out[i] = X_i . v (fp64 sum of exact products); workspace as flr_row_norms.
+ * FLTrust's torch.dot (src/defenses/fltrust.py:176). */
+int flr_row_dots(const float* X, int64_t K, int64_t P, int64_t ldx, const float* v,
+                 double* out, void* workspace, size_t workspace_bytes, void* stream);
 int flr_weighted_rows(const float* X, int64_t K, int64_t P, int64_t ldx,
                       const int32_t* rows, int64_t m, const float* weights,
                       const float* scales, float divisor, float* out,

@@ -17,6 +17,9 @@
 // reference's fp32 torch.norm itself drifts ~1e-5..3e-4 relative at 1e6..1e7
 // coordinates).  linf is exact.
 //
+// flr_row_dots: X_i . v per row, exact products summed in fp64 (FLTrust's
+// torch.dot, src/defenses/fltrust.py:176).
+//
 // flr_weighted_rows: out = (sum_j fl(fl(X[r_j] * s_j) * w_j)) / divisor,
 // sequential in j from +0 (Python sum() order, each op rounded separately).
 #include "flr_common.h"
@@ -38,9 +41,13 @@ __global__ __launch_bounds__(THREADS) void partial_kernel(const float* __restric
   const float* x = X + (int64_t)i * ldx;
   double acc = 0.0;
   auto one = [&](float xv, float cv) {
-    const float d = CENTER ? xv - cv : xv;
-    if constexpr (TYPE == 0) acc += (double)d * (double)d;
-    else acc = fmax(acc, (double)fabsf(d));
+    if constexpr (TYPE == 2) {  // dot with v (exact products, fp64 sum)
+      acc += (double)xv * (double)cv;
+    } else {
+      const float d = CENTER ? xv - cv : xv;
+      if constexpr (TYPE == 0) acc += (double)d * (double)d;
+      else acc = fmax(acc, (double)fabsf(d));
+    }
   };
   if constexpr (VEC) {  // block b: 4-float vectors [nv*b/NBLK, nv*(b+1)/NBLK); last block also the tail
     const int64_t nv = P / 4, q0 = nv * b / NBLK, q1 = nv * (b + 1) / NBLK;
@@ -60,13 +67,13 @@ __global__ __launch_bounds__(THREADS) void partial_kernel(const float* __restric
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const double w = __shfl_xor(acc, o, 64);
-    acc = TYPE == 0 ? acc + w : fmax(acc, w);
+    acc = TYPE == 1 ? fmax(acc, w) : acc + w;
   }
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
     double s = red[0];
-    for (int w = 1; w < THREADS / 64; ++w) s = TYPE == 0 ? s + red[w] : fmax(s, red[w]);
+    for (int w = 1; w < THREADS / 64; ++w) s = TYPE == 1 ? fmax(s, red[w]) : s + red[w];
     part[(int64_t)i * NBLK + b] = s;
   }
 }
@@ -76,7 +83,7 @@ __global__ void finish_kernel(const double* __restrict__ part, int K, double* __
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= K) return;
   double s = part[(int64_t)i * NBLK];
-  for (int b = 1; b < NBLK; ++b) s = TYPE == 0 ? s + part[(int64_t)i * NBLK + b] : fmax(s, part[(int64_t)i * NBLK + b]);
+  for (int b = 1; b < NBLK; ++b) s = TYPE == 1 ? fmax(s, part[(int64_t)i * NBLK + b]) : s + part[(int64_t)i * NBLK + b];
   out[i] = TYPE == 0 ? sqrt(s) : s;
 }
 
@@ -169,6 +176,23 @@ extern "C" int flr_row_norms(const float* X, int64_t K, int64_t P, int64_t ldx, 
   if (type == 0) hipLaunchKernelGGL(norm::finish_kernel<0>, dim3(g), dim3(256), 0, st, part, (int)K, out);
   else hipLaunchKernelGGL(norm::finish_kernel<1>, dim3(g), dim3(256), 0, st, part, (int)K, out);
   return launch_status("row_norms finish");
+}
+
+extern "C" int flr_row_dots(const float* X, int64_t K, int64_t P, int64_t ldx, const float* v, double* out,
+                            void* ws, size_t ws_bytes, void* stream) {
+  if (K < 1 || P < 0 || ldx < P || !X || !v || !out) return FLR_ERR_ARG;
+  if (!ws || ws_bytes < flr_row_norms_workspace(K)) return FLR_ERR_WORKSPACE;
+  if (K > 65535) return FLR_ERR_UNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  double* part = static_cast<double*>(ws);
+  const dim3 grid(norm::NBLK, (unsigned)K);
+  const bool vec = ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(v)) & 15) == 0 && ldx % 4 == 0;
+  if (vec) hipLaunchKernelGGL((norm::partial_kernel<2, true, true>), grid, dim3(norm::THREADS), 0, st, X, P, ldx, v, part);
+  else hipLaunchKernelGGL((norm::partial_kernel<2, true, false>), grid, dim3(norm::THREADS), 0, st, X, P, ldx, v, part);
+  int rc = launch_status("row_dots partial");
+  if (rc != FLR_OK) return rc;
+  hipLaunchKernelGGL(norm::finish_kernel<2>, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, part, (int)K, out);
+  return launch_status("row_dots finish");
 }
 
 extern "C" int flr_weighted_rows(const float* X, int64_t K, int64_t P, int64_t ldx, const int32_t* rows, int64_t m,

@@ -57,6 +57,7 @@ SIGNATURES = {
     "flr_row_norms_workspace": (_size_t, [_i64]),
     "flr_row_norms": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _int, _c_void_p, _c_void_p, _size_t,
                              _c_void_p]),
+    "flr_row_dots": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "flr_weighted_rows": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p, _c_void_p,
                                  ctypes.c_float, _c_void_p, _c_void_p]),
     "flr_batchnorm_fwd": (_int, [_c_void_p] * 7 + [_i64] * 3 + [ctypes.c_float, _int, _c_void_p]),

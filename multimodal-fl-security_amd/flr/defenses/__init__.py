@@ -1,12 +1,11 @@
 """Defense registry (mirror of src/defenses/__init__.py:28-59).
 
-The names of the reference factory are all registered and run on the HIP
-kernels, except FLTrust (needs server-side root-set
-training), which raises NotImplementedError instead of silently doing
-something else.
+Every name of the reference factory is registered and runs on the HIP kernels
+(FLTrust's server update runs on the client-batched trainer).
 """
 from .base_defense import BaseDefense, NoDefense
 from .krum import KrumDefense, MultiKrumDefense
+from .fltrust import FLTrustDefense
 from .geometric_median import GeometricMedianDefense
 from .norm_based import DPSGDDefense, GradientClippingDefense, NormBoundingDefense
 from .trimmed_mean import MedianDefense, TrimmedMeanDefense
@@ -14,18 +13,8 @@ from .trimmed_mean import MedianDefense, TrimmedMeanDefense
 __all__ = [
     "BaseDefense", "NoDefense", "KrumDefense", "MultiKrumDefense",
     "TrimmedMeanDefense", "MedianDefense", "GeometricMedianDefense",
-    "GradientClippingDefense", "NormBoundingDefense", "DPSGDDefense", "get_defense",
+    "GradientClippingDefense", "NormBoundingDefense", "DPSGDDefense", "FLTrustDefense", "get_defense",
 ]
-
-_NOT_IN_SCOPE = ("fltrust",)
-
-
-def _out_of_scope(name):
-    def make(_cfg):
-        raise NotImplementedError(
-            f"defense {name!r} is not on this engine's hot path (see DESIGN.md, out-of-scope rows)")
-    return make
-
 
 _DEFENSES = {
     "none": NoDefense,
@@ -38,8 +27,8 @@ _DEFENSES = {
     "dp_sgd": DPSGDDefense,
     "gradient_clipping": GradientClippingDefense,
     "norm_bounding": NormBoundingDefense,
+    "fltrust": FLTrustDefense,
 }
-_DEFENSES.update({n: _out_of_scope(n) for n in _NOT_IN_SCOPE})
 
 
 def get_defense(defense_type: str, defense_config: dict):

@@ -132,6 +132,20 @@ def row_norms(X: torch.Tensor, center: Optional[torch.Tensor] = None, kind: str 
     return out
 
 
+def row_dots(X: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    """float64 [K]: X_i . v (fltrust.py:176), exact products, fp64 fixed-order sum."""
+    K, P, ldx = _check_matrix(X)
+    if not v.is_cuda or v.dtype != torch.float32 or v.numel() != P:
+        raise ValueError("v must be a float32 device vector of length P")
+    v = v.contiguous()
+    out = torch.empty(K, dtype=torch.float64, device=X.device)
+    nbytes = int(_capi.lib().flr_row_norms_workspace(K))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=X.device)
+    _capi.call("flr_row_dots", X.data_ptr(), K, P, ldx, v.data_ptr(), out.data_ptr(), ws.data_ptr(), nbytes,
+               _stream(X))
+    return out
+
+
 def weighted_rows(X: torch.Tensor, weights, divisor: float, rows=None, scales=None,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = (sum_j fl(fl(X[rows[j]] * scales[j]) * weights[j])) / divisor, in j order

@@ -170,6 +170,36 @@ def geometric_median(updates: Sequence[Update], max_iters: int = 100, tolerance:
     return current, num_iters
 
 
+def fltrust(updates: Sequence[Update], server_gradient: Update):
+    """fltrust.py:158-270 given the server update g.  Returns (aggregate, trust_scores)."""
+    sflat = torch.cat([t.flatten().float() for t in server_gradient])
+    trust = []
+    for u in updates:
+        cflat = torch.cat([t.flatten().float() for t in u])
+        dot = torch.dot(cflat, sflat)
+        cn, sn = torch.norm(cflat), torch.norm(sflat)
+        if cn < 1e-10 or sn < 1e-10:
+            trust.append(0.0)
+        else:
+            trust.append(max(0.0, (dot / (cn * sn)).item()))
+    normalized = []
+    for u in updates:
+        un = torch.norm(torch.cat([t.flatten().float() for t in u]))
+        if un < 1e-10:
+            normalized.append(list(u))
+        else:
+            scale = torch.norm(sflat) / un
+            normalized.append([t * scale for t in u])
+    total = sum(trust)
+    if total < 1e-10:
+        return list(server_gradient), trust
+    agg = []
+    for pi in range(len(normalized[0])):
+        weighted = sum(trust[i] * normalized[i][pi] for i in range(len(normalized)))
+        agg.append(weighted / total)
+    return agg, trust
+
+
 def sign_flip(update: Update) -> List[torch.Tensor]:
     """model_poisoning.py:274-276 — IPM without a benign mean negates the update."""
     return [-p for p in update]
