@@ -23,6 +23,7 @@
 #include "flr_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace flr {
 namespace conv {
@@ -67,8 +68,18 @@ struct Geom {
 // ---- problem accessors -----------------------------------------------------
 // A(m, r) and B(n, r); FAST_*: the dimension consecutive threads walk when
 // loading a tile (true = m / n, false = r), chosen for contiguous addresses.
+// Tile slot mapping (the kernel's LDS stash uses the same): element e = tid +
+// 256 i of a 64 x 32 tile sits at (e % 64, e / 64) when FAST along m / n and at
+// (e / 32, e % 32) when FAST along r.
+__device__ __forceinline__ void slot_of(bool fast_mn, int tid, int i, int& mn, int& kk) {
+  const int e = tid + THREADS * i;
+  if (fast_mn) { mn = e % BM; kk = e / BM; } else { kk = e % BK; mn = e / BK; }
+}
 
-struct Fwd {  // y = conv(x, w): M = Cout, N = B*Ho*Wo, R = Cin*KH*KW
+// Generic accessors (any channel count; the stem's Cin = 3): every element's
+// index is decomposed on its own.
+
+struct FwdG {  // y = conv(x, w): M = Cout, N = B*Ho*Wo, R = Cin*KH*KW
   Geom g;
   const float* x;
   const float* w;
@@ -96,7 +107,7 @@ struct Fwd {  // y = conv(x, w): M = Cout, N = B*Ho*Wo, R = Cin*KH*KW
   }
 };
 
-struct Wgt {  // dw = sum_q dy(co, q) im(r, q): M = Cout, N = R, reduction over q = B*Ho*Wo
+struct WgtG {  // dw = sum_q dy(co, q) im(r, q): M = Cout, N = R, reduction over q = B*Ho*Wo
   Geom g;
   const float* x;
   const float* dy;
@@ -124,7 +135,7 @@ struct Wgt {  // dw = sum_q dy(co, q) im(r, q): M = Cout, N = R, reduction over 
   }
 };
 
-struct Dgrad {  // dx = conv^T(dy, w): M = Cin, N = B*H*W, R = Cout*KH*KW
+struct DgradG {  // dx = conv^T(dy, w): M = Cin, N = B*H*W, R = Cout*KH*KW
   Geom g;
   const float* dy;
   const float* w;
@@ -154,6 +165,167 @@ struct Dgrad {  // dx = conv^T(dy, w): M = Cin, N = B*H*W, R = Cout*KH*KW
   }
 };
 
+
+template <class G>
+struct GenericLoad : G {
+  struct State { int k, m0, n0, tid; };
+  __device__ State init(int k, int m0, int n0, int tid) const { return State{k, m0, n0, tid}; }
+  __device__ void load(const State& s, int r0, int re, float (&ra)[8], float (&rb)[8]) const {
+    const int M = this->M(), N = this->N();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      int mm, ak, nn, bk;
+      slot_of(G::FAST_A_M, s.tid, i, mm, ak);
+      slot_of(G::FAST_B_N, s.tid, i, nn, bk);
+      const int m = s.m0 + mm, r = r0 + ak, n = s.n0 + nn, rr = r0 + bk;
+      ra[i] = (m < M && r < re) ? this->a(s.k, m, r) : 0.f;
+      rb[i] = (n < N && rr < re) ? this->b(s.k, n, rr) : 0.f;
+    }
+  }
+};
+using Fwd = GenericLoad<FwdG>;
+using Wgt = GenericLoad<WgtG>;
+using Dgrad = GenericLoad<DgradG>;
+
+// ---- fast accessors (channel counts multiple of 32; Wgt: Cin multiple of 64) --
+// r = slot * C + c with C % 32 == 0, so a 32-deep K-tile never straddles two
+// kernel taps: the tap and channel base are tile-uniform (scalar), each
+// thread's spatial coordinates are decomposed once per kernel, and an element
+// costs one add + one load.
+
+struct FwdF : FwdG {  // A fast along r (ci), B fast along n (pixels)
+  struct State {
+    const float* wk; const float* xk;
+    int abase[8]; bool mok[8];
+    int ih0, iw0, xoff, rl;  // B: this thread's pixel
+    bool nok;
+  };
+  __device__ State init(int k, int m0, int n0, int tid) const {
+    State s;
+    s.wk = w + (int64_t)k * g.Cout * g.Cin * g.KH * g.KW;
+    s.xk = x + (int64_t)k * g.Cin * g.H * g.W;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + tid / BK + 8 * i;
+      s.mok[i] = m < g.Cout;
+      s.abase[i] = m * g.Cin * g.KH * g.KW + (tid % BK) * g.KH * g.KW;
+    }
+    const int n = n0 + tid % BN;
+    s.nok = n < g.B * g.Ho * g.Wo;
+    const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
+    const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+    s.ih0 = (int)oh * g.stride - g.pad;
+    s.iw0 = (int)ow * g.stride - g.pad;
+    s.xoff = (int)(bb * g.xbs) + (tid / BN) * g.H * g.W;
+    s.rl = tid / BN;
+    return s;
+  }
+  __device__ void load(const State& s, int r0, int re, float (&ra)[8], float (&rb)[8]) const {
+    const int slot = __builtin_amdgcn_readfirstlane(r0 / g.Cin);
+    const int ci0 = r0 - slot * g.Cin;
+    const int kh = g.tap_kh[slot], kw = g.tap_kw[slot];
+    const int KK = g.KH * g.KW, HW = g.H * g.W;
+    const int aoff = ci0 * KK + kh * g.KW + kw;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ra[i] = s.mok[i] ? s.wk[s.abase[i] + aoff] : 0.f;
+    const int ih = s.ih0 + kh, iw = s.iw0 + kw;
+    const bool ok = s.nok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+    const int boff = s.xoff + ci0 * HW + ih * g.W + iw;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rb[i] = ok ? s.xk[boff + 4 * i * HW] : 0.f;
+  }
+};
+
+struct DgradF : DgradG {  // A fast along m (ci), B fast along n (input pixels)
+  static constexpr bool FAST_A_M = true, FAST_B_N = true;
+  struct State {
+    const float* wk; const float* dyk;
+    int abase; bool mok;
+    int ih, iw, yoff;
+    bool nok;
+  };
+  __device__ State init(int k, int m0, int n0, int tid) const {
+    State s;
+    const int KK = g.KH * g.KW;
+    s.wk = w + (int64_t)k * g.Cout * g.Cin * KK;
+    s.dyk = dy + (int64_t)k * g.Cout * g.Ho * g.Wo;
+    const int m = m0 + tid % BM;
+    s.mok = m < g.Cin;
+    s.abase = m * KK + (tid / BM) * g.Cin * KK;
+    const int n = n0 + tid % BN;
+    s.nok = n < g.B * g.H * g.W;
+    const uint32_t bb = udiv(n, g.d_hw), p = n - bb * g.H * g.W;
+    const uint32_t ih = udiv(p, g.d_w), iw = p - ih * g.W;
+    s.ih = (int)ih + g.pad;
+    s.iw = (int)iw + g.pad;
+    s.yoff = (int)(bb * g.ybs) + (tid / BN) * g.Ho * g.Wo;
+    return s;
+  }
+  __device__ void load(const State& s, int r0, int re, float (&ra)[8], float (&rb)[8]) const {
+    const int slot = __builtin_amdgcn_readfirstlane(r0 / g.Cout);
+    const int co0 = r0 - slot * g.Cout;
+    const int kh = g.tap_kh[slot], kw = g.tap_kw[slot];
+    const int KK = g.KH * g.KW, HoWo = g.Ho * g.Wo;
+    const int aoff = co0 * g.Cin * KK + kh * g.KW + kw;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ra[i] = s.mok ? s.wk[s.abase + aoff + 4 * i * g.Cin * KK] : 0.f;
+    const int nh = s.ih - kh, nw = s.iw - kw;
+    int oh, ow;
+    bool ok = s.nok && nh >= 0 && nw >= 0;
+    if (g.stride == 1) {
+      oh = nh; ow = nw;
+    } else {
+      oh = nh / g.stride; ow = nw / g.stride;
+      ok = ok && oh * g.stride == nh && ow * g.stride == nw;
+    }
+    ok = ok && oh < g.Ho && ow < g.Wo;
+    const int boff = s.yoff + co0 * HoWo + oh * g.Wo + ow;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rb[i] = ok ? s.dyk[boff + 4 * i * HoWo] : 0.f;
+  }
+};
+
+struct WgtF : WgtG {  // n-tile inside one tap (Cin % 64 == 0); A and B fast along r (q)
+  struct State {
+    const float* dyk; const float* xk;
+    int abase[8]; bool mok[8];
+    int bbase[8];
+    int kh, kw, ci0, ql;
+  };
+  __device__ State init(int k, int m0, int n0, int tid) const {
+    State s;
+    s.dyk = dy + (int64_t)k * g.Cout * g.Ho * g.Wo;
+    s.xk = x + (int64_t)k * g.Cin * g.H * g.W;
+    const int slot = n0 / g.Cin;
+    s.ci0 = n0 - slot * g.Cin;
+    s.kh = g.tap_kh[slot];
+    s.kw = g.tap_kw[slot];
+    s.ql = tid % BK;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + tid / BK + 8 * i;
+      s.mok[i] = m < g.Cout;
+      s.abase[i] = m * g.Ho * g.Wo;
+      s.bbase[i] = (s.ci0 + tid / BK + 8 * i) * g.H * g.W;
+    }
+    return s;
+  }
+  __device__ void load(const State& s, int r0, int re, float (&ra)[8], float (&rb)[8]) const {
+    const int q = r0 + s.ql;
+    const bool qok = q < re;
+    const uint32_t bb = udiv(q, g.d_howo), p = q - bb * g.Ho * g.Wo;
+    const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+    const int aoff = (int)(bb * g.ybs + p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ra[i] = (qok && s.mok[i]) ? s.dyk[s.abase[i] + aoff] : 0.f;
+    const int ih = (int)oh * g.stride - g.pad + s.kh, iw = (int)ow * g.stride - g.pad + s.kw;
+    const bool ok = qok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+    const int boff = (int)(bb * g.xbs) + ih * g.W + iw;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rb[i] = ok ? s.xk[s.bbase[i] + boff] : 0.f;
+  }
+};
+
 // ---- the implicit-GEMM kernel ---------------------------------------------
 // Split-K: blockIdx.z = client * S + split; split s reduces the BK-aligned
 // range [rb, re) and, when S > 1, writes its tile to part[(s*K + k)][M][N];
@@ -172,35 +344,23 @@ __global__ __launch_bounds__(THREADS, 2) void cgemm_kernel(const Prob pb, int S,
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, l32 = lane & 31;
 
-  // this thread's 8 A and 8 B tile slots: (mm, kk) / (nn, kk)
-  int am[8], ak[8], bn[8], bk[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int e = tid + THREADS * i;
-    if (Prob::FAST_A_M) { am[i] = e % BM; ak[i] = e / BM; } else { ak[i] = e % BK; am[i] = e / BK; }
-    if (Prob::FAST_B_N) { bn[i] = e % BN; bk[i] = e / BN; } else { bk[i] = e % BK; bn[i] = e / BK; }
-  }
   float ra[8], rb_[8];
   auto stash = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      As[buf][ak[i] * LDS_STRIDE + am[i]] = ra[i];
-      Bs[buf][bk[i] * LDS_STRIDE + bn[i]] = rb_[i];
+      int am, ak, bn, bk;
+      slot_of(Prob::FAST_A_M, tid, i, am, ak);
+      slot_of(Prob::FAST_B_N, tid, i, bn, bk);
+      As[buf][ak * LDS_STRIDE + am] = ra[i];
+      Bs[buf][bk * LDS_STRIDE + bn] = rb_[i];
     }
   };
+  const auto st = pb.init(k, m0, n0, tid);
 
   f32x16 acc;
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-  auto loadr = [&](int r0) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + am[i], r = r0 + ak[i];
-      ra[i] = (m < M && r < re) ? pb.a(k, m, r) : 0.f;
-      const int n = n0 + bn[i], rr = r0 + bk[i];
-      rb_[i] = (n < N && rr < re) ? pb.b(k, n, rr) : 0.f;
-    }
-  };
+  auto loadr = [&](int r0) { pb.load(st, r0, re, ra, rb_); };
   loadr(rb);
   stash(0);
   __syncthreads();
@@ -319,6 +479,15 @@ int launch(const Prob& pb, void* ws, size_t ws_bytes, hipStream_t st, const char
 using namespace flr;
 using namespace flr::conv;
 
+// FLR_CONV_GENERIC=1 forces the generic gathers (A/B timing and cross-checks).
+static int getenv_generic() {
+  static const int v = [] {
+    const char* e = getenv("FLR_CONV_GENERIC");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v;
+}
+
 extern "C" size_t flr_conv2d_workspace(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
                                        int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
   if (!geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return 0;
@@ -334,9 +503,14 @@ extern "C" int flr_conv2d_fwd(const float* x, const float* w, float* y, int64_t 
                               int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
                               void* ws, size_t ws_bytes, void* stream) {
   if (!x || !w || !y || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
+  const Geom g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  if (Cin % BK == 0 && getenv_generic() == 0) {
+    FwdF pb;
+    pb.g = g; pb.x = x; pb.w = w; pb.y = y;
+    return launch(pb, ws, ws_bytes, as_stream(stream), "conv fwd");
+  }
   Fwd pb;
-  pb.g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
-  pb.x = x; pb.w = w; pb.y = y;
+  pb.g = g; pb.x = x; pb.w = w; pb.y = y;
   return launch(pb, ws, ws_bytes, as_stream(stream), "conv fwd");
 }
 
@@ -344,9 +518,14 @@ extern "C" int flr_conv2d_bwd_data(const float* dy, const float* w, float* dx, i
                                    int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                                    int64_t pad, void* ws, size_t ws_bytes, void* stream) {
   if (!dy || !w || !dx || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
+  const Geom g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  if (Cout % BK == 0 && getenv_generic() == 0) {
+    DgradF pb;
+    pb.g = g; pb.dy = dy; pb.w = w; pb.dx = dx;
+    return launch(pb, ws, ws_bytes, as_stream(stream), "conv bwd data");
+  }
   Dgrad pb;
-  pb.g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
-  pb.dy = dy; pb.w = w; pb.dx = dx;
+  pb.g = g; pb.dy = dy; pb.w = w; pb.dx = dx;
   return launch(pb, ws, ws_bytes, as_stream(stream), "conv bwd data");
 }
 
@@ -354,12 +533,17 @@ extern "C" int flr_conv2d_bwd_weight(const float* x, const float* dy, float* dw,
                                      int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                                      int64_t pad, void* ws, size_t ws_bytes, void* stream) {
   if (!x || !dy || !dw || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
-  Wgt pb;
-  pb.g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
-  pb.x = x; pb.dy = dy; pb.dw = dw;
+  const Geom g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
   hipStream_t st = as_stream(stream);
-  if (pb.g.ntaps < KH * KW &&  // dead taps get exact-zero gradients
+  if (g.ntaps < KH * KW &&  // dead taps get exact-zero gradients
       hipMemsetAsync(dw, 0, (size_t)K * Cout * Cin * KH * KW * sizeof(float), st) != hipSuccess)
     return FLR_ERR_HIP;
+  if (Cin % BN == 0 && getenv_generic() == 0) {
+    WgtF pb;
+    pb.g = g; pb.x = x; pb.dy = dy; pb.dw = dw;
+    return launch(pb, ws, ws_bytes, st, "conv bwd weight");
+  }
+  Wgt pb;
+  pb.g = g; pb.x = x; pb.dy = dy; pb.dw = dw;
   return launch(pb, ws, ws_bytes, st, "conv bwd weight");
 }

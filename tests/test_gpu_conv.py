@@ -19,6 +19,9 @@ SHAPES = [  # (K, B, Cin, H, W, Cout, KH, stride, pad)
     (8, 32, 256, 4, 4, 256, 3, 1, 1),  # layer3 conv2: split-K path
     (4, 32, 512, 1, 1, 512, 3, 1, 1),  # layer4 at 1x1: 8 of 9 taps dead, split-K
     (4, 32, 256, 2, 2, 512, 3, 2, 1),  # layer4 first conv: 2x2 -> 1x1, 4 taps live
+    (3, 3, 64, 5, 5, 96, 3, 1, 1),     # fast loaders with ragged M and N tiles
+    (2, 5, 32, 7, 7, 64, 3, 2, 1),     # fast fwd/dgrad (stride 2, odd size), generic wgrad (Cin % 64)
+    (2, 4, 64, 8, 8, 128, 1, 2, 0),    # fast 1x1 stride-2 downsample
 ]
 
 

@@ -92,7 +92,7 @@ def test_norm_bounding_vs_oracle(cuda, K, P):
     want, wrej = orc.norm_bounding(ups, n, hi, lo)
     d = get_defense("norm_bounding", {"max_norm": hi, "min_norm": lo})
     got = d.aggregate([[t.to(cuda) for t in u] for u in ups], n)
-    assert d.rejected_clients == wrej and len(wrej) == 3
+    assert d.rejected_clients == wrej and len(wrej) == 4
     for a, b in zip(got, want):
         _close(a, b)
     # nothing kept -> mean of all (differential_privacy.py:320-323)

@@ -1,7 +1,16 @@
+"""List conv (cgemm) dispatches of the last profiled round: name, grid, us.
+usage: cgemm_calls.py DB"""
 import sqlite3, sys
 c = sqlite3.connect(sys.argv[1])
-t = c.execute("select max(start) from kernels where kernel_name like '%orderstat%'").fetchone()[0]
-rows = c.execute("select kernel_name, grid_size_x, grid_size_y, grid_size_z, end-start from kernels "
-                 "where start > ? and kernel_name like '%cgemm%' order by start", (t,)).fetchall()
-for r in rows[:70]:
-    print(f"{r[0][:45]:45s} grid=({r[1]},{r[2]},{r[3]}) {r[4]/1e3:9.1f} us")
+cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+name = "kernel_name" if "kernel_name" in cols else ("name" if "name" in cols else cols[0])
+gx = [x for x in ("grid_size_x", "grid_x", "workgroup_count_x") if x in cols]
+gy = [x for x in ("grid_size_y", "grid_y") if x in cols]
+gz = [x for x in ("grid_size_z", "grid_z") if x in cols]
+print("columns:", cols)
+t = c.execute(f"select max(start) from kernels where {name} like '%orderstat%'").fetchone()[0]
+sel = ", ".join([name] + (gx[:1] + gy[:1] + gz[:1]) + ["end-start"])
+rows = c.execute(f"select {sel} from kernels where start > ? and {name} like '%cgemm%' order by start",
+                 (t,)).fetchall()
+for r in rows[:80]:
+    print(f"{r[0][22:52]:30s} {r[1:-1]} {r[-1]/1e3:9.1f} us")
