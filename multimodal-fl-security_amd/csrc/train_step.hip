@@ -132,8 +132,26 @@ struct BlockTable {
   const float* g[MAXB];
   float* m[MAXB];
   int64_t pre[MAXB + 1];
+  uint8_t vec[MAXB];  // block j may use 16-B accesses (n % 4 == 0, all three bases 16-B aligned)
   int nb;
 };
+
+// Visits e in [lo, hi) of a block whose client segment starts 256-B aligned
+// when n % 4 == 0: scalar head up to a 4-element boundary, float4 body, scalar
+// tail.  f1(e) handles one element, f4(e) four consecutive ones.
+template <class F1, class F4>
+__device__ __forceinline__ void visit_range(int64_t lo, int64_t hi, int64_t pre, bool vec, F1 f1, F4 f4) {
+  if (!vec) {
+    for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) f1(e);
+    return;
+  }
+  int64_t vlo = pre + ((lo - pre + 3) & ~(int64_t)3);
+  if (vlo > hi) vlo = hi;
+  const int64_t vhi = pre + ((hi - pre) & ~(int64_t)3);
+  for (int64_t e = lo + threadIdx.x; e < vlo; e += THREADS) f1(e);
+  for (int64_t e = vlo + 4 * (int64_t)threadIdx.x; e < vhi; e += 4 * THREADS) f4(e);
+  for (int64_t e = (vhi > vlo ? vhi : vlo) + threadIdx.x; e < hi; e += THREADS) f1(e);
+}
 
 __global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable tb, int64_t P,
                                                                 double* __restrict__ partial) {
@@ -147,10 +165,17 @@ __global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable
     if (lo >= hi) continue;
     const int64_t n = tb.pre[j + 1] - tb.pre[j];
     const float* g = tb.g[j] + (int64_t)k * n - tb.pre[j];
-    for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) {
-      const double v = (double)g[e];
-      acc += v * v;
-    }
+    visit_range(
+        lo, hi, tb.pre[j], tb.vec[j] != 0,
+        [&](int64_t e) {
+          const double v = (double)g[e];
+          acc += v * v;
+        },
+        [&](int64_t e) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(g + e);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc += (double)v[q] * (double)v[q];
+        });
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
@@ -181,24 +206,37 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
     float* x = tb.x[j] + base;
     const float* g = tb.g[j] + base;
     float* m = tb.m[j] + base;
-    if (first) {
-      for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) {
-        const float xp = x[e];
-        float gp = g[e] * c;
-        if (wd != 0.0f) gp = __builtin_fmaf(wd, xp, gp);
-        m[e] = gp;
-        x[e] = __builtin_fmaf(nlr, gp, xp);
-      }
-    } else {
-      for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) {
-        const float xp = x[e];
-        float gp = g[e] * c;
-        if (wd != 0.0f) gp = __builtin_fmaf(wd, xp, gp);
-        const float bb = m[e] * mom + gp;
-        m[e] = bb;
-        x[e] = __builtin_fmaf(nlr, bb, xp);
-      }
-    }
+    auto upd = [&](float xp, float gr, float mp, float& mo, float& xo) {
+      float gp = gr * c;
+      if (wd != 0.0f) gp = __builtin_fmaf(wd, xp, gp);
+      const float bb = first ? gp : mp * mom + gp;  // buf.mul_(mom).add_(g): two roundings
+      mo = bb;
+      xo = __builtin_fmaf(nlr, bb, xp);
+    };
+    visit_range(
+        lo, hi, tb.pre[j], tb.vec[j] != 0,
+        [&](int64_t e) {
+          float mo, xo;
+          upd(x[e], g[e], first ? 0.f : m[e], mo, xo);
+          m[e] = mo;
+          x[e] = xo;
+        },
+        [&](int64_t e) {
+          const f32x4 xv = *reinterpret_cast<const f32x4*>(x + e);
+          const f32x4 gv = *reinterpret_cast<const f32x4*>(g + e);
+          f32x4 mv = {0.f, 0.f, 0.f, 0.f};
+          if (!first) mv = *reinterpret_cast<const f32x4*>(m + e);
+          f32x4 mo, xo;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float a, b;
+            upd(xv[q], gv[q], mv[q], a, b);
+            mo[q] = a;
+            xo[q] = b;
+          }
+          *reinterpret_cast<f32x4*>(m + e) = mo;
+          *reinterpret_cast<f32x4*>(x + e) = xo;
+        });
   }
 }
 
@@ -275,6 +313,9 @@ extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* co
     tb.g[j] = g_blocks[j];
     tb.m[j] = m_blocks[j];
     tb.pre[j + 1] = tb.pre[j] + block_numel[j];
+    const uintptr_t al = reinterpret_cast<uintptr_t>(x_blocks[j]) | reinterpret_cast<uintptr_t>(g_blocks[j]) |
+                         reinterpret_cast<uintptr_t>(m_blocks[j]);
+    tb.vec[j] = (block_numel[j] % 4 == 0 && (al & 15) == 0) ? 1 : 0;
   }
   const int64_t P = tb.pre[tb.nb];
   if (P == 0) return FLR_OK;
