@@ -178,6 +178,31 @@ int flr_cross_entropy(const float* logits, const int64_t* labels, int64_t K,
 int flr_scale_client_rows(float* d, const float* gk, int64_t K, int64_t B,
                           int64_t C, void* stream);
 
+/* Tap-major variants (the training engine's conv layout when Cin and Cout are
+ * multiples of 64): w_t / dw_t are [K][KH][KW][Cin][Cout] per client, i.e.
+ * torch's [Cout][Cin][KH][KW] permuted (0, 2, 3, 1) per client.  Same
+ * activations, outputs and semantics as flr_conv2d_fwd / _bwd_data /
+ * _bwd_weight; FLR_ERR_UNSUPPORTED when the channel counts do not qualify
+ * (flr_conv2d_tap_major_ok).  Workspace (optional, split-K) from
+ * flr_conv2d_t_workspace. */
+int flr_conv2d_tap_major_ok(int64_t Cin, int64_t Cout);
+size_t flr_conv2d_t_workspace(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W,
+                              int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                              int64_t pad);
+int flr_conv2d_fwd_t(const float* x, const float* w_t, float* y, int64_t K, int64_t B,
+                     int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH,
+                     int64_t KW, int64_t stride, int64_t pad, void* workspace,
+                     size_t workspace_bytes, void* stream);
+int flr_conv2d_bwd_data_t(const float* dy, const float* w_t, float* dx, int64_t K,
+                          int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
+                          int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+                          void* workspace, size_t workspace_bytes, void* stream);
+int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* dw_t, int64_t K,
+                            int64_t B, int64_t Cin, int64_t H, int64_t W,
+                            int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                            int64_t pad, void* workspace, size_t workspace_bytes,
+                            void* stream);
+
 /* ---- §8(f): per-client norms and weighted row combinations ---------------
  * Building blocks of GradientClippingDefense / NormBoundingDefense /
  * DPSGDDefense (src/defenses/differential_privacy.py:74-164, 223-334) and

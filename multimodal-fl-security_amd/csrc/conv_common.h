@@ -1,0 +1,80 @@
+// Client-batched convolution: geometry shared by the conv kernels (gfx950).
+#pragma once
+
+#include "flr_common.h"
+
+namespace flr {
+namespace conv {
+
+struct FastDiv {  // n / d for 0 <= n < 2^31 via mul-hi (Granlund-Montgomery)
+  uint32_t d, m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  const uint32_t t = __umulhi(n, f.m);
+  return (t + ((n - t) >> 1)) >> (f.s ? f.s - 1 : 0);
+}
+// d == 1 needs s = 0: (t + ((n - t) >> 1)) >> 0 with m = 1 gives n/2 ... handle explicitly
+__device__ __forceinline__ uint32_t udiv(uint32_t n, const FastDiv& f) { return f.d == 1 ? n : fdiv(n, f); }
+
+constexpr int MAXTAPS = 49;
+
+struct Geom {
+  int Kc, B, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo;
+  int64_t xbs, ybs;  // batch strides of x ([B][K*Cin][H][W]) and y ([B][K*Cout][Ho][Wo])
+  FastDiv d_howo, d_wo, d_hw, d_w, d_cin, d_cout;
+  // Kernel taps that read at least one non-padding input pixel.  A tap that
+  // only ever reads the zero padding contributes exact zeros to y, dx and dw,
+  // so the reduction runs over (valid tap, channel) only: r = slot * C + c.
+  int ntaps;
+  int8_t tap_kh[MAXTAPS], tap_kw[MAXTAPS];
+};
+
+inline Geom make_geom(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH,
+                      int64_t KW, int64_t stride, int64_t pad) {
+  Geom g;
+  g.Kc = (int)K; g.B = (int)B; g.Cin = (int)Cin; g.H = (int)H; g.W = (int)W; g.Cout = (int)Cout;
+  g.KH = (int)KH; g.KW = (int)KW; g.stride = (int)stride; g.pad = (int)pad;
+  g.Ho = (int)((H + 2 * pad - KH) / stride + 1);
+  g.Wo = (int)((W + 2 * pad - KW) / stride + 1);
+  g.xbs = K * Cin * H * W;
+  g.ybs = K * Cout * g.Ho * g.Wo;
+  g.d_howo = make_fastdiv((uint32_t)(g.Ho * g.Wo));
+  g.d_wo = make_fastdiv((uint32_t)g.Wo);
+  g.d_hw = make_fastdiv((uint32_t)(H * W));
+  g.d_w = make_fastdiv((uint32_t)W);
+  g.d_cin = make_fastdiv((uint32_t)Cin);
+  g.d_cout = make_fastdiv((uint32_t)Cout);
+  g.ntaps = 0;
+  for (int kh = 0; kh < KH; ++kh) {
+    bool hv = false;
+    for (int oh = 0; oh < g.Ho && !hv; ++oh) { const int ih = oh * (int)stride - (int)pad + kh; hv = ih >= 0 && ih < H; }
+    for (int kw = 0; kw < KW; ++kw) {
+      bool wv = false;
+      for (int ow = 0; ow < g.Wo && !wv; ++ow) { const int iw = ow * (int)stride - (int)pad + kw; wv = iw >= 0 && iw < W; }
+      if (hv && wv) { g.tap_kh[g.ntaps] = (int8_t)kh; g.tap_kw[g.ntaps] = (int8_t)kw; ++g.ntaps; }
+    }
+  }
+  return g;
+}
+
+inline bool geom_ok(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+                    int64_t stride, int64_t pad) {
+  if (K < 1 || B < 1 || Cin < 1 || H < 1 || W < 1 || Cout < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0)
+    return false;
+  if (H + 2 * pad < KH || W + 2 * pad < KW || KH * KW > MAXTAPS) return false;
+  // 32-bit index space per client for the GEMM dims and offsets
+  return K * Cin * H * W * B < (int64_t(1) << 31) && K * Cout * H * W * B < (int64_t(1) << 31) &&
+         K <= 65535;
+}
+
+}  // namespace conv
+}  // namespace flr

@@ -1,0 +1,463 @@
+// a2 — client-batched convolution with TAP-MAJOR weights, the training
+// engine's layout for every conv whose channel counts are multiples of 64
+// (all of ResNet-18 but the stem).  Same products as train_conv.hip
+// (nn.Conv2d(bias=False) of the conv blocks, src/models/cub200_cnn.py:71-77
+// template; trained per client in run_experiments.py:216-235), with the
+// weights of client k stored as W_t[k][kh][kw][Cin][Cout] instead of torch's
+// [Cout][Cin][kh][kw].  The trainer converts at the round boundaries
+// (load_global / export); inside the round nothing else sees the layout.
+//
+// Why: at a fixed kernel tap the weight slab is a plain [Cin][Cout] matrix, so
+//   fwd   A(m = co, k = ci) is contiguous along m -> 16-B loads, [k][m] LDS image
+//   dgrad A(m = ci, k = co) is contiguous along k -> 16-B loads, [m][k] LDS image
+//   wgrad writes C(m = ci, n = co) with coalesced rows.
+// The activation operand is an im2col gather; it uses raw buffer loads whose
+// per-element stride sits in soffset (an SGPR) and whose padding taps carry an
+// out-of-range voffset (the hardware returns 0), so a gathered element costs
+// no VALU work — f32 MFMA shares the VALU's issue rate on gfx950, so address
+// arithmetic comes straight out of matrix throughput.
+//
+// Tiles: 64 x 64 outputs per workgroup, 32-deep K-tiles (one kernel tap each:
+// C % 64 == 0), 4 waves of 32 x 32, v_mfma_f32_32x32x2_f32; MFMA (j, t) of a
+// K-tile feeds reduction index 8j + 4h + t from lane half h, so an operand
+// held as [row][k] is read with one ds_read_b128 per four MFMAs and one held
+// as [k][row] with ds_read_b32.  Register-staged one K-tile ahead, double-
+// buffered LDS, deterministic split-K for long reductions (partials reduced
+// in split order).
+#include "conv_common.h"
+
+#include <algorithm>
+
+namespace flr {
+namespace convt {
+
+using conv::Geom;
+using conv::udiv;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 64, BN = 64, BK = 32, THREADS = 256;
+constexpr int SKR = 68;  // [k][row] image row stride (floats)
+constexpr int SRK = 36;  // [row][k] image row stride
+constexpr int TILE = 64 * SRK;
+constexpr unsigned SENT = 0x80000000u;  // out-of-range voffset: the load returns 0
+
+enum Lay { KR_VEC = 0, KR_GATHER = 1, RK_VEC = 2, RK_GATHER = 3 };
+
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t nfloats) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int bytes = __builtin_amdgcn_readfirstlane((int)(nfloats * 4));
+  void* b = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ float ld1(rsrc_t r, unsigned voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ f32x4 ld4(rsrc_t r, unsigned voff, int soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+// ---- LDS images -------------------------------------------------------------
+template <int LAY>
+__device__ __forceinline__ void stash(float* buf, const float (&v)[8], int tid) {
+  if constexpr (LAY == KR_VEC) {  // thread: 4 rows (tid % 16), k = tid / 16 + 16 i
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *reinterpret_cast<f32x4*>(buf + (tid / 16 + 16 * i) * SKR + 4 * (tid % 16)) =
+          f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+  } else if constexpr (LAY == KR_GATHER) {  // row tid % 64, k = tid / 64 + 4 i
+#pragma unroll
+    for (int i = 0; i < 8; ++i) buf[(tid / 64 + 4 * i) * SKR + tid % 64] = v[i];
+  } else if constexpr (LAY == RK_VEC) {  // row tid / 8 + 32 i, k = 4 (tid % 8) .. +3
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *reinterpret_cast<f32x4*>(buf + (tid / 8 + 32 * i) * SRK + 4 * (tid % 8)) =
+          f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+  } else {  // RK_GATHER: row tid / 32 + 8 i, k = tid % 32
+#pragma unroll
+    for (int i = 0; i < 8; ++i) buf[(tid / 32 + 8 * i) * SRK + tid % 32] = v[i];
+  }
+}
+
+// Operand values of MFMAs (j, 0..3) for this lane: k = 8j + 4h + t, row = rb.
+template <int LAY>
+__device__ __forceinline__ f32x4 frag(const float* buf, int rb, int j, int h) {
+  if constexpr (LAY == RK_VEC || LAY == RK_GATHER) {
+    return *reinterpret_cast<const f32x4*>(buf + rb * SRK + 8 * j + 4 * h);
+  } else {
+    const float* p = buf + (8 * j + 4 * h) * SKR + rb;
+    return f32x4{p[0], p[SKR], p[2 * SKR], p[3 * SKR]};
+  }
+}
+
+// ---- load plans ---------------------------------------------------------------
+// Tap of a reduction slot: W_t offset of (tap, 0, 0) = tap_index * Cin * Cout.
+__device__ __forceinline__ int tap_index(const Geom& g, int slot) { return g.tap_kh[slot] * g.KW + g.tap_kw[slot]; }
+// Tile-uniform values the compiler cannot prove uniform (the tap table is
+// indexed by a computed slot): broadcast so they live in SGPRs and the buffer
+// loads that take them as soffset need no waterfall loop.
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
+  Geom g;
+  const float* x;
+  const float* w;
+  float* y;
+  static constexpr int LA = KR_VEC, LB = KR_GATHER;
+  __host__ __device__ int M() const { return g.Cout; }
+  __host__ __device__ int N() const { return g.B * g.Ho * g.Wo; }
+  __host__ __device__ int R() const { return g.ntaps * g.Cin; }
+  struct State {
+    rsrc_t ra, rb;
+    unsigned a0;            // byte offset of (k-row tid/16, m 4*(tid%16)) at tap 0, ci 0
+    int ih0, iw0, xoff;     // this thread's output pixel (B operand)
+    bool nok;
+  };
+  __device__ State init(int k, int m0, int n0, int tid) const {
+    State s;
+    const int KK = g.KH * g.KW, HW = g.H * g.W;
+    s.ra = make_rsrc(w + (int64_t)k * KK * g.Cin * g.Cout, (int64_t)KK * g.Cin * g.Cout);
+    s.rb = make_rsrc(x + (int64_t)k * g.Cin * HW, (int64_t)(g.B - 1) * g.xbs + (int64_t)g.Cin * HW);
+    s.a0 = (unsigned)(((tid / 16) * g.Cout + m0 + 4 * (tid % 16)) * 4);
+    const int n = n0 + tid % 64;
+    s.nok = n < N();
+    const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
+    const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+    s.ih0 = (int)oh * g.stride - g.pad;
+    s.iw0 = (int)ow * g.stride - g.pad;
+    s.xoff = (int)(bb * g.xbs) + (tid / 64) * HW;
+    return s;
+  }
+  __device__ void load(const State& s, int r0, float (&a)[8], float (&b)[8]) const {
+    const int slot = uni(r0 / g.Cin), ci0 = r0 - slot * g.Cin;
+    const int kh = uni(g.tap_kh[slot]), kw = uni(g.tap_kw[slot]);
+    const int HW = g.H * g.W;
+    const int arow = ((kh * g.KW + kw) * g.Cin + ci0) * g.Cout * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 q = ld4(s.ra, s.a0, arow + i * 16 * g.Cout * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[4 * i + e] = q[e];
+    }
+    const int ih = s.ih0 + kh, iw = s.iw0 + kw;
+    const bool ok = s.nok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+    const unsigned vb = ok ? (unsigned)((s.xoff + ih * g.W + iw) * 4) : SENT;
+    const int cb = ci0 * HW * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, cb + i * 4 * HW * 4);
+  }
+  __device__ void store(int k, int m, int n, float v) const {
+    const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
+    y[bb * g.ybs + ((int64_t)k * g.Cout + m) * g.Ho * g.Wo + p] = v;
+  }
+};
+
+struct DgradT {  // dx = conv^T(dy, W_t): M = Cin, N = B*H*W, R = ntaps*Cout
+  Geom g;
+  const float* dy;
+  const float* w;
+  float* dx;
+  static constexpr int LA = RK_VEC, LB = KR_GATHER;
+  __host__ __device__ int M() const { return g.Cin; }
+  __host__ __device__ int N() const { return g.B * g.H * g.W; }
+  __host__ __device__ int R() const { return g.ntaps * g.Cout; }
+  struct State {
+    rsrc_t ra, rb;
+    unsigned a0;
+    int ih, iw, yoff;
+    bool nok;
+  };
+  __device__ State init(int k, int m0, int n0, int tid) const {
+    State s;
+    const int KK = g.KH * g.KW, HoWo = g.Ho * g.Wo;
+    s.ra = make_rsrc(w + (int64_t)k * KK * g.Cin * g.Cout, (int64_t)KK * g.Cin * g.Cout);
+    s.rb = make_rsrc(dy + (int64_t)k * g.Cout * HoWo, (int64_t)(g.B - 1) * g.ybs + (int64_t)g.Cout * HoWo);
+    s.a0 = (unsigned)(((m0 + tid / 8) * g.Cout + 4 * (tid % 8)) * 4);
+    const int n = n0 + tid % 64;
+    s.nok = n < N();
+    const uint32_t bb = udiv(n, g.d_hw), p = n - bb * g.H * g.W;
+    const uint32_t ih = udiv(p, g.d_w), iw = p - ih * g.W;
+    s.ih = (int)ih + g.pad;
+    s.iw = (int)iw + g.pad;
+    s.yoff = (int)(bb * g.ybs) + (tid / 64) * HoWo;
+    return s;
+  }
+  __device__ void load(const State& s, int r0, float (&a)[8], float (&b)[8]) const {
+    const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
+    const int kh = uni(g.tap_kh[slot]), kw = uni(g.tap_kw[slot]);
+    const int HoWo = g.Ho * g.Wo;
+    const int abase = ((kh * g.KW + kw) * g.Cin * g.Cout + co0) * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 q = ld4(s.ra, s.a0, abase + i * 32 * g.Cout * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[4 * i + e] = q[e];
+    }
+    const int nh = s.ih - kh, nw = s.iw - kw;
+    int oh, ow;
+    bool ok = s.nok && nh >= 0 && nw >= 0;
+    if (g.stride == 1) {
+      oh = nh;
+      ow = nw;
+    } else {
+      oh = nh / g.stride;
+      ow = nw / g.stride;
+      ok = ok && oh * g.stride == nh && ow * g.stride == nw;
+    }
+    ok = ok && oh < g.Ho && ow < g.Wo;
+    const unsigned vb = ok ? (unsigned)((s.yoff + oh * g.Wo + ow) * 4) : SENT;
+    const int cb = co0 * HoWo * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, cb + i * 4 * HoWo * 4);
+  }
+  __device__ void store(int k, int m, int n, float v) const {
+    const uint32_t bb = udiv(n, g.d_hw), p = n - bb * g.H * g.W;
+    dx[bb * g.xbs + ((int64_t)k * g.Cin + m) * g.H * g.W + p] = v;
+  }
+};
+
+// dW_t[tap][ci][co] = sum_q x(q; tap, ci) dy(q; co): M = ntaps*Cin (slot, ci),
+// N = Cout, R = B*Ho*Wo.  A 64-row m-tile lies inside one tap (Cin % 64 == 0).
+template <bool BVEC>
+struct WgtT {
+  Geom g;
+  const float* x;
+  const float* dy;
+  float* dw;
+  static constexpr int LA = RK_GATHER, LB = BVEC ? RK_VEC : RK_GATHER;
+  __host__ __device__ int M() const { return g.ntaps * g.Cin; }
+  __host__ __device__ int N() const { return g.Cout; }
+  __host__ __device__ int R() const { return g.B * g.Ho * g.Wo; }
+  struct State {
+    rsrc_t ra, rb;
+    int kh, kw, aoff, boff;
+  };
+  __device__ State init(int k, int m0, int n0, int tid) const {
+    State s;
+    const int HW = g.H * g.W, HoWo = g.Ho * g.Wo;
+    s.ra = make_rsrc(x + (int64_t)k * g.Cin * HW, (int64_t)(g.B - 1) * g.xbs + (int64_t)g.Cin * HW);
+    s.rb = make_rsrc(dy + (int64_t)k * g.Cout * HoWo, (int64_t)(g.B - 1) * g.ybs + (int64_t)g.Cout * HoWo);
+    const int slot = uni(m0 / g.Cin), ci0 = m0 - slot * g.Cin;
+    s.kh = uni(g.tap_kh[slot]);
+    s.kw = uni(g.tap_kw[slot]);
+    s.aoff = (ci0 + tid / 32) * HW;
+    s.boff = BVEC ? (n0 + tid / 8) * HoWo : (n0 + tid / 32) * HoWo;
+    return s;
+  }
+  __device__ void load(const State& s, int r0, float (&a)[8], float (&b)[8]) const {
+    const int tid = threadIdx.x;
+    const int HW = g.H * g.W, HoWo = g.Ho * g.Wo, R = this->R();
+    {  // A: x gathered at q = r0 + tid % 32
+      const int q = r0 + tid % 32;
+      const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
+      const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+      const int ih = (int)oh * g.stride - g.pad + s.kh, iw = (int)ow * g.stride - g.pad + s.kw;
+      const bool ok = q < R && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const unsigned va = ok ? (unsigned)(((int)(bb * g.xbs) + s.aoff + ih * g.W + iw) * 4) : SENT;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = ld1(s.ra, va, i * 8 * HW * 4);
+    }
+    if constexpr (BVEC) {  // B: dy[b][co][p .. p+3], q = r0 + 4 (tid % 8)
+      const int q = r0 + 4 * (tid % 8);
+      const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
+      const unsigned vb = q < R ? (unsigned)(((int)(bb * g.ybs) + s.boff + (int)p) * 4) : SENT;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const f32x4 v = ld4(s.rb, vb, i * 32 * HoWo * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b[4 * i + e] = v[e];
+      }
+    } else {  // B: dy gathered at q = r0 + tid % 32
+      const int q = r0 + tid % 32;
+      const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
+      const unsigned vb = q < R ? (unsigned)(((int)(bb * g.ybs) + s.boff + (int)p) * 4) : SENT;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, i * 8 * HoWo * 4);
+    }
+  }
+  __device__ void store(int k, int m, int n, float v) const {
+    const int slot = m / g.Cin, ci = m - slot * g.Cin;
+    dw[(((int64_t)k * g.KH * g.KW + tap_index(g, slot)) * g.Cin + ci) * g.Cout + n] = v;
+  }
+};
+
+// ---- the kernel ---------------------------------------------------------------
+template <class Plan>
+__global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float As[2][TILE];
+  __shared__ __attribute__((aligned(16))) float Bs[2][TILE];
+  const int k = blockIdx.z / S, split = blockIdx.z % S;
+  const int M = pl.M(), N = pl.N(), R = pl.R();
+  const int ktiles = cdiv(R, BK);
+  const int rbeg = (int)((int64_t)ktiles * split / S) * BK;
+  const int rend = std::min(R, (int)((int64_t)ktiles * (split + 1) / S) * BK);
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, l32 = lane & 31;
+
+  const auto st = pl.init(k, m0, n0, tid);
+  float ra[8], rb[8];
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  if (rbeg < rend) {
+    pl.load(st, rbeg, ra, rb);
+    stash<Plan::LA>(As[0], ra, tid);
+    stash<Plan::LB>(Bs[0], rb, tid);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int r0 = rbeg; r0 < rend; r0 += BK) {
+    const bool more = r0 + BK < rend;
+    if (more) pl.load(st, r0 + BK, ra, rb);  // in flight during the MFMAs below
+    f32x4 fa[4], fb[4];  // all of the tile's fragments first: the reads overlap the MFMA chain
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      fa[j] = frag<Plan::LA>(As[cur], 32 * wm + l32, j, h);
+      fb[j] = frag<Plan::LB>(Bs[cur], 32 * wn + l32, j, h);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the chain (the scheduler would interleave them)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[j][t], fb[j][t], acc, 0, 0, 0);
+    if (more) {
+      stash<Plan::LA>(As[cur ^ 1], ra, tid);
+      stash<Plan::LB>(Bs[cur ^ 1], rb, tid);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  // C/D map of the 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int m = m0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+    const int n = n0 + 32 * wn + l32;
+    if (m < M && n < N) {
+      if (S == 1) pl.store(k, m, n, acc[e]);
+      else part[(((int64_t)split * pl.g.Kc + k) * M + m) * N + n] = acc[e];
+    }
+  }
+}
+
+template <class Plan>
+__global__ void treduce_kernel(const Plan pl, int S, const float* __restrict__ part) {
+  const int M = pl.M(), N = pl.N(), K = pl.g.Kc;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t MN = (int64_t)M * N;
+  if (idx >= MN * K) return;
+  const int k = (int)(idx / MN);
+  const int m = (int)((idx % MN) / N), n = (int)(idx % N);
+  float v = part[idx];
+  for (int s = 1; s < S; ++s) v += part[(int64_t)s * MN * K + idx];
+  pl.store(k, m, n, v);
+}
+
+inline int choose_splits(int M, int N, int R, int K) {
+  const int tiles = cdiv(M, BM) * cdiv(N, BN) * K;
+  const int ktiles = cdiv(R, BK);
+  int S = 1;
+  while (S < 16 && tiles * S < 2048 && ktiles / (2 * S) >= 8) S *= 2;
+  return S;
+}
+
+template <class Plan>
+size_t splits_bytes(const Plan& pl) {
+  const int S = choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc);
+  return S > 1 ? (size_t)S * pl.g.Kc * pl.M() * pl.N() * sizeof(float) : 0;
+}
+
+template <class Plan>
+int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
+  const int M = pl.M(), N = pl.N(), R = pl.R(), K = pl.g.Kc;
+  if (R == 0) return FLR_OK;
+  int S = choose_splits(M, N, R, K);
+  if (S > 1 && (!ws || ws_bytes < splits_bytes(pl))) S = 1;
+  const dim3 grid((unsigned)cdiv(N, BN), (unsigned)cdiv(M, BM), (unsigned)(K * S));
+  hipLaunchKernelGGL(tgemm_kernel<Plan>, grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws));
+  int rc = launch_status(name);
+  if (rc != FLR_OK || S == 1) return rc;
+  const int64_t total = (int64_t)M * N * K;
+  hipLaunchKernelGGL(treduce_kernel<Plan>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, pl, S,
+                     static_cast<const float*>(ws));
+  return launch_status(name);
+}
+
+inline bool shape_ok(int64_t Cin, int64_t Cout) { return Cin % 64 == 0 && Cout % 64 == 0; }
+
+inline bool args_ok(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+                    int64_t stride, int64_t pad) {
+  if (!conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) || !shape_ok(Cin, Cout)) return false;
+  // byte offsets inside one client's buffer view must fit the 31-bit voffset
+  return B * K * Cin * H * W * 4 < (int64_t(1) << 31) && B * K * Cout * H * W * 4 < (int64_t(1) << 31) &&
+         KH * KW * Cin * Cout * 4 < (int64_t(1) << 31);
+}
+
+}  // namespace convt
+}  // namespace flr
+
+using namespace flr;
+
+extern "C" int flr_conv2d_tap_major_ok(int64_t Cin, int64_t Cout) { return convt::shape_ok(Cin, Cout) ? 1 : 0; }
+
+extern "C" size_t flr_conv2d_t_workspace(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
+                                         int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
+  if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return 0;
+  const conv::Geom g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  convt::FwdT f; f.g = g;
+  convt::DgradT d; d.g = g;
+  convt::WgtT<false> w; w.g = g;
+  return std::max(convt::splits_bytes(f), std::max(convt::splits_bytes(d), convt::splits_bytes(w)));
+}
+
+extern "C" int flr_conv2d_fwd_t(const float* x, const float* w_t, float* y, int64_t K, int64_t B, int64_t Cin,
+                                int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                                int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !w_t || !y) return FLR_ERR_ARG;
+  if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad))
+    return conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) ? FLR_ERR_UNSUPPORTED : FLR_ERR_ARG;
+  convt::FwdT pl;
+  pl.g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  pl.x = x; pl.w = w_t; pl.y = y;
+  return convt::launch(pl, ws, ws_bytes, as_stream(stream), "conv fwd (tap-major)");
+}
+
+extern "C" int flr_conv2d_bwd_data_t(const float* dy, const float* w_t, float* dx, int64_t K, int64_t B, int64_t Cin,
+                                     int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                                     int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+  if (!dy || !w_t || !dx) return FLR_ERR_ARG;
+  if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad))
+    return conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) ? FLR_ERR_UNSUPPORTED : FLR_ERR_ARG;
+  convt::DgradT pl;
+  pl.g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  pl.dy = dy; pl.w = w_t; pl.dx = dx;
+  return convt::launch(pl, ws, ws_bytes, as_stream(stream), "conv bwd data (tap-major)");
+}
+
+extern "C" int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* dw_t, int64_t K, int64_t B,
+                                       int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+                                       int64_t stride, int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !dy || !dw_t) return FLR_ERR_ARG;
+  if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad))
+    return conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) ? FLR_ERR_UNSUPPORTED : FLR_ERR_ARG;
+  const conv::Geom g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  hipStream_t st = as_stream(stream);
+  if (g.ntaps < KH * KW &&  // dead taps get exact-zero gradients
+      hipMemsetAsync(dw_t, 0, (size_t)K * KH * KW * Cin * Cout * sizeof(float), st) != hipSuccess)
+    return FLR_ERR_HIP;
+  if ((g.Ho * g.Wo) % 4 == 0) {
+    convt::WgtT<true> pl;
+    pl.g = g; pl.x = x; pl.dy = dy; pl.dw = dw_t;
+    return convt::launch(pl, ws, ws_bytes, st, "conv bwd weight (tap-major)");
+  }
+  convt::WgtT<false> pl;
+  pl.g = g; pl.x = x; pl.dy = dy; pl.dw = dw_t;
+  return convt::launch(pl, ws, ws_bytes, st, "conv bwd weight (tap-major)");
+}

@@ -136,8 +136,35 @@ def split_params(X: torch.Tensor, spec: ModelSpec) -> Dict[str, torch.Tensor]:
 _LAYERS = os.environ.get("FLR_LAYERS", "native")
 
 
-def _gconv(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, need_dx: bool = True) -> torch.Tensor:
-    """x [B, K*Cin, H, W], w [K, Cout, Cin, kh, kw] -> [B, K*Cout, H', W']."""
+def tap_major_names(spec: ModelSpec) -> frozenset:
+    """Conv weights the engine trains in tap-major layout [K, KH, KW, Cin, Cout]
+    (flr_conv2d_*_t kernels): Cin and Cout multiples of 64
+    (flr_conv2d_tap_major_ok)."""
+    return frozenset(n for n, s in param_layout(spec)
+                     if len(s) == 4 and s[0] % 64 == 0 and s[1] % 64 == 0)
+
+
+def to_tap_major(w: torch.Tensor) -> torch.Tensor:
+    """[..., Cout, Cin, KH, KW] -> [..., KH, KW, Cin, Cout] (a view)."""
+    d = w.dim()
+    return w.permute(*range(d - 4), d - 2, d - 1, d - 3, d - 4)
+
+
+def from_tap_major(w_t: torch.Tensor) -> torch.Tensor:
+    """[..., KH, KW, Cin, Cout] -> [..., Cout, Cin, KH, KW] (a view)."""
+    d = w_t.dim()
+    return w_t.permute(*range(d - 4), d - 1, d - 2, d - 4, d - 3)
+
+
+def _gconv(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, need_dx: bool = True,
+           tap_major: bool = False) -> torch.Tensor:
+    """x [B, K*Cin, H, W], w [K, Cout, Cin, kh, kw] (or [K, kh, kw, Cin, Cout]
+    when tap_major) -> [B, K*Cout, H', W']."""
+    if tap_major:
+        if not x.is_cuda:
+            raise RuntimeError("tap-major conv weights need the HIP kernels (no CPU path)")
+        from ..nn import client_conv2d_t
+        return client_conv2d_t(x, w, stride, pad, need_dx)
     if _LAYERS == "native" and x.is_cuda:
         from ..nn import client_conv2d
         return client_conv2d(x, w, stride, pad, need_dx)
@@ -183,15 +210,19 @@ def _bn_act(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, residual: Optiona
 
 
 def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: torch.Tensor, spec: ModelSpec,
-                    dropout_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    dropout_mask: Optional[torch.Tensor] = None, tap_major: frozenset = frozenset()) -> torch.Tensor:
     """images [K, B, C, H, W], tokens [K, B, T] -> logits [K, B, num_classes].
 
     dropout_mask: optional [K, B, fusion] tensor of {0, 1/(1-p)} (explicit masks
     make the step reproducible); None applies no dropout.
+    tap_major: names of conv weights given as [K, KH, KW, Cin, Cout].
     """
+    def conv(name, x, stride, pad, need_dx=True):
+        return _gconv(x, p[name], stride, pad, need_dx, name in tap_major)
+
     K, B = images.shape[:2]
     x = images.transpose(0, 1).reshape(B, K * spec.in_channels, *images.shape[3:])
-    x = _bn_act(_gconv(x, p["conv1.weight"], 2, 3, need_dx=False), p["bn1.weight"], p["bn1.bias"])
+    x = _bn_act(conv("conv1.weight", x, 2, 3, need_dx=False), p["bn1.weight"], p["bn1.bias"])
     x = F.max_pool2d(x, 3, 2, 1)
     w = spec.widths
     for li, nblk in enumerate(spec.blocks):
@@ -200,10 +231,10 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
             stride = 2 if (bi == 0 and li > 0) else 1
             idt = x
             if (pre + "downsample.0.weight") in p:
-                idt = _bn_act(_gconv(x, p[pre + "downsample.0.weight"], stride, 0), p[pre + "downsample.1.weight"],
+                idt = _bn_act(conv(pre + "downsample.0.weight", x, stride, 0), p[pre + "downsample.1.weight"],
                               p[pre + "downsample.1.bias"], relu=False)
-            y = _bn_act(_gconv(x, p[pre + "conv1.weight"], stride, 1), p[pre + "bn1.weight"], p[pre + "bn1.bias"])
-            x = _bn_act(_gconv(y, p[pre + "conv2.weight"], 1, 1), p[pre + "bn2.weight"], p[pre + "bn2.bias"],
+            y = _bn_act(conv(pre + "conv1.weight", x, stride, 1), p[pre + "bn1.weight"], p[pre + "bn1.bias"])
+            x = _bn_act(conv(pre + "conv2.weight", y, 1, 1), p[pre + "bn2.weight"], p[pre + "bn2.bias"],
                         residual=idt)
     img = x.mean(dim=(2, 3)).view(B, K, w[-1]).transpose(0, 1)  # [K, B, 512]
 

@@ -59,6 +59,64 @@ class ClientConv2d(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+class ClientConv2dT(torch.autograd.Function):
+    """ClientConv2d with tap-major weights w_t [K, KH, KW, Cin, Cout]
+    (flr_conv2d_fwd_t / _bwd_data_t / _bwd_weight_t; Cin, Cout multiples of 64)."""
+
+    @staticmethod
+    def forward(ctx, x, w_t, stride: int, pad: int, need_dx: bool = True):
+        x = x.contiguous()
+        w_t = w_t.contiguous()
+        K, KH, KW, Cin, Cout = w_t.shape
+        B, KC, H, W = x.shape
+        assert KC == K * Cin, (x.shape, w_t.shape)
+        Ho = (H + 2 * pad - KH) // stride + 1
+        Wo = (W + 2 * pad - KW) // stride + 1
+        y = torch.empty(B, K * Cout, Ho, Wo, dtype=x.dtype, device=x.device)
+        geom = (K, B, Cin, H, W, Cout, KH, KW, stride, pad)
+        ws, n = _workspace_t(geom, x.device)
+        _capi.call("flr_conv2d_fwd_t", x.data_ptr(), w_t.data_ptr(), y.data_ptr(), *geom,
+                   None if ws is None else ws.data_ptr(), n, _stream(x))
+        ctx.save_for_backward(x, w_t)
+        ctx.geom = geom
+        ctx.need_dx = need_dx
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w_t = ctx.saved_tensors
+        dy = dy.contiguous()
+        g = ctx.geom
+        ws, n = _workspace_t(g, dy.device)
+        wsp = None if ws is None else ws.data_ptr()
+        dx = None
+        if ctx.need_dx and ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _capi.call("flr_conv2d_bwd_data_t", dy.data_ptr(), w_t.data_ptr(), dx.data_ptr(), *g, wsp, n,
+                       _stream(dy))
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w_t)
+            _capi.call("flr_conv2d_bwd_weight_t", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *g, wsp, n,
+                       _stream(dy))
+        return dx, dw, None, None, None
+
+
+def _workspace_t(geom, device):
+    n = int(_capi.lib().flr_conv2d_t_workspace(*geom))
+    if n == 0:
+        return None, 0
+    return torch.empty(n, dtype=torch.uint8, device=device), n
+
+
+def tap_major_ok(cin: int, cout: int) -> bool:
+    return bool(_capi.lib().flr_conv2d_tap_major_ok(int(cin), int(cout)))
+
+
+def client_conv2d_t(x: torch.Tensor, w_t: torch.Tensor, stride: int, pad: int, need_dx: bool = True) -> torch.Tensor:
+    return ClientConv2dT.apply(x, w_t, stride, pad, need_dx)
+
+
 def client_conv2d(x, w, stride: int, pad: int, need_dx: bool = True):
     return ClientConv2d.apply(x, w, stride, pad, need_dx)
 

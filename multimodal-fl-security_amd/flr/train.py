@@ -28,7 +28,8 @@ import torch
 
 from . import _capi
 from .matrix import ClientMatrix
-from .models.multimodal import ModelSpec, batched_forward, param_layout
+from .models import multimodal as _mm
+from .models.multimodal import ModelSpec, batched_forward, param_layout, tap_major_names, to_tap_major
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -91,6 +92,12 @@ class ClientBatchTrainer:
         layout = param_layout(spec)
         self.names = [n for n, _ in layout]
         self.shapes = [s for _, s in layout]
+        # conv weights kept tap-major [K, KH, KW, Cin, Cout] during the round
+        # (flr_conv2d_*_t); converted at load_global / export only
+        native = self.device.type == "cuda" and _mm._LAYERS == "native"
+        self.tap_major = tap_major_names(spec) if native else frozenset()
+        self.train_shapes = [torch.Size((s[2], s[3], s[1], s[0])) if n in self.tap_major else s
+                             for n, s in zip(self.names, self.shapes)]
         self.X = matrix if matrix is not None else ClientMatrix.empty(num_clients, self.shapes, self.device)
         self.K = self.X.K
         self.P = self.X.P
@@ -103,8 +110,10 @@ class ClientBatchTrainer:
             tot += (self.K * n + 63) // 64 * 64
         self._wbuf = torch.zeros(tot, dtype=torch.float32, device=self.device)
         self._mbuf = torch.zeros(tot, dtype=torch.float32, device=self.device)
-        self.W = [self._wbuf[o:o + self.K * n].view(self.K, *s) for o, n, s in zip(self._boffs, self.numels, self.shapes)]
-        self.Mb = [self._mbuf[o:o + self.K * n].view(self.K, *s) for o, n, s in zip(self._boffs, self.numels, self.shapes)]
+        self.W = [self._wbuf[o:o + self.K * n].view(self.K, *s)
+                  for o, n, s in zip(self._boffs, self.numels, self.train_shapes)]
+        self.Mb = [self._mbuf[o:o + self.K * n].view(self.K, *s)
+                   for o, n, s in zip(self._boffs, self.numels, self.train_shapes)]
         nbytes = int(_capi.lib().flr_clip_sgd_workspace(self.K))
         self._ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
         self._ws_off = (-self._ws.data_ptr()) % 256
@@ -118,20 +127,27 @@ class ClientBatchTrainer:
     def load_global(self, global_flat: torch.Tensor) -> None:
         """Every client starts from the global model (run_experiments.py:203)."""
         g = global_flat.to(self.device)
-        for w, off, n in zip(self.W, self.offsets, self.numels):
-            w.view(self.K, n).copy_(g[off:off + n].view(1, n).expand(self.K, n))
+        for name, w, off, n, shp in zip(self.names, self.W, self.offsets, self.numels, self.shapes):
+            src = g[off:off + n].view(shp)
+            if name in self.tap_major:
+                src = to_tap_major(src)
+            w.copy_(src.unsqueeze(0).expand_as(w))
 
     def export(self) -> ClientMatrix:
         """Client-major client matrix for the server (row k = client k)."""
-        for w, off, n in zip(self.W, self.offsets, self.numels):
-            self.X.data[:, off:off + n].copy_(w.view(self.K, n))
+        for name, w, off, n, shp in zip(self.names, self.W, self.offsets, self.numels, self.shapes):
+            dst = self.X.data[:, off:off + n]
+            if name in self.tap_major:
+                dst.view(self.K, *shp).copy_(_mm.from_tap_major(w))
+            else:
+                dst.copy_(w.view(self.K, n))
         return self.X
 
     # ---- one optimizer step for every client -----------------------------
     def step(self, images, tokens, labels, first: bool, dropout_mask=None) -> torch.Tensor:
         leaves = [w.detach().requires_grad_(True) for w in self.W]
         params: Dict[str, torch.Tensor] = dict(zip(self.names, leaves))
-        logits = batched_forward(params, images, tokens, self.spec, dropout_mask)
+        logits = batched_forward(params, images, tokens, self.spec, dropout_mask, self.tap_major)
         loss_k = CrossEntropy.apply(logits, labels)
         grads = [g.contiguous() for g in torch.autograd.grad(loss_k.sum(), leaves)]
         gp = (ctypes.c_void_p * len(grads))(*[g.data_ptr() for g in grads])

@@ -50,3 +50,14 @@ def test_argument_validation_without_gpu():
     assert lib.flr_krum_select(None, 5, 2, None, None, None) == _capi.FLR_ERR_ARG
     assert lib.flr_rows_mean(None, 4, 10, 10, None, 2, 2, None, None) == _capi.FLR_ERR_ARG
     assert lib.flr_trimmed_mean(None, 4, 10, 10, 2, None, None) == _capi.FLR_ERR_ARG
+
+
+def test_tap_major_rule_matches_library():
+    from flr import _capi
+    from flr.models.multimodal import ModelSpec, param_layout, tap_major_names
+    lib = _capi.lib()
+    names = tap_major_names(ModelSpec())
+    for n, s in param_layout(ModelSpec()):
+        if len(s) == 4:
+            assert (n in names) == bool(lib.flr_conv2d_tap_major_ok(s[1], s[0])), n
+    assert len(names) == 19

@@ -44,3 +44,36 @@ def test_conv_fwd_bwd_vs_fp64(cuda, shape):
         err = (got.detach().cpu().double() - ref.detach()).abs().max().item()
         scale = ref.detach().abs().max().item()
         assert err <= 2e-6 * max(scale, 1.0), (err, scale)
+
+
+TAP_SHAPES = [s for s in SHAPES if s[2] % 64 == 0 and s[5] % 64 == 0] + [
+    (2, 3, 64, 3, 5, 128, 3, 1, 1),    # ragged N tile, odd spatial
+    (3, 2, 128, 2, 2, 64, 1, 1, 0),    # 1x1 stride 1, HoWo % 4 == 0
+    (2, 5, 64, 3, 3, 64, 3, 2, 1),     # wgrad B gather (HoWo = 4 -> vec), dgrad stride 2
+    (2, 3, 64, 3, 3, 64, 3, 1, 1),     # HoWo = 9: wgrad B gather path
+]
+
+
+@pytest.mark.parametrize("shape", TAP_SHAPES, ids=[str(s) for s in TAP_SHAPES])
+def test_tap_major_conv_vs_fp64(cuda, shape):
+    from flr.models.multimodal import from_tap_major, to_tap_major
+    from flr.nn import client_conv2d_t, tap_major_ok
+    K, B, Cin, H, W, Cout, KS, stride, pad = shape
+    assert tap_major_ok(Cin, Cout)
+    g = torch.Generator(device="cpu").manual_seed(sum(shape) + 1)
+    x = torch.randn(B, K * Cin, H, W, generator=g)
+    w = torch.randn(K, Cout, Cin, KS, KS, generator=g) * 0.1
+    xg = x.to(cuda).requires_grad_(True)
+    wt = to_tap_major(w).contiguous().to(cuda).requires_grad_(True)
+    y = client_conv2d_t(xg, wt, stride, pad)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy.to(cuda))
+    xd = x.double().requires_grad_(True)
+    wd = w.double().requires_grad_(True)
+    yr = F.conv2d(xd, wd.reshape(K * Cout, Cin, KS, KS), stride=stride, padding=pad, groups=K)
+    yr.backward(dy.double())
+    dw = from_tap_major(wt.grad.detach().cpu())
+    for got, ref in ((y, yr), (xg.grad, xd.grad), (dw, wd.grad)):
+        err = (got.detach().cpu().double() - ref.detach()).abs().max().item()
+        scale = ref.detach().abs().max().item()
+        assert err <= 2e-6 * max(scale, 1.0), (err, scale)

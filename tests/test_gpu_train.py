@@ -15,13 +15,16 @@ pytestmark = pytest.mark.gpu
 SPEC = TINY
 SPEC_DROP = ModelSpec(widths=(8, 16, 16, 32), blocks=(1, 1, 1, 1), vocab=50, embed=8, hidden=16, fusion=16,
                       dropout=0.5)
+# channel counts that put every non-stem conv on the tap-major kernels
+SPEC_WIDE = ModelSpec(widths=(64, 64, 128, 128), blocks=(1, 1, 1, 1), vocab=50, embed=8, hidden=16, fusion=16,
+                      dropout=0.0)
 
 
 def _rel(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("spec", [SPEC, SPEC_DROP], ids=["p0", "dropout-masks"])
+@pytest.mark.parametrize("spec", [SPEC, SPEC_DROP, SPEC_WIDE], ids=["p0", "dropout-masks", "tap-major"])
 def test_batched_training_matches_reference_loop(cuda, spec):
     K, B, steps = 3, 8, 3
     glob = initial_global(spec, 42, cuda)
@@ -68,3 +71,24 @@ def test_full_model_single_step_runs(cuda):
     b = synthetic_batches(spec, 1, [0, 1], 4, cuda)
     loss = tr.local_update(b, make_dropout_masks(spec, 1, 2, 4, cuda, 1))
     assert torch.isfinite(loss).all()
+
+
+def test_full_model_matches_reference_loop(cuda):
+    """The C3 model itself (every ResNet-18 layer shape: tap-major convs, dead
+    taps at 1x1, split-K) for 2 clients x 2 steps vs the oracle loop."""
+    spec = ModelSpec()
+    K, B, steps = 2, 4, 2
+    glob = initial_global(spec, 42, cuda)
+    tr = ClientBatchTrainer(spec, K, cuda, TrainConfig(local_steps=steps))
+    assert len(tr.tap_major) == 19  # all convs but the 7x7 stem
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    masks = make_dropout_masks(spec, steps, K, B, cuda, seed=5)
+    tr.load_global(glob)
+    loss = tr.local_update(batches, masks).cpu()
+    for k in range(K):
+        cb = [(im[k].cpu(), tk[k].cpu(), lb[k].cpu()) for im, tk, lb in batches]
+        upd, ref_loss = otrain.local_update(MultimodalNet, spec, glob.cpu(), cb, masks=[m[k].cpu() for m in masks])
+        ref = torch.cat([u.reshape(-1) for u in upd])
+        got = tr.X.data[k, : tr.P].cpu()
+        assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+        assert _rel(got, ref) < 1e-5, _rel(got, ref)

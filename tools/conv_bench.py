@@ -1,0 +1,78 @@
+"""Per-layer timing of the client-batched conv kernels at the C3 shapes
+(K=128 clients, B=32): fwd / dgrad / wgrad, us and TFLOP/s (useful FLOPs of
+the valid taps).  usage: conv_bench.py [--only NAME] [--reps N]"""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-fl-security_amd"))
+import torch
+from flr import _capi
+from flr.nn import _workspace, _stream
+
+K, B = int(os.environ.get("K", 128)), 32
+LAYERS = [  # name, Cin, H, Cout, k, stride, pad
+    ("stem", 3, 32, 64, 7, 2, 3),
+    ("l1", 64, 8, 64, 3, 1, 1),
+    ("l2a", 64, 8, 128, 3, 2, 1),
+    ("l2b", 128, 4, 128, 3, 1, 1),
+    ("l2ds", 64, 8, 128, 1, 2, 0),
+    ("l3a", 128, 4, 256, 3, 2, 1),
+    ("l3b", 256, 2, 256, 3, 1, 1),
+    ("l3ds", 128, 4, 256, 1, 2, 0),
+    ("l4a", 256, 2, 512, 3, 2, 1),
+    ("l4b", 512, 1, 512, 3, 1, 1),
+    ("l4ds", 256, 2, 512, 1, 2, 0),
+]
+
+
+def taps(H, k, s, p):
+    Ho = (H + 2 * p - k) // s + 1
+    v = [kh for kh in range(k) if any(0 <= o * s - p + kh < H for o in range(Ho))]
+    return len(v) ** 2, Ho
+
+
+def main():
+    reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 5
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+    dev = "cuda"
+    tot = 0.0
+    for name, Cin, H, Cout, k, s, p in LAYERS:
+        if only and name != only:
+            continue
+        nt, Ho = taps(H, k, s, p)
+        x = torch.randn(B, K * Cin, H, H, device=dev)
+        w = torch.randn(K, Cout, Cin, k, k, device=dev) * 0.05
+        y = torch.empty(B, K * Cout, Ho, Ho, device=dev)
+        dy = torch.randn_like(y)
+        dx = torch.empty_like(x)
+        dw = torch.empty_like(w)
+        geom = (K, B, Cin, H, H, Cout, k, k, s, p)
+        ws, n = _workspace(geom, dev)
+        wsp = None if ws is None else ws.data_ptr()
+        st = _stream(x)
+        calls = {
+            "fwd": lambda: _capi.call("flr_conv2d_fwd", x.data_ptr(), w.data_ptr(), y.data_ptr(), *geom, wsp, n, st),
+            "dgrad": lambda: _capi.call("flr_conv2d_bwd_data", dy.data_ptr(), w.data_ptr(), dx.data_ptr(), *geom,
+                                        wsp, n, st),
+            "wgrad": lambda: _capi.call("flr_conv2d_bwd_weight", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *geom,
+                                        wsp, n, st),
+        }
+        flops = 2.0 * K * B * Ho * Ho * Cout * Cin * nt
+        for op, fn in calls.items():
+            if name == "stem" and op == "dgrad":
+                continue
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps
+            tot += us
+            print(f"{name:5s} {op:6s} {us:9.1f} us  {flops / us / 1e6:7.1f} TF/s", flush=True)
+    print(f"sum {tot / 1e3:.2f} ms (one of each per layer)")
+
+
+if __name__ == "__main__":
+    main()
