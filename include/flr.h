@@ -124,12 +124,16 @@ int flr_clip_sgd_step(float* X, const float* G, float* M, int64_t K, int64_t P,
                       float max_norm, int first_step, float* norms_out,
                       void* workspace, size_t workspace_bytes, void* stream);
 
-/* Same step on the parameter-major training layout: parameter j of all K
- * clients is one contiguous block [K][block_numel[j]]; x/g/m_blocks are host
- * arrays of nblocks device pointers (nblocks <= 96).  Client k's flattened
- * parameter e (parameters() order) is block j's element k*n_j + e - pre_j. */
+/* Same step on the parameter-major training layout: block j holds block_numel[j]
+ * elements per client at client stride block_client_stride[j] (NULL: the
+ * blocks are whole parameters, stride = numel); x/g/m_blocks are host arrays
+ * of nblocks device pointers (nblocks <= 96).  Client k's element e of block j
+ * is at ptr_j + k*stride_j + e.  Elements not covered by any block (dead
+ * kernel taps, whose gradient is identically zero) are neither read nor
+ * updated; with weight_decay == 0 that is exactly the reference's update. */
 int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* const* g_blocks,
                               float* const* m_blocks, const int64_t* block_numel,
+                              const int64_t* block_client_stride,
                               int64_t nblocks, int64_t K, float lr, float momentum,
                               float weight_decay, float max_norm, int first_step,
                               float* norms_out, void* workspace,
@@ -197,11 +201,14 @@ int flr_conv2d_bwd_data_t(const float* dy, const float* w_t, float* dx, int64_t 
                           int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
                           int64_t KH, int64_t KW, int64_t stride, int64_t pad,
                           void* workspace, size_t workspace_bytes, void* stream);
+/* zero_dead_taps: write the dead taps' slabs of dw_t as zeros (1) or leave
+ * them untouched (0: the caller never reads them, see
+ * flr_clip_sgd_step_blocked). */
 int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* dw_t, int64_t K,
                             int64_t B, int64_t Cin, int64_t H, int64_t W,
                             int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
-                            int64_t pad, void* workspace, size_t workspace_bytes,
-                            void* stream);
+                            int64_t pad, int zero_dead_taps, void* workspace,
+                            size_t workspace_bytes, void* stream);
 
 /* ---- §8(f): per-client norms and weighted row combinations ---------------
  * Building blocks of GradientClippingDefense / NormBoundingDefense /

@@ -360,6 +360,17 @@ __global__ void treduce_kernel(const Plan pl, int S, const float* __restrict__ p
   pl.store(k, m, n, v);
 }
 
+// dw_t slabs [k][t] of the taps set in `dead` = 0 (grid: 64 x K).
+__global__ void zero_taps_kernel(float* __restrict__ dw, int KK, int64_t slab, uint64_t dead) {
+  const int k = blockIdx.y;
+  for (int t = 0; t < KK; ++t) {
+    if (!((dead >> t) & 1)) continue;
+    f32x4* p = reinterpret_cast<f32x4*>(dw + ((int64_t)k * KK + t) * slab);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < slab / 4; i += (int64_t)gridDim.x * blockDim.x)
+      p[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
 inline int choose_splits(int M, int N, int R, int K) {
   const int tiles = cdiv(M, BM) * cdiv(N, BN) * K;
   const int ktiles = cdiv(R, BK);
@@ -443,15 +454,21 @@ extern "C" int flr_conv2d_bwd_data_t(const float* dy, const float* w_t, float* d
 
 extern "C" int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* dw_t, int64_t K, int64_t B,
                                        int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
-                                       int64_t stride, int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+                                       int64_t stride, int64_t pad, int zero_dead_taps, void* ws, size_t ws_bytes,
+                                       void* stream) {
   if (!x || !dy || !dw_t) return FLR_ERR_ARG;
   if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad))
     return conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) ? FLR_ERR_UNSUPPORTED : FLR_ERR_ARG;
   const conv::Geom g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
   hipStream_t st = as_stream(stream);
-  if (g.ntaps < KH * KW &&  // dead taps get exact-zero gradients
-      hipMemsetAsync(dw_t, 0, (size_t)K * KH * KW * Cin * Cout * sizeof(float), st) != hipSuccess)
-    return FLR_ERR_HIP;
+  if (zero_dead_taps && g.ntaps < KH * KW) {  // dead taps: exact-zero gradients, one slab each
+    uint64_t dead = (KH * KW >= 64) ? ~0ull : ((1ull << (KH * KW)) - 1);
+    for (int t = 0; t < g.ntaps; ++t) dead &= ~(1ull << (g.tap_kh[t] * KW + g.tap_kw[t]));
+    hipLaunchKernelGGL(convt::zero_taps_kernel, dim3(64, (unsigned)K), dim3(256), 0, st, dw_t, (int)(KH * KW),
+                       (int64_t)Cin * Cout, dead);
+    const int rc = launch_status("conv bwd weight: zero dead taps");
+    if (rc != FLR_OK) return rc;
+  }
   if ((g.Ho * g.Wo) % 4 == 0) {
     convt::WgtT<true> pl;
     pl.g = g; pl.x = x; pl.dy = dy; pl.dw = dw_t;

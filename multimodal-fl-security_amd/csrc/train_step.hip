@@ -125,13 +125,17 @@ __global__ void scale_rows_kernel(float* __restrict__ d, const float* __restrict
 // Training keeps each parameter as its own contiguous [K][n_j] block (so a
 // grouped convolution's weight view is free and autograd's gradient tensors
 // are used in place).  A client's flattened index e in [0, P) lives in block
-// j with pre[j] <= e < pre[j+1], at x[j] + k*n[j] + (e - pre[j]).
+// j with pre[j] <= e < pre[j+1], at x[j] + k*cs[j] + (e - pre[j]), where the
+// client stride cs[j] is n[j] for a whole parameter and larger for a sub-slab
+// (the live kernel taps of a tap-major conv weight; the dead taps' slabs are
+// left out of the step altogether).
 constexpr int MAXB = 96;
 struct BlockTable {
   float* x[MAXB];
   const float* g[MAXB];
   float* m[MAXB];
   int64_t pre[MAXB + 1];
+  int32_t cs[MAXB];   // client stride of block j (elements)
   uint8_t vec[MAXB];  // block j may use 16-B accesses (n % 4 == 0, all three bases 16-B aligned)
   int nb;
 };
@@ -163,8 +167,7 @@ __global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable
     const int64_t lo = p0 > tb.pre[j] ? p0 : tb.pre[j];
     const int64_t hi = p1 < tb.pre[j + 1] ? p1 : tb.pre[j + 1];
     if (lo >= hi) continue;
-    const int64_t n = tb.pre[j + 1] - tb.pre[j];
-    const float* g = tb.g[j] + (int64_t)k * n - tb.pre[j];
+    const float* g = tb.g[j] + (int64_t)k * tb.cs[j] - tb.pre[j];
     visit_range(
         lo, hi, tb.pre[j], tb.vec[j] != 0,
         [&](int64_t e) {
@@ -201,8 +204,7 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
     const int64_t lo = p0 > tb.pre[j] ? p0 : tb.pre[j];
     const int64_t hi = p1 < tb.pre[j + 1] ? p1 : tb.pre[j + 1];
     if (lo >= hi) continue;
-    const int64_t n = tb.pre[j + 1] - tb.pre[j];
-    const int64_t base = (int64_t)k * n - tb.pre[j];
+    const int64_t base = (int64_t)k * tb.cs[j] - tb.pre[j];
     float* x = tb.x[j] + base;
     const float* g = tb.g[j] + base;
     float* m = tb.m[j] + base;
@@ -298,7 +300,8 @@ extern "C" int flr_scale_client_rows(float* d, const float* gk, int64_t K, int64
 }
 
 extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* const* g_blocks, float* const* m_blocks,
-                                         const int64_t* block_numel, int64_t nblocks, int64_t K, float lr,
+                                         const int64_t* block_numel, const int64_t* block_client_stride,
+                                         int64_t nblocks, int64_t K, float lr,
                                          float momentum, float weight_decay, float max_norm, int first_step,
                                          float* norms_out, void* workspace, size_t workspace_bytes, void* stream) {
   if (K < 1 || nblocks < 1 || nblocks > train::MAXB || !x_blocks || !g_blocks || !m_blocks || !block_numel)
@@ -313,9 +316,12 @@ extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* co
     tb.g[j] = g_blocks[j];
     tb.m[j] = m_blocks[j];
     tb.pre[j + 1] = tb.pre[j] + block_numel[j];
+    const int64_t cs = block_client_stride ? block_client_stride[j] : block_numel[j];
+    if (cs < block_numel[j] || cs >= ((int64_t)1 << 31)) return FLR_ERR_ARG;
+    tb.cs[j] = (int32_t)cs;
     const uintptr_t al = reinterpret_cast<uintptr_t>(x_blocks[j]) | reinterpret_cast<uintptr_t>(g_blocks[j]) |
                          reinterpret_cast<uintptr_t>(m_blocks[j]);
-    tb.vec[j] = (block_numel[j] % 4 == 0 && (al & 15) == 0) ? 1 : 0;
+    tb.vec[j] = (block_numel[j] % 4 == 0 && cs % 4 == 0 && (al & 15) == 0) ? 1 : 0;
   }
   const int64_t P = tb.pre[tb.nb];
   if (P == 0) return FLR_OK;

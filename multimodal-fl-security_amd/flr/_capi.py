@@ -45,7 +45,8 @@ SIGNATURES = {
     "flr_clip_sgd_workspace": (_size_t, [_i64]),
     "flr_clip_sgd_step": (_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64, ctypes.c_float, ctypes.c_float,
                                  ctypes.c_float, ctypes.c_float, _int, _c_void_p, _c_void_p, _size_t, _c_void_p]),
-    "flr_clip_sgd_step_blocked": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64, ctypes.c_float,
+    "flr_clip_sgd_step_blocked": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
+                                         ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_float, _int, _c_void_p, _c_void_p,
                                          _size_t, _c_void_p]),
     "flr_conv2d_workspace": (_size_t, [_i64] * 10),
@@ -53,7 +54,8 @@ SIGNATURES = {
     "flr_conv2d_t_workspace": (_size_t, [_i64] * 10),
     "flr_conv2d_fwd_t": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_data_t": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
-    "flr_conv2d_bwd_weight_t": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
+    "flr_conv2d_bwd_weight_t": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_int, _c_void_p, _size_t,
+                                                                                         _c_void_p]),
     "flr_conv2d_fwd": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_data": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_weight": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),

@@ -144,6 +144,35 @@ def tap_major_names(spec: ModelSpec) -> frozenset:
                      if len(s) == 4 and s[0] % 64 == 0 and s[1] % 64 == 0)
 
 
+def conv_geometry(spec: ModelSpec) -> Dict[str, Tuple[int, int, int, int, int]]:
+    """name -> (H_in, kernel, stride, pad, H_out) of every conv weight (square maps)."""
+    out = {}
+    H = spec.image_size
+    Ho = (H + 6 - 7) // 2 + 1
+    out["conv1.weight"] = (H, 7, 2, 3, Ho)
+    H = (Ho + 2 - 3) // 2 + 1  # 3x3/2 max-pool
+    cin = spec.widths[0]
+    for li, (cout, nblk) in enumerate(zip(spec.widths, spec.blocks)):
+        for bi in range(nblk):
+            s = 2 if (bi == 0 and li > 0) else 1
+            pre = f"layers.{li}.{bi}."
+            H1 = (H + 2 - 3) // s + 1
+            out[pre + "conv1.weight"] = (H, 3, s, 1, H1)
+            out[pre + "conv2.weight"] = (H1, 3, 1, 1, H1)
+            if s != 1 or cin != cout:
+                out[pre + "downsample.0.weight"] = (H, 1, s, 0, (H - 1) // s + 1)
+            H, cin = H1, cout
+    return out
+
+
+def live_taps(H: int, k: int, stride: int, pad: int) -> List[int]:
+    """Tap indices kh*k + kw that read at least one non-padding pixel (square
+    map; the rule of conv_common.h make_geom)."""
+    Ho = (H + 2 * pad - k) // stride + 1
+    rows = [t for t in range(k) if any(0 <= o * stride - pad + t < H for o in range(Ho))]
+    return [kh * k + kw for kh in rows for kw in rows]
+
+
 def to_tap_major(w: torch.Tensor) -> torch.Tensor:
     """[..., Cout, Cin, KH, KW] -> [..., KH, KW, Cin, Cout] (a view)."""
     d = w.dim()
@@ -157,14 +186,14 @@ def from_tap_major(w_t: torch.Tensor) -> torch.Tensor:
 
 
 def _gconv(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, need_dx: bool = True,
-           tap_major: bool = False) -> torch.Tensor:
+           tap_major: bool = False, zero_dead: bool = True) -> torch.Tensor:
     """x [B, K*Cin, H, W], w [K, Cout, Cin, kh, kw] (or [K, kh, kw, Cin, Cout]
     when tap_major) -> [B, K*Cout, H', W']."""
     if tap_major:
         if not x.is_cuda:
             raise RuntimeError("tap-major conv weights need the HIP kernels (no CPU path)")
         from ..nn import client_conv2d_t
-        return client_conv2d_t(x, w, stride, pad, need_dx)
+        return client_conv2d_t(x, w, stride, pad, need_dx, zero_dead)
     if _LAYERS == "native" and x.is_cuda:
         from ..nn import client_conv2d
         return client_conv2d(x, w, stride, pad, need_dx)
@@ -210,15 +239,18 @@ def _bn_act(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, residual: Optiona
 
 
 def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: torch.Tensor, spec: ModelSpec,
-                    dropout_mask: Optional[torch.Tensor] = None, tap_major: frozenset = frozenset()) -> torch.Tensor:
+                    dropout_mask: Optional[torch.Tensor] = None, tap_major: frozenset = frozenset(),
+                    skip_dead: frozenset = frozenset()) -> torch.Tensor:
     """images [K, B, C, H, W], tokens [K, B, T] -> logits [K, B, num_classes].
 
     dropout_mask: optional [K, B, fusion] tensor of {0, 1/(1-p)} (explicit masks
     make the step reproducible); None applies no dropout.
     tap_major: names of conv weights given as [K, KH, KW, Cin, Cout].
+    skip_dead: tap-major weights whose dead-tap gradient slabs are left
+    unwritten (the trainer's optimizer step never reads them).
     """
     def conv(name, x, stride, pad, need_dx=True):
-        return _gconv(x, p[name], stride, pad, need_dx, name in tap_major)
+        return _gconv(x, p[name], stride, pad, need_dx, name in tap_major, name not in skip_dead)
 
     K, B = images.shape[:2]
     x = images.transpose(0, 1).reshape(B, K * spec.in_channels, *images.shape[3:])

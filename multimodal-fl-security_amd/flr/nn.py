@@ -64,9 +64,10 @@ class ClientConv2dT(torch.autograd.Function):
     (flr_conv2d_fwd_t / _bwd_data_t / _bwd_weight_t; Cin, Cout multiples of 64)."""
 
     @staticmethod
-    def forward(ctx, x, w_t, stride: int, pad: int, need_dx: bool = True):
+    def forward(ctx, x, w_t, stride: int, pad: int, need_dx: bool = True, zero_dead: bool = True):
         x = x.contiguous()
         w_t = w_t.contiguous()
+        ctx.zero_dead = zero_dead
         K, KH, KW, Cin, Cout = w_t.shape
         B, KC, H, W = x.shape
         assert KC == K * Cin, (x.shape, w_t.shape)
@@ -97,9 +98,9 @@ class ClientConv2dT(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w_t)
-            _capi.call("flr_conv2d_bwd_weight_t", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *g, wsp, n,
-                       _stream(dy))
-        return dx, dw, None, None, None
+            _capi.call("flr_conv2d_bwd_weight_t", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *g,
+                       int(ctx.zero_dead), wsp, n, _stream(dy))
+        return dx, dw, None, None, None, None
 
 
 def _workspace_t(geom, device):
@@ -113,8 +114,9 @@ def tap_major_ok(cin: int, cout: int) -> bool:
     return bool(_capi.lib().flr_conv2d_tap_major_ok(int(cin), int(cout)))
 
 
-def client_conv2d_t(x: torch.Tensor, w_t: torch.Tensor, stride: int, pad: int, need_dx: bool = True) -> torch.Tensor:
-    return ClientConv2dT.apply(x, w_t, stride, pad, need_dx)
+def client_conv2d_t(x: torch.Tensor, w_t: torch.Tensor, stride: int, pad: int, need_dx: bool = True,
+                    zero_dead: bool = True) -> torch.Tensor:
+    return ClientConv2dT.apply(x, w_t, stride, pad, need_dx, zero_dead)
 
 
 def client_conv2d(x, w, stride: int, pad: int, need_dx: bool = True):

@@ -29,7 +29,8 @@ import torch
 from . import _capi
 from .matrix import ClientMatrix
 from .models import multimodal as _mm
-from .models.multimodal import ModelSpec, batched_forward, param_layout, tap_major_names, to_tap_major
+from .models.multimodal import (ModelSpec, batched_forward, conv_geometry, live_taps, param_layout, tap_major_names,
+                                to_tap_major)
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -119,10 +120,39 @@ class ClientBatchTrainer:
         self._ws_off = (-self._ws.data_ptr()) % 256
         self._ws_bytes = nbytes
         self.norms = torch.zeros(self.K, dtype=torch.float32, device=self.device)
-        nb = len(self.W)
-        self._xp = (ctypes.c_void_p * nb)(*[w.data_ptr() for w in self.W])
-        self._mp = (ctypes.c_void_p * nb)(*[m.data_ptr() for m in self.Mb])
-        self._np = (ctypes.c_int64 * nb)(*self.numels)
+        # optimizer blocks: (param j, element offset, numel, client stride).  A
+        # tap-major conv weight with dead taps (taps that only read zero padding
+        # at this input size) contributes only its live-tap runs: with
+        # weight_decay == 0 a dead tap's gradient is exactly 0 at every step,
+        # so its weights and momentum never change and the step skips them.
+        self.skip_dead = frozenset()
+        blocks = []
+        geo = conv_geometry(spec)
+        for j, (name, n, shp) in enumerate(zip(self.names, self.numels, self.shapes)):
+            live = None
+            if name in self.tap_major and cfg.weight_decay == 0.0:
+                H, k, st, pd, _ = geo[name]
+                live = live_taps(H, k, st, pd)
+                if len(live) == k * k:
+                    live = None
+            if live is None:
+                blocks.append((j, 0, n, n))
+                continue
+            self.skip_dead = self.skip_dead | {name}
+            slab = shp[0] * shp[1]
+            runs, t0 = [], live[0]
+            for a, b in zip(live, live[1:] + [None]):
+                if b != a + 1:
+                    runs.append((t0, a + 1))
+                    t0 = b
+            for lo, hi in runs:
+                blocks.append((j, lo * slab, (hi - lo) * slab, n))
+        self.blocks = blocks
+        nb = len(blocks)
+        self._xp = (ctypes.c_void_p * nb)(*[self.W[j].data_ptr() + 4 * o for j, o, _, _ in blocks])
+        self._mp = (ctypes.c_void_p * nb)(*[self.Mb[j].data_ptr() + 4 * o for j, o, _, _ in blocks])
+        self._np = (ctypes.c_int64 * nb)(*[c for _, _, c, _ in blocks])
+        self._cs = (ctypes.c_int64 * nb)(*[cs for _, _, _, cs in blocks])
 
     def load_global(self, global_flat: torch.Tensor) -> None:
         """Every client starts from the global model (run_experiments.py:203)."""
@@ -147,13 +177,13 @@ class ClientBatchTrainer:
     def step(self, images, tokens, labels, first: bool, dropout_mask=None) -> torch.Tensor:
         leaves = [w.detach().requires_grad_(True) for w in self.W]
         params: Dict[str, torch.Tensor] = dict(zip(self.names, leaves))
-        logits = batched_forward(params, images, tokens, self.spec, dropout_mask, self.tap_major)
+        logits = batched_forward(params, images, tokens, self.spec, dropout_mask, self.tap_major, self.skip_dead)
         loss_k = CrossEntropy.apply(logits, labels)
         grads = [g.contiguous() for g in torch.autograd.grad(loss_k.sum(), leaves)]
-        gp = (ctypes.c_void_p * len(grads))(*[g.data_ptr() for g in grads])
+        gp = (ctypes.c_void_p * len(self.blocks))(*[grads[j].data_ptr() + 4 * o for j, o, _, _ in self.blocks])
         c = self.cfg
-        _capi.call("flr_clip_sgd_step_blocked", self._xp, gp, self._mp, self._np, len(grads), self.K, c.lr,
-                   c.momentum, c.weight_decay, c.clip, int(first), self.norms.data_ptr(),
+        _capi.call("flr_clip_sgd_step_blocked", self._xp, gp, self._mp, self._np, self._cs, len(self.blocks), self.K,
+                   c.lr, c.momentum, c.weight_decay, c.clip, int(first), self.norms.data_ptr(),
                    self._ws.data_ptr() + self._ws_off, self._ws_bytes, _stream(self._wbuf))
         return loss_k.detach()
 

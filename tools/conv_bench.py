@@ -6,7 +6,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "multimodal-fl-security_amd"))
 import torch
 from flr import _capi
-from flr.nn import _workspace, _stream
+from flr.nn import _workspace, _workspace_t, _stream, tap_major_ok
 
 K, B = int(os.environ.get("K", 128)), 32
 LAYERS = [  # name, Cin, H, Cout, k, stride, pad
@@ -46,15 +46,18 @@ def main():
         dx = torch.empty_like(x)
         dw = torch.empty_like(w)
         geom = (K, B, Cin, H, H, Cout, k, k, s, p)
-        ws, n = _workspace(geom, dev)
+        tm = tap_major_ok(Cin, Cout) and "--generic" not in sys.argv
+        sfx = "_t" if tm else ""
+        ws, n = (_workspace_t if tm else _workspace)(geom, dev)
         wsp = None if ws is None else ws.data_ptr()
         st = _stream(x)
         calls = {
-            "fwd": lambda: _capi.call("flr_conv2d_fwd", x.data_ptr(), w.data_ptr(), y.data_ptr(), *geom, wsp, n, st),
-            "dgrad": lambda: _capi.call("flr_conv2d_bwd_data", dy.data_ptr(), w.data_ptr(), dx.data_ptr(), *geom,
-                                        wsp, n, st),
-            "wgrad": lambda: _capi.call("flr_conv2d_bwd_weight", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *geom,
-                                        wsp, n, st),
+            "fwd": lambda: _capi.call("flr_conv2d_fwd" + sfx, x.data_ptr(), w.data_ptr(), y.data_ptr(), *geom, wsp,
+                                      n, st),
+            "dgrad": lambda: _capi.call("flr_conv2d_bwd_data" + sfx, dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
+                                        *geom, wsp, n, st),
+            "wgrad": lambda: _capi.call("flr_conv2d_bwd_weight" + sfx, x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
+                                        *geom, wsp, n, st),
         }
         flops = 2.0 * K * B * Ho * Ho * Cout * Cin * nt
         for op, fn in calls.items():
