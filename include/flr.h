@@ -210,6 +210,20 @@ int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* dw_t, int64_
                             int64_t pad, int zero_dead_taps, void* workspace,
                             size_t workspace_bytes, void* stream);
 
+/* ---- a1 / a8 / a15: round-boundary layout moves of the training state ----
+ * flr_broadcast_rows: dst[k*dst_stride + i] = src[i] (load_global: every
+ * client starts from the global model, run_experiments.py:203).
+ * flr_copy_rows: dst[k*dst_stride + i] = src[k*src_stride + i] (parameter
+ * block -> client-matrix columns, run_experiments.py:238 + krum.py:55-57).
+ * flr_tap_major_to_torch: w_t [K][KK][Cin][Cout] -> torch order
+ * [Cout][Cin][KK] at dst + k*dst_stride (KK <= 9). */
+int flr_broadcast_rows(const float* src, int64_t n, float* dst, int64_t K,
+                       int64_t dst_stride, void* stream);
+int flr_copy_rows(const float* src, int64_t src_stride, int64_t n, float* dst,
+                  int64_t dst_stride, int64_t K, void* stream);
+int flr_tap_major_to_torch(const float* w_t, int64_t K, int64_t KK, int64_t Cin,
+                           int64_t Cout, float* dst, int64_t dst_stride, void* stream);
+
 /* ---- §8(f): per-client norms and weighted row combinations ---------------
  * Building blocks of GradientClippingDefense / NormBoundingDefense /
  * DPSGDDefense (src/defenses/differential_privacy.py:74-164, 223-334) and

@@ -1,0 +1,132 @@
+// a1 / a8 / a15 — round-boundary layout moves of the training state.
+//
+// load_global (run_experiments.py:203, every client starts from the global
+// model): broadcast one parameter block to all K clients' blocks.
+// export (run_experiments.py:238-240 + krum.py:55-57, the update list
+// flattened in parameters() order): the parameter-major training blocks ->
+// rows of the client-major client matrix, and for tap-major conv weights the
+// [KH*KW][Cin][Cout] -> [Cout][Cin][KH*KW] permutation back to torch order.
+// All HBM-bound copies: 16-B accesses where alignment allows; the transpose
+// goes through a [taps][16][64] LDS tile so both sides are coalesced.
+#include "flr_common.h"
+
+namespace flr {
+namespace layout {
+
+constexpr int THREADS = 256;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// dst[k * dstride + i] = src[i], i < n, k < K  (grid: chunks x K)
+template <bool VEC>
+__global__ __launch_bounds__(THREADS) void broadcast_kernel(const float* __restrict__ src, int64_t n,
+                                                            float* __restrict__ dst, int64_t dstride) {
+  float* d = dst + (int64_t)blockIdx.y * dstride;
+  if constexpr (VEC) {
+    const int64_t nv = n / 4;
+    for (int64_t i = (int64_t)blockIdx.x * THREADS + threadIdx.x; i < nv; i += (int64_t)gridDim.x * THREADS)
+      reinterpret_cast<f32x4*>(d)[i] = reinterpret_cast<const f32x4*>(src)[i];
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) d[4 * nv + threadIdx.x] = src[4 * nv + threadIdx.x];
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * THREADS)
+      d[i] = src[i];
+  }
+}
+
+// dst[k * dstride + i] = src[k * sstride + i]
+template <bool VEC>
+__global__ __launch_bounds__(THREADS) void copy_rows_kernel(const float* __restrict__ src, int64_t sstride,
+                                                            int64_t n, float* __restrict__ dst, int64_t dstride) {
+  const float* s = src + (int64_t)blockIdx.y * sstride;
+  float* d = dst + (int64_t)blockIdx.y * dstride;
+  if constexpr (VEC) {
+    const int64_t nv = n / 4;
+    for (int64_t i = (int64_t)blockIdx.x * THREADS + threadIdx.x; i < nv; i += (int64_t)gridDim.x * THREADS)
+      reinterpret_cast<f32x4*>(d)[i] = reinterpret_cast<const f32x4*>(s)[i];
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) d[4 * nv + threadIdx.x] = s[4 * nv + threadIdx.x];
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * THREADS)
+      d[i] = s[i];
+  }
+}
+
+// Tap-major [k][t][ci][co] (KK taps) -> torch order [k][co][ci][t] at
+// dst + k * dstride.  One workgroup = (16 ci) x (64 co) x all taps of one
+// client: loads walk co (coalesced), stores walk (ci, t) for each co (a
+// contiguous run of 16 * KK floats).
+constexpr int TCI = 16, TCO = 64, MAXKK = 9;
+__global__ __launch_bounds__(THREADS) void tap_to_ref_kernel(const float* __restrict__ wt, int KK, int Cin, int Cout,
+                                                             float* __restrict__ dst, int64_t dstride) {
+  __shared__ float tile[MAXKK * TCI][TCO + 1];
+  const int k = blockIdx.z;
+  const int ci0 = blockIdx.y * TCI, co0 = blockIdx.x * TCO;
+  const float* src = wt + (int64_t)k * KK * Cin * Cout;
+  for (int e = threadIdx.x; e < KK * TCI * TCO; e += THREADS) {
+    const int co = e % TCO, r = e / TCO;  // r = t * TCI + ci
+    const int t = r / TCI, ci = r % TCI;
+    float v = 0.f;
+    if (ci0 + ci < Cin && co0 + co < Cout) v = src[((int64_t)t * Cin + ci0 + ci) * Cout + co0 + co];
+    tile[r][co] = v;
+  }
+  __syncthreads();
+  float* out = dst + (int64_t)k * dstride;
+  const int run = TCI * KK;  // (ci, t) pairs per co
+  for (int e = threadIdx.x; e < TCO * run; e += THREADS) {
+    const int co = e / run, q = e % run;  // q = ci * KK + t
+    const int ci = q / KK, t = q % KK;
+    if (ci0 + ci < Cin && co0 + co < Cout)
+      out[((int64_t)(co0 + co) * Cin + ci0 + ci) * KK + t] = tile[t * TCI + ci][co];
+  }
+}
+
+inline unsigned grid_x(int64_t work) {
+  int64_t g = (work + THREADS - 1) / THREADS;
+  return (unsigned)(g < 1 ? 1 : (g > 256 ? 256 : g));
+}
+
+inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace layout
+}  // namespace flr
+
+using namespace flr;
+
+extern "C" int flr_broadcast_rows(const float* src, int64_t n, float* dst, int64_t K, int64_t dst_stride,
+                                  void* stream) {
+  if (!src || !dst || n < 0 || K < 1 || K > 65535 || dst_stride < n) return FLR_ERR_ARG;
+  if (n == 0) return FLR_OK;
+  const bool vec = layout::al16(src) && layout::al16(dst) && dst_stride % 4 == 0;
+  const dim3 grid(layout::grid_x(vec ? n / 4 : n), (unsigned)K);
+  if (vec)
+    hipLaunchKernelGGL(layout::broadcast_kernel<true>, grid, dim3(layout::THREADS), 0, as_stream(stream), src, n, dst,
+                       dst_stride);
+  else
+    hipLaunchKernelGGL(layout::broadcast_kernel<false>, grid, dim3(layout::THREADS), 0, as_stream(stream), src, n,
+                       dst, dst_stride);
+  return launch_status("broadcast_rows");
+}
+
+extern "C" int flr_copy_rows(const float* src, int64_t src_stride, int64_t n, float* dst, int64_t dst_stride,
+                             int64_t K, void* stream) {
+  if (!src || !dst || n < 0 || K < 1 || K > 65535 || src_stride < n || dst_stride < n) return FLR_ERR_ARG;
+  if (n == 0) return FLR_OK;
+  const bool vec = layout::al16(src) && layout::al16(dst) && src_stride % 4 == 0 && dst_stride % 4 == 0;
+  const dim3 grid(layout::grid_x(vec ? n / 4 : n), (unsigned)K);
+  if (vec)
+    hipLaunchKernelGGL(layout::copy_rows_kernel<true>, grid, dim3(layout::THREADS), 0, as_stream(stream), src,
+                       src_stride, n, dst, dst_stride);
+  else
+    hipLaunchKernelGGL(layout::copy_rows_kernel<false>, grid, dim3(layout::THREADS), 0, as_stream(stream), src,
+                       src_stride, n, dst, dst_stride);
+  return launch_status("copy_rows");
+}
+
+extern "C" int flr_tap_major_to_torch(const float* w_t, int64_t K, int64_t KK, int64_t Cin, int64_t Cout, float* dst,
+                                      int64_t dst_stride, void* stream) {
+  if (!w_t || !dst || K < 1 || K > 65535 || KK < 1 || KK > layout::MAXKK || Cin < 1 || Cout < 1 ||
+      dst_stride < KK * Cin * Cout)
+    return FLR_ERR_ARG;
+  const dim3 grid((unsigned)cdiv((int)Cout, layout::TCO), (unsigned)cdiv((int)Cin, layout::TCI), (unsigned)K);
+  hipLaunchKernelGGL(layout::tap_to_ref_kernel, grid, dim3(layout::THREADS), 0, as_stream(stream), w_t, (int)KK,
+                     (int)Cin, (int)Cout, dst, dst_stride);
+  return launch_status("tap_major_to_torch");
+}

@@ -156,21 +156,27 @@ class ClientBatchTrainer:
 
     def load_global(self, global_flat: torch.Tensor) -> None:
         """Every client starts from the global model (run_experiments.py:203)."""
-        g = global_flat.to(self.device)
+        g = global_flat.to(self.device, torch.float32)
+        st = _stream(self._wbuf)
         for name, w, off, n, shp in zip(self.names, self.W, self.offsets, self.numels, self.shapes):
-            src = g[off:off + n].view(shp)
-            if name in self.tap_major:
-                src = to_tap_major(src)
-            w.copy_(src.unsqueeze(0).expand_as(w))
+            src = g[off:off + n]
+            if name in self.tap_major:  # one client's worth, permuted once
+                src = to_tap_major(src.view(shp)).contiguous()
+            else:
+                src = src.contiguous()
+            _capi.call("flr_broadcast_rows", src.data_ptr(), n, w.data_ptr(), self.K, n, st)
 
     def export(self) -> ClientMatrix:
         """Client-major client matrix for the server (row k = client k)."""
+        st = _stream(self._wbuf)
+        ld = self.X.data.stride(0)
+        base = self.X.data.data_ptr()
         for name, w, off, n, shp in zip(self.names, self.W, self.offsets, self.numels, self.shapes):
-            dst = self.X.data[:, off:off + n]
             if name in self.tap_major:
-                dst.view(self.K, *shp).copy_(_mm.from_tap_major(w))
+                cout, cin, kh, kw = shp
+                _capi.call("flr_tap_major_to_torch", w.data_ptr(), self.K, kh * kw, cin, cout, base + 4 * off, ld, st)
             else:
-                dst.copy_(w.view(self.K, n))
+                _capi.call("flr_copy_rows", w.data_ptr(), n, n, base + 4 * off, ld, self.K, st)
         return self.X
 
     # ---- one optimizer step for every client -----------------------------

@@ -92,3 +92,26 @@ def test_full_model_matches_reference_loop(cuda):
         got = tr.X.data[k, : tr.P].cpu()
         assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
         assert _rel(got, ref) < 1e-5, _rel(got, ref)
+
+
+def test_layout_kernels(cuda):
+    """flr_broadcast_rows / flr_copy_rows / flr_tap_major_to_torch on odd sizes
+    and unaligned bases (scalar paths) as well as aligned ones."""
+    from flr import _capi
+    from flr.models.multimodal import to_tap_major
+    st = torch.cuda.current_stream().cuda_stream
+    for n, off in [(7, 0), (1000, 0), (1001, 1), (64, 3)]:
+        src = torch.randn(n + off, device=cuda)[off:]
+        dst = torch.full((5, n + 9), -1.0, device=cuda)
+        _capi.call("flr_broadcast_rows", src.data_ptr(), n, dst.data_ptr() + 4 * off, 5, n + 9, st)
+        assert torch.equal(dst[:, off:off + n], src.expand(5, n))
+        out = torch.zeros(5, n + 9 + off, device=cuda)
+        _capi.call("flr_copy_rows", dst.data_ptr(), n + 9, n + 9, out.data_ptr(), n + 9 + off, 5, st)
+        assert torch.equal(out[:, : n + 9], dst)
+    for K, cout, cin, k in [(3, 64, 64, 3), (2, 70, 20, 3), (2, 128, 64, 1), (1, 5, 3, 2)]:
+        w = torch.randn(K, cout, cin, k, k, device=cuda)
+        wt = to_tap_major(w).contiguous()
+        n = cout * cin * k * k
+        X = torch.zeros(K, n + 13, device=cuda)
+        _capi.call("flr_tap_major_to_torch", wt.data_ptr(), K, k * k, cin, cout, X.data_ptr() + 4 * 5, n + 13, st)
+        assert torch.equal(X[:, 5:5 + n], w.reshape(K, n))
