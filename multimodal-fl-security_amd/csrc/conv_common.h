@@ -77,4 +77,16 @@ inline bool geom_ok(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int
 }
 
 }  // namespace conv
+
+// Explicit-im2col path for convs with a short reduction (the 7x7 stem:
+// Cin*KH*KW = 147), implemented in train_conv_t.hip and used by the
+// generic-layout entry points of train_conv.hip.
+namespace convt {
+bool im2col_eligible(const conv::Geom& g);
+size_t im2col_workspace(const conv::Geom& g);
+int fwd_im2col(const conv::Geom& g, const float* x, const float* w, float* y, void* ws, size_t ws_bytes,
+               hipStream_t st);
+int wgrad_im2col(const conv::Geom& g, const float* x, const float* dy, float* dw, void* ws, size_t ws_bytes,
+                 hipStream_t st);
+}  // namespace convt
 }  // namespace flr

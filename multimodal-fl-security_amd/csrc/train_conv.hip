@@ -426,6 +426,7 @@ extern "C" size_t flr_conv2d_workspace(int64_t K, int64_t B, int64_t Cin, int64_
   size_t m = splits_workspace(f);
   m = std::max(m, splits_workspace(d));
   m = std::max(m, splits_workspace(w));
+  if (convt::im2col_eligible(g)) m = std::max(m, convt::im2col_workspace(g));
   return m;
 }
 
@@ -434,6 +435,8 @@ extern "C" int flr_conv2d_fwd(const float* x, const float* w, float* y, int64_t 
                               void* ws, size_t ws_bytes, void* stream) {
   if (!x || !w || !y || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
   const Geom g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  if (getenv_generic() == 0 && convt::im2col_eligible(g) && ws && ws_bytes >= convt::im2col_workspace(g))
+    return convt::fwd_im2col(g, x, w, y, ws, ws_bytes, as_stream(stream));
   if (Cin % BK == 0 && getenv_generic() == 0) {
     FwdF pb;
     pb.g = g; pb.x = x; pb.w = w; pb.y = y;
@@ -468,6 +471,8 @@ extern "C" int flr_conv2d_bwd_weight(const float* x, const float* dy, float* dw,
   if (g.ntaps < KH * KW &&  // dead taps get exact-zero gradients
       hipMemsetAsync(dw, 0, (size_t)K * Cout * Cin * KH * KW * sizeof(float), st) != hipSuccess)
     return FLR_ERR_HIP;
+  if (getenv_generic() == 0 && convt::im2col_eligible(g) && ws && ws_bytes >= convt::im2col_workspace(g))
+    return convt::wgrad_im2col(g, x, dy, dw, ws, ws_bytes, st);
   if (Cin % BN == 0 && getenv_generic() == 0) {
     WgtF pb;
     pb.g = g; pb.x = x; pb.dy = dy; pb.dw = dw;

@@ -286,6 +286,140 @@ struct WgtT {
   }
 };
 
+// ---- explicit im2col (short reductions: the stem) -----------------------------
+// col[k][pix][RP], pix = b*Ho*Wo + oh*Wo + ow, r = (ci*KH + kh)*KW + kw (torch
+// weight order), zero for padding taps and for r >= R (RP = R rounded up to 4).
+// The weights are used as wp[k][co][RP] (a zero-padded copy), so both GEMM
+// operands are k-contiguous rows and load as 16-B vectors.
+struct DenseFwd {  // y[co][pix] = sum_r wp[co][r] col[pix][r]: M = Cout, N = B*Ho*Wo, R = RP
+  Geom g;
+  int RP;
+  const float* col;
+  const float* wp;
+  float* y;
+  static constexpr int LA = RK_VEC, LB = RK_VEC;
+  __host__ __device__ int M() const { return g.Cout; }
+  __host__ __device__ int N() const { return g.B * g.Ho * g.Wo; }
+  __host__ __device__ int R() const { return RP; }
+  struct State {
+    rsrc_t ra, rb;
+    unsigned a0, b0;
+    bool aok[2], bok[2];
+  };
+  __device__ State init(int k, int m0, int n0, int tid) const {
+    State s;
+    s.ra = make_rsrc(wp + (int64_t)k * g.Cout * RP, (int64_t)g.Cout * RP);
+    s.rb = make_rsrc(col + (int64_t)k * N() * RP, (int64_t)N() * RP);
+    s.a0 = (unsigned)(((m0 + tid / 8) * RP + 4 * (tid % 8)) * 4);
+    s.b0 = (unsigned)(((n0 + tid / 8) * RP + 4 * (tid % 8)) * 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      s.aok[i] = m0 + tid / 8 + 32 * i < M();
+      s.bok[i] = n0 + tid / 8 + 32 * i < N();
+    }
+    return s;
+  }
+  __device__ void load(const State& s, int r0, float (&a)[8], float (&b)[8]) const {
+    const bool kok = r0 + 4 * (int)(threadIdx.x % 8) < RP;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 qa = ld4(s.ra, (kok && s.aok[i]) ? s.a0 + (unsigned)((r0 + 32 * i * RP) * 4) : SENT, 0);
+      const f32x4 qb = ld4(s.rb, (kok && s.bok[i]) ? s.b0 + (unsigned)((r0 + 32 * i * RP) * 4) : SENT, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[4 * i + e] = qa[e];
+        b[4 * i + e] = qb[e];
+      }
+    }
+  }
+  __device__ void store(int k, int m, int n, float v) const {
+    const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
+    y[bb * g.ybs + ((int64_t)k * g.Cout + m) * g.Ho * g.Wo + p] = v;
+  }
+};
+
+struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N = RP, R = B*Ho*Wo (HoWo % 4 == 0)
+  Geom g;
+  int RP;
+  const float* col;
+  const float* dy;
+  float* dwp;
+  static constexpr int LA = RK_VEC, LB = KR_VEC;
+  __host__ __device__ int M() const { return g.Cout; }
+  __host__ __device__ int N() const { return RP; }
+  __host__ __device__ int R() const { return g.B * g.Ho * g.Wo; }
+  struct State {
+    rsrc_t ra, rb;
+    int arow;
+    bool aok[2], nok;
+    unsigned b0;
+  };
+  __device__ State init(int k, int m0, int n0, int tid) const {
+    State s;
+    const int HoWo = g.Ho * g.Wo;
+    s.ra = make_rsrc(dy + (int64_t)k * g.Cout * HoWo, (int64_t)(g.B - 1) * g.ybs + (int64_t)g.Cout * HoWo);
+    s.rb = make_rsrc(col + (int64_t)k * R() * RP, (int64_t)R() * RP);
+    s.arow = (m0 + tid / 8) * HoWo;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) s.aok[i] = m0 + tid / 8 + 32 * i < M();
+    const int n = n0 + 4 * (tid % 16);
+    s.nok = n < RP;
+    s.b0 = (unsigned)(((tid / 16) * RP + n) * 4);
+    return s;
+  }
+  __device__ void load(const State& s, int r0, float (&a)[8], float (&b)[8]) const {
+    const int tid = threadIdx.x, HoWo = g.Ho * g.Wo, R = this->R();
+    const int q = r0 + 4 * (tid % 8);
+    const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
+    const unsigned va = (unsigned)(((int)(bb * g.ybs) + s.arow + (int)p) * 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 qa = ld4(s.ra, (q < R && s.aok[i]) ? va + (unsigned)(i * 32 * HoWo * 4) : SENT, 0);
+      const int pix = r0 + tid / 16 + 16 * i;
+      const f32x4 qb = ld4(s.rb, (pix < R && s.nok) ? s.b0 + (unsigned)((r0 + 16 * i) * RP * 4) : SENT, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[4 * i + e] = qa[e];
+        b[4 * i + e] = qb[e];
+      }
+    }
+  }
+  __device__ void store(int k, int m, int n, float v) const { dwp[((int64_t)k * g.Cout + m) * RP + n] = v; }
+};
+
+// col[k][pix][RP] (grid: chunks x K)
+__global__ __launch_bounds__(THREADS) void im2col_kernel(const Geom g, const float* __restrict__ x, int RP,
+                                                         float* __restrict__ col) {
+  const int k = blockIdx.y;
+  const int N = g.B * g.Ho * g.Wo, R = g.Cin * g.KH * g.KW;
+  const int64_t total = (int64_t)N * RP;
+  float* c = col + (int64_t)k * total;
+  const float* xk = x + (int64_t)k * g.Cin * g.H * g.W;
+  for (int64_t e = (int64_t)blockIdx.x * THREADS + threadIdx.x; e < total; e += (int64_t)gridDim.x * THREADS) {
+    const int pix = (int)(e / RP), r = (int)(e - (int64_t)pix * RP);
+    float v = 0.f;
+    if (r < R) {
+      const int ci = r / (g.KH * g.KW), t = r - ci * g.KH * g.KW, kh = t / g.KW, kw = t - kh * g.KW;
+      const uint32_t bb = udiv(pix, g.d_howo), p = pix - bb * g.Ho * g.Wo;
+      const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+      const int ih = (int)oh * g.stride - g.pad + kh, iw = (int)ow * g.stride - g.pad + kw;
+      if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) v = xk[bb * g.xbs + (int64_t)ci * g.H * g.W + ih * g.W + iw];
+    }
+    c[e] = v;
+  }
+}
+
+// dst[k][co][RP] <- src[k][co][R] (zero pad) or the reverse (unpad) (grid: chunks x K)
+__global__ __launch_bounds__(THREADS) void repad_kernel(const float* __restrict__ src, int sld, float* __restrict__ dst,
+                                                        int dld, int rows, int R) {
+  const int k = blockIdx.y;
+  const int64_t total = (int64_t)rows * dld;
+  for (int64_t e = (int64_t)blockIdx.x * THREADS + threadIdx.x; e < total; e += (int64_t)gridDim.x * THREADS) {
+    const int row = (int)(e / dld), r = (int)(e - (int64_t)row * dld);
+    dst[(int64_t)k * total + e] = r < R ? src[((int64_t)k * rows + row) * sld + r] : 0.f;
+  }
+}
+
 // ---- the kernel ---------------------------------------------------------------
 template <class Plan>
 __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S, float* __restrict__ part) {
@@ -402,6 +536,69 @@ int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char
 }
 
 inline bool shape_ok(int64_t Cin, int64_t Cout) { return Cin % 64 == 0 && Cout % 64 == 0; }
+
+// ---- im2col path (declared in conv_common.h) ----------------------------------
+inline int padded_r(const Geom& g) { return (g.Cin * g.KH * g.KW + 3) / 4 * 4; }
+
+bool im2col_eligible(const Geom& g) {
+  const int64_t N = (int64_t)g.B * g.Ho * g.Wo;
+  return g.Cin * g.KH * g.KW <= 512 && !shape_ok(g.Cin, g.Cout) && (g.Ho * g.Wo) % 4 == 0 &&
+         N * padded_r(g) * 4 < (int64_t(1) << 31) && (int64_t)g.Cout * padded_r(g) * 4 < (int64_t(1) << 31);
+}
+
+size_t im2col_workspace(const Geom& g) {
+  const size_t col = align_up((size_t)g.Kc * g.B * g.Ho * g.Wo * padded_r(g) * sizeof(float), 256);
+  const size_t wp = align_up((size_t)g.Kc * g.Cout * padded_r(g) * sizeof(float), 256);
+  DenseFwd f; f.g = g; f.RP = padded_r(g);
+  DenseWgt w; w.g = g; w.RP = padded_r(g);
+  return col + wp + std::max(splits_bytes(f), splits_bytes(w));
+}
+
+static int run_im2col(const Geom& g, const float* x, float* col, hipStream_t st) {
+  const int64_t total = (int64_t)g.B * g.Ho * g.Wo * padded_r(g);
+  const unsigned gx = (unsigned)std::min<int64_t>((total + THREADS - 1) / THREADS, 1024);
+  hipLaunchKernelGGL(im2col_kernel, dim3(gx, (unsigned)g.Kc), dim3(THREADS), 0, st, g, x, padded_r(g), col);
+  return launch_status("conv im2col");
+}
+
+int fwd_im2col(const Geom& g, const float* x, const float* w, float* y, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (!ws || ws_bytes < im2col_workspace(g)) return FLR_ERR_WORKSPACE;
+  const int RP = padded_r(g), R = g.Cin * g.KH * g.KW;
+  char* base = static_cast<char*>(ws);
+  float* col = reinterpret_cast<float*>(base);
+  const size_t colb = align_up((size_t)g.Kc * g.B * g.Ho * g.Wo * RP * sizeof(float), 256);
+  float* wp = reinterpret_cast<float*>(base + colb);
+  const size_t wpb = align_up((size_t)g.Kc * g.Cout * RP * sizeof(float), 256);
+  int rc = run_im2col(g, x, col, st);
+  if (rc != FLR_OK) return rc;
+  const int64_t wtot = (int64_t)g.Cout * RP;
+  hipLaunchKernelGGL(repad_kernel, dim3((unsigned)std::min<int64_t>((wtot + THREADS - 1) / THREADS, 256), (unsigned)g.Kc),
+                     dim3(THREADS), 0, st, w, R, wp, RP, g.Cout, R);
+  if ((rc = launch_status("conv pad weights")) != FLR_OK) return rc;
+  DenseFwd pl;
+  pl.g = g; pl.RP = RP; pl.col = col; pl.wp = wp; pl.y = y;
+  return launch(pl, base + colb + wpb, ws_bytes - colb - wpb, st, "conv fwd (im2col)");
+}
+
+int wgrad_im2col(const Geom& g, const float* x, const float* dy, float* dw, void* ws, size_t ws_bytes,
+                 hipStream_t st) {
+  if (!ws || ws_bytes < im2col_workspace(g)) return FLR_ERR_WORKSPACE;
+  const int RP = padded_r(g), R = g.Cin * g.KH * g.KW;
+  char* base = static_cast<char*>(ws);
+  float* col = reinterpret_cast<float*>(base);
+  const size_t colb = align_up((size_t)g.Kc * g.B * g.Ho * g.Wo * RP * sizeof(float), 256);
+  float* dwp = reinterpret_cast<float*>(base + colb);
+  const size_t wpb = align_up((size_t)g.Kc * g.Cout * RP * sizeof(float), 256);
+  int rc = run_im2col(g, x, col, st);
+  if (rc != FLR_OK) return rc;
+  DenseWgt pl;
+  pl.g = g; pl.RP = RP; pl.col = col; pl.dy = dy; pl.dwp = dwp;
+  if ((rc = launch(pl, base + colb + wpb, ws_bytes - colb - wpb, st, "conv bwd weight (im2col)")) != FLR_OK) return rc;
+  const int64_t wtot = (int64_t)g.Cout * R;
+  hipLaunchKernelGGL(repad_kernel, dim3((unsigned)std::min<int64_t>((wtot + THREADS - 1) / THREADS, 256), (unsigned)g.Kc),
+                     dim3(THREADS), 0, st, dwp, RP, dw, R, g.Cout, R);
+  return launch_status("conv unpad dw");
+}
 
 inline bool args_ok(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
                     int64_t stride, int64_t pad) {

@@ -54,27 +54,46 @@ __global__ __launch_bounds__(THREADS) void copy_rows_kernel(const float* __restr
 // client: loads walk co (coalesced), stores walk (ci, t) for each co (a
 // contiguous run of 16 * KK floats).
 constexpr int TCI = 16, TCO = 64, MAXKK = 9;
+template <bool VEC>
 __global__ __launch_bounds__(THREADS) void tap_to_ref_kernel(const float* __restrict__ wt, int KK, int Cin, int Cout,
                                                              float* __restrict__ dst, int64_t dstride) {
   __shared__ float tile[MAXKK * TCI][TCO + 1];
   const int k = blockIdx.z;
   const int ci0 = blockIdx.y * TCI, co0 = blockIdx.x * TCO;
   const float* src = wt + (int64_t)k * KK * Cin * Cout;
-  for (int e = threadIdx.x; e < KK * TCI * TCO; e += THREADS) {
-    const int co = e % TCO, r = e / TCO;  // r = t * TCI + ci
-    const int t = r / TCI, ci = r % TCI;
-    float v = 0.f;
-    if (ci0 + ci < Cin && co0 + co < Cout) v = src[((int64_t)t * Cin + ci0 + ci) * Cout + co0 + co];
-    tile[r][co] = v;
-  }
-  __syncthreads();
   float* out = dst + (int64_t)k * dstride;
   const int run = TCI * KK;  // (ci, t) pairs per co
-  for (int e = threadIdx.x; e < TCO * run; e += THREADS) {
-    const int co = e / run, q = e % run;  // q = ci * KK + t
-    const int ci = q / KK, t = q % KK;
-    if (ci0 + ci < Cin && co0 + co < Cout)
-      out[((int64_t)(co0 + co) * Cin + ci0 + ci) * KK + t] = tile[t * TCI + ci][co];
+  if constexpr (VEC) {  // full tile (Cin % 16 == 0, Cout % 64 == 0), 16-B aligned rows
+    for (int e = threadIdx.x; e < KK * TCI * (TCO / 4); e += THREADS) {
+      const int c4 = e % (TCO / 4), r = e / (TCO / 4);  // r = t * TCI + ci
+      const int t = r / TCI, ci = r % TCI;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + ((int64_t)t * Cin + ci0 + ci) * Cout + co0 + 4 * c4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tile[r][4 * c4 + q] = v[q];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < TCO * (run / 4); e += THREADS) {
+      const int co = e / (run / 4), q0 = 4 * (e % (run / 4));  // q = ci * KK + t
+      f32x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = tile[((q0 + q) % KK) * TCI + (q0 + q) / KK][co];
+      *reinterpret_cast<f32x4*>(out + ((int64_t)(co0 + co) * Cin + ci0) * KK + q0) = v;
+    }
+  } else {
+    for (int e = threadIdx.x; e < KK * TCI * TCO; e += THREADS) {
+      const int co = e % TCO, r = e / TCO;
+      const int t = r / TCI, ci = r % TCI;
+      float v = 0.f;
+      if (ci0 + ci < Cin && co0 + co < Cout) v = src[((int64_t)t * Cin + ci0 + ci) * Cout + co0 + co];
+      tile[r][co] = v;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < TCO * run; e += THREADS) {
+      const int co = e / run, q = e % run;
+      const int ci = q / KK, t = q % KK;
+      if (ci0 + ci < Cin && co0 + co < Cout)
+        out[((int64_t)(co0 + co) * Cin + ci0 + ci) * KK + t] = tile[t * TCI + ci][co];
+    }
   }
 }
 
@@ -126,7 +145,13 @@ extern "C" int flr_tap_major_to_torch(const float* w_t, int64_t K, int64_t KK, i
       dst_stride < KK * Cin * Cout)
     return FLR_ERR_ARG;
   const dim3 grid((unsigned)cdiv((int)Cout, layout::TCO), (unsigned)cdiv((int)Cin, layout::TCI), (unsigned)K);
-  hipLaunchKernelGGL(layout::tap_to_ref_kernel, grid, dim3(layout::THREADS), 0, as_stream(stream), w_t, (int)KK,
-                     (int)Cin, (int)Cout, dst, dst_stride);
+  const bool vec = Cin % layout::TCI == 0 && Cout % layout::TCO == 0 && layout::al16(w_t) && layout::al16(dst) &&
+                   dst_stride % 4 == 0 && (layout::TCI * KK) % 4 == 0;
+  if (vec)
+    hipLaunchKernelGGL(layout::tap_to_ref_kernel<true>, grid, dim3(layout::THREADS), 0, as_stream(stream), w_t,
+                       (int)KK, (int)Cin, (int)Cout, dst, dst_stride);
+  else
+    hipLaunchKernelGGL(layout::tap_to_ref_kernel<false>, grid, dim3(layout::THREADS), 0, as_stream(stream), w_t,
+                       (int)KK, (int)Cin, (int)Cout, dst, dst_stride);
   return launch_status("tap_major_to_torch");
 }
