@@ -387,25 +387,31 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
   __device__ void store(int k, int m, int n, float v) const { dwp[((int64_t)k * g.Cout + m) * RP + n] = v; }
 };
 
-// col[k][pix][RP] (grid: chunks x K)
+// col[k][pix][RP] (grid: chunks x K).  One thread per (pix, ci, kh) writes
+// the KW-long run r = (ci*KH + kh)*KW + 0..KW-1 (consecutive threads ->
+// consecutive runs: coalesced); the pixel's last thread also zeroes r >= R.
 __global__ __launch_bounds__(THREADS) void im2col_kernel(const Geom g, const float* __restrict__ x, int RP,
                                                          float* __restrict__ col) {
   const int k = blockIdx.y;
-  const int N = g.B * g.Ho * g.Wo, R = g.Cin * g.KH * g.KW;
-  const int64_t total = (int64_t)N * RP;
-  float* c = col + (int64_t)k * total;
+  const int N = g.B * g.Ho * g.Wo, CK = g.Cin * g.KH, R = CK * g.KW;
+  const int64_t total = (int64_t)N * CK;
+  float* c = col + (int64_t)k * N * RP;
   const float* xk = x + (int64_t)k * g.Cin * g.H * g.W;
   for (int64_t e = (int64_t)blockIdx.x * THREADS + threadIdx.x; e < total; e += (int64_t)gridDim.x * THREADS) {
-    const int pix = (int)(e / RP), r = (int)(e - (int64_t)pix * RP);
-    float v = 0.f;
-    if (r < R) {
-      const int ci = r / (g.KH * g.KW), t = r - ci * g.KH * g.KW, kh = t / g.KW, kw = t - kh * g.KW;
-      const uint32_t bb = udiv(pix, g.d_howo), p = pix - bb * g.Ho * g.Wo;
-      const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
-      const int ih = (int)oh * g.stride - g.pad + kh, iw = (int)ow * g.stride - g.pad + kw;
-      if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) v = xk[bb * g.xbs + (int64_t)ci * g.H * g.W + ih * g.W + iw];
+    const int pix = (int)(e / CK), j = (int)(e - (int64_t)pix * CK);
+    const int ci = j / g.KH, kh = j - ci * g.KH;
+    const uint32_t bb = udiv(pix, g.d_howo), p = pix - bb * g.Ho * g.Wo;
+    const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+    const int ih = (int)oh * g.stride - g.pad + kh, iw0 = (int)ow * g.stride - g.pad;
+    const bool hok = ih >= 0 && ih < g.H;
+    const float* src = xk + bb * g.xbs + (int64_t)ci * g.H * g.W + (int64_t)ih * g.W;
+    float* dst = c + (int64_t)pix * RP + j * g.KW;
+    for (int kw = 0; kw < g.KW; ++kw) {
+      const int iw = iw0 + kw;
+      dst[kw] = (hok && iw >= 0 && iw < g.W) ? src[iw] : 0.f;
     }
-    c[e] = v;
+    if (j == CK - 1)
+      for (int r = R; r < RP; ++r) c[(int64_t)pix * RP + r] = 0.f;
   }
 }
 
@@ -555,7 +561,7 @@ size_t im2col_workspace(const Geom& g) {
 }
 
 static int run_im2col(const Geom& g, const float* x, float* col, hipStream_t st) {
-  const int64_t total = (int64_t)g.B * g.Ho * g.Wo * padded_r(g);
+  const int64_t total = (int64_t)g.B * g.Ho * g.Wo * g.Cin * g.KH;
   const unsigned gx = (unsigned)std::min<int64_t>((total + THREADS - 1) / THREADS, 1024);
   hipLaunchKernelGGL(im2col_kernel, dim3(gx, (unsigned)g.Kc), dim3(THREADS), 0, st, g, x, padded_r(g), col);
   return launch_status("conv im2col");
