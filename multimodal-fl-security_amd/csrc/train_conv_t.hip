@@ -387,32 +387,39 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
   __device__ void store(int k, int m, int n, float v) const { dwp[((int64_t)k * g.Cout + m) * RP + n] = v; }
 };
 
-// col[k][pix][RP] (grid: chunks x K).  One thread per (pix, ci, kh) writes
-// the KW-long run r = (ci*KH + kh)*KW + 0..KW-1 (consecutive threads ->
-// consecutive runs: coalesced); the pixel's last thread also zeroes r >= R.
+// col[k][pix][RP] (grid: pixel blocks x K).  A workgroup builds IM_PB whole
+// rows in LDS — one thread per (pix, ci, kh) fills the KW-long run
+// r = (ci*KH + kh)*KW + 0..KW-1 — then streams the IM_PB*RP contiguous floats
+// out as 16-B stores (RP % 4 == 0).
+constexpr int IM_PB = 32, IM_MAXRP = 512;
 __global__ __launch_bounds__(THREADS) void im2col_kernel(const Geom g, const float* __restrict__ x, int RP,
                                                          float* __restrict__ col) {
+  extern __shared__ __attribute__((aligned(16))) float rows[];  // [IM_PB][RP]
   const int k = blockIdx.y;
   const int N = g.B * g.Ho * g.Wo, CK = g.Cin * g.KH, R = CK * g.KW;
-  const int64_t total = (int64_t)N * CK;
-  float* c = col + (int64_t)k * N * RP;
+  const int pix0 = blockIdx.x * IM_PB;
+  const int np = min(IM_PB, N - pix0);
   const float* xk = x + (int64_t)k * g.Cin * g.H * g.W;
-  for (int64_t e = (int64_t)blockIdx.x * THREADS + threadIdx.x; e < total; e += (int64_t)gridDim.x * THREADS) {
-    const int pix = (int)(e / CK), j = (int)(e - (int64_t)pix * CK);
+  for (int e = threadIdx.x; e < np * CK; e += THREADS) {
+    const int pl = e / CK, j = e - pl * CK;
     const int ci = j / g.KH, kh = j - ci * g.KH;
+    const int pix = pix0 + pl;
     const uint32_t bb = udiv(pix, g.d_howo), p = pix - bb * g.Ho * g.Wo;
     const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
     const int ih = (int)oh * g.stride - g.pad + kh, iw0 = (int)ow * g.stride - g.pad;
     const bool hok = ih >= 0 && ih < g.H;
     const float* src = xk + bb * g.xbs + (int64_t)ci * g.H * g.W + (int64_t)ih * g.W;
-    float* dst = c + (int64_t)pix * RP + j * g.KW;
+    float* dst = rows + pl * RP + j * g.KW;
     for (int kw = 0; kw < g.KW; ++kw) {
       const int iw = iw0 + kw;
       dst[kw] = (hok && iw >= 0 && iw < g.W) ? src[iw] : 0.f;
     }
-    if (j == CK - 1)
-      for (int r = R; r < RP; ++r) c[(int64_t)pix * RP + r] = 0.f;
   }
+  for (int e = threadIdx.x; e < np * (RP - R); e += THREADS) rows[(e / (RP - R)) * RP + R + e % (RP - R)] = 0.f;
+  __syncthreads();
+  f32x4* out = reinterpret_cast<f32x4*>(col + ((int64_t)k * N + pix0) * RP);
+  const f32x4* in = reinterpret_cast<const f32x4*>(rows);
+  for (int e = threadIdx.x; e < np * RP / 4; e += THREADS) out[e] = in[e];
 }
 
 // dst[k][co][RP] <- src[k][co][R] (zero pad) or the reverse (unpad) (grid: chunks x K)
@@ -548,7 +555,7 @@ inline int padded_r(const Geom& g) { return (g.Cin * g.KH * g.KW + 3) / 4 * 4; }
 
 bool im2col_eligible(const Geom& g) {
   const int64_t N = (int64_t)g.B * g.Ho * g.Wo;
-  return g.Cin * g.KH * g.KW <= 512 && !shape_ok(g.Cin, g.Cout) && (g.Ho * g.Wo) % 4 == 0 &&
+  return padded_r(g) <= IM_MAXRP && !shape_ok(g.Cin, g.Cout) && (g.Ho * g.Wo) % 4 == 0 &&
          N * padded_r(g) * 4 < (int64_t(1) << 31) && (int64_t)g.Cout * padded_r(g) * 4 < (int64_t(1) << 31);
 }
 
@@ -561,9 +568,9 @@ size_t im2col_workspace(const Geom& g) {
 }
 
 static int run_im2col(const Geom& g, const float* x, float* col, hipStream_t st) {
-  const int64_t total = (int64_t)g.B * g.Ho * g.Wo * g.Cin * g.KH;
-  const unsigned gx = (unsigned)std::min<int64_t>((total + THREADS - 1) / THREADS, 1024);
-  hipLaunchKernelGGL(im2col_kernel, dim3(gx, (unsigned)g.Kc), dim3(THREADS), 0, st, g, x, padded_r(g), col);
+  const int N = g.B * g.Ho * g.Wo, RP = padded_r(g);
+  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)cdiv(N, IM_PB), (unsigned)g.Kc), dim3(THREADS),
+                     (size_t)IM_PB * RP * sizeof(float), st, g, x, RP, col);
   return launch_status("conv im2col");
 }
 

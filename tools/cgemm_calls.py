@@ -10,7 +10,7 @@ gz = [x for x in ("grid_size_z", "grid_z") if x in cols]
 print("columns:", cols)
 t = c.execute(f"select max(start) from kernels where {name} like '%orderstat%'").fetchone()[0]
 sel = ", ".join([name] + (gx[:1] + gy[:1] + gz[:1]) + ["end-start"])
-rows = c.execute(f"select {sel} from kernels where start > ? and {name} like '%cgemm%' order by start",
+rows = c.execute(f"select {sel} from kernels where start > ? and ({name} like '%gemm_kernel%' or {name} like '%im2col%' or {name} like '%reduce_kernel<flr::convt%' or {name} like '%repad%') order by start",
                  (t,)).fetchall()
-for r in rows[:80]:
-    print(f"{r[0][22:52]:30s} {r[1:-1]} {r[-1]/1e3:9.1f} us")
+for r in rows[:140]:
+    print(f"{r[0][:60]:60s} {r[1:-1]} {r[-1]/1e3:9.1f} us")
