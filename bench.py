@@ -5,14 +5,17 @@ Workload (BASELINE.json configs[2], "C3"): K = 128 clients, ResNet-18 image +
 1-layer GRU text late-fusion model (P = 11,800,394 fp32 parameters), 5 local
 SGD steps per client per round (batch 32, lr 0.01, momentum 0.9, clip 1.0),
 20 % sign-flip attackers (f = 25), Multi-Krum aggregation (multi_k = 64).
-One "step" = one full round: every client's local update + the all-gather
-(N > 1) + Krum (pairwise distances, scores, selection, mean) + global
-write-back.  Synthetic inputs are generated on the device before timing.
+One "step" = one full round: every client's local update + the exchange
+(N > 1: one all-to-all of client rows -> coordinate ranges, flr.shard) +
+Krum (pairwise distances, scores, selection, mean of each GPU's range) + the
+all-gather of the aggregated vector (global write-back).  Synthetic inputs
+are generated on the device before timing.
 
 N = 1: python bench.py [--steps K --warmup W]
 N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 Clients shard over ranks (K/N each), so the total work per round is fixed
 and the scaling is "strong".  Rank 0 prints one JSON line.
+--exchange allgather selects the whole-matrix all-gather instead.
 """
 from __future__ import annotations
 
@@ -90,6 +93,7 @@ def main() -> None:
     ap.add_argument("--local-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "allgather"])
     args = ap.parse_args()
 
     import torch
@@ -107,7 +111,7 @@ def main() -> None:
     P = num_params(spec)
     K = args.clients
     f = int(0.2 * K)
-    rcfg = RoundConfig(num_clients=K, defense="krum", num_attackers=f)
+    rcfg = RoundConfig(num_clients=K, defense="krum", num_attackers=f, exchange=args.exchange)
     tcfg = TrainConfig(local_steps=args.local_steps)
     eng = RoundEngine(spec, rcfg, tcfg, device, rank, world)
     multi_k = eng.defense.multi_k
@@ -125,21 +129,31 @@ def main() -> None:
 
     # ---- untimed diagnostics after the timed region ----
     reps = 5
+    sharded = eng.exchange == "alltoall"
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
-    for _ in range(reps):
-        eng.defense.aggregate_flat(eng.full, eng.num_examples, publish=False)
+    for _ in range(reps):  # Server.aggregate alone (sharded: this GPU's range + the P-vector all-gather)
+        if sharded:
+            eng.slice.gather_vector(eng.defense.aggregate_sharded(eng.slice, eng.num_examples, publish=False),
+                                    torch.empty_like(eng.global_flat))
+        else:
+            eng.defense.aggregate_flat(eng.full, eng.num_examples, publish=False)
     ev1.record()
     torch.cuda.synchronize()
     aggregate_ms = ev0.elapsed_time(ev1) / reps
-    # the dominant aggregation kernel: centred-Gram pairwise (HIP events around its launch)
+    # the dominant aggregation kernel: centred-Gram pairwise (HIP events around
+    # its launch, on the stream it runs on); sharded: this GPU's coordinates
     kms = []
     for _ in range(reps):
         ev = HipEventPair()
-        ops.pairwise_l2(eng.full.X, "gram", events=ev.handles)
+        if sharded:
+            ops.pairwise_l2_sharded(eng.slice, events=ev.handles)
+        else:
+            ops.pairwise_l2(eng.full.X, "gram", events=ev.handles)
         kms.append(ev.elapsed_ms())
     kernel_ms = sum(kms) / len(kms)
-    pair_bytes = 4.0 * K * P + 8.0 * K * K
+    n_coords = eng.slice.n if sharded else P
+    pair_bytes = 4.0 * K * n_coords + 8.0 * K * K
     achieved = pair_bytes / (kernel_ms * 1e-3) / 1e9
     # training-phase time (one round's local updates, this rank's clients)
     ev0.record()
@@ -170,7 +184,10 @@ def main() -> None:
                         "5 local SGD steps/round",
             "clients": K, "params": P, "local_steps": args.local_steps, "batch": rcfg.batch,
             "defense": f"krum(f={f}, multi_k={multi_k})", "attackers": f,
-            "parallelism": f"clients sharded {K // world}/GPU x {world}, one all-gather of the client matrix",
+            "parallelism": (f"clients sharded {K // world}/GPU x {world}; " + (
+                "one all-to-all (client rows -> coordinate ranges), per-GPU aggregation of its range, "
+                "all-gather of the aggregated vector" if sharded else "one all-gather of the client matrix")),
+            "exchange": eng.exchange,
         },
         "aggregate_ms": aggregate_ms,
         "train_ms_per_round": train_ms,
@@ -179,7 +196,7 @@ def main() -> None:
             "kernel": "gram_partials_kernel (Krum pairwise, centred Gram on MFMA)",
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel_ms": kernel_ms, "algorithmic_bytes": pair_bytes,
+            "kernel_ms": kernel_ms, "algorithmic_bytes": pair_bytes, "coords_per_gpu": n_coords,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

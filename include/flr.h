@@ -55,6 +55,41 @@ int flr_pairwise_l2_ex(const float* X, int64_t K, int64_t P, int64_t ldx,
                        double* D, void* workspace, size_t workspace_bytes,
                        void* stream, void* ev_begin, void* ev_end);
 
+/* Coordinate-sharded form of the same computation (the exchange mode where
+ * GPU g holds ALL K clients but only a contiguous range of coordinates, see
+ * DESIGN.md §2).  The full chunks (64 coordinates) of the vector are cut into
+ * FLR_PW_SLICES canonical slices; flr_pairwise_l2 itself runs on exactly these
+ * slices, so composing the phases below over any split of the slices gives
+ * D bit-identical to flr_pairwise_l2 on the whole matrix:
+ *   1. flr_pairwise_sample on every holder, then an exact SUM of the [K][S]
+ *      samples (the positions a holder does not own are written as 0);
+ *   2. flr_pairwise_pivot on the combined sample (replicated);
+ *   3. flr_pairwise_gram_slices for the holder's slices [q0, q1): X's column
+ *      0 is the first coordinate of slice q0 (chunk flr_pw_slice_chunks(q0));
+ *      gsum [q1-q0][flr_pairwise_gsum_len(K)] fp64;
+ *   4. flr_pairwise_tail on the holder of the coordinates past the last full
+ *      chunk (everyone else: p0 == p1, writes zeros), then an exact SUM;
+ *   5. gather the gsum blocks of all slices in slice order ->
+ *      [FLR_PW_SLICES][gsum_len]; flr_pairwise_finish -> D.
+ * P is always the WHOLE vector's length. */
+#define FLR_PW_SLICES 8
+int flr_pw_slice_chunks(int64_t P, int64_t q, int64_t* chunk_begin, int64_t* chunk_end);
+int64_t flr_pairwise_sample_len(int64_t P);
+size_t flr_pairwise_gsum_len(int64_t K);
+size_t flr_pairwise_sliced_workspace(int64_t K, int64_t P, int64_t nslices);
+int flr_pairwise_sample(const float* X, int64_t K, int64_t ldx, int64_t P, int64_t chunk0,
+                        int64_t chunk1, float* Xs, void* stream);
+int flr_pairwise_pivot(const float* Xs, int64_t K, int64_t P, int* pivot, void* workspace,
+                       size_t workspace_bytes, void* stream);
+int flr_pairwise_gram_slices(const float* X, int64_t K, int64_t ldx, int64_t P, int64_t q0,
+                             int64_t q1, const int* pivot, double* gsum, void* workspace,
+                             size_t workspace_bytes, void* stream, void* ev_begin,
+                             void* ev_end);
+int flr_pairwise_tail(const float* X, int64_t K, int64_t ldx, int64_t p0, int64_t p1,
+                      double* tail, void* stream);
+int flr_pairwise_finish(const double* gsum, const double* tail, int64_t K, double* D,
+                        void* stream);
+
 /* Direct-difference VALU variant (same contract, exact fp32 differences);
  * a slower second implementation used to cross-check the MFMA path. */
 size_t flr_pairwise_l2_direct_workspace(int64_t K, int64_t P);

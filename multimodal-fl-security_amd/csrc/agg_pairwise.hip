@@ -42,6 +42,9 @@ constexpr int REC_TILES = 10;   // max tiles per group
 constexpr int REC_DIAG = 6 * 32;
 constexpr int REC = REC_TILES * 1024 + REC_DIAG;   // floats per partial record
 constexpr int MAX_SEG = 512;
+// Gram workgroups per full call (all slices and groups): 2 rounds of the
+// 2-per-CU residency on 256 CUs; 1/G of them per GPU when sharded.
+constexpr int TARGET_BLOCKS = 1024;
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -154,10 +157,18 @@ __device__ __forceinline__ GroupDesc group_desc(int g, int K, bool cross) {
   return d;
 }
 
+// Canonical coordinate slices: the NCH full chunks of the whole client vector
+// are cut into FLR_PW_SLICES contiguous slices, slice q = chunks
+// [q*NCH/NS, (q+1)*NCH/NS).  Segment records are kept per slice and the
+// slices are summed in slice order, so a GPU that holds only a few slices'
+// coordinates (the coordinate-sharded exchange) computes exactly the records
+// the single-GPU call computes for them.
+__host__ __device__ inline int64_t slice_chunk(int64_t nch, int q) { return nch * q / FLR_PW_SLICES; }
+
 template <int NL, bool CROSS, int TERMS, int ABLATE = 0>
 __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
-    const float* __restrict__ X, int K, int64_t ldx, int nchunks, int group_base,
-    const int* __restrict__ pivot_ptr, float* __restrict__ partials, int nseg) {
+    const float* __restrict__ X, int K, int64_t ldx, int64_t nch_total, int q_base, int64_t chunk0,
+    int group_base, int ngroups, const int* __restrict__ pivot_ptr, float* __restrict__ partials, int nseg) {
   using TS = TileSet<NL, CROSS>;
   constexpr int NT = TS::N;
   constexpr int ROWS = 32 * NL;
@@ -172,10 +183,13 @@ __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
   const int h = lane >> 5, r = lane & 31;
   const GroupDesc gd = group_desc(g, K, CROSS);
 
-  // Round-robin chunks: at any moment the grid reads one contiguous span of
-  // nseg*256 B of every row (DRAM-page friendly), not nseg scattered 256-B runs.
-  const int c_begin = seg;
-  const int c_end = nchunks;
+  // Round-robin chunks within the slice: at any moment the slice's blocks read
+  // one contiguous span of nseg*256 B of every row (DRAM-page friendly), not
+  // nseg scattered 256-B runs.  Chunk indices are local to X (X's column 0 is
+  // global chunk chunk0).
+  const int q = q_base + (int)blockIdx.z;
+  const int c_begin = (int)(slice_chunk(nch_total, q) - chunk0) + seg;
+  const int c_end = (int)(slice_chunk(nch_total, q + 1) - chunk0);
   const int c_step = nseg;
 
   // Per-lane DMA source rows: instruction q of this wave covers LDS rows
@@ -303,7 +317,7 @@ __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
   }
 
   // ---- epilogue: reduce the 4 waves in fixed order, write the record ----
-  float* rec = partials + ((int64_t)blockIdx.y * nseg + seg) * REC;
+  float* rec = partials + (((int64_t)blockIdx.z * ngroups + g) * nseg + seg) * REC;
   float* red = lds;
   static_for<0, NT>([&](auto tc) {
     constexpr int t = decltype(tc)::value;
@@ -392,7 +406,8 @@ __device__ __forceinline__ int tile_entry(int row, int col) {
   return reg * 64 + lane;
 }
 
-__global__ void assemble_kernel(const double* __restrict__ gsum, const double* __restrict__ tail,
+// D from the per-slice group sums, adding the slices in slice order.
+__global__ void assemble_kernel(const double* __restrict__ gsum, int ngroups, const double* __restrict__ tail,
                                 int K, double* __restrict__ D) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)K * K) return;
@@ -431,10 +446,13 @@ __global__ void assemble_kernel(const double* __restrict__ gsum, const double* _
       t = lb_i * 4 + bj;
     }
   }
-  const double* rec = gsum + (int64_t)g * REC;
-  const double gij = rec[t * 1024 + tile_entry(ri, rj)];
-  const double gii = rec[REC_TILES * 1024 + 32 * lb_i + ri];
-  const double gjj = rec[REC_TILES * 1024 + 32 * lb_j + rj];
+  double gij = 0.0, gii = 0.0, gjj = 0.0;
+  for (int q = 0; q < FLR_PW_SLICES; ++q) {
+    const double* rec = gsum + ((int64_t)q * ngroups + g) * REC;
+    gij += rec[t * 1024 + tile_entry(ri, rj)];
+    gii += rec[REC_TILES * 1024 + 32 * lb_i + ri];
+    gjj += rec[REC_TILES * 1024 + 32 * lb_j + rj];
+  }
   double d2 = gii + gjj - 2.0 * gij + tail[idx];
   if (d2 < 0.0) d2 = 0.0;
   D[idx] = (double)(float)sqrt(d2);
@@ -447,12 +465,16 @@ constexpr int SAMPLE = 2048;
 constexpr int MAXK_PIVOT = 1024;
 constexpr int SAMPLE_NSEG = 8;
 
+// Xs[i][s] = X[i][s*stride - 64*chunk0] for the sample positions s*stride that
+// fall in X's global chunk range [chunk0, chunk1); 0 for the others (the
+// per-rank samples of the sharded path are then combined by an exact sum).
 __global__ void sample_gather_kernel(const float* __restrict__ X, int K, int64_t ldx, int S, int64_t stride,
-                                     float* __restrict__ Xs) {
+                                     int64_t chunk0, int64_t chunk1, float* __restrict__ Xs) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)K * S) return;
   const int i = (int)(idx / S), s = (int)(idx % S);
-  Xs[idx] = X[(int64_t)i * ldx + (int64_t)s * stride];
+  const int64_t pos = (int64_t)s * stride - chunk0 * CW;
+  Xs[idx] = (pos >= 0 && pos < (chunk1 - chunk0) * CW) ? X[(int64_t)i * ldx + pos] : 0.f;
 }
 
 // One workgroup: rowsum_i = sum_j Ds[i][j] (fp64, j order), then argmin
@@ -485,17 +507,19 @@ __global__ __launch_bounds__(256) void pivot_kernel(const double* __restrict__ D
 }
 
 struct Plan {
-  int nchunks;       // full 64-coordinate chunks
-  int nseg;          // segments per group
+  int64_t nchunks;   // full 64-coordinate chunks of the whole vector
+  int nseg;          // segments per (slice, group)
   int ngroups_diag;  // groups launched with the DIAG kernel
   int ngroups_cross; // groups launched with the CROSS kernel
   int nl_diag;       // loaded blocks per DIAG group
   int ngroups() const { return ngroups_diag + ngroups_cross; }
 };
 
+// Depends on (K, P) only — never on how the slices are spread over GPUs — so
+// every segment record is the same whichever GPU computes it.
 inline Plan make_plan(int64_t K, int64_t P) {
   Plan p;
-  p.nchunks = (int)(P / CW);
+  p.nchunks = P / CW;
   if (K <= SUPER) {
     p.ngroups_diag = 1;
     p.ngroups_cross = 0;
@@ -506,8 +530,9 @@ inline Plan make_plan(int64_t K, int64_t P) {
     p.ngroups_cross = nsb * (nsb - 1);  // two half-groups per super-block pair
     p.nl_diag = 4;
   }
-  const int target = std::max(1, 2 * 256 / std::max(1, p.ngroups()));
-  p.nseg = std::max(1, std::min(p.nchunks, std::min(MAX_SEG, target)));
+  const int64_t min_slice = p.nchunks / FLR_PW_SLICES;
+  const int target = std::max(1, TARGET_BLOCKS / (FLR_PW_SLICES * p.ngroups()));
+  p.nseg = (int)std::max<int64_t>(1, std::min<int64_t>(min_slice, std::min(MAX_SEG, target)));
   return p;
 }
 
@@ -516,18 +541,23 @@ inline int direct_npairs(int64_t K) {
   return nb * (nb + 1) / 2;
 }
 
-// Workspace carve-up (every piece 256-B aligned).
+inline int64_t sample_len(int64_t P) { return std::min<int64_t>(SAMPLE, (P / CW) * CW); }
+
+inline size_t gsum_doubles(int64_t K) { return (size_t)make_plan(K, (int64_t)CW * FLR_PW_SLICES).ngroups() * REC; }
+
+// Workspace carve-up (every piece 256-B aligned).  `nsl` = slices computed by
+// this call (FLR_PW_SLICES for the whole-vector call).
 struct Layout {
   size_t partials, stage1, gsum, tail, xs, spart, ds, pivot, total;
 };
-inline Layout layout(int64_t K, int64_t P) {
+inline Layout layout(int64_t K, int64_t P, int nsl = FLR_PW_SLICES) {
   const Plan p = make_plan(K, P);
   Layout l;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += align_up(bytes, 256); return o; };
-  l.partials = take((size_t)p.ngroups() * p.nseg * REC * sizeof(float));
-  l.stage1 = take((size_t)p.ngroups() * RSPLIT * REC * sizeof(double));
-  l.gsum = take((size_t)p.ngroups() * REC * sizeof(double));
+  l.partials = take((size_t)nsl * p.ngroups() * p.nseg * REC * sizeof(float));
+  l.stage1 = take((size_t)nsl * p.ngroups() * RSPLIT * REC * sizeof(double));
+  l.gsum = take((size_t)FLR_PW_SLICES * p.ngroups() * REC * sizeof(double));
   l.tail = take((size_t)K * K * sizeof(double));
   l.xs = take((size_t)K * SAMPLE * sizeof(float));
   l.spart = take((size_t)direct_npairs(K) * SAMPLE_NSEG * 1024 * sizeof(float));
@@ -548,37 +578,46 @@ inline int gram_ablate() {
 // bf16 terms per value: 3 (hi+mid+lo, 6 MFMA products) removes the split's
 // representation error, which dominates below ~1M coordinates; above that the
 // fp32 accumulation dominates and 2 terms (4 products) measure the same error
-// at 2/3 of the kernel time.  FLR_GRAM_TERMS=2|3 overrides.
+// at 2/3 of the kernel time.  FLR_GRAM_TERMS=2|3 overrides.  P is the WHOLE
+// vector's length (the same choice on every GPU of a sharded call).
 inline int gram_terms(int64_t P) {
   const char* e = getenv("FLR_GRAM_TERMS");
   if (e && (e[0] == '2' || e[0] == '3')) return e[0] - '0';
   return P < (int64_t(1) << 20) ? 3 : 2;
 }
 
+struct GramArgs {
+  const float* X;
+  int K;
+  int64_t ldx, P, chunk0;
+  int q0, nsl;
+  const int* pivot;
+  float* partials;
+};
+
 template <int NL, bool CROSS>
-int launch_gram(const float* X, int K, int64_t ldx, int64_t P, const Plan& p, int group_base, int ngroups,
-                const int* pivot, float* partials, hipStream_t st) {
+int launch_gram(const GramArgs& a, const Plan& p, int group_base, int ngroups, hipStream_t st) {
   const size_t lds = (size_t)2 * 32 * NL * CW * sizeof(float);
-  dim3 grid(p.nseg, ngroups);
-  if (gram_terms(P) == 3) {
-    hipLaunchKernelGGL((gram_partials_kernel<NL, CROSS, 3>), grid, dim3(THREADS), lds, st, X, K, ldx,
-                       p.nchunks, group_base, pivot, partials + (size_t)group_base * p.nseg * REC, p.nseg);
+  dim3 grid(p.nseg, ngroups, a.nsl);
+#define FLR_GRAM_LAUNCH(T, AB)                                                                              \
+  hipLaunchKernelGGL((gram_partials_kernel<NL, CROSS, T, AB>), grid, dim3(THREADS), lds, st, a.X, a.K, a.ldx, \
+                     p.nchunks, a.q0, a.chunk0, group_base, p.ngroups(), a.pivot, a.partials, p.nseg)
+  if (gram_terms(a.P) == 3) {
+    FLR_GRAM_LAUNCH(3, 0);
     return launch_status("gram_partials_kernel");
   }
   if constexpr (NL == 4 && !CROSS) {
     if (gram_ablate() == 1) {
-      hipLaunchKernelGGL((gram_partials_kernel<4, false, 2, 1>), grid, dim3(THREADS), lds, st, X, K, ldx,
-                         p.nchunks, group_base, pivot, partials + (size_t)group_base * p.nseg * REC, p.nseg);
+      FLR_GRAM_LAUNCH(2, 1);
       return launch_status("gram_partials_kernel");
     }
     if (gram_ablate() == 2) {
-      hipLaunchKernelGGL((gram_partials_kernel<4, false, 2, 2>), grid, dim3(THREADS), lds, st, X, K, ldx,
-                         p.nchunks, group_base, pivot, partials + (size_t)group_base * p.nseg * REC, p.nseg);
+      FLR_GRAM_LAUNCH(2, 2);
       return launch_status("gram_partials_kernel");
     }
   }
-  hipLaunchKernelGGL((gram_partials_kernel<NL, CROSS, 2>), grid, dim3(THREADS), lds, st, X, K, ldx,
-                     p.nchunks, group_base, pivot, partials + (size_t)group_base * p.nseg * REC, p.nseg);
+  FLR_GRAM_LAUNCH(2, 0);
+#undef FLR_GRAM_LAUNCH
   return launch_status("gram_partials_kernel");
 }
 
@@ -667,6 +706,53 @@ inline int direct_nseg(int64_t K, int64_t P) {
 using namespace flr;
 using namespace flr::pw;
 
+namespace {
+
+// Pivot = medoid of the sample Xs [K][S] (exact differences, direct kernel).
+int pivot_phase(const float* Xs, int K, int S, float* spart, double* Ds, int* pivot, hipStream_t st) {
+  int rc;
+  const int nblk = (int)(((int64_t)K * K + 255) / 256);
+  const int snseg = std::min(SAMPLE_NSEG, cdiv(S, DCW));
+  hipLaunchKernelGGL(direct_partials_kernel, dim3(snseg, direct_npairs(K)), dim3(256), 0, st, Xs, K,
+                     (int64_t)S, (int64_t)S, snseg, spart);
+  if ((rc = launch_status("direct_partials_kernel(sample)")) != FLR_OK) return rc;
+  hipLaunchKernelGGL(direct_assemble_kernel, dim3(nblk), dim3(256), 0, st, spart, K, snseg, Ds);
+  if ((rc = launch_status("direct_assemble_kernel(sample)")) != FLR_OK) return rc;
+  hipLaunchKernelGGL(pivot_kernel, dim3(1), dim3(256), 0, st, Ds, K, pivot);
+  return launch_status("pivot_kernel");
+}
+
+// Centred-Gram records of slices [q0, q0 + nsl), reduced per (slice, group)
+// in fixed order into gsum [nsl][ngroups][REC] (fp64).
+int gram_phase(const GramArgs& a, double* stage1, double* gsum, hipStream_t st, void* ev_begin, void* ev_end) {
+  const Plan p = make_plan(a.K, a.P);
+  int rc;
+  if (ev_begin && hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), st) != hipSuccess) return FLR_ERR_HIP;
+  if (a.K <= SUPER) {
+    switch (p.nl_diag) {
+      case 1: rc = launch_gram<1, false>(a, p, 0, 1, st); break;
+      case 2: rc = launch_gram<2, false>(a, p, 0, 1, st); break;
+      case 3: rc = launch_gram<3, false>(a, p, 0, 1, st); break;
+      default: rc = launch_gram<4, false>(a, p, 0, 1, st); break;
+    }
+  } else {
+    rc = launch_gram<4, false>(a, p, 0, p.ngroups_diag, st);
+    if (rc == FLR_OK) rc = launch_gram<6, true>(a, p, p.ngroups_diag, p.ngroups_cross, st);
+  }
+  if (rc != FLR_OK) return rc;
+  if (ev_end && hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), st) != hipSuccess) return FLR_ERR_HIP;
+  const int nrec = a.nsl * p.ngroups();  // (slice, group) pairs, slice-major
+  hipLaunchKernelGGL(reduce_records_kernel, dim3(cdiv(REC, 64), nrec, RSPLIT), dim3(256), 0, st, a.partials,
+                     p.nseg, stage1);
+  if ((rc = launch_status("reduce_records_kernel")) != FLR_OK) return rc;
+  hipLaunchKernelGGL(reduce_splits_kernel, dim3(cdiv(nrec * REC, 256)), dim3(256), 0, st, stage1, nrec, gsum);
+  return launch_status("reduce_splits_kernel");
+}
+
+bool aligned16(const void* p, int64_t ld) { return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (ld % 4 == 0); }
+
+}  // namespace
+
 extern "C" size_t flr_pairwise_l2_workspace(int64_t K, int64_t P) {
   if (K < 1 || P < 0) return 0;
   return layout(K, P).total;
@@ -688,66 +774,109 @@ extern "C" int flr_pairwise_l2_ex(const float* X, int64_t K, int64_t P, int64_t 
   hipStream_t st = as_stream(stream);
   const Plan p = make_plan(K, P);
   char* w = static_cast<char*>(workspace);
-  float* partials = reinterpret_cast<float*>(w + L.partials);
-  double* stage1 = reinterpret_cast<double*>(w + L.stage1);
   double* gsum = reinterpret_cast<double*>(w + L.gsum);
   double* tail = reinterpret_cast<double*>(w + L.tail);
   float* Xs = reinterpret_cast<float*>(w + L.xs);
-  float* spart = reinterpret_cast<float*>(w + L.spart);
-  double* Ds = reinterpret_cast<double*>(w + L.ds);
   int* pivot = reinterpret_cast<int*>(w + L.pivot);
 
   // The DMA path reads 16-B pieces: it needs 16-B aligned rows.
-  const bool aligned = ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && (ldx % 4 == 0);
-  const int64_t p_main = aligned ? (int64_t)p.nchunks * CW : 0;
+  const bool aligned = aligned16(X, ldx);
+  const int64_t p_main = aligned ? p.nchunks * CW : 0;
   const int K32 = (int)K;
   const int nblk = (int)((K * K + 255) / 256);
   int rc = FLR_OK;
   if (p_main > 0) {
     // 1. pivot: medoid of a strided sample of the main region (exact differences)
-    const int S = (int)std::min<int64_t>(SAMPLE, p_main);
-    const int64_t stride = p_main / S;
+    const int S = (int)sample_len(P);
     hipLaunchKernelGGL(sample_gather_kernel, dim3((unsigned)cdiv(K32 * S, 256)), dim3(256), 0, st, X, K32, ldx,
-                       S, stride, Xs);
+                       S, p_main / S, (int64_t)0, p.nchunks, Xs);
     if ((rc = launch_status("sample_gather_kernel")) != FLR_OK) return rc;
-    const int snseg = std::min(SAMPLE_NSEG, cdiv(S, DCW));
-    hipLaunchKernelGGL(direct_partials_kernel, dim3(snseg, direct_npairs(K)), dim3(256), 0, st, Xs, K32,
-                       (int64_t)S, (int64_t)S, snseg, spart);
-    if ((rc = launch_status("direct_partials_kernel(sample)")) != FLR_OK) return rc;
-    hipLaunchKernelGGL(direct_assemble_kernel, dim3(nblk), dim3(256), 0, st, spart, K32, snseg, Ds);
-    if ((rc = launch_status("direct_assemble_kernel(sample)")) != FLR_OK) return rc;
-    hipLaunchKernelGGL(pivot_kernel, dim3(1), dim3(256), 0, st, Ds, K32, pivot);
-    if ((rc = launch_status("pivot_kernel")) != FLR_OK) return rc;
-    // 2. centred Gram partials over every full chunk
-    if (ev_begin && hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), st) != hipSuccess) return FLR_ERR_HIP;
-    if (K <= SUPER) {
-      switch (p.nl_diag) {
-        case 1: rc = launch_gram<1, false>(X, K32, ldx, P, p, 0, 1, pivot, partials, st); break;
-        case 2: rc = launch_gram<2, false>(X, K32, ldx, P, p, 0, 1, pivot, partials, st); break;
-        case 3: rc = launch_gram<3, false>(X, K32, ldx, P, p, 0, 1, pivot, partials, st); break;
-        default: rc = launch_gram<4, false>(X, K32, ldx, P, p, 0, 1, pivot, partials, st); break;
-      }
-    } else {
-      rc = launch_gram<4, false>(X, K32, ldx, P, p, 0, p.ngroups_diag, pivot, partials, st);
-      if (rc == FLR_OK)
-        rc = launch_gram<6, true>(X, K32, ldx, P, p, p.ngroups_diag, p.ngroups_cross, pivot, partials, st);
-    }
+    rc = pivot_phase(Xs, K32, S, reinterpret_cast<float*>(w + L.spart), reinterpret_cast<double*>(w + L.ds), pivot,
+                     st);
     if (rc != FLR_OK) return rc;
-    if (ev_end && hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), st) != hipSuccess) return FLR_ERR_HIP;
-    // 3. fixed-order fp64 reduction of the per-segment records
-    hipLaunchKernelGGL(reduce_records_kernel, dim3(cdiv(REC, 64), p.ngroups(), RSPLIT), dim3(256), 0, st, partials,
-                       p.nseg, stage1);
-    if ((rc = launch_status("reduce_records_kernel")) != FLR_OK) return rc;
-    hipLaunchKernelGGL(reduce_splits_kernel, dim3(cdiv(p.ngroups() * REC, 256)), dim3(256), 0, st, stage1,
-                       p.ngroups(), gsum);
-    if ((rc = launch_status("reduce_splits_kernel")) != FLR_OK) return rc;
+    // 2.-3. centred Gram records of every canonical slice, fixed-order fp64 sums
+    const GramArgs a{X, K32, ldx, P, 0, 0, FLR_PW_SLICES, pivot, reinterpret_cast<float*>(w + L.partials)};
+    rc = gram_phase(a, reinterpret_cast<double*>(w + L.stage1), gsum, st, ev_begin, ev_end);
+    if (rc != FLR_OK) return rc;
   } else {
-    if (hipMemsetAsync(gsum, 0, (size_t)p.ngroups() * REC * sizeof(double), st) != hipSuccess) return FLR_ERR_HIP;
+    if (hipMemsetAsync(gsum, 0, (size_t)FLR_PW_SLICES * p.ngroups() * REC * sizeof(double), st) != hipSuccess)
+      return FLR_ERR_HIP;
   }
-  // 4. exact contribution of the trailing partial chunk, then D
+  // 4. exact contribution of the trailing partial chunk, then D (slices in order)
   hipLaunchKernelGGL(tail_d2_kernel, dim3(nblk), dim3(256), 0, st, X, K32, ldx, p_main, P, tail);
   if ((rc = launch_status("tail_d2_kernel")) != FLR_OK) return rc;
-  hipLaunchKernelGGL(assemble_kernel, dim3(nblk), dim3(256), 0, st, gsum, tail, K32, D);
+  hipLaunchKernelGGL(assemble_kernel, dim3(nblk), dim3(256), 0, st, gsum, p.ngroups(), tail, K32, D);
+  return launch_status("assemble_kernel");
+}
+
+/* ---- phases of the coordinate-sharded call ---- */
+
+extern "C" int flr_pw_slice_chunks(int64_t P, int64_t q, int64_t* chunk_begin, int64_t* chunk_end) {
+  if (P < 0 || q < 0 || q >= FLR_PW_SLICES || !chunk_begin || !chunk_end) return FLR_ERR_ARG;
+  *chunk_begin = slice_chunk(P / CW, (int)q);
+  *chunk_end = slice_chunk(P / CW, (int)q + 1);
+  return FLR_OK;
+}
+
+extern "C" int64_t flr_pairwise_sample_len(int64_t P) { return P < 0 ? 0 : sample_len(P); }
+
+extern "C" size_t flr_pairwise_gsum_len(int64_t K) { return K < 1 ? 0 : gsum_doubles(K); }
+
+extern "C" size_t flr_pairwise_sliced_workspace(int64_t K, int64_t P, int64_t nslices) {
+  if (K < 1 || P < 0 || nslices < 1 || nslices > FLR_PW_SLICES) return 0;
+  return layout(K, P, (int)nslices).total;
+}
+
+extern "C" int flr_pairwise_sample(const float* X, int64_t K, int64_t ldx, int64_t P, int64_t chunk0,
+                                   int64_t chunk1, float* Xs, void* stream) {
+  const int64_t nch = P / CW;
+  if (K < 1 || K > MAXK_PIVOT || P < CW || !Xs || chunk0 < 0 || chunk1 < chunk0 || chunk1 > nch) return FLR_ERR_ARG;
+  if (chunk1 > chunk0 && (!X || ldx < (chunk1 - chunk0) * CW)) return FLR_ERR_ARG;
+  const int S = (int)sample_len(P);
+  hipLaunchKernelGGL(sample_gather_kernel, dim3((unsigned)cdiv((int)K * S, 256)), dim3(256), 0, as_stream(stream), X,
+                     (int)K, ldx, S, nch * CW / S, chunk0, chunk1, Xs);
+  return launch_status("sample_gather_kernel");
+}
+
+extern "C" int flr_pairwise_pivot(const float* Xs, int64_t K, int64_t P, int* pivot, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  if (K < 1 || K > MAXK_PIVOT || P < CW || !Xs || !pivot) return FLR_ERR_ARG;
+  const Layout L = layout(K, P, 1);
+  if (!workspace || workspace_bytes < L.total || (reinterpret_cast<uintptr_t>(workspace) & 255))
+    return FLR_ERR_WORKSPACE;
+  char* w = static_cast<char*>(workspace);
+  return pivot_phase(Xs, (int)K, (int)sample_len(P), reinterpret_cast<float*>(w + L.spart),
+                     reinterpret_cast<double*>(w + L.ds), pivot, as_stream(stream));
+}
+
+extern "C" int flr_pairwise_gram_slices(const float* X, int64_t K, int64_t ldx, int64_t P, int64_t q0, int64_t q1,
+                                        const int* pivot, double* gsum, void* workspace, size_t workspace_bytes,
+                                        void* stream, void* ev_begin, void* ev_end) {
+  if (K < 1 || K > MAXK_PIVOT || P < 0 || q0 < 0 || q1 <= q0 || q1 > FLR_PW_SLICES || !pivot || !gsum)
+    return FLR_ERR_ARG;
+  const int64_t nch = P / CW;
+  const int64_t c0 = slice_chunk(nch, (int)q0), c1 = slice_chunk(nch, (int)q1);
+  if (c1 > c0 && (!X || ldx < (c1 - c0) * CW || !aligned16(X, ldx))) return FLR_ERR_ARG;
+  const Layout L = layout(K, P, (int)(q1 - q0));
+  if (!workspace || workspace_bytes < L.total || (reinterpret_cast<uintptr_t>(workspace) & 255))
+    return FLR_ERR_WORKSPACE;
+  char* w = static_cast<char*>(workspace);
+  const GramArgs a{X, (int)K, ldx, P, c0, (int)q0, (int)(q1 - q0), pivot, reinterpret_cast<float*>(w + L.partials)};
+  return gram_phase(a, reinterpret_cast<double*>(w + L.stage1), gsum, as_stream(stream), ev_begin, ev_end);
+}
+
+extern "C" int flr_pairwise_tail(const float* X, int64_t K, int64_t ldx, int64_t p0, int64_t p1, double* tail,
+                                 void* stream) {
+  if (K < 1 || p0 < 0 || p1 < p0 || !tail || (p1 > p0 && (!X || ldx < p1))) return FLR_ERR_ARG;
+  hipLaunchKernelGGL(tail_d2_kernel, dim3((unsigned)((K * K + 255) / 256)), dim3(256), 0, as_stream(stream), X,
+                     (int)K, ldx, p0, p1, tail);
+  return launch_status("tail_d2_kernel");
+}
+
+extern "C" int flr_pairwise_finish(const double* gsum, const double* tail, int64_t K, double* D, void* stream) {
+  if (K < 1 || K > MAXK_PIVOT || !gsum || !tail || !D) return FLR_ERR_ARG;
+  hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((K * K + 255) / 256)), dim3(256), 0, as_stream(stream), gsum,
+                     make_plan(K, (int64_t)CW * FLR_PW_SLICES).ngroups(), tail, (int)K, D);
   return launch_status("assemble_kernel");
 }
 

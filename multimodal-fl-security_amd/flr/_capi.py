@@ -35,6 +35,16 @@ SIGNATURES = {
     "flr_pairwise_l2": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "flr_pairwise_l2_ex": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p, _c_void_p,
                                   _c_void_p]),
+    "flr_pw_slice_chunks": (_int, [_i64, _i64, _c_void_p, _c_void_p]),
+    "flr_pairwise_sample_len": (_i64, [_i64]),
+    "flr_pairwise_gsum_len": (_size_t, [_i64]),
+    "flr_pairwise_sliced_workspace": (_size_t, [_i64, _i64, _i64]),
+    "flr_pairwise_sample": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p]),
+    "flr_pairwise_pivot": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "flr_pairwise_gram_slices": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p,
+                                        _size_t, _c_void_p, _c_void_p, _c_void_p]),
+    "flr_pairwise_tail": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p]),
+    "flr_pairwise_finish": (_int, [_c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p]),
     "flr_pairwise_l2_direct_workspace": (_size_t, [_i64, _i64]),
     "flr_pairwise_l2_direct": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "flr_krum_select": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),

@@ -51,6 +51,15 @@ class BaseDefense(ABC):
         flat = self.aggregate_flat(cm, num_examples)
         return cm.unflatten(flat, source_device(client_updates))
 
+    # Coordinate-sharded form (flr.shard): aggregate one GPU's coordinate
+    # range of all K clients; returns the [cs.n] slice of the aggregate.
+    # Defenses that need whole rows (norms, dots) do not implement it and run
+    # on the all-gathered matrix instead.
+    supports_sharded = False
+
+    def aggregate_sharded(self, cs, num_examples: List[int]) -> torch.Tensor:
+        raise NotImplementedError(f"{self.name} has no coordinate-sharded form")
+
     def detect_malicious(self, client_updates: Updates, num_examples: List[int]) -> List[int]:
         return []
 
@@ -69,3 +78,8 @@ class NoDefense(BaseDefense):
 
     def aggregate_flat(self, cm: ClientMatrix, num_examples: List[int]) -> torch.Tensor:
         return ops.fedavg(cm.X, list(num_examples))
+
+    supports_sharded = True
+
+    def aggregate_sharded(self, cs, num_examples: List[int]) -> torch.Tensor:
+        return ops.fedavg(cs.X, list(num_examples))

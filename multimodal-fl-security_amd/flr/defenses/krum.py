@@ -52,6 +52,24 @@ class KrumDefense(BaseDefense):
             return cm.data[int(order[0].item()), : cm.P]
         return ops.rows_mean(cm.X, order[: min(self.multi_k, cm.K)], divisor=self.multi_k)
 
+    supports_sharded = True
+
+    def aggregate_sharded(self, cs, num_examples: List[int], publish: bool = True, events=None) -> torch.Tensor:
+        """Coordinate-sharded Krum (flr.shard): distances from the per-slice
+        Gram sums of every GPU (bit-identical to the one-GPU D), scores and
+        order replicated, then the Multi-Krum mean of this GPU's range."""
+        n, f = cs.K, self.num_malicious
+        if n < 2 * f + 3:  # krum.py:153-157
+            raise ValueError(
+                f"Krum requires n >= 2f + 3. Got n={n}, f={f}. Need at least {2 * f + 3} clients.")
+        self.distances = ops.pairwise_l2_sharded(cs, events=events)
+        self.scores_device, self.order_device = ops.krum_select(self.distances, f)
+        if publish:
+            self.publish()
+        if self.multi_k == 1:
+            return cs.data[self.order_device[0].long(), : cs.n]
+        return ops.rows_mean(cs.X, self.order_device[: min(self.multi_k, n)], divisor=self.multi_k)
+
     def publish(self) -> None:
         """Host copies of scores / selected / rejected (krum.py:171-176)."""
         order_host = self.order_device.cpu().tolist()

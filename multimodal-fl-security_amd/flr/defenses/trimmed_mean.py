@@ -25,6 +25,11 @@ class TrimmedMeanDefense(BaseDefense):
             return ops.median_lower(cm.X)
         return ops.trimmed_mean(cm.X, self.num_trimmed_per_end)
 
+    supports_sharded = True
+
+    def aggregate_sharded(self, cs, num_examples: List[int]) -> torch.Tensor:
+        return self.aggregate_flat(cs, num_examples)  # coordinate-wise: the slice is a client matrix
+
     def get_metrics(self) -> Dict[str, Any]:
         return {
             "defense_type": "trimmed_mean",
@@ -44,6 +49,11 @@ class MedianDefense(BaseDefense):
 
     def aggregate_flat(self, cm: ClientMatrix, num_examples: List[int]) -> torch.Tensor:
         return ops.median_lower(cm.X)
+
+    supports_sharded = True
+
+    def aggregate_sharded(self, cs, num_examples: List[int]) -> torch.Tensor:
+        return ops.median_lower(cs.X)
 
     def get_metrics(self) -> Dict[str, Any]:
         return {"defense_type": "median"}

@@ -14,6 +14,7 @@ import torch
 from . import _capi
 
 CHUNK = 64  # coordinates per pairwise chunk; client matrices pad ldx to this
+PW_SLICES = 8  # FLR_PW_SLICES: canonical coordinate slices of the pairwise kernels
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -171,3 +172,52 @@ def weighted_rows(X: torch.Tensor, weights, divisor: float, rows=None, scales=No
     _capi.call("flr_weighted_rows", X.data_ptr(), K, P, ldx, _ptr(r), m, w.data_ptr(), _ptr(s), float(divisor),
                out.data_ptr(), _stream(X))
     return out
+
+
+# ---- coordinate-sharded Krum distances (flr_pairwise_* phases, include/flr.h) ----
+
+def _ws(nbytes: int, device) -> Tuple[torch.Tensor, int]:
+    ws = torch.empty(max(nbytes, 256) + 256, dtype=torch.uint8, device=device)
+    return ws, ws.data_ptr() + (-ws.data_ptr()) % 256
+
+
+def pairwise_l2_sharded(cs, events=None) -> torch.Tensor:
+    """K×K float64 distances from a coordinate slice (flr.shard.CoordSlice):
+    every rank ends with the same D, bit-identical to pairwise_l2 on the
+    whole matrix.  Collectives: one exact sum of the pivot sample, one exact
+    sum of the tail term, one all-gather of the per-slice Gram sums."""
+    lib = _capi.lib()
+    K, P, dev = cs.K, cs.P, cs.data.device
+    X, ld = cs.data, cs.data.stride(0)
+    st = _stream(X)
+    c0, c1 = cs.plan.chunks(cs.rank)
+    S = int(lib.flr_pairwise_sample_len(P))
+    D = torch.empty((K, K), dtype=torch.float64, device=dev)
+    tail = torch.empty((K, K), dtype=torch.float64, device=dev)
+    # tail: coordinates past the last full chunk (held by the last rank)
+    t0 = (P // CHUNK) * CHUNK - cs.begin
+    t0 = min(max(t0, 0), cs.n)
+    _capi.call("flr_pairwise_tail", X.data_ptr(), K, ld, t0, cs.n, tail.data_ptr(), st)
+    if S == 0:  # no full chunk anywhere: the tail is everything
+        cs.comm.all_reduce_sum(tail)
+        gsum = torch.zeros(PW_SLICES * int(lib.flr_pairwise_gsum_len(K)), dtype=torch.float64, device=dev)
+        _capi.call("flr_pairwise_finish", gsum.data_ptr(), tail.data_ptr(), K, D.data_ptr(), st)
+        return D
+    Xs = torch.empty((K, S), dtype=torch.float32, device=dev)
+    _capi.call("flr_pairwise_sample", X.data_ptr(), K, ld, P, c0, c1, Xs.data_ptr(), st)
+    cs.comm.all_reduce_sum(Xs)
+    nsl = cs.q1 - cs.q0
+    nbytes = int(lib.flr_pairwise_sliced_workspace(K, P, nsl))
+    ws, wp = _ws(nbytes, dev)
+    pivot = torch.empty(1, dtype=torch.int32, device=dev)
+    _capi.call("flr_pairwise_pivot", Xs.data_ptr(), K, P, pivot.data_ptr(), wp, nbytes, st)
+    glen = int(lib.flr_pairwise_gsum_len(K))
+    mine = torch.empty(nsl * glen, dtype=torch.float64, device=dev)
+    ev = (None, None) if events is None else events
+    _capi.call("flr_pairwise_gram_slices", X.data_ptr(), K, ld, P, cs.q0, cs.q1, pivot.data_ptr(), mine.data_ptr(),
+               wp, nbytes, st, ev[0], ev[1])
+    cs.comm.all_reduce_sum(tail)
+    gsum = torch.empty(PW_SLICES * glen, dtype=torch.float64, device=dev)
+    cs.comm.all_gather(gsum, mine)
+    _capi.call("flr_pairwise_finish", gsum.data_ptr(), tail.data_ptr(), K, D.data_ptr(), st)
+    return D

@@ -7,8 +7,14 @@ experiments/run_experiments.py:188-259, minus evaluation and checkpointing).
   global params <- aggregated                                      (:257-259)
 
 The K clients are sharded over the GPUs (flr.dist); each GPU trains its rows
-of the client matrix together, one all-gather assembles the K×P matrix, and
-the aggregation kernels read it in place.
+of the client matrix together.  The exchange is then either
+* "alltoall" (default for FedAvg / Krum / trimmed mean / median): one
+  all-to-all hands every GPU all K clients' values of its coordinate range
+  (flr.shard), each GPU aggregates its range, and one all-gather of the
+  P-vector slices rebuilds the global model; or
+* "allgather": one all-gather assembles the whole K×P matrix on every GPU and
+  the aggregation runs replicated (defenses that need whole rows).
+Both give the bit-identical global model at every GPU count.
 """
 from __future__ import annotations
 
@@ -21,6 +27,7 @@ from . import dist as fdist
 from .attacks import Backdoor, poison_batches_
 from .defenses import get_defense
 from .matrix import ClientMatrix
+from .shard import PW_SLICES, Comm, CoordExchange
 from .models.multimodal import ModelSpec, MultimodalNet, param_layout
 from .train import ClientBatchTrainer, TrainConfig, make_dropout_masks, synthetic_batches
 
@@ -34,6 +41,7 @@ class RoundConfig:
     attack: str = "sign_flip"            # "sign_flip" (model_poisoning.py:274-276) | "backdoor" | "none"
     num_attackers: int = 25              # f = int(0.2 K), clients 0..f-1 (experiment_matrix.py:67-68)
     seed: int = 42                       # run_experiments.py:43
+    exchange: str = "auto"               # "alltoall" | "allgather" | "auto" (alltoall when the defense shards)
 
 
 def initial_global(spec: ModelSpec, seed: int, device) -> torch.Tensor:
@@ -53,17 +61,31 @@ class RoundEngine:
         self.lo, self.hi = fdist.shard(K, world, rank)
         shapes = [s for _, s in param_layout(spec)]
         self.trainer = ClientBatchTrainer(spec, self.hi - self.lo, self.device, tcfg)
-        self.full = self.trainer.X if world == 1 else ClientMatrix.empty(K, shapes, self.device)
         cfg = dict(rcfg.defense_cfg)
         if rcfg.defense in ("krum", "multi_krum"):  # run_experiments.py:155-162
             cfg.setdefault("num_malicious", rcfg.num_attackers)
             cfg.setdefault("multi_k", max(1, K // 2))
         self.defense = get_defense(rcfg.defense, cfg)
+        mode = rcfg.exchange
+        if mode == "auto":
+            mode = "alltoall" if (self.defense.supports_sharded and PW_SLICES % world == 0) else "allgather"
+        if mode not in ("alltoall", "allgather"):
+            raise ValueError(f"unknown exchange mode {rcfg.exchange!r}")
+        if mode == "alltoall" and not self.defense.supports_sharded:
+            raise ValueError(f"{self.defense!r} needs whole client rows: use exchange='allgather'")
+        self.exchange = mode
+        self.full = None
+        self.xchg = None
+        self.slice = None
+        if mode == "alltoall":
+            self.xchg = CoordExchange(K, self.hi - self.lo, self.trainer.P, self.device, Comm())
+        else:
+            self.full = self.trainer.X if world == 1 else ClientMatrix.empty(K, shapes, self.device)
         self.global_flat = initial_global(spec, rcfg.seed, self.device)
         steps = tcfg.local_steps
         self.batches = synthetic_batches(spec, steps, range(self.lo, self.hi), rcfg.batch, self.device)
-        self.masks = make_dropout_masks(spec, steps, self.hi - self.lo, rcfg.batch, self.device,
-                                        seed=rcfg.seed + 7919 * (rank + 1))
+        self.masks = make_dropout_masks(spec, steps, range(self.lo, self.hi), rcfg.batch, self.device,
+                                        seed=rcfg.seed + 7919)
         if rcfg.attack == "backdoor":  # data poisoning of the malicious clients (run_experiments.py:173-175)
             cols = [c - self.lo for c in range(self.lo, min(self.hi, rcfg.num_attackers))]
             poison_batches_(self.batches, cols, Backdoor(image_size=(spec.image_size, spec.image_size)))
@@ -80,8 +102,13 @@ class RoundEngine:
         self.trainer.load_global(self.global_flat)
         self.losses = self.trainer.local_update(self.batches, self.masks)
         self._poison()
+        kw = {"publish": False} if hasattr(self.defense, "publish") else {}
+        if self.exchange == "alltoall":
+            self.slice = self.xchg.exchange(self.trainer.X.data)
+            part = self.defense.aggregate_sharded(self.slice, self.num_examples, **kw)
+            self.slice.gather_vector(part, self.global_flat)
+            return self.global_flat
         fdist.allgather_rows(self.trainer.X.data, self.full.data)
-        agg = self.defense.aggregate_flat(self.full, self.num_examples, **(
-            {"publish": False} if hasattr(self.defense, "publish") else {}))
+        agg = self.defense.aggregate_flat(self.full, self.num_examples, **kw)
         self.global_flat.copy_(agg)
         return self.global_flat

@@ -1,0 +1,197 @@
+"""Coordinate-sharded exchange: the round's one data exchange as an all-to-all.
+
+The reference aggregates one K×P client matrix on one host
+(src/defenses/krum.py:55-99, trimmed_mean.py:74-101, base_defense.py:80-97).
+With the K clients sharded over G GPUs (flr.dist), the straightforward
+exchange is an all-gather of every GPU's (K/G)×P row block: each GPU then
+receives (G-1)/G · 4KP bytes (C3 at G = 8: 5.3 GB) and holds all of X.
+
+Every aggregator of the hot path is either coordinate-wise (FedAvg,
+trimmed mean, median, the Multi-Krum mean) or a sum over coordinates of
+per-coordinate terms (Krum's Gram matrix).  So the exchange here is the
+TRANSPOSE of the client sharding instead: GPU g receives all K clients'
+values for its own contiguous coordinate range (one all-to-all,
+(G-1)/G · 4KP/G bytes received per GPU: 8x less at G = 8), aggregates its
+range, and one all-gather of the P-vector slices rebuilds the global model.
+
+Coordinate ranges are unions of the pairwise kernel's canonical slices
+(FLR_PW_SLICES = 8, include/flr.h): GPU g owns slices [8g/G, 8(g+1)/G), and
+the coordinates past the last full 64-chunk belong to the last GPU.  The
+pairwise kernels compute per-slice records that do not depend on G, and the
+coordinate-wise kernels compute each coordinate independently, so every
+aggregate — and Krum's distance matrix — is bit-identical at G = 1, 2, 4, 8.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import _capi
+from .ops import CHUNK
+
+PW_SLICES = 8  # FLR_PW_SLICES
+
+
+def slice_chunks(P: int, q: int) -> Tuple[int, int]:
+    """Full-chunk range [c0, c1) of canonical slice q (flr_pw_slice_chunks)."""
+    nch = P // CHUNK
+    return nch * q // PW_SLICES, nch * (q + 1) // PW_SLICES
+
+
+@dataclass(frozen=True)
+class CoordPlan:
+    """Who owns which coordinates when the K×P matrix is split by columns."""
+    P: int
+    world: int
+
+    def __post_init__(self):
+        if PW_SLICES % self.world != 0:
+            raise ValueError(f"coordinate sharding needs world | {PW_SLICES} (got {self.world})")
+
+    def slices(self, rank: int) -> Tuple[int, int]:
+        per = PW_SLICES // self.world
+        return rank * per, (rank + 1) * per
+
+    def chunks(self, rank: int) -> Tuple[int, int]:
+        q0, q1 = self.slices(rank)
+        return slice_chunks(self.P, q0)[0], slice_chunks(self.P, q1 - 1)[1]
+
+    def coords(self, rank: int) -> Tuple[int, int]:
+        """[begin, end) of the coordinates rank owns (tail goes to the last rank)."""
+        c0, c1 = self.chunks(rank)
+        end = self.P if rank == self.world - 1 else c1 * CHUNK
+        return c0 * CHUNK, end
+
+    @property
+    def ld(self) -> int:
+        """Row stride of every exchanged block: the longest range, 64-aligned."""
+        n = max(e - b for b, e in (self.coords(r) for r in range(self.world)))
+        return max(CHUNK, (n + CHUNK - 1) // CHUNK * CHUNK)
+
+
+class Comm:
+    """The collectives of a sharded round.  ``nccl`` (RCCL over xGMI) runs on
+    the device tensors; ``gloo`` stages CUDA tensors through host memory (the
+    world_size > 1 rehearsal on one GPU or on CPU)."""
+
+    def __init__(self, group: Optional[dist.ProcessGroup] = None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.staged = dist.is_initialized() and dist.get_backend(group) == "gloo"
+
+    def _host(self, t: torch.Tensor) -> torch.Tensor:
+        return t.cpu() if (self.staged and t.is_cuda) else t
+
+    def all_reduce_sum(self, t: torch.Tensor) -> None:
+        if self.world == 1:
+            return
+        h = self._host(t)
+        dist.all_reduce(h, group=self.group)
+        if h is not t:
+            t.copy_(h)
+
+    def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> None:
+        """out [world * n] <- concat over ranks of t [n] (rank order)."""
+        if self.world == 1:
+            out.copy_(t.reshape(out.shape))
+            return
+        ho, ht = self._host(out), self._host(t.contiguous())
+        dist.all_gather_into_tensor(ho, ht, group=self.group)
+        if ho is not out:
+            out.copy_(ho)
+
+    def all_to_all(self, out: torch.Tensor, t: torch.Tensor) -> None:
+        """Equal splits along dim 0: block r of t goes to rank r; out block s came from rank s."""
+        if self.world == 1:
+            out.copy_(t)
+            return
+        ho, ht = self._host(out), self._host(t.contiguous())
+        dist.all_to_all_single(ho, ht, group=self.group)
+        if ho is not out:
+            out.copy_(ho)
+
+
+class CoordSlice:
+    """All K clients' values of one GPU's coordinate range: data [K, ld], the
+    valid columns [:, :n] are global coordinates [begin, begin + n)."""
+
+    def __init__(self, data: torch.Tensor, plan: CoordPlan, rank: int, comm: Comm):
+        self.data, self.plan, self.rank, self.comm = data, plan, rank, comm
+        self.begin, self.end = plan.coords(rank)
+        self.q0, self.q1 = plan.slices(rank)
+
+    @property
+    def K(self) -> int:
+        return self.data.shape[0]
+
+    @property
+    def n(self) -> int:
+        return self.end - self.begin
+
+    @property
+    def P(self) -> int:
+        """Length of the WHOLE client vector."""
+        return self.plan.P
+
+    @property
+    def X(self) -> torch.Tensor:
+        return self.data[:, : self.n]
+
+    def gather_vector(self, part: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """out [P] <- concatenation of every rank's aggregated range (all-gather)."""
+        plan, world = self.plan, self.plan.world
+        if world == 1:
+            out.copy_(part[: self.n])
+            return out
+        buf = torch.zeros(world * plan.ld, dtype=torch.float32, device=part.device)
+        mine = torch.zeros(plan.ld, dtype=torch.float32, device=part.device)
+        mine[: self.n].copy_(part[: self.n])
+        self.comm.all_gather(buf, mine)
+        for r in range(world):
+            b, e = plan.coords(r)
+            out[b:e].copy_(buf[r * plan.ld: r * plan.ld + (e - b)])
+        return out
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream if t.is_cuda else 0
+
+
+def pack_for_exchange(local: torch.Tensor, P: int, plan: CoordPlan, send: torch.Tensor) -> None:
+    """send [world, K_local, ld] <- local [K_local, >=P] cut at the ranks'
+    coordinate ranges (block r = columns plan.coords(r))."""
+    K_l = local.shape[0]
+    for r in range(plan.world):
+        b, e = plan.coords(r)
+        if local.is_cuda:
+            _capi.call("flr_copy_rows", local.data_ptr() + 4 * b, local.stride(0), e - b, send[r].data_ptr(),
+                       plan.ld, K_l, _stream(local))
+        else:
+            send[r, :, : e - b].copy_(local[:, b:e])
+
+
+class CoordExchange:
+    """The all-to-all of a round: client-sharded rows in, coordinate slice out.
+    Buffers are allocated once and reused every round."""
+
+    def __init__(self, K: int, K_local: int, P: int, device, comm: Optional[Comm] = None):
+        self.comm = comm or Comm()
+        self.plan = CoordPlan(P, self.comm.world)
+        self.K, self.K_local = K, K_local
+        ld = self.plan.ld
+        world = self.comm.world
+        self.send = self.recv = None
+        if world > 1:
+            self.send = torch.zeros(world, K_local, ld, dtype=torch.float32, device=device)
+            self.recv = torch.zeros(world, K_local, ld, dtype=torch.float32, device=device)
+
+    def exchange(self, local: torch.Tensor) -> CoordSlice:
+        if self.comm.world == 1:  # one GPU holds every coordinate: no copy
+            return CoordSlice(local, self.plan, 0, self.comm)
+        pack_for_exchange(local, self.plan.P, self.plan, self.send)
+        self.comm.all_to_all(self.recv, self.send)  # recv block s = rank s's clients
+        return CoordSlice(self.recv.view(self.K, self.plan.ld), self.plan, self.comm.rank, self.comm)

@@ -205,14 +205,23 @@ class ClientBatchTrainer:
         return total / max(1, len(batches))
 
 
-def make_dropout_masks(spec: ModelSpec, steps: int, K: int, B: int, device, seed: int) -> Optional[List[torch.Tensor]]:
-    """Explicit inverted-dropout masks {0, 1/(1-p)} per step (reproducible)."""
+def make_dropout_masks(spec: ModelSpec, steps: int, client_ids, B: int, device,
+                       seed: int) -> Optional[List[torch.Tensor]]:
+    """Explicit inverted-dropout masks {0, 1/(1-p)} per step, [K, B, fusion]
+    each.  client_ids: the global ids of the rows (an int K means 0..K-1);
+    client c's masks come from its own stream seeded seed + c, so they do not
+    depend on how clients are sharded over GPUs."""
     if spec.dropout <= 0:
         return None
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
+    ids = range(client_ids) if isinstance(client_ids, int) else client_ids
     keep = 1.0 - spec.dropout
-    return [(torch.rand(K, B, spec.fusion, generator=g, device=device) < keep).float() / keep for _ in range(steps)]
+    u = torch.empty(steps, len(ids), B, spec.fusion)
+    for j, c in enumerate(ids):
+        g = torch.Generator(device="cpu")
+        g.manual_seed(seed + int(c))
+        u[:, j] = torch.rand(steps, B, spec.fusion, generator=g)
+    m = ((u < keep).float() / keep).to(device)
+    return [m[s] for s in range(steps)]
 
 
 def synthetic_batches(spec: ModelSpec, steps: int, client_ids: Sequence[int], batch: int, device,

@@ -1,0 +1,161 @@
+"""GPU: the coordinate-sharded exchange (flr.shard).
+
+Bars: Krum's distance matrix from the per-slice phases, composed over any
+split of the canonical slices, is BIT-identical to flr_pairwise_l2 on the
+whole matrix; the aggregates of a sharded round are bit-identical to the
+one-GPU round (2 ranks on one GPU over gloo, CUDA tensors staged through the
+host — the RCCL path runs the same code with device collectives)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from flr import _capi, ops
+from flr.defenses import get_defense
+from flr.matrix import ClientMatrix
+from flr.shard import PW_SLICES, Comm, CoordPlan, CoordSlice, slice_chunks
+from flr.workload import update_matrix
+
+pytestmark = pytest.mark.gpu
+
+
+def _phases(X_full, K, P, world):
+    """The five phases of include/flr.h with the collectives done by hand."""
+    lib = _capi.lib()
+    dev = X_full.device
+    plan = CoordPlan(P, world)
+    ld = plan.ld
+    st = torch.cuda.current_stream().cuda_stream
+    parts = []
+    for r in range(world):  # what rank r would receive from the all-to-all
+        b, e = plan.coords(r)
+        part = torch.zeros((K, ld), dtype=torch.float32, device=dev)
+        part[:, : e - b] = X_full[:, b:e]
+        parts.append(part)
+    S = int(lib.flr_pairwise_sample_len(P))
+    Xs = torch.zeros((K, S), dtype=torch.float32, device=dev)
+    for r in range(world):
+        c0, c1 = plan.chunks(r)
+        xs_r = torch.full((K, S), float("nan"), device=dev)
+        _capi.call("flr_pairwise_sample", parts[r].data_ptr(), K, ld, P, c0, c1, xs_r.data_ptr(), st)
+        Xs += xs_r
+    nsl = PW_SLICES // world
+    nbytes = int(lib.flr_pairwise_sliced_workspace(K, P, nsl))
+    ws, wp = ops._ws(nbytes, dev)
+    pivot = torch.empty(1, dtype=torch.int32, device=dev)
+    _capi.call("flr_pairwise_pivot", Xs.data_ptr(), K, P, pivot.data_ptr(), wp, nbytes, st)
+    glen = int(lib.flr_pairwise_gsum_len(K))
+    gsum = torch.empty((PW_SLICES, glen), dtype=torch.float64, device=dev)
+    tail = torch.zeros((K, K), dtype=torch.float64, device=dev)
+    for r in range(world):
+        q0, q1 = plan.slices(r)
+        _capi.call("flr_pairwise_gram_slices", parts[r].data_ptr(), K, ld, P, q0, q1, pivot.data_ptr(),
+                   gsum[q0].data_ptr(), wp, nbytes, st, None, None)
+        b, e = plan.coords(r)
+        t0 = min(max((P // 64) * 64 - b, 0), e - b)
+        t = torch.empty((K, K), dtype=torch.float64, device=dev)
+        _capi.call("flr_pairwise_tail", parts[r].data_ptr(), K, ld, t0, e - b, t.data_ptr(), st)
+        tail += t
+    D = torch.empty((K, K), dtype=torch.float64, device=dev)
+    _capi.call("flr_pairwise_finish", gsum.data_ptr(), tail.data_ptr(), K, D.data_ptr(), st)
+    return D
+
+
+@pytest.mark.parametrize("K,P", [(16, 64 * 8 * 3 + 5), (40, 4099), (128, 100_000 + 37), (130, 20_000),
+                                 (9, 70)])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_sharded_distances_bit_identical(cuda, K, P, world):
+    X = update_matrix(K, P, f=K // 5, seed=K * 7 + P, device=cuda)
+    D_full = ops.pairwise_l2(X[:, :P], "gram")
+    D = _phases(X, K, P, world)
+    assert torch.equal(D, D_full)
+
+
+def test_slice_chunks_match_library():
+    lib = _capi.lib()
+    import ctypes
+    for P in (0, 63, 64, 511, 512, 4099, 11_800_394):
+        for q in range(PW_SLICES):
+            a, b = ctypes.c_int64(), ctypes.c_int64()
+            assert lib.flr_pw_slice_chunks(P, q, ctypes.byref(a), ctypes.byref(b)) == 0
+            assert (a.value, b.value) == slice_chunks(P, q)
+
+
+@pytest.mark.parametrize("name,cfg", [("krum", {"num_malicious": 3, "multi_k": 8}),
+                                      ("krum", {"num_malicious": 3, "multi_k": 1}),
+                                      ("trimmed_mean", {"trim_ratio": 0.2}), ("median", {}), ("fedavg", {})])
+def test_sharded_defense_world1_equals_flat(cuda, name, cfg):
+    """World 1: the sharded entry point on the whole matrix == aggregate_flat."""
+    K, P = 16, 5000
+    X = update_matrix(K, P, f=3, seed=5, device=cuda)
+    cm = ClientMatrix(X, P, [torch.Size([P])])
+    ne = list(range(1, K + 1))
+    d1 = get_defense(name, dict(cfg))
+    ref = d1.aggregate_flat(cm, ne)
+    d2 = get_defense(name, dict(cfg))
+    cs = CoordSlice(X, CoordPlan(P, 1), 0, Comm())
+    out = torch.empty(P, device=cuda)
+    cs.gather_vector(d2.aggregate_sharded(cs, ne), out)
+    assert torch.equal(out, ref[:P])
+    if name == "krum":
+        assert d1.selected_clients == d2.selected_clients
+
+
+# ---------------- 2 ranks on one GPU (gloo) vs 1 rank ----------------
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _round_worker(rank, world, port, defense, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from flr.models.multimodal import TINY
+    from flr.round import RoundConfig, RoundEngine
+    from flr.train import TrainConfig
+    rc = RoundConfig(num_clients=8, batch=4, defense=defense, num_attackers=1, exchange="alltoall",
+                     defense_cfg={"trim_ratio": 0.2} if defense == "trimmed_mean" else {})
+    eng = RoundEngine(TINY, rc, TrainConfig(local_steps=2), torch.device("cuda:0"), rank, world)
+    for _ in range(2):
+        g = eng.run_round()
+    torch.cuda.synchronize()
+    sel = None
+    if defense == "krum":
+        eng.defense.publish()
+        sel = eng.defense.selected_clients
+    q.put((rank, g.cpu().numpy(), sel))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _run(world, defense):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_round_worker, args=(r, world, port, defense, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("defense", ["krum", "trimmed_mean"])
+def test_sharded_round_two_ranks_equals_one(cuda, defense):
+    one = _run(1, defense)
+    two = _run(2, defense)
+    assert np.array_equal(one[0][1], two[0][1]) and np.array_equal(two[0][1], two[1][1])
+    assert one[0][2] == two[0][2] == two[1][2]
