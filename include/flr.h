@@ -314,6 +314,19 @@ int flr_batchnorm_bwd(const float* dy, const float* x, const float* y,
                       float* dx, float* dgamma, float* dbeta, float* dresidual,
                       int64_t B, int64_t KC, int64_t HW, int relu, void* stream);
 
+/* ---- a2: max pooling of the image branch (the stem's 3x3/2 pad-1 pool) ----
+ * Replaces nn.MaxPool2d / F.max_pool2d on x [nplanes][H][W] (planes = B*K*C of
+ * the grouped layout).  torch's CPU rule: first in-bounds element of the
+ * row-major window scan with (v > max || isnan(v)) wins; argmax [nplanes][Ho][Wo]
+ * holds its window offset kh*KW + kw.  bwd: dx[e] = sum of dy over the windows
+ * whose argmax is e, in output raster order (overwrites dx). */
+int flr_maxpool2d_fwd(const float* x, float* y, uint8_t* argmax, int64_t nplanes, int64_t H,
+                      int64_t W, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+                      void* stream);
+int flr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* dx, int64_t nplanes,
+                      int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t stride,
+                      int64_t pad, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

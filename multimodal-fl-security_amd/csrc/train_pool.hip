@@ -1,0 +1,115 @@
+// a2 — 2-D max pooling of the image branch (the ResNet stem's 3x3/2 pad-1
+// max-pool; the reference's conv blocks pool with nn.MaxPool2d,
+// src/models/cub200_cnn.py:71-77 template), forward and backward, on the
+// client-batched activation layout x[B][K*C][H][W] (planes are independent).
+//
+// torch's CPU kernel (aten/src/ATen/native/cpu/MaxPoolKernel.cpp) is restated:
+// the window is scanned row-major over its in-bounds elements and the first
+// element with (v > max || isnan(v)) wins, starting from max = -inf; the
+// backward adds each window's gradient to its argmax in output-raster order,
+// so an input element shared by several windows sums their gradients in the
+// same order (bit-identical, no atomics).
+//
+// Forward: one lane per output; the argmax is kept as a 1-byte window offset
+// (kh*KW + kw).  Backward: one lane per INPUT element, gathering from the <=
+// ceil(KH/S)*ceil(KW/S) windows that contain it, in raster order.
+#include "flr_common.h"
+
+namespace flr {
+namespace pool {
+
+constexpr int THREADS = 256;
+
+struct PoolGeom {
+  int H, W, Ho, Wo, KH, KW, S, P;
+};
+
+__global__ __launch_bounds__(THREADS) void fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                      uint8_t* __restrict__ arg, int64_t nplanes, PoolGeom g) {
+  const int64_t idx = (int64_t)blockIdx.x * THREADS + threadIdx.x;
+  const int64_t total = nplanes * g.Ho * g.Wo;
+  if (idx >= total) return;
+  const int64_t plane = idx / (g.Ho * g.Wo);
+  const int o = (int)(idx - plane * g.Ho * g.Wo);
+  const int oh = o / g.Wo, ow = o - oh * g.Wo;
+  const float* xp = x + plane * g.H * g.W;
+  const int ih0 = oh * g.S - g.P, iw0 = ow * g.S - g.P;
+  float best = -__builtin_huge_valf();
+  int bi = -1;
+  for (int kh = 0; kh < g.KH; ++kh) {
+    const int ih = ih0 + kh;
+    if (ih < 0 || ih >= g.H) continue;
+    for (int kw = 0; kw < g.KW; ++kw) {
+      const int iw = iw0 + kw;
+      if (iw < 0 || iw >= g.W) continue;
+      const float v = xp[ih * g.W + iw];
+      if (bi < 0) bi = kh * g.KW + kw;  // torch's initial maxindex: the first in-bounds element
+      if (v > best || v != v) {
+        best = v;
+        bi = kh * g.KW + kw;
+      }
+    }
+  }
+  y[idx] = best;
+  arg[idx] = (uint8_t)bi;
+}
+
+__global__ __launch_bounds__(THREADS) void bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                      float* __restrict__ dx, int64_t nplanes, PoolGeom g) {
+  const int64_t idx = (int64_t)blockIdx.x * THREADS + threadIdx.x;
+  const int64_t total = nplanes * g.H * g.W;
+  if (idx >= total) return;
+  const int64_t plane = idx / (g.H * g.W);
+  const int e = (int)(idx - plane * g.H * g.W);
+  const int ih = e / g.W, iw = e - ih * g.W;
+  // windows oh with oh*S - P <= ih <= oh*S - P + KH - 1
+  const int oh_lo = max(0, (ih + g.P - g.KH + g.S) / g.S), oh_hi = min(g.Ho - 1, (ih + g.P) / g.S);
+  const int ow_lo = max(0, (iw + g.P - g.KW + g.S) / g.S), ow_hi = min(g.Wo - 1, (iw + g.P) / g.S);
+  const float* dyp = dy + plane * g.Ho * g.Wo;
+  const uint8_t* ap = arg + plane * g.Ho * g.Wo;
+  float acc = 0.f;
+  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+    const int kh = ih - (oh * g.S - g.P);
+    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+      const int kw = iw - (ow * g.S - g.P);
+      if (ap[oh * g.Wo + ow] == kh * g.KW + kw) acc = add_rn(acc, dyp[oh * g.Wo + ow]);
+    }
+  }
+  dx[idx] = acc;
+}
+
+inline bool geom(int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t S, int64_t P, PoolGeom& g) {
+  if (H < 1 || W < 1 || KH < 1 || KW < 1 || S < 1 || P < 0 || 2 * P > KH || 2 * P > KW || KH * KW > 255)
+    return false;
+  g.H = (int)H; g.W = (int)W; g.KH = (int)KH; g.KW = (int)KW; g.S = (int)S; g.P = (int)P;
+  g.Ho = (int)((H + 2 * P - KH) / S + 1);
+  g.Wo = (int)((W + 2 * P - KW) / S + 1);
+  return g.Ho >= 1 && g.Wo >= 1;
+}
+
+}  // namespace pool
+}  // namespace flr
+
+using namespace flr;
+
+extern "C" int flr_maxpool2d_fwd(const float* x, float* y, uint8_t* argmax, int64_t nplanes, int64_t H, int64_t W,
+                                 int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* stream) {
+  pool::PoolGeom g;
+  if (!x || !y || !argmax || nplanes < 0 || !pool::geom(H, W, KH, KW, stride, pad, g)) return FLR_ERR_ARG;
+  const int64_t total = nplanes * g.Ho * g.Wo;
+  if (total == 0) return FLR_OK;
+  hipLaunchKernelGGL(pool::fwd_kernel, dim3((unsigned)((total + pool::THREADS - 1) / pool::THREADS)),
+                     dim3(pool::THREADS), 0, as_stream(stream), x, y, argmax, nplanes, g);
+  return launch_status("maxpool fwd");
+}
+
+extern "C" int flr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* dx, int64_t nplanes, int64_t H,
+                                 int64_t W, int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* stream) {
+  pool::PoolGeom g;
+  if (!dy || !dx || !argmax || nplanes < 0 || !pool::geom(H, W, KH, KW, stride, pad, g)) return FLR_ERR_ARG;
+  const int64_t total = nplanes * H * W;
+  if (total == 0) return FLR_OK;
+  hipLaunchKernelGGL(pool::bwd_kernel, dim3((unsigned)((total + pool::THREADS - 1) / pool::THREADS)),
+                     dim3(pool::THREADS), 0, as_stream(stream), dy, argmax, dx, nplanes, g);
+  return launch_status("maxpool bwd");
+}

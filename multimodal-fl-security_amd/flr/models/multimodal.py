@@ -255,7 +255,11 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     K, B = images.shape[:2]
     x = images.transpose(0, 1).reshape(B, K * spec.in_channels, *images.shape[3:])
     x = _bn_act(conv("conv1.weight", x, 2, 3, need_dx=False), p["bn1.weight"], p["bn1.bias"])
-    x = F.max_pool2d(x, 3, 2, 1)
+    if _LAYERS == "native" and x.is_cuda:
+        from ..nn import client_maxpool2d
+        x = client_maxpool2d(x, 3, 2, 1)
+    else:
+        x = F.max_pool2d(x, 3, 2, 1)
     w = spec.widths
     for li, nblk in enumerate(spec.blocks):
         for bi in range(nblk):

@@ -222,3 +222,34 @@ class ClientBatchNorm(torch.autograd.Function):
 
 def client_batchnorm(x, gamma, beta, residual=None, relu: bool = True, eps: float = 1e-5):
     return ClientBatchNorm.apply(x, gamma, beta, residual, relu, eps)
+
+
+class ClientMaxPool2d(torch.autograd.Function):
+    """F.max_pool2d over every (batch, client, channel) plane (flr_maxpool2d_fwd/_bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, k: int, stride: int, pad: int):
+        x = x.contiguous()
+        B, KC, H, W = x.shape
+        Ho = (H + 2 * pad - k) // stride + 1
+        Wo = (W + 2 * pad - k) // stride + 1
+        y = torch.empty(B, KC, Ho, Wo, dtype=x.dtype, device=x.device)
+        arg = torch.empty(B, KC, Ho, Wo, dtype=torch.uint8, device=x.device)
+        _capi.call("flr_maxpool2d_fwd", x.data_ptr(), y.data_ptr(), arg.data_ptr(), B * KC, H, W, k, k, stride, pad,
+                   _stream(x))
+        ctx.save_for_backward(arg)
+        ctx.geom = (B * KC, H, W, k, k, stride, pad)
+        ctx.xshape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device)
+        _capi.call("flr_maxpool2d_bwd", dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), *ctx.geom, _stream(dy))
+        return dx, None, None, None
+
+
+def client_maxpool2d(x, k: int, stride: int, pad: int):
+    return ClientMaxPool2d.apply(x, k, stride, pad)
