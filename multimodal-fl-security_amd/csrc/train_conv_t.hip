@@ -27,6 +27,7 @@
 #include "conv_common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace flr {
 namespace convt {
@@ -157,19 +158,28 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
   }
 };
 
-struct DgradT {  // dx = conv^T(dy, W_t): M = Cin, N = B*H*W, R = ntaps*Cout
+// dx = conv^T(dy, W_t) over ONE stride-parity class of input pixels:
+// ih = ca + stride*ihc, iw = cb + stride*iwc.  Only the taps kh = (ih + pad)
+// mod stride (same for kw) reach such a pixel, so a class is a dense GEMM
+// M = Cin, N = B*Hc*Wc, R = ntc*Cout with no zero-padded taps — a stride-2
+// dgrad runs the four classes and does the fwd's MFMA work, not four times
+// it.  Stride 1 is the single class (0, 0) with every live tap.
+struct DgradT {
   Geom g;
   const float* dy;
   const float* w;
   float* dx;
+  int ca, cb, Hc, Wc, ntc;
+  conv::FastDiv d_hcwc, d_wc;
+  int8_t ckh[conv::MAXTAPS], ckw[conv::MAXTAPS];
   static constexpr int LA = RK_VEC, LB = KR_GATHER;
   __host__ __device__ int M() const { return g.Cin; }
-  __host__ __device__ int N() const { return g.B * g.H * g.W; }
-  __host__ __device__ int R() const { return g.ntaps * g.Cout; }
+  __host__ __device__ int N() const { return g.B * Hc * Wc; }
+  __host__ __device__ int R() const { return ntc * g.Cout; }
   struct State {
     rsrc_t ra, rb;
     unsigned a0;
-    int ih, iw, yoff;
+    int ih, iw, yoff;  // ih, iw: this lane's input pixel + pad
     bool nok;
   };
   __device__ State init(int k, int m0, int n0, int tid) const {
@@ -180,16 +190,16 @@ struct DgradT {  // dx = conv^T(dy, W_t): M = Cin, N = B*H*W, R = ntaps*Cout
     s.a0 = (unsigned)(((m0 + tid / 8) * g.Cout + 4 * (tid % 8)) * 4);
     const int n = n0 + tid % 64;
     s.nok = n < N();
-    const uint32_t bb = udiv(n, g.d_hw), p = n - bb * g.H * g.W;
-    const uint32_t ih = udiv(p, g.d_w), iw = p - ih * g.W;
-    s.ih = (int)ih + g.pad;
-    s.iw = (int)iw + g.pad;
+    const uint32_t bb = udiv(n, d_hcwc), p = n - bb * Hc * Wc;
+    const uint32_t ihc = udiv(p, d_wc), iwc = p - ihc * Wc;
+    s.ih = ca + (int)ihc * g.stride + g.pad;
+    s.iw = cb + (int)iwc * g.stride + g.pad;
     s.yoff = (int)(bb * g.ybs) + (tid / 64) * HoWo;
     return s;
   }
   __device__ void load(const State& s, int r0, float (&a)[8], float (&b)[8]) const {
     const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
-    const int kh = uni(g.tap_kh[slot]), kw = uni(g.tap_kw[slot]);
+    const int kh = uni(ckh[slot]), kw = uni(ckw[slot]);
     const int HoWo = g.Ho * g.Wo;
     const int abase = ((kh * g.KW + kw) * g.Cin * g.Cout + co0) * 4;
 #pragma unroll
@@ -198,28 +208,49 @@ struct DgradT {  // dx = conv^T(dy, W_t): M = Cin, N = B*H*W, R = ntaps*Cout
 #pragma unroll
       for (int e = 0; e < 4; ++e) a[4 * i + e] = q[e];
     }
+    // the class guarantees (ih + pad - kh) % stride == 0
     const int nh = s.ih - kh, nw = s.iw - kw;
-    int oh, ow;
-    bool ok = s.nok && nh >= 0 && nw >= 0;
-    if (g.stride == 1) {
-      oh = nh;
-      ow = nw;
-    } else {
-      oh = nh / g.stride;
-      ow = nw / g.stride;
-      ok = ok && oh * g.stride == nh && ow * g.stride == nw;
-    }
-    ok = ok && oh < g.Ho && ow < g.Wo;
+    const int oh = g.stride == 1 ? nh : nh / g.stride, ow = g.stride == 1 ? nw : nw / g.stride;
+    const bool ok = s.nok && nh >= 0 && nw >= 0 && oh < g.Ho && ow < g.Wo;
     const unsigned vb = ok ? (unsigned)((s.yoff + oh * g.Wo + ow) * 4) : SENT;
-    const int cb = co0 * HoWo * 4;
+    const int cb0 = co0 * HoWo * 4;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, cb + i * 4 * HoWo * 4);
+    for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, cb0 + i * 4 * HoWo * 4);
   }
   __device__ void store(int k, int m, int n, float v) const {
-    const uint32_t bb = udiv(n, g.d_hw), p = n - bb * g.H * g.W;
-    dx[bb * g.xbs + ((int64_t)k * g.Cin + m) * g.H * g.W + p] = v;
+    const uint32_t bb = udiv(n, d_hcwc), p = n - bb * Hc * Wc;
+    const uint32_t ihc = udiv(p, d_wc), iwc = p - ihc * Wc;
+    const int ih = ca + (int)ihc * g.stride, iw = cb + (int)iwc * g.stride;
+    dx[bb * g.xbs + ((int64_t)k * g.Cin + m) * g.H * g.W + ih * g.W + iw] = v;
   }
 };
+
+// The parity classes of a dgrad (stride^2 of them, fewer when H or W < stride).
+inline int dgrad_classes(const Geom& g, DgradT* out) {
+  int n = 0;
+  for (int ca = 0; ca < std::min(g.stride, g.H); ++ca)
+    for (int cb = 0; cb < std::min(g.stride, g.W); ++cb) {
+      DgradT& c = out[n++];
+      c.g = g;
+      c.ca = ca;
+      c.cb = cb;
+      c.Hc = (g.H - ca + g.stride - 1) / g.stride;
+      c.Wc = (g.W - cb + g.stride - 1) / g.stride;
+      c.d_hcwc = conv::make_fastdiv((uint32_t)(c.Hc * c.Wc));
+      c.d_wc = conv::make_fastdiv((uint32_t)c.Wc);
+      c.ntc = 0;
+      for (int t = 0; t < g.ntaps; ++t) {
+        const int kh = g.tap_kh[t], kw = g.tap_kw[t];
+        if (((ca + g.pad - kh) % g.stride + g.stride) % g.stride != 0) continue;
+        if (((cb + g.pad - kw) % g.stride + g.stride) % g.stride != 0) continue;
+        c.ckh[c.ntc] = (int8_t)kh;
+        c.ckw[c.ntc] = (int8_t)kw;
+        ++c.ntc;
+      }
+    }
+  return n;
+}
+constexpr int MAX_CLASSES = 16;
 
 // dW_t[tap][ci][co] = sum_q x(q; tap, ci) dy(q; co): M = ntaps*Cin (slot, ci),
 // N = Cout, R = B*Ho*Wo.  A 64-row m-tile lies inside one tap (Cin % 64 == 0).
@@ -535,7 +566,7 @@ size_t splits_bytes(const Plan& pl) {
 template <class Plan>
 int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   const int M = pl.M(), N = pl.N(), R = pl.R(), K = pl.g.Kc;
-  if (R == 0) return FLR_OK;
+  if (R == 0 && !std::is_same<Plan, DgradT>::value) return FLR_OK;  // a dgrad class with no tap stores zeros
   int S = choose_splits(M, N, R, K);
   if (S > 1 && (!ws || ws_bytes < splits_bytes(pl))) S = 1;
   const dim3 grid((unsigned)cdiv(N, BN), (unsigned)cdiv(M, BM), (unsigned)(K * S));
@@ -633,9 +664,14 @@ extern "C" size_t flr_conv2d_t_workspace(int64_t K, int64_t B, int64_t Cin, int6
   if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return 0;
   const conv::Geom g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
   convt::FwdT f; f.g = g;
-  convt::DgradT d; d.g = g;
   convt::WgtT<false> w; w.g = g;
-  return std::max(convt::splits_bytes(f), std::max(convt::splits_bytes(d), convt::splits_bytes(w)));
+  size_t m = std::max(convt::splits_bytes(f), convt::splits_bytes(w));
+  if (stride <= 4) {
+    convt::DgradT cls[convt::MAX_CLASSES];
+    const int nc = convt::dgrad_classes(g, cls);
+    for (int c = 0; c < nc; ++c) m = std::max(m, convt::splits_bytes(cls[c]));
+  }
+  return m;
 }
 
 extern "C" int flr_conv2d_fwd_t(const float* x, const float* w_t, float* y, int64_t K, int64_t B, int64_t Cin,
@@ -656,10 +692,16 @@ extern "C" int flr_conv2d_bwd_data_t(const float* dy, const float* w_t, float* d
   if (!dy || !w_t || !dx) return FLR_ERR_ARG;
   if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad))
     return conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) ? FLR_ERR_UNSUPPORTED : FLR_ERR_ARG;
-  convt::DgradT pl;
-  pl.g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
-  pl.dy = dy; pl.w = w_t; pl.dx = dx;
-  return convt::launch(pl, ws, ws_bytes, as_stream(stream), "conv bwd data (tap-major)");
+  if (stride > 4) return FLR_ERR_UNSUPPORTED;  // <= MAX_CLASSES parity classes
+  const conv::Geom g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  convt::DgradT cls[convt::MAX_CLASSES];
+  const int nc = convt::dgrad_classes(g, cls);
+  for (int c = 0; c < nc; ++c) {
+    cls[c].dy = dy; cls[c].w = w_t; cls[c].dx = dx;
+    const int rc = convt::launch(cls[c], ws, ws_bytes, as_stream(stream), "conv bwd data (tap-major)");
+    if (rc != FLR_OK) return rc;
+  }
+  return FLR_OK;
 }
 
 extern "C" int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* dw_t, int64_t K, int64_t B,

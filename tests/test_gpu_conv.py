@@ -51,6 +51,11 @@ TAP_SHAPES = [s for s in SHAPES if s[2] % 64 == 0 and s[5] % 64 == 0] + [
     (3, 2, 128, 2, 2, 64, 1, 1, 0),    # 1x1 stride 1, HoWo % 4 == 0
     (2, 5, 64, 3, 3, 64, 3, 2, 1),     # wgrad B gather (HoWo = 4 -> vec), dgrad stride 2
     (2, 3, 64, 3, 3, 64, 3, 1, 1),     # HoWo = 9: wgrad B gather path
+    (2, 4, 64, 7, 6, 64, 3, 2, 1),     # dgrad parity classes of unequal size (odd H, even W)
+    (1, 2, 64, 7, 7, 64, 3, 3, 1),     # stride 3: nine classes
+    (2, 3, 64, 5, 4, 128, 1, 2, 0),    # 1x1/2: three of four classes have no tap (zero dx)
+    (32, 32, 512, 1, 1, 512, 3, 1, 1),  # flattened multi-tile wgrad (R = 32, 2 tiles per workgroup)
+    (16, 32, 256, 2, 2, 256, 3, 1, 1),  # flattened wgrad, R = 128 (4 K-tiles per tile)
 ]
 
 
