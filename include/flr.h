@@ -177,9 +177,10 @@ int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* const* g_bloc
 /* ---- a2: client-batched 2-D convolution (bias-free, as in the conv blocks)
  * Replaces nn.Conv2d forward/backward for every client of a GPU at once
  * (image branch, src/models/cub200_cnn.py:71-77 template).  Layouts:
- *   x  [B][K*Cin][H][W]    (grouped: client k owns channels k*Cin .. k*Cin+Cin-1)
+ *   x  [K][Cin][B][H][W]   (client-channel major: for one (client, channel)
+ *                           the B*H*W pixels the GEMM walks are contiguous)
  *   w  [K][Cout][Cin][KH][KW]
- *   y  [B][K*Cout][Ho][Wo], Ho = (H + 2 pad - KH) / stride + 1
+ *   y  [K][Cout][B][Ho][Wo], Ho = (H + 2 pad - KH) / stride + 1
  * fp32 in, fp32 accumulate (exact-fp32 MFMA).  bwd_data writes dx, bwd_weight
  * writes dw (both overwrite).  Kernel taps that only read zero padding are
  * skipped (their dw is written as exact zeros).  The workspace (optional,
@@ -300,7 +301,8 @@ int flr_gru_bwd_step(const float* dh, const float* gates, const float* hseq,
 
 /* ---- a2: per-client BatchNorm (train mode) + fused residual add / ReLU ----
  * Replaces nn.BatchNorm2d(train) [+ identity add] [+ ReLU] of the conv blocks.
- * x, y, residual: [B][KC][HW] (kc = client*C + channel), gamma/beta/mean/
+ * x, y, residual: [B][KC][HW] (kc = client*C + channel; the engine's
+ * [K][C][B][H][W] activations are passed as B = 1, HW = B*H*W), gamma/beta/mean/
  * invstd: [KC].  fwd: y = act(x*alpha + (beta - mean*alpha) [+ residual]),
  * alpha = gamma/sqrt(var + eps), batch statistics over B*HW, act = ReLU if
  * relu != 0.  bwd: g = dy * (y > 0) if relu else dy; writes dx, dgamma,

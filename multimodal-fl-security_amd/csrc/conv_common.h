@@ -29,7 +29,11 @@ constexpr int MAXTAPS = 49;
 
 struct Geom {
   int Kc, B, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo;
-  int64_t xbs, ybs;  // batch strides of x ([B][K*Cin][H][W]) and y ([B][K*Cout][Ho][Wo])
+  // Activation layout x[K][Cin][B][H][W], y[K][Cout][B][Ho][Wo] ("client-
+  // channel major"): for a fixed (client, channel) the GEMM's pixel dimension
+  // n = b*H*W + h*W + w is one contiguous run of B*H*W floats.  Strides in
+  // floats: client, channel, batch; extents = floats per client.
+  int64_t sxk, sxc, sxb, syk, syc, syb, xext, yext;
   FastDiv d_howo, d_wo, d_hw, d_w, d_cin, d_cout;
   // Kernel taps that read at least one non-padding input pixel.  A tap that
   // only ever reads the zero padding contributes exact zeros to y, dx and dw,
@@ -45,8 +49,14 @@ inline Geom make_geom(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, i
   g.KH = (int)KH; g.KW = (int)KW; g.stride = (int)stride; g.pad = (int)pad;
   g.Ho = (int)((H + 2 * pad - KH) / stride + 1);
   g.Wo = (int)((W + 2 * pad - KW) / stride + 1);
-  g.xbs = K * Cin * H * W;
-  g.ybs = K * Cout * g.Ho * g.Wo;
+  g.sxb = H * W;
+  g.sxc = B * H * W;
+  g.sxk = Cin * B * H * W;
+  g.syb = (int64_t)g.Ho * g.Wo;
+  g.syc = B * g.syb;
+  g.syk = Cout * g.syc;
+  g.xext = g.sxk;
+  g.yext = g.syk;
   g.d_howo = make_fastdiv((uint32_t)(g.Ho * g.Wo));
   g.d_wo = make_fastdiv((uint32_t)g.Wo);
   g.d_hw = make_fastdiv((uint32_t)(H * W));

@@ -67,11 +67,11 @@ struct FwdG {  // y = conv(x, w): M = Cout, N = B*Ho*Wo, R = Cin*KH*KW
     const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
     const int ih = (int)(oh * g.stride + kh) - g.pad, iw = (int)(ow * g.stride + kw) - g.pad;
     if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return 0.f;
-    return x[bb * g.xbs + ((int64_t)k * g.Cin + ci) * g.H * g.W + ih * g.W + iw];
+    return x[k * g.sxk + ci * g.sxc + bb * g.sxb + ih * g.W + iw];
   }
   __device__ void store(int k, int m, int n, float v) const {
     const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
-    y[bb * g.ybs + ((int64_t)k * g.Cout + m) * g.Ho * g.Wo + p] = v;
+    y[k * g.syk + m * g.syc + bb * g.syb + p] = v;
   }
 };
 
@@ -86,7 +86,7 @@ struct WgtG {  // dw = sum_q dy(co, q) im(r, q): M = Cout, N = R, reduction over
   __host__ __device__ int R() const { return g.B * g.Ho * g.Wo; }
   __device__ float a(int k, int m, int q) const {
     const uint32_t bb = udiv(q, g.d_howo), p = q - bb * g.Ho * g.Wo;
-    return dy[bb * g.ybs + ((int64_t)k * g.Cout + m) * g.Ho * g.Wo + p];
+    return dy[k * g.syk + m * g.syc + bb * g.syb + p];
   }
   __device__ float b(int k, int r, int q) const {
     const uint32_t slot = udiv(r, g.d_cin), ci = r - slot * g.Cin;
@@ -95,7 +95,7 @@ struct WgtG {  // dw = sum_q dy(co, q) im(r, q): M = Cout, N = R, reduction over
     const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
     const int ih = (int)(oh * g.stride + kh) - g.pad, iw = (int)(ow * g.stride + kw) - g.pad;
     if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return 0.f;
-    return x[bb * g.xbs + ((int64_t)k * g.Cin + ci) * g.H * g.W + ih * g.W + iw];
+    return x[k * g.sxk + ci * g.sxc + bb * g.sxb + ih * g.W + iw];
   }
   __device__ void store(int k, int m, int n, float v) const {
     const uint32_t slot = udiv(n, g.d_cin), ci = n - slot * g.Cin;
@@ -125,11 +125,11 @@ struct DgradG {  // dx = conv^T(dy, w): M = Cin, N = B*H*W, R = Cout*KH*KW
     if (nh < 0 || nw < 0) return 0.f;
     const int oh = nh / g.stride, ow = nw / g.stride;
     if (oh * g.stride != nh || ow * g.stride != nw || oh >= g.Ho || ow >= g.Wo) return 0.f;
-    return dy[bb * g.ybs + ((int64_t)k * g.Cout + co) * g.Ho * g.Wo + oh * g.Wo + ow];
+    return dy[k * g.syk + co * g.syc + bb * g.syb + oh * g.Wo + ow];
   }
   __device__ void store(int k, int m, int n, float v) const {
     const uint32_t bb = udiv(n, g.d_hw), p = n - bb * g.H * g.W;
-    dx[bb * g.xbs + ((int64_t)k * g.Cin + m) * g.H * g.W + p] = v;
+    dx[k * g.sxk + m * g.sxc + bb * g.sxb + p] = v;
   }
 };
 
@@ -171,7 +171,7 @@ struct FwdF : FwdG {  // A fast along r (ci), B fast along n (pixels)
   __device__ State init(int k, int m0, int n0, int tid) const {
     State s;
     s.wk = w + (int64_t)k * g.Cout * g.Cin * g.KH * g.KW;
-    s.xk = x + (int64_t)k * g.Cin * g.H * g.W;
+    s.xk = x + k * g.sxk;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = m0 + tid / BK + 8 * i;
@@ -184,7 +184,7 @@ struct FwdF : FwdG {  // A fast along r (ci), B fast along n (pixels)
     const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
     s.ih0 = (int)oh * g.stride - g.pad;
     s.iw0 = (int)ow * g.stride - g.pad;
-    s.xoff = (int)(bb * g.xbs) + (tid / BN) * g.H * g.W;
+    s.xoff = (int)(bb * g.sxb + (tid / BN) * g.sxc);
     s.rl = tid / BN;
     return s;
   }
@@ -192,7 +192,7 @@ struct FwdF : FwdG {  // A fast along r (ci), B fast along n (pixels)
     const int slot = __builtin_amdgcn_readfirstlane(r0 / g.Cin);
     const int ci0 = r0 - slot * g.Cin;
     const int kh = g.tap_kh[slot], kw = g.tap_kw[slot];
-    const int KK = g.KH * g.KW, HW = g.H * g.W;
+    const int KK = g.KH * g.KW, HW = (int)g.sxc;  // channel stride
     const int aoff = ci0 * KK + kh * g.KW + kw;
 #pragma unroll
     for (int i = 0; i < 8; ++i) ra[i] = s.mok[i] ? s.wk[s.abase[i] + aoff] : 0.f;
@@ -216,7 +216,7 @@ struct DgradF : DgradG {  // A fast along m (ci), B fast along n (input pixels)
     State s;
     const int KK = g.KH * g.KW;
     s.wk = w + (int64_t)k * g.Cout * g.Cin * KK;
-    s.dyk = dy + (int64_t)k * g.Cout * g.Ho * g.Wo;
+    s.dyk = dy + k * g.syk;
     const int m = m0 + tid % BM;
     s.mok = m < g.Cin;
     s.abase = m * KK + (tid / BM) * g.Cin * KK;
@@ -226,14 +226,14 @@ struct DgradF : DgradG {  // A fast along m (ci), B fast along n (input pixels)
     const uint32_t ih = udiv(p, g.d_w), iw = p - ih * g.W;
     s.ih = (int)ih + g.pad;
     s.iw = (int)iw + g.pad;
-    s.yoff = (int)(bb * g.ybs) + (tid / BN) * g.Ho * g.Wo;
+    s.yoff = (int)(bb * g.syb + (tid / BN) * g.syc);
     return s;
   }
   __device__ void load(const State& s, int r0, int re, float (&ra)[8], float (&rb)[8]) const {
     const int slot = __builtin_amdgcn_readfirstlane(r0 / g.Cout);
     const int co0 = r0 - slot * g.Cout;
     const int kh = g.tap_kh[slot], kw = g.tap_kw[slot];
-    const int KK = g.KH * g.KW, HoWo = g.Ho * g.Wo;
+    const int KK = g.KH * g.KW, HoWo = (int)g.syc;  // channel stride
     const int aoff = co0 * g.Cin * KK + kh * g.KW + kw;
 #pragma unroll
     for (int i = 0; i < 8; ++i) ra[i] = s.mok ? s.wk[s.abase + aoff + 4 * i * g.Cin * KK] : 0.f;
@@ -262,8 +262,8 @@ struct WgtF : WgtG {  // n-tile inside one tap (Cin % 64 == 0); A and B fast alo
   };
   __device__ State init(int k, int m0, int n0, int tid) const {
     State s;
-    s.dyk = dy + (int64_t)k * g.Cout * g.Ho * g.Wo;
-    s.xk = x + (int64_t)k * g.Cin * g.H * g.W;
+    s.dyk = dy + k * g.syk;
+    s.xk = x + k * g.sxk;
     const int slot = n0 / g.Cin;
     s.ci0 = n0 - slot * g.Cin;
     s.kh = g.tap_kh[slot];
@@ -273,8 +273,8 @@ struct WgtF : WgtG {  // n-tile inside one tap (Cin % 64 == 0); A and B fast alo
     for (int i = 0; i < 8; ++i) {
       const int m = m0 + tid / BK + 8 * i;
       s.mok[i] = m < g.Cout;
-      s.abase[i] = m * g.Ho * g.Wo;
-      s.bbase[i] = (s.ci0 + tid / BK + 8 * i) * g.H * g.W;
+      s.abase[i] = (int)(m * g.syc);
+      s.bbase[i] = (int)((s.ci0 + tid / BK + 8 * i) * g.sxc);
     }
     return s;
   }
@@ -283,12 +283,12 @@ struct WgtF : WgtG {  // n-tile inside one tap (Cin % 64 == 0); A and B fast alo
     const bool qok = q < re;
     const uint32_t bb = udiv(q, g.d_howo), p = q - bb * g.Ho * g.Wo;
     const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
-    const int aoff = (int)(bb * g.ybs + p);
+    const int aoff = (int)(bb * g.syb + p);
 #pragma unroll
     for (int i = 0; i < 8; ++i) ra[i] = (qok && s.mok[i]) ? s.dyk[s.abase[i] + aoff] : 0.f;
     const int ih = (int)oh * g.stride - g.pad + s.kh, iw = (int)ow * g.stride - g.pad + s.kw;
     const bool ok = qok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-    const int boff = (int)(bb * g.xbs) + ih * g.W + iw;
+    const int boff = (int)(bb * g.sxb) + ih * g.W + iw;
 #pragma unroll
     for (int i = 0; i < 8; ++i) rb[i] = ok ? s.xk[s.bbase[i] + boff] : 0.f;
   }

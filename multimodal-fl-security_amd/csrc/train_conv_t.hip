@@ -121,9 +121,9 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
   };
   __device__ State init(int k, int m0, int n0, int tid) const {
     State s;
-    const int KK = g.KH * g.KW, HW = g.H * g.W;
+    const int KK = g.KH * g.KW;
     s.ra = make_rsrc(w + (int64_t)k * KK * g.Cin * g.Cout, (int64_t)KK * g.Cin * g.Cout);
-    s.rb = make_rsrc(x + (int64_t)k * g.Cin * HW, (int64_t)(g.B - 1) * g.xbs + (int64_t)g.Cin * HW);
+    s.rb = make_rsrc(x + k * g.sxk, g.xext);
     s.a0 = (unsigned)(((tid / 16) * g.Cout + m0 + 4 * (tid % 16)) * 4);
     const int n = n0 + tid % 64;
     s.nok = n < N();
@@ -131,13 +131,13 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
     const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
     s.ih0 = (int)oh * g.stride - g.pad;
     s.iw0 = (int)ow * g.stride - g.pad;
-    s.xoff = (int)(bb * g.xbs) + (tid / 64) * HW;
+    s.xoff = (int)(bb * g.sxb + (tid / 64) * g.sxc);
     return s;
   }
   __device__ void load(const State& s, int r0, float (&a)[8], float (&b)[8]) const {
     const int slot = uni(r0 / g.Cin), ci0 = r0 - slot * g.Cin;
     const int kh = uni(g.tap_kh[slot]), kw = uni(g.tap_kw[slot]);
-    const int HW = g.H * g.W;
+    const int HW = (int)g.sxc;  // channel stride
     const int arow = ((kh * g.KW + kw) * g.Cin + ci0) * g.Cout * 4;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -152,10 +152,12 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
 #pragma unroll
     for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, cb + i * 4 * HW * 4);
   }
-  __device__ void store(int k, int m, int n, float v) const {
-    const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
-    y[bb * g.ybs + ((int64_t)k * g.Cout + m) * g.Ho * g.Wo + p] = v;
-  }
+  // y[k][m][n]: n = b*Ho*Wo + p is linear in the [K][C][B][Ho][Wo] layout
+  __device__ void store(int k, int m, int n, float v) const { y[k * g.syk + m * g.syc + n] = v; }
+  __device__ bool linear() const { return true; }
+  __device__ float* out() const { return y; }
+  __device__ int64_t tile_base(int k, int m0, int n0) const { return k * g.syk + m0 * g.syc + n0; }
+  __device__ int64_t ldm() const { return g.syc; }
 };
 
 // dx = conv^T(dy, W_t) over ONE stride-parity class of input pixels:
@@ -184,9 +186,9 @@ struct DgradT {
   };
   __device__ State init(int k, int m0, int n0, int tid) const {
     State s;
-    const int KK = g.KH * g.KW, HoWo = g.Ho * g.Wo;
+    const int KK = g.KH * g.KW;
     s.ra = make_rsrc(w + (int64_t)k * KK * g.Cin * g.Cout, (int64_t)KK * g.Cin * g.Cout);
-    s.rb = make_rsrc(dy + (int64_t)k * g.Cout * HoWo, (int64_t)(g.B - 1) * g.ybs + (int64_t)g.Cout * HoWo);
+    s.rb = make_rsrc(dy + k * g.syk, g.yext);
     s.a0 = (unsigned)(((m0 + tid / 8) * g.Cout + 4 * (tid % 8)) * 4);
     const int n = n0 + tid % 64;
     s.nok = n < N();
@@ -194,13 +196,12 @@ struct DgradT {
     const uint32_t ihc = udiv(p, d_wc), iwc = p - ihc * Wc;
     s.ih = ca + (int)ihc * g.stride + g.pad;
     s.iw = cb + (int)iwc * g.stride + g.pad;
-    s.yoff = (int)(bb * g.ybs) + (tid / 64) * HoWo;
+    s.yoff = (int)(bb * g.syb + (tid / 64) * g.syc);
     return s;
   }
   __device__ void load(const State& s, int r0, float (&a)[8], float (&b)[8]) const {
     const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
     const int kh = uni(ckh[slot]), kw = uni(ckw[slot]);
-    const int HoWo = g.Ho * g.Wo;
     const int abase = ((kh * g.KW + kw) * g.Cin * g.Cout + co0) * 4;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -213,16 +214,22 @@ struct DgradT {
     const int oh = g.stride == 1 ? nh : nh / g.stride, ow = g.stride == 1 ? nw : nw / g.stride;
     const bool ok = s.nok && nh >= 0 && nw >= 0 && oh < g.Ho && ow < g.Wo;
     const unsigned vb = ok ? (unsigned)((s.yoff + oh * g.Wo + ow) * 4) : SENT;
-    const int cb0 = co0 * HoWo * 4;
+    const int cs = (int)g.syc;  // channel stride
+    const int cb0 = co0 * cs * 4;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, cb0 + i * 4 * HoWo * 4);
+    for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, cb0 + i * 4 * cs * 4);
   }
   __device__ void store(int k, int m, int n, float v) const {
     const uint32_t bb = udiv(n, d_hcwc), p = n - bb * Hc * Wc;
     const uint32_t ihc = udiv(p, d_wc), iwc = p - ihc * Wc;
     const int ih = ca + (int)ihc * g.stride, iw = cb + (int)iwc * g.stride;
-    dx[bb * g.xbs + ((int64_t)k * g.Cin + m) * g.H * g.W + ih * g.W + iw] = v;
+    dx[k * g.sxk + m * g.sxc + bb * g.sxb + ih * g.W + iw] = v;
   }
+  // stride 1 (the one class is every pixel): dx[k][m][n] is linear in n
+  __device__ bool linear() const { return g.stride == 1; }
+  __device__ float* out() const { return dx; }
+  __device__ int64_t tile_base(int k, int m0, int n0) const { return k * g.sxk + m0 * g.sxc + n0; }
+  __device__ int64_t ldm() const { return g.sxc; }
 };
 
 // The parity classes of a dgrad (stride^2 of them, fewer when H or W < stride).
@@ -270,51 +277,57 @@ struct WgtT {
   };
   __device__ State init(int k, int m0, int n0, int tid) const {
     State s;
-    const int HW = g.H * g.W, HoWo = g.Ho * g.Wo;
-    s.ra = make_rsrc(x + (int64_t)k * g.Cin * HW, (int64_t)(g.B - 1) * g.xbs + (int64_t)g.Cin * HW);
-    s.rb = make_rsrc(dy + (int64_t)k * g.Cout * HoWo, (int64_t)(g.B - 1) * g.ybs + (int64_t)g.Cout * HoWo);
+    s.ra = make_rsrc(x + k * g.sxk, g.xext);
+    s.rb = make_rsrc(dy + k * g.syk, g.yext);
     const int slot = uni(m0 / g.Cin), ci0 = m0 - slot * g.Cin;
     s.kh = uni(g.tap_kh[slot]);
     s.kw = uni(g.tap_kw[slot]);
-    s.aoff = (ci0 + tid / 32) * HW;
-    s.boff = BVEC ? (n0 + tid / 8) * HoWo : (n0 + tid / 32) * HoWo;
+    s.aoff = (int)((ci0 + tid / 32) * g.sxc);
+    s.boff = (int)((BVEC ? (n0 + tid / 8) : (n0 + tid / 32)) * g.syc);
     return s;
   }
   __device__ void load(const State& s, int r0, float (&a)[8], float (&b)[8]) const {
     const int tid = threadIdx.x;
-    const int HW = g.H * g.W, HoWo = g.Ho * g.Wo, R = this->R();
+    const int HoWo = g.Ho * g.Wo, R = this->R();
     {  // A: x gathered at q = r0 + tid % 32
       const int q = r0 + tid % 32;
       const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
       const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
       const int ih = (int)oh * g.stride - g.pad + s.kh, iw = (int)ow * g.stride - g.pad + s.kw;
       const bool ok = q < R && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-      const unsigned va = ok ? (unsigned)(((int)(bb * g.xbs) + s.aoff + ih * g.W + iw) * 4) : SENT;
+      const unsigned va = ok ? (unsigned)(((int)(bb * g.sxb) + s.aoff + ih * g.W + iw) * 4) : SENT;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = ld1(s.ra, va, i * 8 * HW * 4);
+      for (int i = 0; i < 8; ++i) a[i] = ld1(s.ra, va, i * 8 * (int)g.sxc * 4);
     }
     if constexpr (BVEC) {  // B: dy[b][co][p .. p+3], q = r0 + 4 (tid % 8)
       const int q = r0 + 4 * (tid % 8);
       const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
-      const unsigned vb = q < R ? (unsigned)(((int)(bb * g.ybs) + s.boff + (int)p) * 4) : SENT;
+      const unsigned vb = q < R ? (unsigned)(((int)(bb * g.syb) + s.boff + (int)p) * 4) : SENT;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const f32x4 v = ld4(s.rb, vb, i * 32 * HoWo * 4);
+        const f32x4 v = ld4(s.rb, vb, i * 32 * (int)g.syc * 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) b[4 * i + e] = v[e];
       }
     } else {  // B: dy gathered at q = r0 + tid % 32
       const int q = r0 + tid % 32;
       const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
-      const unsigned vb = q < R ? (unsigned)(((int)(bb * g.ybs) + s.boff + (int)p) * 4) : SENT;
+      const unsigned vb = q < R ? (unsigned)(((int)(bb * g.syb) + s.boff + (int)p) * 4) : SENT;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, i * 8 * HoWo * 4);
+      for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, i * 8 * (int)g.syc * 4);
     }
   }
   __device__ void store(int k, int m, int n, float v) const {
-    const int slot = m / g.Cin, ci = m - slot * g.Cin;
+    const int slot = (int)udiv(m, g.d_cin), ci = m - slot * g.Cin;
     dw[(((int64_t)k * g.KH * g.KW + tap_index(g, slot)) * g.Cin + ci) * g.Cout + n] = v;
   }
+  __device__ bool linear() const { return true; }
+  __device__ float* out() const { return dw; }
+  __device__ int64_t tile_base(int k, int m0, int n0) const {
+    const int slot = m0 / g.Cin, ci0 = m0 - slot * g.Cin;
+    return (((int64_t)k * g.KH * g.KW + tap_index(g, slot)) * g.Cin + ci0) * g.Cout + n0;
+  }
+  __device__ int64_t ldm() const { return g.Cout; }
 };
 
 // ---- explicit im2col (short reductions: the stem) -----------------------------
@@ -363,10 +376,12 @@ struct DenseFwd {  // y[co][pix] = sum_r wp[co][r] col[pix][r]: M = Cout, N = B*
       }
     }
   }
-  __device__ void store(int k, int m, int n, float v) const {
-    const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
-    y[bb * g.ybs + ((int64_t)k * g.Cout + m) * g.Ho * g.Wo + p] = v;
-  }
+  // y[k][m][n]: n = b*Ho*Wo + p is linear in the [K][C][B][Ho][Wo] layout
+  __device__ void store(int k, int m, int n, float v) const { y[k * g.syk + m * g.syc + n] = v; }
+  __device__ bool linear() const { return true; }
+  __device__ float* out() const { return y; }
+  __device__ int64_t tile_base(int k, int m0, int n0) const { return k * g.syk + m0 * g.syc + n0; }
+  __device__ int64_t ldm() const { return g.syc; }
 };
 
 struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N = RP, R = B*Ho*Wo (HoWo % 4 == 0)
@@ -387,10 +402,9 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
   };
   __device__ State init(int k, int m0, int n0, int tid) const {
     State s;
-    const int HoWo = g.Ho * g.Wo;
-    s.ra = make_rsrc(dy + (int64_t)k * g.Cout * HoWo, (int64_t)(g.B - 1) * g.ybs + (int64_t)g.Cout * HoWo);
+    s.ra = make_rsrc(dy + k * g.syk, g.yext);
     s.rb = make_rsrc(col + (int64_t)k * R() * RP, (int64_t)R() * RP);
-    s.arow = (m0 + tid / 8) * HoWo;
+    s.arow = (int)((m0 + tid / 8) * g.syc);
 #pragma unroll
     for (int i = 0; i < 2; ++i) s.aok[i] = m0 + tid / 8 + 32 * i < M();
     const int n = n0 + 4 * (tid % 16);
@@ -402,10 +416,10 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
     const int tid = threadIdx.x, HoWo = g.Ho * g.Wo, R = this->R();
     const int q = r0 + 4 * (tid % 8);
     const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
-    const unsigned va = (unsigned)(((int)(bb * g.ybs) + s.arow + (int)p) * 4);
+    const unsigned va = (unsigned)(((int)(bb * g.syb) + s.arow + (int)p) * 4);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const f32x4 qa = ld4(s.ra, (q < R && s.aok[i]) ? va + (unsigned)(i * 32 * HoWo * 4) : SENT, 0);
+      const f32x4 qa = ld4(s.ra, (q < R && s.aok[i]) ? va + (unsigned)(i * 32 * (int)g.syc * 4) : SENT, 0);
       const int pix = r0 + tid / 16 + 16 * i;
       const f32x4 qb = ld4(s.rb, (pix < R && s.nok) ? s.b0 + (unsigned)((r0 + 16 * i) * RP * 4) : SENT, 0);
 #pragma unroll
@@ -416,6 +430,10 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
     }
   }
   __device__ void store(int k, int m, int n, float v) const { dwp[((int64_t)k * g.Cout + m) * RP + n] = v; }
+  __device__ bool linear() const { return true; }
+  __device__ float* out() const { return dwp; }
+  __device__ int64_t tile_base(int k, int m0, int n0) const { return ((int64_t)k * g.Cout + m0) * RP + n0; }
+  __device__ int64_t ldm() const { return RP; }
 };
 
 // col[k][pix][RP] (grid: pixel blocks x K).  A workgroup builds IM_PB whole
@@ -430,7 +448,7 @@ __global__ __launch_bounds__(THREADS) void im2col_kernel(const Geom g, const flo
   const int N = g.B * g.Ho * g.Wo, CK = g.Cin * g.KH, R = CK * g.KW;
   const int pix0 = blockIdx.x * IM_PB;
   const int np = min(IM_PB, N - pix0);
-  const float* xk = x + (int64_t)k * g.Cin * g.H * g.W;
+  const float* xk = x + k * g.sxk;
   for (int e = threadIdx.x; e < np * CK; e += THREADS) {
     const int pl = e / CK, j = e - pl * CK;
     const int ci = j / g.KH, kh = j - ci * g.KH;
@@ -439,7 +457,7 @@ __global__ __launch_bounds__(THREADS) void im2col_kernel(const Geom g, const flo
     const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
     const int ih = (int)oh * g.stride - g.pad + kh, iw0 = (int)ow * g.stride - g.pad;
     const bool hok = ih >= 0 && ih < g.H;
-    const float* src = xk + bb * g.xbs + (int64_t)ci * g.H * g.W + (int64_t)ih * g.W;
+    const float* src = xk + bb * g.sxb + ci * g.sxc + (int64_t)ih * g.W;
     float* dst = rows + pl * RP + j * g.KW;
     for (int kw = 0; kw < g.KW; ++kw) {
       const int iw = iw0 + kw;
@@ -514,6 +532,17 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
     cur ^= 1;
   }
   // C/D map of the 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+  if (S == 1 && pl.linear()) {  // one tile base, then row * ldm + col per element
+    float* base = pl.out() + pl.tile_base(k, m0, n0);
+    const int64_t ldm = pl.ldm();
+    const int nl = 32 * wn + l32;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int ml = 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (m0 + ml < M && n0 + nl < N) base[ml * ldm + nl] = acc[e];
+    }
+    return;
+  }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int m = m0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
@@ -527,12 +556,14 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
 
 template <class Plan>
 __global__ void treduce_kernel(const Plan pl, int S, const float* __restrict__ part) {
+  // grid (cdiv(M*N, 256), K): one client per grid row, 32-bit index math
   const int M = pl.M(), N = pl.N(), K = pl.g.Kc;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t MN = (int64_t)M * N;
-  if (idx >= MN * K) return;
-  const int k = (int)(idx / MN);
-  const int m = (int)((idx % MN) / N), n = (int)(idx % N);
+  if (e >= MN) return;
+  const int m = e / N, n = e - m * N;
+  const int64_t idx = k * MN + e;
   float v = part[idx];
   for (int s = 1; s < S; ++s) v += part[(int64_t)s * MN * K + idx];
   pl.store(k, m, n, v);
@@ -573,8 +604,8 @@ int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char
   hipLaunchKernelGGL(tgemm_kernel<Plan>, grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws));
   int rc = launch_status(name);
   if (rc != FLR_OK || S == 1) return rc;
-  const int64_t total = (int64_t)M * N * K;
-  hipLaunchKernelGGL(treduce_kernel<Plan>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, pl, S,
+  const int64_t mn = (int64_t)M * N;
+  hipLaunchKernelGGL(treduce_kernel<Plan>, dim3((unsigned)((mn + 255) / 256), (unsigned)K), dim3(256), 0, st, pl, S,
                      static_cast<const float*>(ws));
   return launch_status(name);
 }

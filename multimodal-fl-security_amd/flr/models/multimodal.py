@@ -187,8 +187,9 @@ def from_tap_major(w_t: torch.Tensor) -> torch.Tensor:
 
 def _gconv(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, need_dx: bool = True,
            tap_major: bool = False, zero_dead: bool = True) -> torch.Tensor:
-    """x [B, K*Cin, H, W], w [K, Cout, Cin, kh, kw] (or [K, kh, kw, Cin, Cout]
-    when tap_major) -> [B, K*Cout, H', W']."""
+    """w [K, Cout, Cin, kh, kw] (or [K, kh, kw, Cin, Cout] when tap_major).
+    Native (flr kernels): x [K*Cin, B, H, W] -> [K*Cout, B, H', W'];
+    torch: x [B, K*Cin, H, W] -> [B, K*Cout, H', W'] (grouped conv)."""
     if tap_major:
         if not x.is_cuda:
             raise RuntimeError("tap-major conv weights need the HIP kernels (no CPU path)")
@@ -253,9 +254,13 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
         return _gconv(x, p[name], stride, pad, need_dx, name in tap_major, name not in skip_dead)
 
     K, B = images.shape[:2]
-    x = images.transpose(0, 1).reshape(B, K * spec.in_channels, *images.shape[3:])
+    native = _LAYERS == "native" and images.is_cuda
+    if native:  # the flr kernels' client-channel-major layout [K*C, B, H, W]
+        x = images.transpose(1, 2).reshape(K * spec.in_channels, B, *images.shape[3:])
+    else:       # torch's grouped-conv layout [B, K*C, H, W]
+        x = images.transpose(0, 1).reshape(B, K * spec.in_channels, *images.shape[3:])
     x = _bn_act(conv("conv1.weight", x, 2, 3, need_dx=False), p["bn1.weight"], p["bn1.bias"])
-    if _LAYERS == "native" and x.is_cuda:
+    if native:
         from ..nn import client_maxpool2d
         x = client_maxpool2d(x, 3, 2, 1)
     else:
@@ -272,7 +277,10 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
             y = _bn_act(conv(pre + "conv1.weight", x, stride, 1), p[pre + "bn1.weight"], p[pre + "bn1.bias"])
             x = _bn_act(conv(pre + "conv2.weight", y, 1, 1), p[pre + "bn2.weight"], p[pre + "bn2.bias"],
                         residual=idt)
-    img = x.mean(dim=(2, 3)).view(B, K, w[-1]).transpose(0, 1)  # [K, B, 512]
+    if native:
+        img = x.mean(dim=(2, 3)).view(K, w[-1], B).transpose(1, 2)  # [K, B, 512]
+    else:
+        img = x.mean(dim=(2, 3)).view(B, K, w[-1]).transpose(0, 1)
 
     # text: embedding gather + GRU with per-client weights (gate order r, z, n)
     V, E, H = spec.vocab, spec.embed, spec.hidden

@@ -18,19 +18,20 @@ def _workspace(geom, device):
 
 
 class ClientConv2d(torch.autograd.Function):
-    """y[B, K*Cout, Ho, Wo] = conv(x[B, K*Cin, H, W], w[K, Cout, Cin, KH, KW]) per client
-    (flr_conv2d_fwd / _bwd_data / _bwd_weight)."""
+    """y[K*Cout, B, Ho, Wo] = conv(x[K*Cin, B, H, W], w[K, Cout, Cin, KH, KW]) per client
+    (flr_conv2d_fwd / _bwd_data / _bwd_weight).  Activations are in the
+    engine's client-channel-major layout [K][C][B][H][W]."""
 
     @staticmethod
     def forward(ctx, x, w, stride: int, pad: int, need_dx: bool = True):
         x = x.contiguous()
         w = w.contiguous()
         K, Cout, Cin, KH, KW = w.shape
-        B, KC, H, W = x.shape
+        KC, B, H, W = x.shape
         assert KC == K * Cin, (x.shape, w.shape)
         Ho = (H + 2 * pad - KH) // stride + 1
         Wo = (W + 2 * pad - KW) // stride + 1
-        y = torch.empty(B, K * Cout, Ho, Wo, dtype=x.dtype, device=x.device)
+        y = torch.empty(K * Cout, B, Ho, Wo, dtype=x.dtype, device=x.device)
         geom = (K, B, Cin, H, W, Cout, KH, KW, stride, pad)
         ws, n = _workspace(geom, x.device)
         _capi.call("flr_conv2d_fwd", x.data_ptr(), w.data_ptr(), y.data_ptr(), *geom,
@@ -69,11 +70,11 @@ class ClientConv2dT(torch.autograd.Function):
         w_t = w_t.contiguous()
         ctx.zero_dead = zero_dead
         K, KH, KW, Cin, Cout = w_t.shape
-        B, KC, H, W = x.shape
+        KC, B, H, W = x.shape
         assert KC == K * Cin, (x.shape, w_t.shape)
         Ho = (H + 2 * pad - KH) // stride + 1
         Wo = (W + 2 * pad - KW) // stride + 1
-        y = torch.empty(B, K * Cout, Ho, Wo, dtype=x.dtype, device=x.device)
+        y = torch.empty(K * Cout, B, Ho, Wo, dtype=x.dtype, device=x.device)
         geom = (K, B, Cin, H, W, Cout, KH, KW, stride, pad)
         ws, n = _workspace_t(geom, x.device)
         _capi.call("flr_conv2d_fwd_t", x.data_ptr(), w_t.data_ptr(), y.data_ptr(), *geom,
@@ -183,13 +184,15 @@ def _ptr(t):
 
 class ClientBatchNorm(torch.autograd.Function):
     """out = act(BN_train(x) [+ residual]) per (client, channel) plane of the
-    grouped layout x[B, K*C, H, W]; gamma/beta [K, C] (flr_batchnorm_fwd/_bwd)."""
+    client-channel-major layout x[K*C, B, H, W] — each plane is one contiguous
+    run of B*H*W values, passed to flr_batchnorm_fwd/_bwd as B = 1;
+    gamma/beta [K, C]."""
 
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, relu: bool, eps: float):
         x = x.contiguous()
-        B, KC = x.shape[:2]
-        HW = x[0, 0].numel()
+        B, KC = 1, x.shape[0]
+        HW = x[0].numel()
         g = gamma.contiguous()
         b = beta.contiguous()
         assert g.numel() == KC and b.numel() == KC, (x.shape, gamma.shape)
@@ -208,8 +211,8 @@ class ClientBatchNorm(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, g, mean, invstd = ctx.saved_tensors
         dy = dy.contiguous()
-        B, KC = x.shape[:2]
-        HW = x[0, 0].numel()
+        B, KC = 1, x.shape[0]
+        HW = x[0].numel()
         dx = torch.empty_like(x)
         dg = torch.empty_like(g)
         db = torch.empty_like(g)
@@ -225,20 +228,21 @@ def client_batchnorm(x, gamma, beta, residual=None, relu: bool = True, eps: floa
 
 
 class ClientMaxPool2d(torch.autograd.Function):
-    """F.max_pool2d over every (batch, client, channel) plane (flr_maxpool2d_fwd/_bwd)."""
+    """F.max_pool2d over every H x W plane of x[..., H, W] (flr_maxpool2d_fwd/_bwd)."""
 
     @staticmethod
     def forward(ctx, x, k: int, stride: int, pad: int):
         x = x.contiguous()
-        B, KC, H, W = x.shape
+        H, W = x.shape[-2:]
+        planes = x.numel() // (H * W)
         Ho = (H + 2 * pad - k) // stride + 1
         Wo = (W + 2 * pad - k) // stride + 1
-        y = torch.empty(B, KC, Ho, Wo, dtype=x.dtype, device=x.device)
-        arg = torch.empty(B, KC, Ho, Wo, dtype=torch.uint8, device=x.device)
-        _capi.call("flr_maxpool2d_fwd", x.data_ptr(), y.data_ptr(), arg.data_ptr(), B * KC, H, W, k, k, stride, pad,
+        y = torch.empty(*x.shape[:-2], Ho, Wo, dtype=x.dtype, device=x.device)
+        arg = torch.empty(*x.shape[:-2], Ho, Wo, dtype=torch.uint8, device=x.device)
+        _capi.call("flr_maxpool2d_fwd", x.data_ptr(), y.data_ptr(), arg.data_ptr(), planes, H, W, k, k, stride, pad,
                    _stream(x))
         ctx.save_for_backward(arg)
-        ctx.geom = (B * KC, H, W, k, k, stride, pad)
+        ctx.geom = (planes, H, W, k, k, stride, pad)
         ctx.xshape = x.shape
         return y
 

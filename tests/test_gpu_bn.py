@@ -1,5 +1,6 @@
 """a2: HIP BatchNorm(train) + residual + ReLU (flr_batchnorm_fwd/_bwd inside
-ClientBatchNorm) vs fp64 torch F.batch_norm on the same grouped layout.
+ClientBatchNorm, on the engine's [K*C, B, H, W] layout) vs fp64 torch
+F.batch_norm on the grouped layout [B, K*C, H, W].
 Covers every plane size of the model (HW = 256, 64, 16, 4, 1), a non power of
 two plane (7x9) and channel counts that leave a wave partially filled."""
 import pytest
@@ -33,10 +34,12 @@ def test_batchnorm_fwd_bwd_vs_fp64(cuda, shape, mode):
     bet = torch.randn(KC, generator=g) * 0.1
     res = torch.randn(B, KC, H, W, generator=g) if with_res else None
     dy = torch.randn(B, KC, H, W, generator=g)
-    ins = [t.to(cuda).requires_grad_(True) for t in (x, gam, bet)]
-    rg = res.to(cuda).requires_grad_(True) if with_res else None
+    # the engine's client-channel-major layout [KC, B, H, W]
+    cb = lambda t: t.transpose(0, 1).contiguous()  # noqa: E731
+    ins = [t.to(cuda).requires_grad_(True) for t in (cb(x), gam, bet)]
+    rg = cb(res).to(cuda).requires_grad_(True) if with_res else None
     y = client_batchnorm(ins[0], ins[1], ins[2], rg, relu)
-    y.backward(dy.to(cuda))
+    y.backward(cb(dy).to(cuda))
     ref = [t.double().requires_grad_(True) for t in (x, gam, bet)]
     rr = res.double().requires_grad_(True) if with_res else None
     yr = F.batch_norm(ref[0], None, None, ref[1], ref[2], training=True, momentum=0.0, eps=1e-5)
@@ -45,9 +48,10 @@ def test_batchnorm_fwd_bwd_vs_fp64(cuda, shape, mode):
     if relu:
         yr = F.relu(yr)
     yr.backward(dy.double())
-    pairs = [(y, yr)] + [(a.grad, r.grad) for a, r in zip(ins, ref)]
+    pairs = [(y.transpose(0, 1), yr), (ins[0].grad.transpose(0, 1), ref[0].grad)]
+    pairs += [(a.grad, r.grad) for a, r in zip(ins[1:], ref[1:])]
     if with_res:
-        pairs.append((rg.grad, rr.grad))
+        pairs.append((rg.grad.transpose(0, 1), rr.grad))
     for got, want in pairs:
         err = (got.detach().cpu().double() - want.detach()).abs().max().item()
         scale = want.detach().abs().max().item()

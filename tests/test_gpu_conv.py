@@ -1,4 +1,5 @@
-"""GPU: the client-batched conv kernels vs fp64 grouped convolution (torch CPU)."""
+"""GPU: the client-batched conv kernels (activations [K*C, B, H, W]) vs fp64
+grouped convolution (torch CPU, [B, K*C, H, W])."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -6,6 +7,11 @@ import torch.nn.functional as F
 from flr.nn import client_conv2d
 
 pytestmark = pytest.mark.gpu
+
+
+def cb(t):
+    """torch's grouped layout [B, K*C, H, W] -> the engine's [K*C, B, H, W]."""
+    return t.transpose(0, 1).contiguous()
 
 SHAPES = [  # (K, B, Cin, H, W, Cout, KH, stride, pad)
     (3, 4, 3, 32, 32, 8, 7, 2, 3),     # stem 7x7/2
@@ -31,16 +37,16 @@ def test_conv_fwd_bwd_vs_fp64(cuda, shape):
     g = torch.Generator(device="cpu").manual_seed(sum(shape))
     x = torch.randn(B, K * Cin, H, W, generator=g)
     w = torch.randn(K, Cout, Cin, KS, KS, generator=g) * 0.1
-    xg = x.to(cuda).requires_grad_(True)
+    xg = cb(x).to(cuda).requires_grad_(True)
     wg = w.to(cuda).requires_grad_(True)
-    y = client_conv2d(xg, wg, stride, pad)
+    y = client_conv2d(xg, wg, stride, pad).transpose(0, 1)
     dy = torch.randn(y.shape, generator=g)
     y.backward(dy.to(cuda))
     xd = x.double().requires_grad_(True)
     wd = w.double().requires_grad_(True)
     yr = F.conv2d(xd, wd.reshape(K * Cout, Cin, KS, KS), stride=stride, padding=pad, groups=K)
     yr.backward(dy.double())
-    for got, ref in ((y, yr), (xg.grad, xd.grad), (wg.grad, wd.grad)):
+    for got, ref in ((y, yr), (xg.grad.transpose(0, 1), xd.grad), (wg.grad, wd.grad)):
         err = (got.detach().cpu().double() - ref.detach()).abs().max().item()
         scale = ref.detach().abs().max().item()
         assert err <= 2e-6 * max(scale, 1.0), (err, scale)
@@ -68,9 +74,9 @@ def test_tap_major_conv_vs_fp64(cuda, shape):
     g = torch.Generator(device="cpu").manual_seed(sum(shape) + 1)
     x = torch.randn(B, K * Cin, H, W, generator=g)
     w = torch.randn(K, Cout, Cin, KS, KS, generator=g) * 0.1
-    xg = x.to(cuda).requires_grad_(True)
+    xg = cb(x).to(cuda).requires_grad_(True)
     wt = to_tap_major(w).contiguous().to(cuda).requires_grad_(True)
-    y = client_conv2d_t(xg, wt, stride, pad)
+    y = client_conv2d_t(xg, wt, stride, pad).transpose(0, 1)
     dy = torch.randn(y.shape, generator=g)
     y.backward(dy.to(cuda))
     xd = x.double().requires_grad_(True)
@@ -78,7 +84,7 @@ def test_tap_major_conv_vs_fp64(cuda, shape):
     yr = F.conv2d(xd, wd.reshape(K * Cout, Cin, KS, KS), stride=stride, padding=pad, groups=K)
     yr.backward(dy.double())
     dw = from_tap_major(wt.grad.detach().cpu())
-    for got, ref in ((y, yr), (xg.grad, xd.grad), (dw, wd.grad)):
+    for got, ref in ((y, yr), (xg.grad.transpose(0, 1), xd.grad), (dw, wd.grad)):
         err = (got.detach().cpu().double() - ref.detach()).abs().max().item()
         scale = ref.detach().abs().max().item()
         assert err <= 2e-6 * max(scale, 1.0), (err, scale)

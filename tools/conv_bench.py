@@ -57,7 +57,7 @@ def main():
             "dgrad": lambda: _capi.call("flr_conv2d_bwd_data" + sfx, dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
                                         *geom, wsp, n, st),
             "wgrad": lambda: _capi.call("flr_conv2d_bwd_weight" + sfx, x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
-                                        *geom, *((1,) if tm else ()), wsp, n, st),
+                                        *geom, *((0,) if tm else ()), wsp, n, st),  # dead taps skipped, as in training
         }
         flops = 2.0 * K * B * Ho * Ho * Cout * Cin * nt
         for op, fn in calls.items():
