@@ -1,7 +1,7 @@
 // a2 — 2-D max pooling of the image branch (the ResNet stem's 3x3/2 pad-1
 // max-pool; the reference's conv blocks pool with nn.MaxPool2d,
-// src/models/cub200_cnn.py:71-77 template), forward and backward, on the
-// client-batched activation layout x[B][K*C][H][W] (planes are independent).
+// src/models/cub200_cnn.py:71-77 template), forward and backward, over the
+// independent H x W planes of the engine's [K][C][B][H][W] activations.
 //
 // torch's CPU kernel (aten/src/ATen/native/cpu/MaxPoolKernel.cpp) is restated:
 // the window is scanned row-major over its in-bounds elements and the first
@@ -13,7 +13,7 @@
 // Forward: one lane per output; the argmax is kept as a 1-byte window offset
 // (kh*KW + kw).  Backward: one lane per INPUT element, gathering from the <=
 // ceil(KH/S)*ceil(KW/S) windows that contain it, in raster order.
-#include "flr_common.h"
+#include "conv_common.h"
 
 namespace flr {
 namespace pool {
@@ -22,17 +22,17 @@ constexpr int THREADS = 256;
 
 struct PoolGeom {
   int H, W, Ho, Wo, KH, KW, S, P;
+  conv::FastDiv d_hw, d_w, d_howo, d_wo;  // 32-bit index math (total < 2^31)
 };
 
 __global__ __launch_bounds__(THREADS) void fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                       uint8_t* __restrict__ arg, int64_t nplanes, PoolGeom g) {
-  const int64_t idx = (int64_t)blockIdx.x * THREADS + threadIdx.x;
-  const int64_t total = nplanes * g.Ho * g.Wo;
-  if (idx >= total) return;
-  const int64_t plane = idx / (g.Ho * g.Wo);
+  const uint32_t idx = blockIdx.x * THREADS + threadIdx.x;
+  if (idx >= (uint32_t)(nplanes * g.Ho * g.Wo)) return;
+  const uint32_t plane = conv::udiv(idx, g.d_howo);
   const int o = (int)(idx - plane * g.Ho * g.Wo);
-  const int oh = o / g.Wo, ow = o - oh * g.Wo;
-  const float* xp = x + plane * g.H * g.W;
+  const int oh = (int)conv::udiv(o, g.d_wo), ow = o - oh * g.Wo;
+  const float* xp = x + (int64_t)plane * g.H * g.W;
   const int ih0 = oh * g.S - g.P, iw0 = ow * g.S - g.P;
   float best = -__builtin_huge_valf();
   int bi = -1;
@@ -56,17 +56,16 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(const float* __restrict__ 
 
 __global__ __launch_bounds__(THREADS) void bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ arg,
                                                       float* __restrict__ dx, int64_t nplanes, PoolGeom g) {
-  const int64_t idx = (int64_t)blockIdx.x * THREADS + threadIdx.x;
-  const int64_t total = nplanes * g.H * g.W;
-  if (idx >= total) return;
-  const int64_t plane = idx / (g.H * g.W);
+  const uint32_t idx = blockIdx.x * THREADS + threadIdx.x;
+  if (idx >= (uint32_t)(nplanes * g.H * g.W)) return;
+  const uint32_t plane = conv::udiv(idx, g.d_hw);
   const int e = (int)(idx - plane * g.H * g.W);
-  const int ih = e / g.W, iw = e - ih * g.W;
+  const int ih = (int)conv::udiv(e, g.d_w), iw = e - ih * g.W;
   // windows oh with oh*S - P <= ih <= oh*S - P + KH - 1
   const int oh_lo = max(0, (ih + g.P - g.KH + g.S) / g.S), oh_hi = min(g.Ho - 1, (ih + g.P) / g.S);
   const int ow_lo = max(0, (iw + g.P - g.KW + g.S) / g.S), ow_hi = min(g.Wo - 1, (iw + g.P) / g.S);
-  const float* dyp = dy + plane * g.Ho * g.Wo;
-  const uint8_t* ap = arg + plane * g.Ho * g.Wo;
+  const float* dyp = dy + (int64_t)plane * g.Ho * g.Wo;
+  const uint8_t* ap = arg + (int64_t)plane * g.Ho * g.Wo;
   float acc = 0.f;
   for (int oh = oh_lo; oh <= oh_hi; ++oh) {
     const int kh = ih - (oh * g.S - g.P);
@@ -84,7 +83,12 @@ inline bool geom(int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t S, int64_
   g.H = (int)H; g.W = (int)W; g.KH = (int)KH; g.KW = (int)KW; g.S = (int)S; g.P = (int)P;
   g.Ho = (int)((H + 2 * P - KH) / S + 1);
   g.Wo = (int)((W + 2 * P - KW) / S + 1);
-  return g.Ho >= 1 && g.Wo >= 1;
+  if (g.Ho < 1 || g.Wo < 1) return false;
+  g.d_hw = conv::make_fastdiv((uint32_t)(H * W));
+  g.d_w = conv::make_fastdiv((uint32_t)W);
+  g.d_howo = conv::make_fastdiv((uint32_t)(g.Ho * g.Wo));
+  g.d_wo = conv::make_fastdiv((uint32_t)g.Wo);
+  return true;
 }
 
 }  // namespace pool
@@ -96,6 +100,7 @@ extern "C" int flr_maxpool2d_fwd(const float* x, float* y, uint8_t* argmax, int6
                                  int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* stream) {
   pool::PoolGeom g;
   if (!x || !y || !argmax || nplanes < 0 || !pool::geom(H, W, KH, KW, stride, pad, g)) return FLR_ERR_ARG;
+  if (nplanes * H * W >= ((int64_t)1 << 31)) return FLR_ERR_UNSUPPORTED;
   const int64_t total = nplanes * g.Ho * g.Wo;
   if (total == 0) return FLR_OK;
   hipLaunchKernelGGL(pool::fwd_kernel, dim3((unsigned)((total + pool::THREADS - 1) / pool::THREADS)),
@@ -107,6 +112,7 @@ extern "C" int flr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* 
                                  int64_t W, int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* stream) {
   pool::PoolGeom g;
   if (!dy || !dx || !argmax || nplanes < 0 || !pool::geom(H, W, KH, KW, stride, pad, g)) return FLR_ERR_ARG;
+  if (nplanes * H * W >= ((int64_t)1 << 31)) return FLR_ERR_UNSUPPORTED;
   const int64_t total = nplanes * H * W;
   if (total == 0) return FLR_OK;
   hipLaunchKernelGGL(pool::bwd_kernel, dim3((unsigned)((total + pool::THREADS - 1) / pool::THREADS)),
