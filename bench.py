@@ -157,8 +157,10 @@ def main() -> None:
     achieved = pair_bytes / (kernel_ms * 1e-3) / 1e9
     # training-phase time (one round's local updates, this rank's clients)
     ev0.record()
-    eng.trainer.load_global(eng.global_flat)
-    eng.trainer.local_update(eng.batches, eng.masks)
+    if eng._graph is not None:
+        eng._graph.replay()
+    else:
+        eng._train_phase()
     ev1.record()
     torch.cuda.synchronize()
     train_ms = ev0.elapsed_time(ev1)
@@ -188,6 +190,7 @@ def main() -> None:
                 "one all-to-all (client rows -> coordinate ranges), per-GPU aggregation of its range, "
                 "all-gather of the aggregated vector" if sharded else "one all-gather of the client matrix")),
             "exchange": eng.exchange,
+            "training_phase": "one captured HIP graph per round" if eng.use_graph else "eager launches",
         },
         "aggregate_ms": aggregate_ms,
         "train_ms_per_round": train_ms,

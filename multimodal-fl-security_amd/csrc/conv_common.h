@@ -27,6 +27,34 @@ __device__ __forceinline__ uint32_t udiv(uint32_t n, const FastDiv& f) { return 
 
 constexpr int MAXTAPS = 49;
 
+// A tap list that is a (strided) rectangle: slot -> (kh0 + step*(slot / nkw),
+// kw0 + step*(slot % nkw)).  Kernels decode a reduction slot with scalar
+// arithmetic instead of indexing the by-value tap table, which the compiler
+// can only read with a vector-memory load per K-tile (a full load latency on
+// the critical path).  ok = false: the list is not a rectangle (use the table).
+struct TapRect {
+  int kh0, kw0, nkw, step;
+  bool ok;
+};
+inline TapRect make_rect(const int8_t* kh, const int8_t* kw, int n, int step) {
+  TapRect r{0, 0, 1, step, false};
+  if (n == 0) { r.ok = true; return r; }
+  r.kh0 = kh[0]; r.kw0 = kw[0];
+  int nkw = 0;
+  while (nkw < n && kh[nkw] == kh[0]) ++nkw;
+  r.nkw = nkw;
+  if (n % nkw != 0) return r;
+  for (int t = 0; t < n; ++t)
+    if (kh[t] != r.kh0 + step * (t / nkw) || kw[t] != r.kw0 + step * (t % nkw)) return r;
+  r.ok = true;
+  return r;
+}
+__device__ __forceinline__ void rect_tap(const TapRect& r, int slot, int& kh, int& kw) {
+  const int i = slot / r.nkw;
+  kh = r.kh0 + r.step * i;
+  kw = r.kw0 + r.step * (slot - i * r.nkw);
+}
+
 struct Geom {
   int Kc, B, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo;
   // Activation layout x[K][Cin][B][H][W], y[K][Cout][B][Ho][Wo] ("client-
@@ -40,6 +68,7 @@ struct Geom {
   // so the reduction runs over (valid tap, channel) only: r = slot * C + c.
   int ntaps;
   int8_t tap_kh[MAXTAPS], tap_kw[MAXTAPS];
+  TapRect rect;  // the live taps as a rectangle (step 1), when they are one
 };
 
 inline Geom make_geom(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH,
@@ -73,6 +102,7 @@ inline Geom make_geom(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, i
       if (hv && wv) { g.tap_kh[g.ntaps] = (int8_t)kh; g.tap_kw[g.ntaps] = (int8_t)kw; ++g.ntaps; }
     }
   }
+  g.rect = make_rect(g.tap_kh, g.tap_kw, g.ntaps, 1);
   return g;
 }
 

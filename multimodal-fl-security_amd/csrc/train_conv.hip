@@ -191,7 +191,8 @@ struct FwdF : FwdG {  // A fast along r (ci), B fast along n (pixels)
   __device__ void load(const State& s, int r0, int re, float (&ra)[8], float (&rb)[8]) const {
     const int slot = __builtin_amdgcn_readfirstlane(r0 / g.Cin);
     const int ci0 = r0 - slot * g.Cin;
-    const int kh = g.tap_kh[slot], kw = g.tap_kw[slot];
+    int kh, kw;
+    if (g.rect.ok) rect_tap(g.rect, slot, kh, kw); else { kh = g.tap_kh[slot]; kw = g.tap_kw[slot]; }
     const int KK = g.KH * g.KW, HW = (int)g.sxc;  // channel stride
     const int aoff = ci0 * KK + kh * g.KW + kw;
 #pragma unroll
@@ -232,7 +233,8 @@ struct DgradF : DgradG {  // A fast along m (ci), B fast along n (input pixels)
   __device__ void load(const State& s, int r0, int re, float (&ra)[8], float (&rb)[8]) const {
     const int slot = __builtin_amdgcn_readfirstlane(r0 / g.Cout);
     const int co0 = r0 - slot * g.Cout;
-    const int kh = g.tap_kh[slot], kw = g.tap_kw[slot];
+    int kh, kw;
+    if (g.rect.ok) rect_tap(g.rect, slot, kh, kw); else { kh = g.tap_kh[slot]; kw = g.tap_kw[slot]; }
     const int KK = g.KH * g.KW, HoWo = (int)g.syc;  // channel stride
     const int aoff = co0 * g.Cin * KK + kh * g.KW + kw;
 #pragma unroll

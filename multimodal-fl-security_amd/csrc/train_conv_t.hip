@@ -99,7 +99,16 @@ __device__ __forceinline__ f32x4 frag(const float* buf, int rb, int j, int h) {
 
 // ---- load plans ---------------------------------------------------------------
 // Tap of a reduction slot: W_t offset of (tap, 0, 0) = tap_index * Cin * Cout.
-__device__ __forceinline__ int tap_index(const Geom& g, int slot) { return g.tap_kh[slot] * g.KW + g.tap_kw[slot]; }
+// (kh, kw) of a tile-uniform reduction slot, by rectangle arithmetic (the host
+// accepts only geometries whose live taps form a rectangle: args_ok)
+__device__ __forceinline__ void slot_tap(const Geom& g, int slot, int& kh, int& kw) {
+  conv::rect_tap(g.rect, slot, kh, kw);
+}
+__device__ __forceinline__ int tap_index(const Geom& g, int slot) {
+  int kh, kw;
+  slot_tap(g, slot, kh, kw);
+  return kh * g.KW + kw;
+}
 // Tile-uniform values the compiler cannot prove uniform (the tap table is
 // indexed by a computed slot): broadcast so they live in SGPRs and the buffer
 // loads that take them as soffset need no waterfall loop.
@@ -137,7 +146,10 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
   }
   __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
     const int slot = uni(r0 / g.Cin), ci0 = r0 - slot * g.Cin;
-    const int kh = uni(g.tap_kh[slot]), kw = uni(g.tap_kw[slot]);
+    int kh, kw;
+    slot_tap(g, slot, kh, kw);
+    kh = uni(kh);
+    kw = uni(kw);
     const int arow = ((kh * g.KW + kw) * g.Cin + ci0) * g.Cout * 4;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -148,7 +160,10 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
   }
   __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
     const int slot = uni(r0 / g.Cin), ci0 = r0 - slot * g.Cin;
-    const int kh = uni(g.tap_kh[slot]), kw = uni(g.tap_kw[slot]);
+    int kh, kw;
+    slot_tap(g, slot, kh, kw);
+    kh = uni(kh);
+    kw = uni(kw);
     const int HW = (int)g.sxc;  // channel stride
     const int ih = s.ih0 + kh, iw = s.iw0 + kw;
     const bool ok = s.nok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
@@ -179,6 +194,7 @@ struct DgradT {
   int ca, cb, Hc, Wc, ntc;
   conv::FastDiv d_hcwc, d_wc;
   int8_t ckh[conv::MAXTAPS], ckw[conv::MAXTAPS];
+  conv::TapRect crect;  // the class taps: a rectangle of step = stride
   static constexpr int LA = RK_VEC, LB = KR_GATHER;
   __host__ __device__ int M() const { return g.Cin; }
   __host__ __device__ int N() const { return g.B * Hc * Wc; }
@@ -206,7 +222,10 @@ struct DgradT {
   }
   __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
     const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
-    const int kh = uni(ckh[slot]), kw = uni(ckw[slot]);
+    int kh, kw;
+    conv::rect_tap(crect, slot, kh, kw);
+    kh = uni(kh);
+    kw = uni(kw);
     const int abase = ((kh * g.KW + kw) * g.Cin * g.Cout + co0) * 4;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -217,7 +236,10 @@ struct DgradT {
   }
   __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
     const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
-    const int kh = uni(ckh[slot]), kw = uni(ckw[slot]);
+    int kh, kw;
+    conv::rect_tap(crect, slot, kh, kw);
+    kh = uni(kh);
+    kw = uni(kw);
     // the class guarantees (ih + pad - kh) % stride == 0
     const int nh = s.ih - kh, nw = s.iw - kw;
     const int oh = g.stride == 1 ? nh : nh / g.stride, ow = g.stride == 1 ? nw : nw / g.stride;
@@ -263,6 +285,7 @@ inline int dgrad_classes(const Geom& g, DgradT* out) {
         c.ckw[c.ntc] = (int8_t)kw;
         ++c.ntc;
       }
+      c.crect = conv::make_rect(c.ckh, c.ckw, c.ntc, g.stride);
     }
   return n;
 }
@@ -289,8 +312,10 @@ struct WgtT {
     s.ra = make_rsrc(x + k * g.sxk, g.xext);
     s.rb = make_rsrc(dy + k * g.syk, g.yext);
     const int slot = uni(m0 / g.Cin), ci0 = m0 - slot * g.Cin;
-    s.kh = uni(g.tap_kh[slot]);
-    s.kw = uni(g.tap_kw[slot]);
+    int kh, kw;
+    slot_tap(g, slot, kh, kw);
+    s.kh = uni(kh);
+    s.kw = uni(kw);
     s.aoff = (int)((ci0 + tid / 32) * g.sxc);
     s.boff = (int)((BVEC ? (n0 + tid / 8) : (n0 + tid / 32)) * g.syc);
     return s;
@@ -757,8 +782,19 @@ inline bool args_ok(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int
                     int64_t stride, int64_t pad) {
   if (!conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) || !shape_ok(Cin, Cout)) return false;
   // byte offsets inside one client's buffer view must fit the 31-bit voffset
-  return B * K * Cin * H * W * 4 < (int64_t(1) << 31) && B * K * Cout * H * W * 4 < (int64_t(1) << 31) &&
-         KH * KW * Cin * Cout * 4 < (int64_t(1) << 31);
+  if (!(B * K * Cin * H * W * 4 < (int64_t(1) << 31) && B * K * Cout * H * W * 4 < (int64_t(1) << 31) &&
+        KH * KW * Cin * Cout * 4 < (int64_t(1) << 31)))
+    return false;
+  // the kernels decode taps by rectangle arithmetic (true for any stride <= 4
+  // conv whose live rows / columns are contiguous: every ResNet shape)
+  if (stride > 4) return false;
+  const conv::Geom g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  if (!g.rect.ok) return false;
+  DgradT cls[MAX_CLASSES];
+  const int nc = dgrad_classes(g, cls);
+  for (int c = 0; c < nc; ++c)
+    if (!cls[c].crect.ok) return false;
+  return true;
 }
 
 }  // namespace convt

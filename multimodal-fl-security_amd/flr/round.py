@@ -18,6 +18,7 @@ Both give the bit-identical global model at every GPU count.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Dict, Optional
 
@@ -42,6 +43,7 @@ class RoundConfig:
     num_attackers: int = 25              # f = int(0.2 K), clients 0..f-1 (experiment_matrix.py:67-68)
     seed: int = 42                       # run_experiments.py:43
     exchange: str = "auto"               # "alltoall" | "allgather" | "auto" (alltoall when the defense shards)
+    graph: bool = True                   # replay the training phase as one captured HIP graph (FLR_GRAPH=0: eager)
 
 
 def initial_global(spec: ModelSpec, seed: int, device) -> torch.Tensor:
@@ -91,6 +93,9 @@ class RoundEngine:
             poison_batches_(self.batches, cols, Backdoor(image_size=(spec.image_size, spec.image_size)))
         self.num_examples = [steps * rcfg.batch] * K  # len(client dataset) (run_experiments.py:240)
         self.losses: Optional[torch.Tensor] = None
+        self.use_graph = (rcfg.graph and self.device.type == "cuda" and os.environ.get("FLR_GRAPH", "1") != "0")
+        self._graph = None
+        self._graph_losses: Optional[torch.Tensor] = None
 
     def _poison(self) -> None:
         f = self.rcfg.num_attackers if self.rcfg.attack == "sign_flip" else 0
@@ -98,10 +103,38 @@ class RoundEngine:
         if hi > lo:  # malicious rows submit -update (weights, as the reference negates)
             self.trainer.X.data[: hi - lo, : self.trainer.P].neg_()
 
-    def run_round(self) -> torch.Tensor:
+    def _train_phase(self) -> torch.Tensor:
+        """Every local client: global -> local SGD steps -> client-matrix rows
+        (run_experiments.py:193-240), then the attackers' poisoning."""
         self.trainer.load_global(self.global_flat)
-        self.losses = self.trainer.local_update(self.batches, self.masks)
+        losses = self.trainer.local_update(self.batches, self.masks)
         self._poison()
+        return losses
+
+    def _capture(self) -> None:
+        """Capture the training phase (~2.4k kernel launches per round at C3)
+        as one HIP graph: replay removes the host launch cost, which dominates
+        once a GPU holds few clients (K/G = 16 at 8 GPUs).  Inputs (global
+        vector, batches, masks) and the training state live at fixed addresses,
+        so the graph reads the current round's global model on every replay."""
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):  # warm-up on a side stream: library handles and workspaces
+            self._train_phase()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._graph_losses = self._train_phase()
+        self._graph = g
+
+    def run_round(self) -> torch.Tensor:
+        if self.use_graph:
+            if self._graph is None:
+                self._capture()
+            self._graph.replay()
+            self.losses = self._graph_losses
+        else:
+            self.losses = self._train_phase()
         kw = {"publish": False} if hasattr(self.defense, "publish") else {}
         if self.exchange == "alltoall":
             self.slice = self.xchg.exchange(self.trainer.X.data)
