@@ -32,6 +32,21 @@ METRIC = "FL rounds/sec + aggregate-ms, K=128 clients 10M-param multimodal, 1/2/
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+def gram_traffic(K: int, P: int):
+    """HBM bytes per launch of the Gram kernel from the committed rocprofv3 PMC
+    passes (profiles/gram_traffic.json: FETCH_SIZE and WRITE_SIZE in KiB per
+    dispatch, separate passes, FETCH_SIZE doubled per MI355X_MICROARCH.md's
+    gfx950 correction for wide streaming reads); None unless measured at this
+    exact shape."""
+    path = os.path.join(ROOT, "profiles", "gram_traffic.json")
+    if not os.path.exists(path):
+        return None
+    t = json.load(open(path))
+    if t.get("K") != K or t.get("P") != P:
+        return None
+    return (2.0 * t["fetch_kib"] + t["write_kib"]) * 1024.0
+
+
 def cpu_baseline(spec, P, K, f, multi_k, steps, batch, budget_s: float = 20.0):
     """Time the oracle (the reference's CPU path restated) on a bounded sample
     and extrapolate one round: K clients x local update + K(K-1)/2 pair norms +
@@ -155,6 +170,7 @@ def main() -> None:
     n_coords = eng.slice.n if sharded else P
     pair_bytes = 4.0 * K * n_coords + 8.0 * K * K
     achieved = pair_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = gram_traffic(K, n_coords)
     # training-phase time (one round's local updates, this rank's clients)
     ev0.record()
     if eng._graph is not None:
@@ -198,7 +214,7 @@ def main() -> None:
         "roofline": {
             "kernel": "gram_partials_kernel (Krum pairwise, centred Gram on MFMA)",
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "kernel_ms": kernel_ms, "algorithmic_bytes": pair_bytes, "coords_per_gpu": n_coords,
         },
     }

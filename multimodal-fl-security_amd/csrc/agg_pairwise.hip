@@ -42,9 +42,10 @@ constexpr int REC_TILES = 10;   // max tiles per group
 constexpr int REC_DIAG = 6 * 32;
 constexpr int REC = REC_TILES * 1024 + REC_DIAG;   // floats per partial record
 constexpr int MAX_SEG = 512;
-// Gram workgroups per full call (all slices and groups): 2 rounds of the
-// 2-per-CU residency on 256 CUs; 1/G of them per GPU when sharded.
-constexpr int TARGET_BLOCKS = 1024;
+// Gram workgroups per full call (all slices and groups): one round of the
+// 2-per-CU residency on 256 CUs (measured: 1024 costs 3.5 % in the larger
+// record write + reduction); 1/G of them per GPU when sharded.
+constexpr int TARGET_BLOCKS = 512;
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
