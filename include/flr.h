@@ -316,6 +316,26 @@ int flr_batchnorm_bwd(const float* dy, const float* x, const float* y,
                       float* dx, float* dgamma, float* dbeta, float* dresidual,
                       int64_t B, int64_t KC, int64_t HW, int relu, void* stream);
 
+/* ---- a3 / a4: batched dense GEMM (text branch, late-fusion MLP) ------------
+ * Replaces the nn.Linear / nn.GRU matrix products of the text branch and the
+ * fusion head (src/models/cub200_cnn.py:80-93, 107-117 template) for every
+ * client at once:
+ *   C_k[m][n] = (bias_k[n] or add_k[m][n] or 0) + sum_r A_k(m, r) B_k(n, r)
+ * A(m, r) at A + k*a_k + m*a_m + r*a_r (B, C likewise; any strides, so
+ * transposed operands are views); bias: NULL or [batch][bias_k] row vectors;
+ * add: NULL or a C-shaped addend (may alias C).  Exact-fp32 MFMA, split-K
+ * chosen from (M, N, R) alone, so every client's result is independent of the
+ * batch count.  Workspace (optional, split-K partials): flr_bgemm_workspace.
+ * flr_sum_rows: out[k][n] = sum_m X[k][m][n] in m order (bias gradients). */
+size_t flr_bgemm_workspace(int64_t batch, int64_t M, int64_t N, int64_t R);
+int flr_bgemm(const float* A, int64_t a_k, int64_t a_m, int64_t a_r, const float* B,
+              int64_t b_k, int64_t b_n, int64_t b_r, float* C, int64_t c_k, int64_t c_m,
+              int64_t c_n, const float* bias, int64_t bias_k, const float* add,
+              int64_t batch, int64_t M, int64_t N, int64_t R, void* workspace,
+              size_t workspace_bytes, void* stream);
+int flr_sum_rows(const float* X, int64_t x_k, int64_t x_m, int64_t batch, int64_t M,
+                 int64_t N, float* out, int64_t out_k, void* stream);
+
 /* ---- a2: max pooling of the image branch (the stem's 3x3/2 pad-1 pool) ----
  * Replaces nn.MaxPool2d / F.max_pool2d on x [nplanes][H][W] (planes = B*K*C of
  * the grouped layout).  torch's CPU rule: first in-bounds element of the

@@ -135,6 +135,211 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(const float* __restrict__ 
   }
 }
 
+// ---- register-resident fast path -------------------------------------------------
+// The engine's layout hands every (client, channel) plane over as one contiguous
+// run (B == 1).  When that run is n = 4 * L * V floats (L lanes per plane: a
+// power of two <= 64, or 256 = the whole workgroup; V float4s per lane, <= 8),
+// each value is read from HBM once as part of a 16-B load, kept in registers
+// through the centred second pass and the normalisation, and written once
+// (the general kernels above make three passes).  Per-plane sums: xor shuffles
+// inside the L-lane segment, plus one LDS step across the 4 waves when L = 256.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int L>
+__device__ __forceinline__ float plane_sum(float v, float* red) {
+  if constexpr (L <= 64) {
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  } else {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();  // red is reused by the next call
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
+template <int L, int V>
+struct FastPlane {
+  static constexpr int PPB = L >= THREADS ? 1 : THREADS / L;  // planes per workgroup
+  int kc, lane;
+  bool valid;
+  __device__ explicit FastPlane(int KC) {
+    lane = (int)(threadIdx.x % L);
+    kc = (int)blockIdx.x * PPB + (int)(threadIdx.x / L);
+    valid = kc < KC;
+  }
+  __device__ int64_t at(int i) const { return (int64_t)kc * (L * V) + (int64_t)i * L + lane; }  // float4 index
+};
+
+template <int L, int V, bool RELU, bool RES>
+__global__ __launch_bounds__(THREADS) void fwd_fast_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, const float* __restrict__ res,
+                                                           float* __restrict__ y, float* __restrict__ mean_out,
+                                                           float* __restrict__ invstd_out, int KC, float eps) {
+  __shared__ float red[THREADS / 64];
+  const FastPlane<L, V> pl(KC);
+  const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+  f32x4 v[V];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    v[i] = pl.valid ? x4[pl.at(i)] : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  }
+  const float n = (float)(4 * L * V);
+  const float mean = plane_sum<L>(s, red) / n;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[i][e] - mean;
+      q += d * d;
+    }
+  const float var = plane_sum<L>(q, red) / n;
+  if (!pl.valid) return;
+  const float invstd = 1.0f / sqrtf(var + eps);
+  const float alpha = invstd * gamma[pl.kc];
+  const float shift = beta[pl.kc] - mean * alpha;
+  f32x4* y4 = reinterpret_cast<f32x4*>(y);
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    f32x4 r = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (RES) r = reinterpret_cast<const f32x4*>(res)[pl.at(i)];
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = v[i][e] * alpha + shift;
+      if constexpr (RES) t = t + r[e];
+      if constexpr (RELU) t = fmaxf(t, 0.f);
+      o[e] = t;
+    }
+    y4[pl.at(i)] = o;
+  }
+  if (pl.lane == 0) {
+    mean_out[pl.kc] = mean;
+    invstd_out[pl.kc] = invstd;
+  }
+}
+
+template <int L, int V, bool RELU, bool DRES>
+__global__ __launch_bounds__(THREADS) void bwd_fast_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                           const float* __restrict__ y, const float* __restrict__ gamma,
+                                                           const float* __restrict__ mean_in,
+                                                           const float* __restrict__ invstd_in, float* __restrict__ dx,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                           float* __restrict__ dres, int KC) {
+  __shared__ float red[THREADS / 64];
+  const FastPlane<L, V> pl(KC);
+  const float mean = pl.valid ? mean_in[pl.kc] : 0.f;
+  f32x4 g[V], xc[V];
+  float s = 0.f, d = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    f32x4 gv = pl.valid ? reinterpret_cast<const f32x4*>(dy)[pl.at(i)] : z;
+    f32x4 xv = pl.valid ? reinterpret_cast<const f32x4*>(x)[pl.at(i)] : z;
+    if constexpr (RELU) {
+      const f32x4 yv = pl.valid ? reinterpret_cast<const f32x4*>(y)[pl.at(i)] : z;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gv[e] = yv[e] > 0.f ? gv[e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      xv[e] = xv[e] - mean;
+      s += gv[e];
+      d += xv[e] * gv[e];
+    }
+    g[i] = gv;
+    xc[i] = xv;
+  }
+  s = plane_sum<L>(s, red);
+  d = plane_sum<L>(d, red);
+  if (!pl.valid) return;
+  const float n = (float)(4 * L * V);
+  const float invstd = invstd_in[pl.kc];
+  const float kk = d * invstd * invstd / n;
+  const float mdy = s / n;
+  const float wscale = invstd * gamma[pl.kc];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (g[i][e] - mdy - xc[i][e] * kk) * wscale;
+    if constexpr (DRES) reinterpret_cast<f32x4*>(dres)[pl.at(i)] = g[i];
+    reinterpret_cast<f32x4*>(dx)[pl.at(i)] = o;
+  }
+  if (pl.lane == 0) {
+    dgamma[pl.kc] = d * invstd;
+    dbeta[pl.kc] = s;
+  }
+}
+
+// (L, V) of the fast path for a plane of n floats, or false.
+inline bool fast_shape(int64_t B, int64_t HW, int& L, int& V) {
+  if (B != 1 || HW % 4 != 0) return false;
+  const int64_t n4 = HW / 4;
+  if ((n4 & (n4 - 1)) != 0 || n4 > 2048) return false;
+  if (n4 <= 64) {
+    L = (int)n4;
+    V = 1;
+  } else if (n4 <= 512) {
+    L = 64;
+    V = (int)(n4 / 64);
+  } else {
+    L = 256;
+    V = (int)(n4 / 256);
+  }
+  return true;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+#define FLR_BN_FAST_SHAPES(X) \
+  X(1, 1) X(2, 1) X(4, 1) X(8, 1) X(16, 1) X(32, 1) X(64, 1) X(64, 2) X(64, 4) X(64, 8) X(256, 4) X(256, 8)
+
+template <bool RELU, bool RES>
+bool fwd_fast(const float* x, const float* gamma, const float* beta, const float* res, float* y, float* mean,
+              float* invstd, int64_t B, int64_t KC, int64_t HW, float eps, hipStream_t st) {
+  int L, V;
+  if (!fast_shape(B, HW, L, V) || !aligned16(x) || !aligned16(y) || (RES && !aligned16(res))) return false;
+  const int ppb = L >= THREADS ? 1 : THREADS / L;
+  const dim3 grid((unsigned)((KC + ppb - 1) / ppb));
+#define FLR_BN_FWD_CASE(LL, VV)                                                                                  \
+  if (L == LL && V == VV) {                                                                                      \
+    hipLaunchKernelGGL((fwd_fast_kernel<LL, VV, RELU, RES>), grid, dim3(THREADS), 0, st, x, gamma, beta, res, y, \
+                       mean, invstd, (int)KC, eps);                                                              \
+    return true;                                                                                                 \
+  }
+  FLR_BN_FAST_SHAPES(FLR_BN_FWD_CASE)
+#undef FLR_BN_FWD_CASE
+  return false;
+}
+
+template <bool RELU, bool DRES>
+bool bwd_fast(const float* dy, const float* x, const float* y, const float* gamma, const float* mean,
+              const float* invstd, float* dx, float* dgamma, float* dbeta, float* dres, int64_t B, int64_t KC,
+              int64_t HW, hipStream_t st) {
+  int L, V;
+  if (!fast_shape(B, HW, L, V) || !aligned16(dy) || !aligned16(x) || !aligned16(dx) || (RELU && !aligned16(y)) ||
+      (DRES && !aligned16(dres)))
+    return false;
+  const int ppb = L >= THREADS ? 1 : THREADS / L;
+  const dim3 grid((unsigned)((KC + ppb - 1) / ppb));
+#define FLR_BN_BWD_CASE(LL, VV)                                                                                   \
+  if (L == LL && V == VV) {                                                                                       \
+    hipLaunchKernelGGL((bwd_fast_kernel<LL, VV, RELU, DRES>), grid, dim3(THREADS), 0, st, dy, x, y, gamma, mean, \
+                       invstd, dx, dgamma, dbeta, dres, (int)KC);                                                 \
+    return true;                                                                                                  \
+  }
+  FLR_BN_FAST_SHAPES(FLR_BN_BWD_CASE)
+#undef FLR_BN_BWD_CASE
+  return false;
+}
+
 inline int seg_log2_of(int HW) {
   int l = 0;
   while (l < 6 && (1 << (l + 1)) <= HW) ++l;
@@ -161,6 +366,12 @@ extern "C" int flr_batchnorm_fwd(const float* x, const float* gamma, const float
   const int sl = bn::seg_log2_of((int)HW);
   const dim3 grid = bn::grid_of((int)KC, sl);
   hipStream_t st = as_stream(stream);
+  bool fast;
+  if (relu && residual) fast = bn::fwd_fast<true, true>(x, gamma, beta, residual, y, mean, invstd, B, KC, HW, eps, st);
+  else if (relu) fast = bn::fwd_fast<true, false>(x, gamma, beta, residual, y, mean, invstd, B, KC, HW, eps, st);
+  else if (residual) fast = bn::fwd_fast<false, true>(x, gamma, beta, residual, y, mean, invstd, B, KC, HW, eps, st);
+  else fast = bn::fwd_fast<false, false>(x, gamma, beta, residual, y, mean, invstd, B, KC, HW, eps, st);
+  if (fast) return launch_status("batchnorm fwd (fast)");
 #define FLR_BN_FWD(R, S)                                                                                       \
   hipLaunchKernelGGL((bn::fwd_kernel<R, S>), grid, dim3(bn::THREADS), 0, st, x, gamma, beta, residual, y, mean, \
                      invstd, (int)B, (int)KC, (int)HW, sl, eps)
@@ -181,7 +392,17 @@ extern "C" int flr_batchnorm_bwd(const float* dy, const float* x, const float* y
   const int sl = bn::seg_log2_of((int)HW);
   const dim3 grid = bn::grid_of((int)KC, sl);
   hipStream_t st = as_stream(stream);
-#define FLR_BN_BWD(R, D)                                                                                         \
+  bool fast;
+  if (relu && dresidual)
+    fast = bn::bwd_fast<true, true>(dy, x, y, gamma, mean, invstd, dx, dgamma, dbeta, dresidual, B, KC, HW, st);
+  else if (relu)
+    fast = bn::bwd_fast<true, false>(dy, x, y, gamma, mean, invstd, dx, dgamma, dbeta, dresidual, B, KC, HW, st);
+  else if (dresidual)
+    fast = bn::bwd_fast<false, true>(dy, x, y, gamma, mean, invstd, dx, dgamma, dbeta, dresidual, B, KC, HW, st);
+  else
+    fast = bn::bwd_fast<false, false>(dy, x, y, gamma, mean, invstd, dx, dgamma, dbeta, dresidual, B, KC, HW, st);
+  if (fast) return launch_status("batchnorm bwd (fast)");
+#define FLR_BN_BWD(R, D)                                                                                       \
   hipLaunchKernelGGL((bn::bwd_kernel<R, D>), grid, dim3(bn::THREADS), 0, st, dy, x, y, gamma, mean, invstd, dx, \
                      dgamma, dbeta, dresidual, (int)B, (int)KC, (int)HW, sl)
   if (relu && dresidual) FLR_BN_BWD(true, true);

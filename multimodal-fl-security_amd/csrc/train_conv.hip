@@ -361,6 +361,14 @@ __global__ __launch_bounds__(THREADS, 2) void cgemm_kernel(const Prob pb, int S,
   }
 }
 
+// dw[e] = 0 for every element of a dead kernel tap (e % KK in the dead mask).
+// A kernel rather than hipMemsetAsync: a memset captured inside the training
+// phase's HIP graph was observed not to take effect on replays.
+__global__ void zero_dead_taps_kernel(float* __restrict__ dw, int64_t n, int KK, uint64_t dead) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x)
+    if ((dead >> (int)(e % KK)) & 1ull) dw[e] = 0.f;
+}
+
 template <class Prob>
 __global__ void cgemm_reduce(const Prob pb, int S, const float* __restrict__ part) {
   const int M = pb.M(), N = pb.N(), K = pb.g.Kc;
@@ -375,11 +383,15 @@ __global__ void cgemm_reduce(const Prob pb, int S, const float* __restrict__ par
 }
 
 // Splits so that a launch has >= ~2048 workgroups while each split keeps >= 8 K-tiles.
-inline int choose_splits(int M, int N, int R, int K) {
-  const int tiles = cdiv(M, BM) * cdiv(N, BN) * K;
+// Split-K count from the PER-CLIENT problem only (never the client count K):
+// a client's reduction order — and so its trained weights — must not depend
+// on how many clients share its GPU (bit-identical results at 1/2/4/8 GPUs).
+// 16 tiles per client = the 2048-workgroup target at the nominal 128 clients.
+inline int choose_splits(int M, int N, int R, int /*K*/) {
+  const int tiles = cdiv(M, BM) * cdiv(N, BN);
   const int ktiles = cdiv(R, BK);
   int S = 1;
-  while (S < 16 && tiles * S < 2048 && ktiles / (2 * S) >= 8) S *= 2;
+  while (S < 16 && tiles * S < 16 && ktiles / (2 * S) >= 8) S *= 2;
   return S;
 }
 
@@ -470,9 +482,16 @@ extern "C" int flr_conv2d_bwd_weight(const float* x, const float* dy, float* dw,
   if (!x || !dy || !dw || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
   const Geom g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
   hipStream_t st = as_stream(stream);
-  if (g.ntaps < KH * KW &&  // dead taps get exact-zero gradients
-      hipMemsetAsync(dw, 0, (size_t)K * Cout * Cin * KH * KW * sizeof(float), st) != hipSuccess)
-    return FLR_ERR_HIP;
+  if (g.ntaps < KH * KW) {  // dead taps get exact-zero gradients
+    if (KH * KW > 64) return FLR_ERR_UNSUPPORTED;
+    uint64_t dead = (KH * KW == 64) ? ~0ull : ((1ull << (KH * KW)) - 1);
+    for (int t = 0; t < g.ntaps; ++t) dead &= ~(1ull << (g.tap_kh[t] * KW + g.tap_kw[t]));
+    const int64_t n = K * Cout * Cin * KH * KW;
+    hipLaunchKernelGGL(zero_dead_taps_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                       st, dw, n, (int)(KH * KW), dead);
+    const int rc = launch_status("conv bwd weight: zero dead taps");
+    if (rc != FLR_OK) return rc;
+  }
   if (getenv_generic() == 0 && convt::im2col_eligible(g) && ws && ws_bytes >= convt::im2col_workspace(g))
     return convt::wgrad_im2col(g, x, dy, dw, ws, ws_bytes, st);
   if (Cin % BN == 0 && getenv_generic() == 0) {

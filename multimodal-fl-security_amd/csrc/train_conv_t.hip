@@ -38,6 +38,7 @@ using conv::udiv;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BM = 64, BN = 64, BK = 32, THREADS = 256;
 constexpr int SKR = 68;  // [k][row] image row stride (floats)
@@ -95,6 +96,53 @@ __device__ __forceinline__ f32x4 frag(const float* buf, int rb, int j, int h) {
     const float* p = buf + (8 * j + 4 * h) * SKR + rb;
     return f32x4{p[0], p[SKR], p[2 * SKR], p[3 * SKR]};
   }
+}
+
+// ---- the bf16x6 MFMA form ----------------------------------------------------
+// f32 MFMA runs at 1/16 of the bf16 rate on gfx950.  Each f32 operand is split
+// into three round-to-nearest bf16 terms, x = hi + mid + lo (the residual is
+// below 2^-24 |x|: 24 significand bits in three 8-bit pieces), and the six
+// products whose order is above 2^-24 (hi*hi, hi*mid, mid*hi, mid*mid, hi*lo,
+// lo*hi; every bf16 x bf16 product is exact in the fp32 accumulator) run on
+// v_mfma_f32_32x32x16_bf16: 6 x 32 cycles per 16-deep k-step against 8 x 64 for
+// v_mfma_f32_32x32x2_f32, at a per-product error of a few 2^-24 |a b| — the
+// rounding of an fp32 product.  The LDS images stay fp32; each wave splits
+// the eight values of its fragment: lane (l32, h) supplies row l32 and
+// reduction indices k0 .. k0+7, k0 = 16 s + 8 h.
+template <int LAY>
+__device__ __forceinline__ void frag8(const float* buf, int rb, int k0, float (&v)[8]) {
+  if constexpr (LAY == RK_VEC || LAY == RK_GATHER) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(buf + rb * SRK + k0);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(buf + rb * SRK + k0 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = a[e];
+      v[4 + e] = b[e];
+    }
+  } else {
+    const float* p = buf + k0 * SKR + rb;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = p[e * SKR];
+  }
+}
+
+__device__ __forceinline__ void split3(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 a = (__bf16)v[j];
+    const float r1 = v[j] - (float)a;
+    const __bf16 b = (__bf16)r1;
+    hi[j] = a;
+    mid[j] = b;
+    lo[j] = (__bf16)(r1 - (float)b);
+  }
+}
+
+// FLR_GEMM=f32 selects the exact-f32 MFMA (A/B timing, cross-checks); read per
+// launch so one process can compare both forms.
+inline bool gemm_x6() {
+  const char* e = getenv("FLR_GEMM");
+  return !(e && e[0] == 'f');
 }
 
 // ---- load plans ---------------------------------------------------------------
@@ -485,6 +533,116 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
 // rows in LDS — one thread per (pix, ci, kh) fills the KW-long run
 // r = (ci*KH + kh)*KW + 0..KW-1 — then streams the IM_PB*RP contiguous floats
 // out as 16-B stores (RP % 4 == 0).
+// ---- batched dense GEMM (the text branch and the late-fusion MLP) -------------
+// C_k[m][n] = (bias_k[n] | add_k[m][n]) + sum_r A_k(m, r) B_k(n, r) for every
+// client k, with arbitrary strides: A(m, r) at a + k a_k + m a_m + r a_r, etc.
+// Operand modes: RK (r contiguous: 16-B loads along r), KR (m / n contiguous:
+// 16-B loads along the row index), G (anything else: scalar gathers).  Same
+// tiled exact-fp32 MFMA kernel and split-K rule as the convolutions, so a
+// client's result never depends on how many clients share the launch.
+struct BatchDim {
+  int Kc;
+};
+enum BMode { BM_RK = 0, BM_KR = 1, BM_G = 2 };
+
+struct BGemmArgs {
+  BatchDim g;
+  int m, n, r;
+  const float* a;
+  int64_t a_k, a_m, a_r, a_ext;
+  const float* b;
+  int64_t b_k, b_n, b_r, b_ext;
+  float* c;
+  int64_t c_k, c_m, c_n;
+  const float* bias;  // bias[k * bias_k + n]
+  int64_t bias_k;
+  const float* add;   // add[k*c_k + m*c_m + n*c_n] (may alias c)
+};
+
+template <int AM, int BMD>
+struct BGemm : BGemmArgs {
+  static constexpr int LA = AM == BM_RK ? RK_VEC : (AM == BM_KR ? KR_VEC : RK_GATHER);
+  static constexpr int LB = BMD == BM_RK ? RK_VEC : (BMD == BM_KR ? KR_VEC : RK_GATHER);
+  __host__ __device__ int M() const { return m; }
+  __host__ __device__ int N() const { return n; }
+  __host__ __device__ int R() const { return r; }
+  struct State {
+    rsrc_t ra, rb;
+    int arow, brow;
+  };
+  // one operand (rows = m or n) of a 64 x 32 tile, in the layout its mode stashes
+  template <int MODE>
+  __device__ static void load_op(rsrc_t rs, int base_row, int rows, int r0, int R, int64_t s_row, int64_t s_r,
+                                 float (&v)[8]) {
+    const int tid = threadIdx.x;
+    if constexpr (MODE == BM_RK) {  // rows tid/8 + 32 i, k = r0 + 4 (tid % 8) .. +3
+      const int kk = r0 + 4 * (tid % 8);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = base_row + tid / 8 + 32 * i;
+        const bool ok = row < rows && kk < R;
+        const f32x4 q = ld4(rs, ok ? (unsigned)((row * s_row + kk) * 4) : SENT, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * i + e] = q[e];
+      }
+    } else if constexpr (MODE == BM_KR) {  // rows 4 (tid % 16) .. +3, k = r0 + tid/16 + 16 i
+      const int row = base_row + 4 * (tid % 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int kk = r0 + tid / 16 + 16 * i;
+        const bool ok = row < rows && kk < R;
+        const f32x4 q = ld4(rs, ok ? (unsigned)((kk * s_r + row) * 4) : SENT, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * i + e] = q[e];
+      }
+    } else {  // rows tid/32 + 8 i, k = r0 + tid % 32
+      const int kk = r0 + tid % 32;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = base_row + tid / 32 + 8 * i;
+        const bool ok = row < rows && kk < R;
+        v[i] = ld1(rs, ok ? (unsigned)((row * s_row + kk * s_r) * 4) : SENT, 0);
+      }
+    }
+  }
+  __device__ State init(int k, int m0, int n0, int) const {
+    State s;
+    s.ra = make_rsrc(a + k * a_k, a_ext);
+    s.rb = make_rsrc(b + k * b_k, b_ext);
+    s.arow = m0;
+    s.brow = n0;
+    return s;
+  }
+  __device__ void load_a(const State& s, int r0, float (&v)[8]) const {
+    load_op<AM>(s.ra, s.arow, m, r0, r, a_m, a_r, v);
+  }
+  __device__ void load_b(const State& s, int r0, float (&v)[8]) const {
+    load_op<BMD>(s.rb, s.brow, n, r0, r, b_n, b_r, v);
+  }
+  __device__ void store(int k, int mm, int nn, float v) const {
+    const int64_t i = k * c_k + mm * c_m + nn * c_n;
+    if (bias) v = bias[k * bias_k + nn] + v;
+    if (add) v = add[i] + v;
+    c[i] = v;
+  }
+  __device__ bool linear() const { return c_n == 1 && !bias && !add; }
+  __device__ float* out() const { return c; }
+  __device__ int64_t tile_base(int k, int m0, int n0) const { return k * c_k + m0 * c_m + n0; }
+  __device__ int64_t ldm() const { return c_m; }
+};
+
+// out[k][n] = sum_m X[k][m][n] in m order (bias gradients of the batched GEMMs)
+__global__ void sum_rows_kernel(const float* __restrict__ x, int64_t x_k, int64_t x_m, int M, int N,
+                                float* __restrict__ out, int64_t out_k) {
+  const int k = blockIdx.y;
+  const int nn = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nn >= N) return;
+  const float* p = x + k * x_k + nn;
+  float s = 0.f;
+  for (int mm = 0; mm < M; ++mm) s += p[mm * x_m];
+  out[k * out_k + nn] = s;
+}
+
 constexpr int IM_PB = 32, IM_MAXRP = 512;
 __global__ __launch_bounds__(THREADS) void im2col_kernel(const Geom g, const float* __restrict__ x, int RP,
                                                          float* __restrict__ col) {
@@ -534,7 +692,7 @@ __global__ __launch_bounds__(THREADS) void repad_kernel(const float* __restrict_
 // LDS feeds NS (A) or MS (B) MFMAs and the MS*NS accumulator chains are
 // independent.  MS or NS = 2 halves the loads, LDS traffic and barriers per
 // MFMA of the 64 x 64 tile.
-template <class Plan, int MS, int NS>
+template <class Plan, int MS, int NS, bool X6>
 __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float As[2][MS][TILE];
   __shared__ __attribute__((aligned(16))) float Bs[2][NS][TILE];
@@ -583,24 +741,56 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
   for (int r0 = rbeg; r0 < rend; r0 += BK) {
     const bool more = r0 + BK < rend;
     if (more) load(r0 + BK);  // in flight during the MFMAs below
-    f32x4 fa[MS][4], fb[NS][4];  // all of the tile's fragments first: the reads overlap the MFMA chain
+    if constexpr (X6) {
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
+      for (int s = 0; s < BK / 16; ++s) {
+        bf16x8 ah[MS], am[MS], al[MS], bh[NS], bm[NS], bl[NS];
 #pragma unroll
-      for (int i = 0; i < MS; ++i) fa[i][jj] = frag<Plan::LA>(As[cur][i], 32 * wm + l32, jj, h);
+        for (int i = 0; i < MS; ++i) {
+          float v[8];
+          frag8<Plan::LA>(As[cur][i], 32 * wm + l32, 16 * s + 8 * h, v);
+          split3(v, ah[i], am[i], al[i]);
+        }
 #pragma unroll
-      for (int j = 0; j < NS; ++j) fb[j][jj] = frag<Plan::LB>(Bs[cur][j], 32 * wn + l32, jj, h);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the chain (the scheduler would interleave them)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int j = 0; j < NS; ++j) {
+          float v[8];
+          frag8<Plan::LB>(Bs[cur][j], 32 * wn + l32, 16 * s + 8 * h, v);
+          split3(v, bh[j], bm[j], bl[j]);
+        }
 #pragma unroll
         for (int i = 0; i < MS; ++i)
 #pragma unroll
-          for (int j = 0; j < NS; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][jj][t], fb[j][jj][t], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < NS; ++j) {  // small terms first
+            f32x16 c = acc[i][j];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c, 0, 0, 0);
+            acc[i][j] = c;
+          }
+      }
+    } else {
+      f32x4 fa[MS][4], fb[NS][4];  // all of the tile's fragments first: the reads overlap the MFMA chain
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+#pragma unroll
+        for (int i = 0; i < MS; ++i) fa[i][jj] = frag<Plan::LA>(As[cur][i], 32 * wm + l32, jj, h);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) fb[j][jj] = frag<Plan::LB>(Bs[cur][j], 32 * wn + l32, jj, h);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the chain (the scheduler would interleave them)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < MS; ++i)
+#pragma unroll
+            for (int j = 0; j < NS; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][jj][t], fb[j][jj][t], acc[i][j], 0, 0, 0);
+    }
     if (more) stash_all(cur ^ 1);
     __syncthreads();
     cur ^= 1;
@@ -660,11 +850,15 @@ __global__ void zero_taps_kernel(float* __restrict__ dw, int KK, int64_t slab, u
   }
 }
 
-inline int choose_splits(int M, int N, int R, int K, int sub = 1) {
-  const int tiles = cdiv(M, BM) * cdiv(N, BN) * K / sub;
+// Split-K count from the PER-CLIENT problem only (never the client count K):
+// a client's reduction order — and so its trained weights — must not depend
+// on how many clients share its GPU (bit-identical results at 1/2/4/8 GPUs).
+// 16 tiles per client = the 2048-workgroup target at the nominal 128 clients.
+inline int choose_splits(int M, int N, int R, int /*K*/, int sub = 1) {
+  const int tiles = cdiv(M, BM) * cdiv(N, BN) / sub;
   const int ktiles = cdiv(R, BK);
   int S = 1;
-  while (S < 16 && tiles * S < 2048 && ktiles / (2 * S) >= 8) S *= 2;
+  while (S < 16 && tiles * S < 16 && ktiles / (2 * S) >= 8) S *= 2;
   return S;
 }
 
@@ -694,7 +888,10 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   int S = choose_splits(M, N, R, K, MS * NS);
   if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) S = 1;
   const dim3 grid((unsigned)cdiv(N, BN * NS), (unsigned)cdiv(M, BM * MS), (unsigned)(K * S));
-  hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws));
+  if (gemm_x6())
+    hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, true>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws));
+  else
+    hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, false>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws));
   int rc = launch_status(name);
   if (rc != FLR_OK || S == 1) return rc;
   const int64_t mn = (int64_t)M * N;
@@ -874,4 +1071,70 @@ extern "C" int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* d
   convt::WgtT<false> pl;
   pl.g = g; pl.x = x; pl.dy = dy; pl.dw = dw_t;
   return convt::launch(pl, ws, ws_bytes, st, "conv bwd weight (tap-major)");
+}
+
+namespace {
+// operand mode from strides: RK (r contiguous) / KR (rows contiguous) / G
+int bgemm_mode(const float* p, int64_t s_k, int64_t s_row, int64_t s_r, int64_t rows, int64_t R) {
+  const bool al = (reinterpret_cast<uintptr_t>(p) & 15) == 0 && s_k % 4 == 0;
+  if (s_r == 1 && al && s_row % 4 == 0 && R % 4 == 0) return convt::BM_RK;
+  if (s_row == 1 && al && s_r % 4 == 0 && rows % 4 == 0) return convt::BM_KR;
+  return convt::BM_G;
+}
+template <int AM, int BMD>
+int bgemm_run(const convt::BGemmArgs& args, void* ws, size_t ws_bytes, hipStream_t st) {
+  convt::BGemm<AM, BMD> pl;
+  static_cast<convt::BGemmArgs&>(pl) = args;
+  return convt::launch_tiles<convt::BGemm<AM, BMD>, 1, 1>(pl, ws, ws_bytes, st, "batched gemm");
+}
+template <int AM>
+int bgemm_b(int bm, const convt::BGemmArgs& args, void* ws, size_t wsb, hipStream_t st) {
+  switch (bm) {
+    case convt::BM_RK: return bgemm_run<AM, convt::BM_RK>(args, ws, wsb, st);
+    case convt::BM_KR: return bgemm_run<AM, convt::BM_KR>(args, ws, wsb, st);
+    default: return bgemm_run<AM, convt::BM_G>(args, ws, wsb, st);
+  }
+}
+}  // namespace
+
+extern "C" size_t flr_bgemm_workspace(int64_t batch, int64_t M, int64_t N, int64_t R) {
+  if (batch < 1 || M < 1 || N < 1 || R < 0 || M > INT32_MAX || N > INT32_MAX || R > INT32_MAX) return 0;
+  const int S = convt::choose_splits((int)M, (int)N, (int)R, (int)batch);
+  return S > 1 ? (size_t)S * batch * M * N * sizeof(float) : 0;
+}
+
+extern "C" int flr_bgemm(const float* A, int64_t a_k, int64_t a_m, int64_t a_r, const float* B, int64_t b_k,
+                         int64_t b_n, int64_t b_r, float* C, int64_t c_k, int64_t c_m, int64_t c_n, const float* bias,
+                         int64_t bias_k, const float* add, int64_t batch, int64_t M, int64_t N, int64_t R, void* ws,
+                         size_t ws_bytes, void* stream) {
+  if (!A || !B || !C || batch < 1 || batch > 65535 || M < 1 || N < 1 || R < 1) return FLR_ERR_ARG;
+  if (a_k < 0 || a_m < 0 || a_r < 0 || b_k < 0 || b_n < 0 || b_r < 0 || c_k < 0 || c_m < 0 || c_n < 0)
+    return FLR_ERR_ARG;
+  const int64_t a_ext = (M - 1) * a_m + (R - 1) * a_r + 1;
+  const int64_t b_ext = (N - 1) * b_n + (R - 1) * b_r + 1;
+  if (a_ext * 4 >= (int64_t(1) << 31) || b_ext * 4 >= (int64_t(1) << 31) || M * N >= (int64_t(1) << 31) ||
+      R >= (int64_t(1) << 30))
+    return FLR_ERR_UNSUPPORTED;
+  convt::BGemmArgs p;
+  p.g.Kc = (int)batch;
+  p.m = (int)M; p.n = (int)N; p.r = (int)R;
+  p.a = A; p.a_k = a_k; p.a_m = a_m; p.a_r = a_r; p.a_ext = a_ext;
+  p.b = B; p.b_k = b_k; p.b_n = b_n; p.b_r = b_r; p.b_ext = b_ext;
+  p.c = C; p.c_k = c_k; p.c_m = c_m; p.c_n = c_n;
+  p.bias = bias; p.bias_k = bias_k; p.add = add;
+  hipStream_t st = as_stream(stream);
+  const int am = bgemm_mode(A, a_k, a_m, a_r, M, R), bm = bgemm_mode(B, b_k, b_n, b_r, N, R);
+  switch (am) {
+    case convt::BM_RK: return bgemm_b<convt::BM_RK>(bm, p, ws, ws_bytes, st);
+    case convt::BM_KR: return bgemm_b<convt::BM_KR>(bm, p, ws, ws_bytes, st);
+    default: return bgemm_b<convt::BM_G>(bm, p, ws, ws_bytes, st);
+  }
+}
+
+extern "C" int flr_sum_rows(const float* X, int64_t x_k, int64_t x_m, int64_t batch, int64_t M, int64_t N, float* out,
+                            int64_t out_k, void* stream) {
+  if (!X || !out || batch < 1 || batch > 65535 || M < 0 || N < 1) return FLR_ERR_ARG;
+  hipLaunchKernelGGL(convt::sum_rows_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)batch), dim3(256), 0,
+                     as_stream(stream), X, x_k, x_m, (int)M, (int)N, out, out_k);
+  return launch_status("sum_rows");
 }

@@ -12,8 +12,11 @@
 //
 // Forward: one lane per output; the argmax is kept as a 1-byte window offset
 // (kh*KW + kw).  Backward: one lane per INPUT element, gathering from the <=
-// ceil(KH/S)*ceil(KW/S) windows that contain it, in raster order.
+// ceil(KH/S)*ceil(KW/S) windows that contain it, in raster order.  Planes are
+// staged through LDS (H*W <= 4096).
 #include "conv_common.h"
+
+#include <algorithm>
 
 namespace flr {
 namespace pool {
@@ -25,56 +28,87 @@ struct PoolGeom {
   conv::FastDiv d_hw, d_w, d_howo, d_wo;  // 32-bit index math (total < 2^31)
 };
 
+// A workgroup owns PPB consecutive planes (PPB * H * W <= LDS_FLOATS): the
+// planes are staged in LDS with coalesced loads, every window / scatter is
+// evaluated from LDS, and the results leave with coalesced stores.
+constexpr int LDS_FLOATS = 4096;
+
+__device__ __forceinline__ void window_range(int i, int P, int K, int S, int n_out, int& lo, int& hi) {
+  // outputs o with o*S - P <= i <= o*S - P + K - 1
+  const int a = i + P - K + 1;  // o*S >= a
+  lo = a <= 0 ? 0 : (a + S - 1) / S;
+  hi = min(n_out - 1, (i + P) / S);
+}
+
 __global__ __launch_bounds__(THREADS) void fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                      uint8_t* __restrict__ arg, int64_t nplanes, PoolGeom g) {
-  const uint32_t idx = blockIdx.x * THREADS + threadIdx.x;
-  if (idx >= (uint32_t)(nplanes * g.Ho * g.Wo)) return;
-  const uint32_t plane = conv::udiv(idx, g.d_howo);
-  const int o = (int)(idx - plane * g.Ho * g.Wo);
-  const int oh = (int)conv::udiv(o, g.d_wo), ow = o - oh * g.Wo;
-  const float* xp = x + (int64_t)plane * g.H * g.W;
-  const int ih0 = oh * g.S - g.P, iw0 = ow * g.S - g.P;
-  float best = -__builtin_huge_valf();
-  int bi = -1;
-  for (int kh = 0; kh < g.KH; ++kh) {
-    const int ih = ih0 + kh;
-    if (ih < 0 || ih >= g.H) continue;
-    for (int kw = 0; kw < g.KW; ++kw) {
-      const int iw = iw0 + kw;
-      if (iw < 0 || iw >= g.W) continue;
-      const float v = xp[ih * g.W + iw];
-      if (bi < 0) bi = kh * g.KW + kw;  // torch's initial maxindex: the first in-bounds element
-      if (v > best || v != v) {
-        best = v;
-        bi = kh * g.KW + kw;
+                                                      uint8_t* __restrict__ arg, int64_t nplanes, int ppb,
+                                                      PoolGeom g) {
+  __shared__ float xs[LDS_FLOATS];
+  const int64_t p0 = (int64_t)blockIdx.x * ppb;
+  const int np = (int)min((int64_t)ppb, nplanes - p0);
+  const int HW = g.H * g.W, HoWo = g.Ho * g.Wo;
+  const float* xb = x + p0 * HW;
+  for (int e = threadIdx.x; e < np * HW; e += THREADS) xs[e] = xb[e];
+  __syncthreads();
+  float* yb = y + p0 * HoWo;
+  uint8_t* ab = arg + p0 * HoWo;
+  for (int o = threadIdx.x; o < np * HoWo; o += THREADS) {
+    const int pl = (int)conv::udiv(o, g.d_howo), q = o - pl * HoWo;
+    const int oh = (int)conv::udiv(q, g.d_wo), ow = q - oh * g.Wo;
+    const float* xp = xs + pl * HW;
+    const int ih0 = oh * g.S - g.P, iw0 = ow * g.S - g.P;
+    float best = -__builtin_huge_valf();
+    int bi = -1;
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int ih = ih0 + kh;
+      if (ih < 0 || ih >= g.H) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int iw = iw0 + kw;
+        if (iw < 0 || iw >= g.W) continue;
+        const float v = xp[ih * g.W + iw];
+        if (bi < 0) bi = kh * g.KW + kw;  // torch's initial maxindex: the first in-bounds element
+        if (v > best || v != v) {
+          best = v;
+          bi = kh * g.KW + kw;
+        }
       }
     }
+    yb[o] = best;
+    ab[o] = (uint8_t)bi;
   }
-  y[idx] = best;
-  arg[idx] = (uint8_t)bi;
 }
 
 __global__ __launch_bounds__(THREADS) void bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ arg,
-                                                      float* __restrict__ dx, int64_t nplanes, PoolGeom g) {
-  const uint32_t idx = blockIdx.x * THREADS + threadIdx.x;
-  if (idx >= (uint32_t)(nplanes * g.H * g.W)) return;
-  const uint32_t plane = conv::udiv(idx, g.d_hw);
-  const int e = (int)(idx - plane * g.H * g.W);
-  const int ih = (int)conv::udiv(e, g.d_w), iw = e - ih * g.W;
-  // windows oh with oh*S - P <= ih <= oh*S - P + KH - 1
-  const int oh_lo = max(0, (ih + g.P - g.KH + g.S) / g.S), oh_hi = min(g.Ho - 1, (ih + g.P) / g.S);
-  const int ow_lo = max(0, (iw + g.P - g.KW + g.S) / g.S), ow_hi = min(g.Wo - 1, (iw + g.P) / g.S);
-  const float* dyp = dy + (int64_t)plane * g.Ho * g.Wo;
-  const uint8_t* ap = arg + (int64_t)plane * g.Ho * g.Wo;
-  float acc = 0.f;
-  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-    const int kh = ih - (oh * g.S - g.P);
-    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-      const int kw = iw - (ow * g.S - g.P);
-      if (ap[oh * g.Wo + ow] == kh * g.KW + kw) acc = add_rn(acc, dyp[oh * g.Wo + ow]);
-    }
+                                                      float* __restrict__ dx, int64_t nplanes, int ppb, PoolGeom g) {
+  __shared__ float ds[LDS_FLOATS];
+  __shared__ uint8_t as[LDS_FLOATS];
+  const int64_t p0 = (int64_t)blockIdx.x * ppb;
+  const int np = (int)min((int64_t)ppb, nplanes - p0);
+  const int HW = g.H * g.W, HoWo = g.Ho * g.Wo;
+  for (int o = threadIdx.x; o < np * HoWo; o += THREADS) {
+    ds[o] = dy[p0 * HoWo + o];
+    as[o] = arg[p0 * HoWo + o];
   }
-  dx[idx] = acc;
+  __syncthreads();
+  float* xb = dx + p0 * HW;
+  for (int e = threadIdx.x; e < np * HW; e += THREADS) {
+    const int pl = (int)conv::udiv(e, g.d_hw), q = e - pl * HW;
+    const int ih = (int)conv::udiv(q, g.d_w), iw = q - ih * g.W;
+    int oh_lo, oh_hi, ow_lo, ow_hi;
+    window_range(ih, g.P, g.KH, g.S, g.Ho, oh_lo, oh_hi);
+    window_range(iw, g.P, g.KW, g.S, g.Wo, ow_lo, ow_hi);
+    const float* dp = ds + pl * HoWo;
+    const uint8_t* ap = as + pl * HoWo;
+    float acc = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int kh = ih - (oh * g.S - g.P);
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int kw = iw - (ow * g.S - g.P);
+        if (ap[oh * g.Wo + ow] == kh * g.KW + kw) acc = add_rn(acc, dp[oh * g.Wo + ow]);
+      }
+    }
+    xb[e] = acc;
+  }
 }
 
 inline bool geom(int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t S, int64_t P, PoolGeom& g) {
@@ -100,11 +134,11 @@ extern "C" int flr_maxpool2d_fwd(const float* x, float* y, uint8_t* argmax, int6
                                  int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* stream) {
   pool::PoolGeom g;
   if (!x || !y || !argmax || nplanes < 0 || !pool::geom(H, W, KH, KW, stride, pad, g)) return FLR_ERR_ARG;
-  if (nplanes * H * W >= ((int64_t)1 << 31)) return FLR_ERR_UNSUPPORTED;
-  const int64_t total = nplanes * g.Ho * g.Wo;
-  if (total == 0) return FLR_OK;
-  hipLaunchKernelGGL(pool::fwd_kernel, dim3((unsigned)((total + pool::THREADS - 1) / pool::THREADS)),
-                     dim3(pool::THREADS), 0, as_stream(stream), x, y, argmax, nplanes, g);
+  if (H * W > pool::LDS_FLOATS) return FLR_ERR_UNSUPPORTED;
+  if (nplanes == 0) return FLR_OK;
+  const int ppb = (int)std::max<int64_t>(1, std::min<int64_t>(pool::LDS_FLOATS / (H * W), 64));
+  hipLaunchKernelGGL(pool::fwd_kernel, dim3((unsigned)((nplanes + ppb - 1) / ppb)), dim3(pool::THREADS), 0,
+                     as_stream(stream), x, y, argmax, nplanes, ppb, g);
   return launch_status("maxpool fwd");
 }
 
@@ -112,10 +146,10 @@ extern "C" int flr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* 
                                  int64_t W, int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* stream) {
   pool::PoolGeom g;
   if (!dy || !dx || !argmax || nplanes < 0 || !pool::geom(H, W, KH, KW, stride, pad, g)) return FLR_ERR_ARG;
-  if (nplanes * H * W >= ((int64_t)1 << 31)) return FLR_ERR_UNSUPPORTED;
-  const int64_t total = nplanes * H * W;
-  if (total == 0) return FLR_OK;
-  hipLaunchKernelGGL(pool::bwd_kernel, dim3((unsigned)((total + pool::THREADS - 1) / pool::THREADS)),
-                     dim3(pool::THREADS), 0, as_stream(stream), dy, argmax, dx, nplanes, g);
+  if (H * W > pool::LDS_FLOATS) return FLR_ERR_UNSUPPORTED;
+  if (nplanes == 0) return FLR_OK;
+  const int ppb = (int)std::max<int64_t>(1, std::min<int64_t>(pool::LDS_FLOATS / (H * W), 64));
+  hipLaunchKernelGGL(pool::bwd_kernel, dim3((unsigned)((nplanes + ppb - 1) / ppb)), dim3(pool::THREADS), 0,
+                     as_stream(stream), dy, argmax, dx, nplanes, ppb, g);
   return launch_status("maxpool bwd");
 }

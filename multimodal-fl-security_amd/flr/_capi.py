@@ -82,6 +82,10 @@ SIGNATURES = {
                                  ctypes.c_float, _c_void_p, _c_void_p]),
     "flr_batchnorm_fwd": (_int, [_c_void_p] * 7 + [_i64] * 3 + [ctypes.c_float, _int, _c_void_p]),
     "flr_batchnorm_bwd": (_int, [_c_void_p] * 10 + [_i64] * 3 + [_int, _c_void_p]),
+    "flr_bgemm_workspace": (_size_t, [_i64] * 4),
+    "flr_bgemm": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _i64, _i64,
+                         _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _size_t, _c_void_p]),
+    "flr_sum_rows": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p]),
     "flr_maxpool2d_fwd": (_int, [_c_void_p] * 3 + [_i64] * 7 + [_c_void_p]),
     "flr_maxpool2d_bwd": (_int, [_c_void_p] * 3 + [_i64] * 7 + [_c_void_p]),
     "flr_gru_fwd_step": (_int, [_c_void_p] * 4 + [_i64] * 5 + [_c_void_p]),

@@ -288,7 +288,12 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     T = tokens.shape[2]
     kofs = (torch.arange(K, device=tokens.device) * V).view(K, 1, 1)
     emb = table.reshape(K * V, E)[(tokens + kofs).reshape(-1)].view(K, B * T, E)
-    gi = torch.baddbmm(p["gru.bias_ih_l0"].unsqueeze(1), emb, p["gru.weight_ih_l0"].transpose(1, 2))
+    if native:  # flr_bgemm (MFMA) for every matrix product of the text branch and the head
+        from ..nn import client_linear as _lin
+    else:
+        def _lin(x, W, b):
+            return torch.baddbmm(b.unsqueeze(1), x, W.transpose(1, 2))
+    gi = _lin(emb, p["gru.weight_ih_l0"], p["gru.bias_ih_l0"])
     gi = gi.view(K, B, T, 3 * H)
     if _LAYERS == "native" and gi.is_cuda:  # flr HIP gate kernels (one launch per step)
         from ..nn import client_gru
@@ -297,7 +302,7 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
         h = _gru_torch(gi, p["gru.weight_hh_l0"], p["gru.bias_hh_l0"])
 
     f = torch.cat([img, h], dim=2)  # [K, B, 512 + H]
-    f = F.relu(torch.baddbmm(p["fc1.bias"].unsqueeze(1), f, p["fc1.weight"].transpose(1, 2)))
+    f = F.relu(_lin(f, p["fc1.weight"], p["fc1.bias"]))
     if dropout_mask is not None:
         f = f * dropout_mask
-    return torch.baddbmm(p["fc2.bias"].unsqueeze(1), f, p["fc2.weight"].transpose(1, 2))
+    return _lin(f, p["fc2.weight"], p["fc2.bias"])

@@ -124,14 +124,72 @@ def client_conv2d(x, w, stride: int, pad: int, need_dx: bool = True):
     return ClientConv2d.apply(x, w, stride, pad, need_dx)
 
 
+def bgemm(A: torch.Tensor, B: torch.Tensor, bias=None, add=None, out=None) -> torch.Tensor:
+    """out[k] = (bias[k] | add[k] | 0) + A[k] @ B[k]^T on flr_bgemm: A [K, M, R] and
+    B [K, N, R] are any strided views (transposes are free), bias [K, N]
+    (row stride 1), add shaped and strided like out (default: contiguous)."""
+    K, M, R = A.shape
+    N = B.shape[1]
+    if B.shape[0] != K or B.shape[2] != R:
+        raise ValueError(f"bgemm operand shapes {tuple(A.shape)} / {tuple(B.shape)}")
+    if out is None:
+        out = torch.empty(K, M, N, dtype=A.dtype, device=A.device)
+    if add is not None and add.stride() != out.stride():
+        raise ValueError("bgemm addend must share the output strides")
+    if bias is not None and (bias.shape != (K, N) or bias.stride(1) != 1):
+        raise ValueError("bgemm bias must be [K, N] with unit row stride")
+    n = int(_capi.lib().flr_bgemm_workspace(K, M, N, R))
+    ws = torch.empty(n, dtype=torch.uint8, device=A.device) if n else None
+    _capi.call("flr_bgemm", A.data_ptr(), *A.stride(), B.data_ptr(), *B.stride(), out.data_ptr(), *out.stride(),
+               _ptr(bias), 0 if bias is None else bias.stride(0), _ptr(add), K, M, N, R,
+               None if ws is None else ws.data_ptr(), n, _stream(A))
+    return out
+
+
+def sum_rows(X: torch.Tensor) -> torch.Tensor:
+    """[K, M, N] -> [K, N]: sum over m in order (flr_sum_rows); X row stride 1."""
+    K, M, N = X.shape
+    if X.stride(2) != 1:
+        X = X.contiguous()
+    out = torch.empty(K, N, dtype=X.dtype, device=X.device)
+    _capi.call("flr_sum_rows", X.data_ptr(), X.stride(0), X.stride(1), K, M, N, out.data_ptr(), N, _stream(X))
+    return out
+
+
+class ClientLinear(torch.autograd.Function):
+    """y[K, M, out] = x[K, M, in] W[K, out, in]^T + b[K, out] — nn.Linear of
+    every client at once (fusion head and GRU input projection,
+    cub200_cnn.py:88-93, 109-117 template) on the flr_bgemm MFMA kernel."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return bgemm(x, W, bias=b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = bgemm(dy, W.transpose(1, 2)) if ctx.needs_input_grad[0] else None
+        dW = bgemm(dy.transpose(1, 2), x.transpose(1, 2)) if ctx.needs_input_grad[1] else None
+        db = sum_rows(dy) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        return dx, dW, db
+
+
+def client_linear(x, W, b=None):
+    return ClientLinear.apply(x, W, b)
+
+
 class ClientGRU(torch.autograd.Function):
     """Final hidden state of a 1-layer GRU (h_0 = 0) for K clients at once.
 
     gi [K, B, T, 3H] = x W_ih^T + b_ih (computed by the caller, so autograd
     handles W_ih, b_ih and the embedding), whh [K, 3H, H], bhh [K, 3H] ->
-    h_T [K, B, H].  Per step: one batched GEMM (h W_hh^T + b_hh) and one
-    flr_gru_fwd_step launch; backward: one flr_gru_bwd_step and one GEMM per
-    step, then dW_hh / db_hh over all steps at once.
+    h_T [K, B, H].  Per step: one flr_bgemm (h W_hh^T + b_hh) and one
+    flr_gru_fwd_step launch; backward: one flr_gru_bwd_step and one flr_bgemm
+    per step, then dW_hh / db_hh over all steps at once (flr_bgemm,
+    flr_sum_rows).
     """
 
     @staticmethod
@@ -143,11 +201,11 @@ class ClientGRU(torch.autograd.Function):
         hseq = torch.empty(K, T + 1, B, H, dtype=gi.dtype, device=dev)
         hseq[:, 0].zero_()
         gates = torch.empty(K, T, B, 4, H, dtype=gi.dtype, device=dev)
-        whh_t = whh.transpose(1, 2)
-        bias = bhh.unsqueeze(1)
+        bias = bhh.contiguous()
         st = _stream(gi)
+        gh = torch.empty(K, B, H3, dtype=gi.dtype, device=dev)
         for t in range(T):
-            gh = torch.baddbmm(bias, hseq[:, t], whh_t)
+            bgemm(hseq[:, t], whh, bias=bias, out=gh)
             _capi.call("flr_gru_fwd_step", gi.data_ptr(), gh.data_ptr(), hseq.data_ptr(), gates.data_ptr(),
                        K, B, T, H, t, st)
         ctx.save_for_backward(whh, hseq, gates)
@@ -167,10 +225,10 @@ class ClientGRU(torch.autograd.Function):
             _capi.call("flr_gru_bwd_step", dh.data_ptr(), gates.data_ptr(), hseq.data_ptr(), dgh.data_ptr(),
                        dgi.data_ptr(), dh_direct.data_ptr(), K, B, T, H, t, st)
             if t > 0:  # dL/dh_t = z-path + dgh_t W_hh   (dL/dh_0 is not needed)
-                dh = torch.baddbmm(dh_direct, dgh[:, t], whh)
+                dh = bgemm(dgh[:, t], whh.transpose(1, 2), add=dh_direct)
         dgh2 = dgh.view(K, T * B, 3 * H)
-        dwhh = torch.bmm(dgh2.transpose(1, 2), hseq[:, :T].reshape(K, T * B, H))
-        dbhh = dgh2.sum(dim=1)
+        dwhh = bgemm(dgh2.transpose(1, 2), hseq[:, :T].reshape(K, T * B, H).transpose(1, 2))
+        dbhh = sum_rows(dgh2)
         return dgi, dwhh, dbhh
 
 

@@ -19,6 +19,9 @@ SHAPES = [  # (B, KC, H, W)
     (32, 130, 1, 1),
     (2, 3, 7, 9),
     (32, 256, 8, 8),
+    (32, 3, 16, 16),   # the stem's planes (8192 values: a whole workgroup per plane)
+    (16, 5, 16, 16),   # 4096 values per plane
+    (2, 9, 1, 2),      # 4 values per plane, 9 planes
 ]
 MODES = [(True, False), (True, True), (False, False), (False, True)]  # (relu, residual)
 
