@@ -140,6 +140,12 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& hi, bf16x8& 
 
 // FLR_GEMM=f32 selects the exact-f32 MFMA (A/B timing, cross-checks); read per
 // launch so one process can compare both forms.
+// FLR_XCD=0 turns the XCD-aware tile order off (A/B timing).
+inline int xcd_remap() {
+  const char* e = getenv("FLR_XCD");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 inline bool gemm_x6() {
   const char* e = getenv("FLR_GEMM");
   return !(e && e[0] == 'f');
@@ -692,16 +698,36 @@ __global__ __launch_bounds__(THREADS) void repad_kernel(const float* __restrict_
 // LDS feeds NS (A) or MS (B) MFMAs and the MS*NS accumulator chains are
 // independent.  MS or NS = 2 halves the loads, LDS traffic and barriers per
 // MFMA of the 64 x 64 tile.
+// XCD-aware tile order.  The hardware deals workgroups round-robin over the 8
+// XCDs (linear id i -> XCD i % 8), each with its own 4 MB L2.  The remap gives
+// XCD x one contiguous range of logical tiles (bijective for any grid size), so
+// the tiles of one client — which re-read the same activations once per kernel
+// tap and the same weight slabs once per pixel tile — run on one XCD and share
+// its L2 instead of streaming every client through all eight.
+__device__ __forceinline__ void xcd_tile(int& bx, int& by, int& bz) {
+  const int gx = (int)gridDim.x, gy = (int)gridDim.y;
+  const int n = gx * gy * (int)gridDim.z;
+  const int lid = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * (int)blockIdx.z);
+  const int xcd = lid & 7, slot = lid >> 3;
+  const int q = n >> 3, r = n & 7;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  bx = t % gx;
+  by = (t / gx) % gy;
+  bz = t / (gx * gy);
+}
+
 template <class Plan, int MS, int NS, bool X6>
-__global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S, float* __restrict__ part) {
+__global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S, float* __restrict__ part, int remap) {
   __shared__ __attribute__((aligned(16))) float As[2][MS][TILE];
   __shared__ __attribute__((aligned(16))) float Bs[2][NS][TILE];
-  const int k = blockIdx.z / S, split = blockIdx.z % S;
+  int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
+  if (remap) xcd_tile(bx, by, bz);
+  const int k = bz / S, split = bz % S;
   const int M = pl.M(), N = pl.N(), R = pl.R();
   const int ktiles = cdiv(R, BK);
   const int rbeg = (int)((int64_t)ktiles * split / S) * BK;
   const int rend = std::min(R, (int)((int64_t)ktiles * (split + 1) / S) * BK);
-  const int m0 = blockIdx.y * BM * MS, n0 = blockIdx.x * BN * NS;
+  const int m0 = by * BM * MS, n0 = bx * BN * NS;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -869,16 +895,22 @@ size_t splits_bytes(const Plan& pl) {  // enough for any sub-tile shape
   return S > 1 ? (size_t)S * pl.g.Kc * pl.M() * pl.N() * sizeof(float) : 0;
 }
 
-// Sub-tile shape: 64 x 64 (MS = NS = 1) measured fastest at every ResNet-18
-// layer on MI355X (4 workgroups/CU beat the 2/CU of the 55-KB 128 x 64 tile);
-// FLR_CONV_TILE=21|12 selects 128 x 64 / 64 x 128 for tuning experiments.
-inline int tile_choice(int M, int N) {
-  static const int forced = [] {
-    const char* e = getenv("FLR_CONV_TILE");
-    return e ? atoi(e) : 0;
-  }();
+// Workgroup tile: 64 x 64 (MS = NS = 1: 4 waves of 32 x 32, 4 workgroups/CU)
+// or 128 x 128 (MS = NS = 2: each wave 64 x 64, its A and B fragments — and
+// their bf16 splits — reused twice; 2 workgroups/CU).  Measured per ResNet-18
+// layer on MI355X (tools/conv_bench.py): 128 x 128 wins where both dimensions
+// allow it and the tile still has work — a reduction of >= 512 or more than
+// 128 x 512 outputs per client; 64 x 64 everywhere else.
+// FLR_CONV_TILE=11|21|12|22 forces a shape (read per launch, for A/B runs).
+inline int tile_choice(int M, int N, int R) {
+  const char* e = getenv("FLR_CONV_TILE");
+  const int forced = e ? atoi(e) : 0;
+  if (forced == 11) return 11;
   if (forced == 21 && M % 128 == 0) return 21;
   if (forced == 12 && N % 128 == 0) return 12;
+  const bool big = M % 128 == 0 && N % 128 == 0;
+  if (forced == 22 && big) return 22;
+  if (forced == 0 && big && (R >= 512 || (int64_t)M * N > 128 * 512)) return 22;
   return 11;
 }
 
@@ -889,9 +921,11 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) S = 1;
   const dim3 grid((unsigned)cdiv(N, BN * NS), (unsigned)cdiv(M, BM * MS), (unsigned)(K * S));
   if (gemm_x6())
-    hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, true>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws));
+    hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, true>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
+                       xcd_remap());
   else
-    hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, false>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws));
+    hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, false>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
+                       xcd_remap());
   int rc = launch_status(name);
   if (rc != FLR_OK || S == 1) return rc;
   const int64_t mn = (int64_t)M * N;
@@ -903,9 +937,10 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
 template <class Plan>
 int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   if (pl.R() == 0 && !std::is_same<Plan, DgradT>::value) return FLR_OK;  // a dgrad class with no tap stores zeros
-  switch (tile_choice(pl.M(), pl.N())) {
+  switch (tile_choice(pl.M(), pl.N(), pl.R())) {
     case 21: return launch_tiles<Plan, 2, 1>(pl, ws, ws_bytes, st, name);
     case 12: return launch_tiles<Plan, 1, 2>(pl, ws, ws_bytes, st, name);
+    case 22: return launch_tiles<Plan, 2, 2>(pl, ws, ws_bytes, st, name);
     default: return launch_tiles<Plan, 1, 1>(pl, ws, ws_bytes, st, name);
   }
 }

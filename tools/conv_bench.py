@@ -1,6 +1,8 @@
 """Per-layer timing of the client-batched conv kernels at the C3 shapes
 (K=128 clients, B=32): fwd / dgrad / wgrad, us and TFLOP/s (useful FLOPs of
-the valid taps).  usage: conv_bench.py [--only NAME] [--reps N]"""
+the valid taps).  usage: conv_bench.py [--only NAME] [--reps N] [--variants "A=1,B=2;C=3"]
+--variants: extra env settings timed in the same process, interleaved with the
+default (one column each; the kernels read FLR_GEMM / FLR_XCD per launch)."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "multimodal-fl-security_amd"))
@@ -34,7 +36,12 @@ def main():
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 5
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     dev = "cuda"
-    tot = 0.0
+    variants = [{}]
+    if "--variants" in sys.argv:
+        for v in sys.argv[sys.argv.index("--variants") + 1].split(";"):
+            variants.append(dict(kv.split("=") for kv in v.split(",") if kv))
+    print("variants:", variants, flush=True)
+    tot = [0.0] * len(variants)
     for name, Cin, H, Cout, k, s, p in LAYERS:
         if only and name != only:
             continue
@@ -63,18 +70,28 @@ def main():
         for op, fn in calls.items():
             if name == "stem" and op == "dgrad":
                 continue
-            fn()
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(reps):
+            cols = []
+            for vi, env in enumerate(variants):
+                saved = {k: os.environ.get(k) for k in env}
+                os.environ.update(env)
                 fn()
-            e1.record()
-            torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / reps
-            tot += us
-            print(f"{name:5s} {op:6s} {us:9.1f} us  {flops / us / 1e6:7.1f} TF/s", flush=True)
-    print(f"sum {tot / 1e3:.2f} ms (one of each per layer)")
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                for k, v in saved.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+                us = e0.elapsed_time(e1) * 1e3 / reps
+                tot[vi] += us
+                cols.append(f"{us:9.1f} us {flops / us / 1e6:7.1f} TF/s")
+            print(f"{name:5s} {op:6s} " + " | ".join(cols), flush=True)
+    print("sum " + " | ".join(f"{t / 1e3:.2f} ms" for t in tot) + " (one of each per layer)")
 
 
 if __name__ == "__main__":
