@@ -165,7 +165,11 @@ int flr_clip_sgd_step(float* X, const float* G, float* M, int64_t K, int64_t P,
  * of nblocks device pointers (nblocks <= 96).  Client k's element e of block j
  * is at ptr_j + k*stride_j + e.  Elements not covered by any block (dead
  * kernel taps, whose gradient is identically zero) are neither read nor
- * updated; with weight_decay == 0 that is exactly the reference's update. */
+ * updated; with weight_decay == 0 that is exactly the reference's update.
+ * first_step is a flag word here: bit 0 = first step (as above), bit 1 = the
+ * optimizer's last step (the momentum buffer is not written back: the
+ * reference re-creates the optimizer per client per round,
+ * run_experiments.py:206-211, so a last step's buffer is never read). */
 int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* const* g_blocks,
                               float* const* m_blocks, const int64_t* block_numel,
                               const int64_t* block_client_stride,
@@ -181,7 +185,10 @@ int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* const* g_bloc
  *                           the B*H*W pixels the GEMM walks are contiguous)
  *   w  [K][Cout][Cin][KH][KW]
  *   y  [K][Cout][B][Ho][Wo], Ho = (H + 2 pad - KH) / stride + 1
- * fp32 in, fp32 accumulate (exact-fp32 MFMA).  bwd_data writes dx, bwd_weight
+ * fp32 in, fp32 accumulate: each operand split into three bf16 terms, six
+ * products per k-step on v_mfma_f32_32x32x16_bf16 (per-product error a few
+ * 2^-24 |a b|, the size of an fp32 product's rounding); FLR_GEMM=f32 selects
+ * the exact-fp32 v_mfma_f32_32x32x2_f32.  bwd_data writes dx, bwd_weight
  * writes dw (both overwrite).  Kernel taps that only read zero padding are
  * skipped (their dw is written as exact zeros).  The workspace (optional,
  * size from flr_conv2d_workspace) enables deterministic split-K for long
@@ -202,6 +209,16 @@ int flr_conv2d_bwd_weight(const float* x, const float* dy, float* dw, int64_t K,
                           int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                           int64_t pad, void* workspace, size_t workspace_bytes,
                           void* stream);
+/* flr_conv2d_bwd_weight given the workspace of the flr_conv2d_fwd call that
+ * consumed the same x (and has not been reused since): when that forward took
+ * the explicit-im2col path (short reductions: the 7x7 stem), its column matrix
+ * heads the workspace and the weight gradient reads it instead of rebuilding
+ * it.  Otherwise identical to flr_conv2d_bwd_weight. */
+int flr_conv2d_bwd_weight_reuse(const float* x, const float* dy, float* dw, int64_t K,
+                                int64_t B, int64_t Cin, int64_t H, int64_t W,
+                                int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                                int64_t pad, void* workspace, size_t workspace_bytes,
+                                void* stream);
 
 /* ---- a5: cross-entropy forward + backward ------------------------------
  * Replaces nn.CrossEntropyLoss() (mean over each client's batch;
@@ -323,10 +340,12 @@ int flr_batchnorm_bwd(const float* dy, const float* x, const float* y,
  *   C_k[m][n] = (bias_k[n] or add_k[m][n] or 0) + sum_r A_k(m, r) B_k(n, r)
  * A(m, r) at A + k*a_k + m*a_m + r*a_r (B, C likewise; any strides, so
  * transposed operands are views); bias: NULL or [batch][bias_k] row vectors;
- * add: NULL or a C-shaped addend (may alias C).  Exact-fp32 MFMA, split-K
- * chosen from (M, N, R) alone, so every client's result is independent of the
- * batch count.  Workspace (optional, split-K partials): flr_bgemm_workspace.
- * flr_sum_rows: out[k][n] = sum_m X[k][m][n] in m order (bias gradients). */
+ * add: NULL or a C-shaped addend (may alias C).  Same MFMA tiles as the
+ * convolutions (three-term bf16 split, fp32 accumulate; FLR_GEMM=f32: exact-fp32
+ * MFMA); split-K chosen from (M, N, R) alone, so every client's result is
+ * independent of the batch count.  Workspace (optional, split-K partials): flr_bgemm_workspace.
+ * flr_sum_rows: out[k][n] = sum_m X[k][m][n] (bias gradients; eight interleaved
+ * partial sums in a fixed order, deterministic). */
 size_t flr_bgemm_workspace(int64_t batch, int64_t M, int64_t N, int64_t R);
 int flr_bgemm(const float* A, int64_t a_k, int64_t a_m, int64_t a_r, const float* B,
               int64_t b_k, int64_t b_n, int64_t b_r, float* C, int64_t c_k, int64_t c_m,

@@ -127,6 +127,6 @@ size_t im2col_workspace(const conv::Geom& g);
 int fwd_im2col(const conv::Geom& g, const float* x, const float* w, float* y, void* ws, size_t ws_bytes,
                hipStream_t st);
 int wgrad_im2col(const conv::Geom& g, const float* x, const float* dy, float* dw, void* ws, size_t ws_bytes,
-                 hipStream_t st);
+                 hipStream_t st, bool have_col);
 }  // namespace convt
 }  // namespace flr

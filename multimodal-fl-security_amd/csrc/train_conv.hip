@@ -476,9 +476,9 @@ extern "C" int flr_conv2d_bwd_data(const float* dy, const float* w, float* dx, i
   return launch(pb, ws, ws_bytes, as_stream(stream), "conv bwd data");
 }
 
-extern "C" int flr_conv2d_bwd_weight(const float* x, const float* dy, float* dw, int64_t K, int64_t B, int64_t Cin,
-                                     int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
-                                     int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+static int bwd_weight(const float* x, const float* dy, float* dw, int64_t K, int64_t B, int64_t Cin, int64_t H,
+                      int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* ws,
+                      size_t ws_bytes, void* stream, bool have_col) {
   if (!x || !dy || !dw || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
   const Geom g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
   hipStream_t st = as_stream(stream);
@@ -493,7 +493,7 @@ extern "C" int flr_conv2d_bwd_weight(const float* x, const float* dy, float* dw,
     if (rc != FLR_OK) return rc;
   }
   if (getenv_generic() == 0 && convt::im2col_eligible(g) && ws && ws_bytes >= convt::im2col_workspace(g))
-    return convt::wgrad_im2col(g, x, dy, dw, ws, ws_bytes, st);
+    return convt::wgrad_im2col(g, x, dy, dw, ws, ws_bytes, st, have_col);
   if (Cin % BN == 0 && getenv_generic() == 0) {
     WgtF pb;
     pb.g = g; pb.x = x; pb.dy = dy; pb.dw = dw;
@@ -502,4 +502,16 @@ extern "C" int flr_conv2d_bwd_weight(const float* x, const float* dy, float* dw,
   Wgt pb;
   pb.g = g; pb.x = x; pb.dy = dy; pb.dw = dw;
   return launch(pb, ws, ws_bytes, st, "conv bwd weight");
+}
+
+extern "C" int flr_conv2d_bwd_weight(const float* x, const float* dy, float* dw, int64_t K, int64_t B, int64_t Cin,
+                                     int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                                     int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+  return bwd_weight(x, dy, dw, K, B, Cin, H, W, Cout, KH, KW, stride, pad, ws, ws_bytes, stream, false);
+}
+
+extern "C" int flr_conv2d_bwd_weight_reuse(const float* x, const float* dy, float* dw, int64_t K, int64_t B,
+                                           int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+                                           int64_t stride, int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+  return bwd_weight(x, dy, dw, K, B, Cin, H, W, Cout, KH, KW, stride, pad, ws, ws_bytes, stream, true);
 }

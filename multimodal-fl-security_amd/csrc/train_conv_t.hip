@@ -637,16 +637,24 @@ struct BGemm : BGemmArgs {
   __device__ int64_t ldm() const { return c_m; }
 };
 
-// out[k][n] = sum_m X[k][m][n] in m order (bias gradients of the batched GEMMs)
+// out[k][n] = sum_m X[k][m][n] (bias gradients of the batched GEMMs).  Eight
+// interleaved accumulators (rows m = 8i + j go to accumulator j), combined in a
+// fixed tree: deterministic, and eight independent load/add chains per lane
+// instead of one M-long dependent chain.
 __global__ void sum_rows_kernel(const float* __restrict__ x, int64_t x_k, int64_t x_m, int M, int N,
                                 float* __restrict__ out, int64_t out_k) {
   const int k = blockIdx.y;
   const int nn = blockIdx.x * blockDim.x + threadIdx.x;
   if (nn >= N) return;
   const float* p = x + k * x_k + nn;
-  float s = 0.f;
-  for (int mm = 0; mm < M; ++mm) s += p[mm * x_m];
-  out[k * out_k + nn] = s;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int mm = 0;
+  for (; mm + 8 <= M; mm += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += p[(int64_t)(mm + j) * x_m];
+  }
+  for (int j = 0; mm < M; ++mm, ++j) a[j] += p[(int64_t)mm * x_m];
+  out[k * out_k + nn] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
 constexpr int IM_PB = 32, IM_MAXRP = 512;
@@ -991,7 +999,7 @@ int fwd_im2col(const Geom& g, const float* x, const float* w, float* y, void* ws
 }
 
 int wgrad_im2col(const Geom& g, const float* x, const float* dy, float* dw, void* ws, size_t ws_bytes,
-                 hipStream_t st) {
+                 hipStream_t st, bool have_col) {
   if (!ws || ws_bytes < im2col_workspace(g)) return FLR_ERR_WORKSPACE;
   const int RP = padded_r(g), R = g.Cin * g.KH * g.KW;
   char* base = static_cast<char*>(ws);
@@ -999,7 +1007,7 @@ int wgrad_im2col(const Geom& g, const float* x, const float* dy, float* dw, void
   const size_t colb = align_up((size_t)g.Kc * g.B * g.Ho * g.Wo * RP * sizeof(float), 256);
   float* dwp = reinterpret_cast<float*>(base + colb);
   const size_t wpb = align_up((size_t)g.Kc * g.Cout * RP * sizeof(float), 256);
-  int rc = run_im2col(g, x, col, st);
+  int rc = have_col ? FLR_OK : run_im2col(g, x, col, st);  // have_col: the forward's column matrix
   if (rc != FLR_OK) return rc;
   DenseWgt pl;
   pl.g = g; pl.RP = RP; pl.col = col; pl.dy = dy; pl.dwp = dwp;

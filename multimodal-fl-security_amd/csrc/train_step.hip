@@ -192,14 +192,26 @@ __global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable
 }
 
 // grid (NSGD, K): workgroup b of client k updates flattened range [P*b/NSGD, P*(b+1)/NSGD).
+// flags: bit 0 = the optimizer's first step (buf = g, the old buffer is not
+// read); bit 1 = its last step (the new buffer is not written: the optimizer
+// is discarded after the client's local update, run_experiments.py:206-211).
+// The float4 body keeps two groups of (x, g, m) loads in flight per lane.
 constexpr int NSGD = 256;
 __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable tb, int64_t P,
                                                               const float* __restrict__ coef, float lr, float mom,
-                                                              float wd, int first) {
+                                                              float wd, int flags) {
   const int k = blockIdx.y, b = blockIdx.x;
+  const bool first = flags & 1, last = flags & 2;
   const float c = coef ? coef[k] : 1.0f;
   const float nlr = -lr;
   const int64_t p0 = P * b / NSGD, p1 = P * (b + 1) / NSGD;
+  auto upd = [&](float xp, float gr, float mp, float& mo, float& xo) {
+    float gp = gr * c;
+    if (wd != 0.0f) gp = __builtin_fmaf(wd, xp, gp);
+    const float bb = first ? gp : mp * mom + gp;  // buf.mul_(mom).add_(g): two roundings
+    mo = bb;
+    xo = __builtin_fmaf(nlr, bb, xp);
+  };
   for (int j = 0; j < tb.nb; ++j) {
     const int64_t lo = p0 > tb.pre[j] ? p0 : tb.pre[j];
     const int64_t hi = p1 < tb.pre[j + 1] ? p1 : tb.pre[j + 1];
@@ -208,37 +220,49 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
     float* x = tb.x[j] + base;
     const float* g = tb.g[j] + base;
     float* m = tb.m[j] + base;
-    auto upd = [&](float xp, float gr, float mp, float& mo, float& xo) {
-      float gp = gr * c;
-      if (wd != 0.0f) gp = __builtin_fmaf(wd, xp, gp);
-      const float bb = first ? gp : mp * mom + gp;  // buf.mul_(mom).add_(g): two roundings
-      mo = bb;
-      xo = __builtin_fmaf(nlr, bb, xp);
+    auto one = [&](int64_t e) {
+      float mo, xo;
+      upd(x[e], g[e], first ? 0.f : m[e], mo, xo);
+      if (!last) m[e] = mo;
+      x[e] = xo;
     };
-    visit_range(
-        lo, hi, tb.pre[j], tb.vec[j] != 0,
-        [&](int64_t e) {
-          float mo, xo;
-          upd(x[e], g[e], first ? 0.f : m[e], mo, xo);
-          m[e] = mo;
-          x[e] = xo;
-        },
-        [&](int64_t e) {
-          const f32x4 xv = *reinterpret_cast<const f32x4*>(x + e);
-          const f32x4 gv = *reinterpret_cast<const f32x4*>(g + e);
-          f32x4 mv = {0.f, 0.f, 0.f, 0.f};
-          if (!first) mv = *reinterpret_cast<const f32x4*>(m + e);
-          f32x4 mo, xo;
+    auto four = [&](const f32x4& xv, const f32x4& gv, const f32x4& mv, int64_t e) {
+      f32x4 mo, xo;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float a, b;
-            upd(xv[q], gv[q], mv[q], a, b);
-            mo[q] = a;
-            xo[q] = b;
-          }
-          *reinterpret_cast<f32x4*>(m + e) = mo;
-          *reinterpret_cast<f32x4*>(x + e) = xo;
-        });
+      for (int q = 0; q < 4; ++q) {
+        float a, bq;
+        upd(xv[q], gv[q], mv[q], a, bq);
+        mo[q] = a;
+        xo[q] = bq;
+      }
+      if (!last) *reinterpret_cast<f32x4*>(m + e) = mo;
+      *reinterpret_cast<f32x4*>(x + e) = xo;
+    };
+    if (!tb.vec[j]) {
+      for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) one(e);
+      continue;
+    }
+    const int64_t pre = tb.pre[j];
+    int64_t vlo = pre + ((lo - pre + 3) & ~(int64_t)3);
+    if (vlo > hi) vlo = hi;
+    const int64_t vhi = pre + ((hi - pre) & ~(int64_t)3);
+    for (int64_t e = lo + threadIdx.x; e < vlo; e += THREADS) one(e);
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    int64_t e = vlo + 4 * (int64_t)threadIdx.x;
+    for (; e + 4 * THREADS < vhi; e += 8 * THREADS) {  // two float4 groups per lane in flight
+      const int64_t e2 = e + 4 * THREADS;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(x + e), x1 = *reinterpret_cast<const f32x4*>(x + e2);
+      const f32x4 g0 = *reinterpret_cast<const f32x4*>(g + e), g1 = *reinterpret_cast<const f32x4*>(g + e2);
+      const f32x4 m0 = first ? z : *reinterpret_cast<const f32x4*>(m + e);
+      const f32x4 m1 = first ? z : *reinterpret_cast<const f32x4*>(m + e2);
+      four(x0, g0, m0, e);
+      four(x1, g1, m1, e2);
+    }
+    if (e < vhi) {
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(x + e), g0 = *reinterpret_cast<const f32x4*>(g + e);
+      four(x0, g0, first ? z : *reinterpret_cast<const f32x4*>(m + e), e);
+    }
+    for (int64_t t = (vhi > vlo ? vhi : vlo) + threadIdx.x; t < hi; t += THREADS) one(t);
   }
 }
 
@@ -340,6 +364,6 @@ extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* co
     if ((rc = launch_status("clip_coef_kernel")) != FLR_OK) return rc;
   }
   hipLaunchKernelGGL(train::sgd_blocked_kernel, dim3(train::NSGD, (unsigned)K), dim3(train::THREADS), 0, st, tb, P,
-                     coef, lr, momentum, weight_decay, first_step);
+                     coef, lr, momentum, weight_decay, first_step & 3);
   return launch_status("sgd_blocked_kernel");
 }

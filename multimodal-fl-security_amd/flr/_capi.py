@@ -69,6 +69,8 @@ SIGNATURES = {
     "flr_conv2d_fwd": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_data": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_weight": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
+    "flr_conv2d_bwd_weight_reuse": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t,
+                                                                                            _c_void_p]),
     "flr_cross_entropy": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "flr_scale_client_rows": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p]),
     "flr_broadcast_rows": (_int, [_c_void_p, _i64, _c_void_p, _i64, _i64, _c_void_p]),

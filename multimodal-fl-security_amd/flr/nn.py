@@ -39,6 +39,7 @@ class ClientConv2d(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.geom = geom
         ctx.need_dx = need_dx
+        ctx.fwd_ws = (ws, n)  # holds the forward's im2col column matrix for the weight gradient
         return y
 
     @staticmethod
@@ -46,6 +47,8 @@ class ClientConv2d(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dy = dy.contiguous()
         g = ctx.geom
+        fws, fn = ctx.fwd_ws
+        ctx.fwd_ws = None
         ws, n = _workspace(g, dy.device)
         wsp = None if ws is None else ws.data_ptr()
         dx = None
@@ -55,8 +58,12 @@ class ClientConv2d(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w)
-            _capi.call("flr_conv2d_bwd_weight", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *g, wsp, n,
-                       _stream(dy))
+            if fws is not None:  # the forward's workspace: its column matrix is reused
+                _capi.call("flr_conv2d_bwd_weight_reuse", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *g,
+                           fws.data_ptr(), fn, _stream(dy))
+            else:
+                _capi.call("flr_conv2d_bwd_weight", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *g, wsp, n,
+                           _stream(dy))
         return dx, dw, None, None, None
 
 

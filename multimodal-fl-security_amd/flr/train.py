@@ -180,7 +180,7 @@ class ClientBatchTrainer:
         return self.X
 
     # ---- one optimizer step for every client -----------------------------
-    def step(self, images, tokens, labels, first: bool, dropout_mask=None) -> torch.Tensor:
+    def step(self, images, tokens, labels, first: bool, dropout_mask=None, last: bool = False) -> torch.Tensor:
         leaves = [w.detach().requires_grad_(True) for w in self.W]
         params: Dict[str, torch.Tensor] = dict(zip(self.names, leaves))
         logits = batched_forward(params, images, tokens, self.spec, dropout_mask, self.tap_major, self.skip_dead)
@@ -189,7 +189,7 @@ class ClientBatchTrainer:
         gp = (ctypes.c_void_p * len(self.blocks))(*[grads[j].data_ptr() + 4 * o for j, o, _, _ in self.blocks])
         c = self.cfg
         _capi.call("flr_clip_sgd_step_blocked", self._xp, gp, self._mp, self._np, self._cs, len(self.blocks), self.K,
-                   c.lr, c.momentum, c.weight_decay, c.clip, int(first), self.norms.data_ptr(),
+                   c.lr, c.momentum, c.weight_decay, c.clip, int(first) | (int(last) << 1), self.norms.data_ptr(),
                    self._ws.data_ptr() + self._ws_off, self._ws_bytes, _stream(self._wbuf))
         return loss_k.detach()
 
@@ -199,7 +199,8 @@ class ClientBatchTrainer:
         total = torch.zeros(self.K, dtype=torch.float32, device=self.device)
         for s, (images, tokens, labels) in enumerate(batches):
             mask = None if dropout_masks is None else dropout_masks[s]
-            total += self.step(images, tokens, labels, first=(s == 0), dropout_mask=mask)
+            total += self.step(images, tokens, labels, first=(s == 0), dropout_mask=mask,
+                               last=(s == len(batches) - 1))
         if export:
             self.export()
         return total / max(1, len(batches))
