@@ -1,5 +1,11 @@
-"""The multimodal client model: ResNet-18 image trunk + 1-layer GRU text
-encoder + late-fusion MLP (BASELINE.json configs C2/C3).
+"""The multimodal client models.
+
+* family "resnet_gru" (BASELINE.json configs C2/C3): ResNet-18 image trunk +
+  1-layer GRU text encoder + late-fusion MLP.
+* family "cub" (config C1): the reference's own multimodal model,
+  CUB200MultimodalCNN (src/models/cub200_cnn.py:57-118) — three conv3x3 / BN /
+  ReLU / MaxPool2 blocks, AdaptiveAvgPool(4, 4), image_fc, the attribute MLP
+  over a multi-hot ("BoW") text vector, and the same fusion head.
 
 The reference's only multimodal model is CUB200MultimodalCNN
 (src/models/cub200_cnn.py:57-118): conv image branch, a second modality
@@ -43,14 +49,24 @@ class ModelSpec:
     hidden: int = 256
     fusion: int = 256
     dropout: float = 0.5
+    family: str = "resnet_gru"  # "resnet_gru" (C2/C3) | "cub" (C1)
 
     @property
     def name(self) -> str:
+        if self.family == "cub":
+            return "cub200-multimodal-cnn (conv img + attribute MLP) late-fusion"
         return "resnet18-img+gru1-text late-fusion"
 
 
 TINY = ModelSpec(widths=(8, 16, 16, 32), blocks=(1, 1, 1, 1), vocab=50, embed=8, hidden=16, fusion=16,
                  dropout=0.0)
+
+# C1: CUB200MultimodalCNN at 32x32 with C = 10 classes and the BoW text modality
+# as its attribute vector (num_attributes = vocab = 312).  widths = the three
+# conv blocks; fusion = image_fc / fusion hidden width; embed, hidden = the
+# attribute MLP's widths (cub200_cnn.py:71-93).
+CUB = ModelSpec(family="cub", num_classes=10, widths=(32, 64, 128), blocks=(), vocab=312, embed=128,
+                hidden=256, fusion=256, dropout=0.5)
 
 
 class BasicBlock(nn.Module):
@@ -105,10 +121,46 @@ class MultimodalNet(nn.Module):
         return self.fc2(z)
 
 
+class CubMultimodalNet(nn.Module):
+    """The C1 model: layer for layer the structure of CUB200MultimodalCNN
+    (cub200_cnn.py:67-93), so parameters() has the reference's names, shapes
+    and order (the client-matrix row layout).  forward(images, attributes=None):
+    without attributes the image features are padded with zeros
+    (cub200_cnn.py:110-115)."""
+
+    def __init__(self, spec: ModelSpec = CUB):
+        super().__init__()
+        self.spec = spec
+        c1, c2, c3 = spec.widths
+
+        def block(cin, cout):
+            return [nn.Conv2d(cin, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(), nn.MaxPool2d(2)]
+        self.image_conv = nn.Sequential(*block(spec.in_channels, c1), *block(c1, c2), *block(c2, c3),
+                                        nn.AdaptiveAvgPool2d((4, 4)))
+        self.image_fc = nn.Linear(c3 * 16, spec.fusion)
+        self.attr_fc = nn.Sequential(nn.Linear(spec.vocab, spec.embed), nn.ReLU(),
+                                     nn.Linear(spec.embed, spec.hidden), nn.ReLU())
+        self.fusion = nn.Sequential(nn.Linear(spec.fusion + spec.hidden, spec.fusion), nn.ReLU(),
+                                    nn.Dropout(spec.dropout), nn.Linear(spec.fusion, spec.num_classes))
+
+    def forward(self, images: torch.Tensor, attributes: Optional[torch.Tensor] = None) -> torch.Tensor:
+        img = F.relu(self.image_fc(self.image_conv(images).flatten(1)))
+        if attributes is None:
+            att = torch.zeros(img.shape[0], self.spec.hidden, device=img.device, dtype=img.dtype)
+        else:
+            att = self.attr_fc(attributes)
+        return self.fusion(torch.cat([img, att], dim=1))
+
+
+def model_class(spec: ModelSpec):
+    """The nn.Module of one client for this spec's family."""
+    return CubMultimodalNet if spec.family == "cub" else MultimodalNet
+
+
 def param_layout(spec: ModelSpec) -> List[Tuple[str, torch.Size]]:
     """(name, shape) in parameters() order — the client-matrix row layout."""
     with torch.device("meta"):
-        m = MultimodalNet(spec)
+        m = model_class(spec)(spec)
     return [(n, p.shape) for n, p in m.named_parameters()]
 
 
@@ -148,6 +200,11 @@ def conv_geometry(spec: ModelSpec) -> Dict[str, Tuple[int, int, int, int, int]]:
     """name -> (H_in, kernel, stride, pad, H_out) of every conv weight (square maps)."""
     out = {}
     H = spec.image_size
+    if spec.family == "cub":
+        for idx in (0, 4, 8):
+            out[f"image_conv.{idx}.weight"] = (H, 3, 1, 1, H)
+            H //= 2
+        return out
     Ho = (H + 6 - 7) // 2 + 1
     out["conv1.weight"] = (H, 7, 2, 3, Ho)
     H = (Ho + 2 - 3) // 2 + 1  # 3x3/2 max-pool
@@ -250,6 +307,9 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     skip_dead: tap-major weights whose dead-tap gradient slabs are left
     unwritten (the trainer's optimizer step never reads them).
     """
+    if spec.family == "cub":
+        return _cub_forward(p, images, tokens, spec, dropout_mask, tap_major)
+
     def conv(name, x, stride, pad, need_dx=True):
         return _gconv(x, p[name], stride, pad, need_dx, name in tap_major, name not in skip_dead)
 
@@ -306,3 +366,52 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     if dropout_mask is not None:
         f = f * dropout_mask
     return _lin(f, p["fc2.weight"], p["fc2.bias"])
+
+
+def _linear_op(native: bool):
+    if native:  # flr_bgemm (MFMA)
+        from ..nn import client_linear
+        return client_linear
+
+    def lin(x, W, b):
+        return torch.baddbmm(b.unsqueeze(1), x, W.transpose(1, 2))
+    return lin
+
+
+def _cub_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, attrs: Optional[torch.Tensor], spec: ModelSpec,
+                 dropout_mask: Optional[torch.Tensor], tap_major: frozenset) -> torch.Tensor:
+    """The C1 model (cub200_cnn.py:95-118) for K clients at once: three
+    conv3x3(+bias) -> BN -> ReLU -> MaxPool2 blocks, AdaptiveAvgPool(4, 4),
+    image_fc + ReLU, the attribute MLP, concat, the fusion head.
+    images [K, B, C, H, W], attrs [K, B, V] (multi-hot) or None."""
+    K, B = images.shape[:2]
+    native = _LAYERS == "native" and images.is_cuda
+    C0, H, W = images.shape[2:]
+    x = (images.transpose(1, 2).reshape(K * C0, B, H, W) if native
+         else images.transpose(0, 1).reshape(B, K * C0, H, W))
+    for i, idx in enumerate((0, 4, 8)):
+        wn = f"image_conv.{idx}.weight"
+        y = _gconv(x, p[wn], 1, 1, need_dx=i > 0, tap_major=wn in tap_major)
+        bias = p[f"image_conv.{idx}.bias"].reshape(-1)  # [K * Cout]
+        y = y + (bias.view(-1, 1, 1, 1) if native else bias.view(1, -1, 1, 1))
+        y = _bn_act(y, p[f"image_conv.{idx + 1}.weight"], p[f"image_conv.{idx + 1}.bias"])
+        if native:
+            from ..nn import client_maxpool2d
+            x = client_maxpool2d(y, 2, 2, 0)
+        else:
+            x = F.max_pool2d(y, 2)
+    if tuple(x.shape[-2:]) != (4, 4):  # at 32x32 input the map is already 4x4 (identity)
+        x = F.adaptive_avg_pool2d(x, (4, 4))
+    c3 = spec.widths[-1]
+    img = x.reshape(K, c3, B, 16).transpose(1, 2) if native else x.reshape(B, K, c3, 16).transpose(0, 1)
+    lin = _linear_op(native)
+    img = F.relu(lin(img.reshape(K, B, c3 * 16), p["image_fc.weight"], p["image_fc.bias"]))
+    if attrs is None:
+        a = torch.zeros(K, B, spec.hidden, device=img.device, dtype=img.dtype)
+    else:
+        a = F.relu(lin(attrs, p["attr_fc.0.weight"], p["attr_fc.0.bias"]))
+        a = F.relu(lin(a, p["attr_fc.2.weight"], p["attr_fc.2.bias"]))
+    f = F.relu(lin(torch.cat([img, a], dim=2), p["fusion.0.weight"], p["fusion.0.bias"]))
+    if dropout_mask is not None:
+        f = f * dropout_mask
+    return lin(f, p["fusion.3.weight"], p["fusion.3.bias"])

@@ -29,7 +29,7 @@ from .attacks import Backdoor, poison_batches_
 from .defenses import get_defense
 from .matrix import ClientMatrix
 from .shard import PW_SLICES, Comm, CoordExchange
-from .models.multimodal import ModelSpec, MultimodalNet, param_layout
+from .models.multimodal import ModelSpec, model_class, param_layout
 from .train import ClientBatchTrainer, TrainConfig, make_dropout_masks, synthetic_batches
 
 
@@ -47,9 +47,9 @@ class RoundConfig:
 
 
 def initial_global(spec: ModelSpec, seed: int, device) -> torch.Tensor:
-    """Global model init: the torch default init of MultimodalNet under seed."""
+    """Global model init: the torch default init of the spec's model under seed."""
     torch.manual_seed(seed)
-    m = MultimodalNet(spec)
+    m = model_class(spec)(spec)
     return torch.cat([p.detach().reshape(-1) for p in m.parameters()]).to(device)
 
 

@@ -229,7 +229,8 @@ def synthetic_batches(spec: ModelSpec, steps: int, client_ids: Sequence[int], ba
                       seed_base: int = 1000):
     """SURVEY §8d inputs: images N(0,1) [B,3,32,32], tokens U{0..V-1} [B,T],
     labels U{0..C-1}; client c's stream seeded 1000 + c (independent of how
-    clients are sharded over GPUs)."""
+    clients are sharded over GPUs).  The C1 ("cub") family gets the tokens as a
+    multi-hot [B, V] float vector (its attribute input)."""
     K = len(client_ids)
     imgs = torch.empty(steps, K, batch, spec.in_channels, spec.image_size, spec.image_size, device=device)
     toks = torch.empty(steps, K, batch, spec.seq_len, dtype=torch.int64, device=device)
@@ -240,4 +241,7 @@ def synthetic_batches(spec: ModelSpec, steps: int, client_ids: Sequence[int], ba
         imgs[:, j] = torch.randn(steps, batch, spec.in_channels, spec.image_size, spec.image_size, generator=g).to(device)
         toks[:, j] = torch.randint(0, spec.vocab, (steps, batch, spec.seq_len), generator=g).to(device)
         labs[:, j] = torch.randint(0, spec.num_classes, (steps, batch), generator=g).to(device)
+    if spec.family == "cub":  # C1's text modality: the multi-hot attribute ("BoW") vector of the tokens
+        text = torch.zeros(steps, K, batch, spec.vocab, device=device).scatter_(3, toks, 1.0)
+        return [(imgs[s], text[s], labs[s]) for s in range(steps)]
     return [(imgs[s], toks[s], labs[s]) for s in range(steps)]

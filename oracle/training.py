@@ -25,6 +25,19 @@ class _MaskDropout(nn.Module):
         return x if self.mask is None else x * self.mask
 
 
+def _mask_dropouts(model: nn.Module) -> List[_MaskDropout]:
+    """Replace every nn.Dropout of the model (an attribute or a Sequential
+    entry) by a module that applies an explicit mask."""
+    out = []
+    for mod in list(model.modules()):
+        for cname, child in list(mod.named_children()):
+            if isinstance(child, nn.Dropout):
+                md = _MaskDropout()
+                setattr(mod, cname, md)
+                out.append(md)
+    return out
+
+
 def local_update(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, lr: float = 0.01,
                  momentum: float = 0.9, weight_decay: float = 0.0, max_norm: float = 1.0,
                  masks: Optional[Sequence[torch.Tensor]] = None, threads: Optional[int] = None
@@ -39,13 +52,14 @@ def local_update(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, 
             n = p.numel()
             p.copy_(global_flat[off:off + n].view(p.shape))
             off += n
-    model.dropout = _MaskDropout()
+    drops = _mask_dropouts(model)
     optimizer = torch.optim.SGD(model.parameters(), lr=lr, momentum=momentum, weight_decay=weight_decay)  # :206-211
     criterion = nn.CrossEntropyLoss()
     model.train()
     losses = []
     for s, (images, tokens, labels) in enumerate(batches):
-        model.dropout.mask = None if masks is None else masks[s]
+        for d in drops:
+            d.mask = None if masks is None else masks[s]
         optimizer.zero_grad()
         outputs = model(images, tokens)
         loss = criterion(outputs, labels)

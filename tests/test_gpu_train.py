@@ -6,7 +6,7 @@ import torch
 
 from oracle import training as otrain
 from flr.client import Client
-from flr.models.multimodal import TINY, ModelSpec, MultimodalNet, num_params
+from flr.models.multimodal import CUB, TINY, ModelSpec, MultimodalNet, model_class, num_params
 from flr.round import initial_global
 from flr.train import ClientBatchTrainer, TrainConfig, make_dropout_masks, synthetic_batches
 
@@ -115,3 +115,51 @@ def test_layout_kernels(cuda):
         X = torch.zeros(K, n + 13, device=cuda)
         _capi.call("flr_tap_major_to_torch", wt.data_ptr(), K, k * k, cin, cout, X.data_ptr() + 4 * 5, n + 13, st)
         assert torch.equal(X[:, 5:5 + n], w.reshape(K, n))
+
+
+def test_cub_c1_model_matches_reference_loop(cuda):
+    """Config C1's model — the reference's CUB200MultimodalCNN structure (conv
+    blocks with bias, attribute MLP over the multi-hot text, fusion head with
+    dropout masks) — with the cub200 optimizer (weight decay 1e-4,
+    run_experiments.py:210), 3 clients x 3 steps vs the oracle loop."""
+    spec = CUB
+    K, B, steps = 3, 8, 3
+    glob = initial_global(spec, 42, cuda)
+    tr = ClientBatchTrainer(spec, K, cuda, TrainConfig(local_steps=steps, weight_decay=1e-4))
+    assert tr.tap_major == {"image_conv.8.weight"}  # 64 -> 128: the tap-major kernels
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    masks = make_dropout_masks(spec, steps, K, B, cuda, seed=9)
+    tr.load_global(glob)
+    loss = tr.local_update(batches, masks).cpu()
+    for k in range(K):
+        cb = [(im[k].cpu(), tx[k].cpu(), lb[k].cpu()) for im, tx, lb in batches]
+        upd, ref_loss = otrain.local_update(model_class(spec), spec, glob.cpu(), cb, weight_decay=1e-4,
+                                            masks=[m[k].cpu() for m in masks])
+        ref = torch.cat([u.reshape(-1) for u in upd])
+        got = tr.X.data[k, : tr.P].cpu()
+        assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+        assert _rel(got, ref) < 1e-5, _rel(got, ref)
+
+
+def test_c1_round_fedavg_matches_reference(cuda):
+    """Config C1 end to end: K = 4 clients, 2 local steps, FedAvg write-back
+    (run_experiments.py:193-259) on the engine vs the oracle's per-client loop
+    + FedAvg (base_defense.py:80-97)."""
+    from oracle import aggregation as orc
+    from flr.round import RoundConfig, RoundEngine
+    spec = CUB
+    K, steps, B = 4, 2, 8
+    rc = RoundConfig(num_clients=K, batch=B, defense="fedavg", attack="none", num_attackers=0)
+    eng = RoundEngine(spec, rc, TrainConfig(local_steps=steps, weight_decay=1e-4), cuda)
+    glob = eng.global_flat.clone().cpu()
+    new = eng.run_round().cpu()
+    batches = synthetic_batches(spec, steps, range(K), B, "cpu")
+    masks = make_dropout_masks(spec, steps, range(K), B, "cpu", seed=rc.seed + 7919)
+    ups = []
+    for k in range(K):
+        cb = [(im[k], tx[k], lb[k]) for im, tx, lb in batches]
+        upd, _ = otrain.local_update(model_class(spec), spec, glob, cb, weight_decay=1e-4,
+                                     masks=[m[k] for m in masks])
+        ups.append(upd)
+    ref = torch.cat([t.reshape(-1) for t in orc.fedavg(ups, [steps * B] * K)])
+    assert _rel(new, ref) < 1e-5, _rel(new, ref)
