@@ -109,11 +109,14 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "allgather"])
+    ap.add_argument("--defense", default="krum", help="secondary configs: fedavg (C2), trimmed_mean, median")
+    ap.add_argument("--model", default="resnet_gru", choices=["resnet_gru", "cub"],
+                    help="cub = the C1 model (the reference's CUB200MultimodalCNN structure)")
     args = ap.parse_args()
 
     import torch
     from flr import dist as fdist
-    from flr.models.multimodal import ModelSpec, num_params
+    from flr.models.multimodal import CUB, ModelSpec, num_params
     from flr.round import RoundConfig, RoundEngine
     from flr.timing import HipEventPair
     from flr.train import TrainConfig
@@ -122,14 +125,16 @@ def main() -> None:
     rank, world, local = fdist.init("nccl")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    spec = ModelSpec()
+    spec = CUB if args.model == "cub" else ModelSpec()
     P = num_params(spec)
     K = args.clients
-    f = int(0.2 * K)
-    rcfg = RoundConfig(num_clients=K, defense="krum", num_attackers=f, exchange=args.exchange)
+    krum = args.defense in ("krum", "multi_krum")
+    f = int(0.2 * K) if krum else 0
+    rcfg = RoundConfig(num_clients=K, defense=args.defense, num_attackers=f, exchange=args.exchange,
+                       attack="sign_flip" if krum else "none")
     tcfg = TrainConfig(local_steps=args.local_steps)
     eng = RoundEngine(spec, rcfg, tcfg, device, rank, world)
-    multi_k = eng.defense.multi_k
+    multi_k = getattr(eng.defense, "multi_k", 0)
 
     for _ in range(args.warmup):
         eng.run_round()
@@ -147,17 +152,19 @@ def main() -> None:
     sharded = eng.exchange == "alltoall"
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
+    kw = {"publish": False} if hasattr(eng.defense, "publish") else {}
     for _ in range(reps):  # Server.aggregate alone (sharded: this GPU's range + the P-vector all-gather)
         if sharded:
-            eng.slice.gather_vector(eng.defense.aggregate_sharded(eng.slice, eng.num_examples, publish=False),
+            eng.slice.gather_vector(eng.defense.aggregate_sharded(eng.slice, eng.num_examples, **kw),
                                     torch.empty_like(eng.global_flat))
         else:
-            eng.defense.aggregate_flat(eng.full, eng.num_examples, publish=False)
+            eng.defense.aggregate_flat(eng.full, eng.num_examples, **kw)
     ev1.record()
     torch.cuda.synchronize()
     aggregate_ms = ev0.elapsed_time(ev1) / reps
-    # the dominant aggregation kernel: centred-Gram pairwise (HIP events around
-    # its launch, on the stream it runs on); sharded: this GPU's coordinates
+    # the dominant aggregation kernel of the headline config: centred-Gram pairwise
+    # (HIP events around its launch, on the stream it runs on); sharded: this
+    # GPU's coordinates.  Timed for every config (the Krum roofline line).
     kms = []
     for _ in range(reps):
         ev = HipEventPair()
@@ -180,8 +187,10 @@ def main() -> None:
     ev1.record()
     torch.cuda.synchronize()
     train_ms = ev0.elapsed_time(ev1)
-    eng.defense.publish()
-    attackers_selected = sorted(set(eng.defense.selected_clients) & set(range(f)))
+    attackers_selected = None
+    if krum:
+        eng.defense.publish()
+        attackers_selected = sorted(set(eng.defense.selected_clients) & set(range(f)))
 
     out = {
         "metric": METRIC,
@@ -198,10 +207,11 @@ def main() -> None:
         "data": "synthetic (SURVEY §8d: N(0,1) 3x32x32 images, U{0..999} 16-token texts, 10 classes; "
                 "random-init weights, seed 42)",
         "config": {
-            "workload": "C3: Multi-Krum K=128, 20% sign-flip, ResNet-18 img + 1-layer GRU text late fusion, "
-                        "5 local SGD steps/round",
+            "workload": ("C3: Multi-Krum K=128, 20% sign-flip, ResNet-18 img + 1-layer GRU text late fusion, "
+                         "5 local SGD steps/round") if (krum and K == 128 and args.model == "resnet_gru") else
+                        f"{args.defense} K={K}, {spec.name}, {args.local_steps} local SGD steps/round",
             "clients": K, "params": P, "local_steps": args.local_steps, "batch": rcfg.batch,
-            "defense": f"krum(f={f}, multi_k={multi_k})", "attackers": f,
+            "defense": f"krum(f={f}, multi_k={multi_k})" if krum else args.defense, "attackers": f,
             "parallelism": (f"clients sharded {K // world}/GPU x {world}; " + (
                 "one all-to-all (client rows -> coordinate ranges), per-GPU aggregation of its range, "
                 "all-gather of the aggregated vector" if sharded else "one all-gather of the client matrix")),
@@ -218,7 +228,7 @@ def main() -> None:
             "kernel_ms": kernel_ms, "algorithmic_bytes": pair_bytes, "coords_per_gpu": n_coords,
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and krum and args.model == "resnet_gru":
         out["cpu_baseline"] = cpu_baseline(spec, P, K, f, multi_k, args.local_steps, rcfg.batch, args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
