@@ -368,6 +368,27 @@ int flr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* dx, int64_t
                       int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t stride,
                       int64_t pad, void* stream);
 
+/* ---- §8(f): per-round evaluation of the global model (forward only) -------
+ * Replaces evaluate_model / compute_attack_success_rate /
+ * compute_label_flip_asr (src/utils/metrics.py:14-157).
+ * flr_batchnorm_infer: model.eval() BatchNorm — running statistics instead of
+ * batch statistics — with the optional residual add and ReLU of the training
+ * kernel; x, residual, y [KC][HW] (one contiguous plane per (client, channel)),
+ * gamma / beta / running_mean / running_var [KC].
+ * flr_classify_rows: logits [R][C] -> pred[r] = first index of the maximum
+ * (torch.max(outputs, 1); NaN counts as the maximum) and, with labels,
+ * loss_rows[r] = logsumexp(z_r) - z_r[label].  counts (int64[5], accumulated:
+ * the caller zeroes them) += {pred == label, pred == target, label == source,
+ * label == source && pred == label, label == source && pred == target}.
+ * labels may be NULL (then only counts[1] is updated). */
+int flr_batchnorm_infer(const float* x, const float* gamma, const float* beta,
+                        const float* running_mean, const float* running_var,
+                        const float* residual, float* y, int64_t KC, int64_t HW, float eps,
+                        int relu, void* stream);
+int flr_classify_rows(const float* logits, const int64_t* labels, int64_t R, int64_t C,
+                      int64_t target, int64_t source, int32_t* pred, float* loss_rows,
+                      int64_t* counts, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -284,9 +284,18 @@ def _gru_torch(gi: torch.Tensor, whh: torch.Tensor, bhh: torch.Tensor) -> torch.
 
 
 def _bn_act(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, residual: Optional[torch.Tensor] = None,
-            relu: bool = True) -> torch.Tensor:
+            relu: bool = True, stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """act(BN(x) [+ residual]) — the block's BN, shortcut add and ReLU, fused
-    into one HIP kernel each way on the native path."""
+    into one HIP kernel each way on the native path.  stats = (running_mean,
+    running_var) [K*C] selects eval mode (model.eval(): running statistics)."""
+    if stats is not None:
+        if _LAYERS == "native" and x.is_cuda:
+            from ..nn import client_batchnorm_infer
+            return client_batchnorm_infer(x, g, b, stats[0], stats[1], residual, relu)
+        y = F.batch_norm(x, stats[0], stats[1], g.reshape(-1), b.reshape(-1), training=False, eps=1e-5)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y
     if _LAYERS == "native" and x.is_cuda:
         from ..nn import client_batchnorm
         return client_batchnorm(x, g, b, residual, relu)
@@ -296,9 +305,26 @@ def _bn_act(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, residual: Optiona
     return F.relu(y) if relu else y
 
 
+def _eval_stats(bn_stats, name: str, gamma: torch.Tensor):
+    """(running_mean, running_var) [K*C] of BatchNorm `name` in eval mode, or
+    None in training mode.  bn_stats: None (training), or a dict name ->
+    (mean, var); a BN missing from the dict gets torch's initial buffers (0, 1),
+    which is what the reference's global model holds — the simulation copies
+    parameters() only and never updates the global buffers
+    (run_experiments.py:257-259)."""
+    if bn_stats is None:
+        return None
+    if name in bn_stats:
+        m, v = bn_stats[name]
+        return m.reshape(-1), v.reshape(-1)
+    n = gamma.numel()
+    return (torch.zeros(n, device=gamma.device, dtype=gamma.dtype),
+            torch.ones(n, device=gamma.device, dtype=gamma.dtype))
+
+
 def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: torch.Tensor, spec: ModelSpec,
                     dropout_mask: Optional[torch.Tensor] = None, tap_major: frozenset = frozenset(),
-                    skip_dead: frozenset = frozenset()) -> torch.Tensor:
+                    skip_dead: frozenset = frozenset(), bn_stats: Optional[Dict] = None) -> torch.Tensor:
     """images [K, B, C, H, W], tokens [K, B, T] -> logits [K, B, num_classes].
 
     dropout_mask: optional [K, B, fusion] tensor of {0, 1/(1-p)} (explicit masks
@@ -306,9 +332,14 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     tap_major: names of conv weights given as [K, KH, KW, Cin, Cout].
     skip_dead: tap-major weights whose dead-tap gradient slabs are left
     unwritten (the trainer's optimizer step never reads them).
+    bn_stats: None (training: batch statistics) or a dict for eval mode (see
+    _eval_stats).
     """
     if spec.family == "cub":
-        return _cub_forward(p, images, tokens, spec, dropout_mask, tap_major)
+        return _cub_forward(p, images, tokens, spec, dropout_mask, tap_major, bn_stats)
+
+    def st(bn):
+        return _eval_stats(bn_stats, bn, p[bn + ".weight"])
 
     def conv(name, x, stride, pad, need_dx=True):
         return _gconv(x, p[name], stride, pad, need_dx, name in tap_major, name not in skip_dead)
@@ -319,7 +350,7 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
         x = images.transpose(1, 2).reshape(K * spec.in_channels, B, *images.shape[3:])
     else:       # torch's grouped-conv layout [B, K*C, H, W]
         x = images.transpose(0, 1).reshape(B, K * spec.in_channels, *images.shape[3:])
-    x = _bn_act(conv("conv1.weight", x, 2, 3, need_dx=False), p["bn1.weight"], p["bn1.bias"])
+    x = _bn_act(conv("conv1.weight", x, 2, 3, need_dx=False), p["bn1.weight"], p["bn1.bias"], stats=st("bn1"))
     if native:
         from ..nn import client_maxpool2d
         x = client_maxpool2d(x, 3, 2, 1)
@@ -333,10 +364,11 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
             idt = x
             if (pre + "downsample.0.weight") in p:
                 idt = _bn_act(conv(pre + "downsample.0.weight", x, stride, 0), p[pre + "downsample.1.weight"],
-                              p[pre + "downsample.1.bias"], relu=False)
-            y = _bn_act(conv(pre + "conv1.weight", x, stride, 1), p[pre + "bn1.weight"], p[pre + "bn1.bias"])
+                              p[pre + "downsample.1.bias"], relu=False, stats=st(pre + "downsample.1"))
+            y = _bn_act(conv(pre + "conv1.weight", x, stride, 1), p[pre + "bn1.weight"], p[pre + "bn1.bias"],
+                        stats=st(pre + "bn1"))
             x = _bn_act(conv(pre + "conv2.weight", y, 1, 1), p[pre + "bn2.weight"], p[pre + "bn2.bias"],
-                        residual=idt)
+                        residual=idt, stats=st(pre + "bn2"))
     if native:
         img = x.mean(dim=(2, 3)).view(K, w[-1], B).transpose(1, 2)  # [K, B, 512]
     else:
@@ -379,7 +411,8 @@ def _linear_op(native: bool):
 
 
 def _cub_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, attrs: Optional[torch.Tensor], spec: ModelSpec,
-                 dropout_mask: Optional[torch.Tensor], tap_major: frozenset) -> torch.Tensor:
+                 dropout_mask: Optional[torch.Tensor], tap_major: frozenset,
+                 bn_stats: Optional[Dict] = None) -> torch.Tensor:
     """The C1 model (cub200_cnn.py:95-118) for K clients at once: three
     conv3x3(+bias) -> BN -> ReLU -> MaxPool2 blocks, AdaptiveAvgPool(4, 4),
     image_fc + ReLU, the attribute MLP, concat, the fusion head.
@@ -394,7 +427,8 @@ def _cub_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, attrs: Option
         y = _gconv(x, p[wn], 1, 1, need_dx=i > 0, tap_major=wn in tap_major)
         bias = p[f"image_conv.{idx}.bias"].reshape(-1)  # [K * Cout]
         y = y + (bias.view(-1, 1, 1, 1) if native else bias.view(1, -1, 1, 1))
-        y = _bn_act(y, p[f"image_conv.{idx + 1}.weight"], p[f"image_conv.{idx + 1}.bias"])
+        bn = f"image_conv.{idx + 1}"
+        y = _bn_act(y, p[bn + ".weight"], p[bn + ".bias"], stats=_eval_stats(bn_stats, bn, p[bn + ".weight"]))
         if native:
             from ..nn import client_maxpool2d
             x = client_maxpool2d(y, 2, 2, 0)

@@ -292,6 +292,21 @@ def client_batchnorm(x, gamma, beta, residual=None, relu: bool = True, eps: floa
     return ClientBatchNorm.apply(x, gamma, beta, residual, relu, eps)
 
 
+def client_batchnorm_infer(x, gamma, beta, running_mean, running_var, residual=None, relu: bool = True,
+                           eps: float = 1e-5):
+    """model.eval() BatchNorm (+ residual, ReLU) on flr_batchnorm_infer; forward
+    only.  x [K*C, ...] (one contiguous plane per row), stats / affine [K*C]."""
+    x = x.contiguous()
+    KC = x.shape[0]
+    res = None if residual is None else residual.contiguous()
+    y = torch.empty_like(x)
+    args = [t.contiguous().reshape(-1) for t in (gamma, beta, running_mean, running_var)]
+    assert all(a.numel() == KC for a in args), (x.shape, [a.numel() for a in args])
+    _capi.call("flr_batchnorm_infer", x.data_ptr(), *[a.data_ptr() for a in args], _ptr(res), y.data_ptr(), KC,
+               x[0].numel(), eps, int(relu), _stream(x))
+    return y
+
+
 class ClientMaxPool2d(torch.autograd.Function):
     """F.max_pool2d over every H x W plane of x[..., H, W] (flr_maxpool2d_fwd/_bwd)."""
 

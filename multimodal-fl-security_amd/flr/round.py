@@ -145,3 +145,21 @@ class RoundEngine:
         agg = self.defense.aggregate_flat(self.full, self.num_examples, **kw)
         self.global_flat.copy_(agg)
         return self.global_flat
+
+    # ---- per-round evaluation (run_experiments.py:261-266, 281-291) ------------
+    def evaluator(self):
+        """The GlobalEvaluator (flr.metrics) of this engine's model, created on
+        first use; evaluate the current global model with
+        ``eng.evaluator().load(eng.global_flat)`` then ``evaluate_model(...)`` /
+        ``attack_success_rate(...)``."""
+        if getattr(self, "_evaluator", None) is None:
+            from .metrics import GlobalEvaluator
+            self._evaluator = GlobalEvaluator(self.spec, self.device, batch_size=self.rcfg.batch)
+        return self._evaluator
+
+    def evaluate(self, images, text, labels):
+        """evaluate_model(global_model, test_loader) of the reference's round
+        loop (run_experiments.py:262) on the current global model."""
+        ev = self.evaluator()
+        ev.load(self.global_flat)
+        return ev.evaluate_model(images, text, labels)
