@@ -48,7 +48,9 @@ class Client:
         steps = config.get("local_steps")
         if steps is not None:
             batches = batches[: int(steps)]
-        masks = None if self.masks is None else [m.unsqueeze(0) for m in self.masks]
+        masks = None if self.masks is None else [m.unsqueeze(0) for m in self.masks] * epochs
+        if masks is not None:
+            masks = masks[: len(batches)]
         loss = self.trainer.local_update(batches, masks)
         if self.malicious:  # sign flip (model_poisoning.py:274-276)
             self.trainer.X.data[0, : self.trainer.P].neg_()
