@@ -146,6 +146,12 @@ inline int xcd_remap() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 
+// FLR_PRIO=1: raise the wave priority around each MFMA cluster (A/B only).
+inline int mfma_prio() {
+  const char* e = getenv("FLR_PRIO");
+  return (e && e[0] == '1') ? 1 : 0;
+}
+
 inline bool gemm_x6() {
   const char* e = getenv("FLR_GEMM");
   return !(e && e[0] == 'f');
@@ -725,7 +731,8 @@ __device__ __forceinline__ void xcd_tile(int& bx, int& by, int& bz) {
 }
 
 template <class Plan, int MS, int NS, bool X6>
-__global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S, float* __restrict__ part, int remap) {
+__global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S, float* __restrict__ part, int remap,
+                                                           int prio) {
   __shared__ __attribute__((aligned(16))) float As[2][MS][TILE];
   __shared__ __attribute__((aligned(16))) float Bs[2][NS][TILE];
   int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
@@ -791,6 +798,7 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
           frag8<Plan::LB>(Bs[cur][j], 32 * wn + l32, 16 * s + 8 * h, v);
           split3(v, bh[j], bm[j], bl[j]);
         }
+        if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < MS; ++i)
 #pragma unroll
@@ -804,6 +812,7 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c, 0, 0, 0);
             acc[i][j] = c;
           }
+        if (prio) __builtin_amdgcn_s_setprio(0);
       }
     } else {
       f32x4 fa[MS][4], fb[NS][4];  // all of the tile's fragments first: the reads overlap the MFMA chain
@@ -930,10 +939,10 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   const dim3 grid((unsigned)cdiv(N, BN * NS), (unsigned)cdiv(M, BM * MS), (unsigned)(K * S));
   if (gemm_x6())
     hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, true>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
-                       xcd_remap());
+                       xcd_remap(), mfma_prio());
   else
     hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, false>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
-                       xcd_remap());
+                       xcd_remap(), mfma_prio());
   int rc = launch_status(name);
   if (rc != FLR_OK || S == 1) return rc;
   const int64_t mn = (int64_t)M * N;
