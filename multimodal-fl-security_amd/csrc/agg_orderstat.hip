@@ -84,17 +84,12 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
       a0 = in ? n0 : a0;
       const bool blk = in && pos < nfull && ((pos + 1) & 15) == 0;
       const int i = pos + 1;
-      const bool l2 = blk && (i & 0xF0) == 0;
-      const bool l3 = l2 && (i & 0xF00) == 0;
       const float n1 = add_rn(a1, a0);
       a1 = blk ? n1 : a1;
       a0 = blk ? 0.f : a0;
-      const float n2 = add_rn(a2, a1);
-      a2 = l2 ? n2 : a2;
-      a1 = l2 ? 0.f : a1;
-      const float n3 = add_rn(a3, a2);
-      a3 = l3 ? n3 : a3;
-      a2 = l3 ? 0.f : a2;
+      // NP <= 128: a block end i = pos + 1 is at most 128, never a multiple of
+      // 256, so the level-2/3 folds (i & 0xF0 == 0, i & 0xF00 == 0) never fire.
+      static_assert(NP <= 128, "level-2 cascade folds not implemented");
     }
     a0 = add_rn(a0, a1);
     a0 = add_rn(a0, a2);
@@ -105,61 +100,48 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
 
 
 // ---- K > 128: one coordinate spread over L = 2 or 4 adjacent lanes ------------
-// Lane g of the group holds clients [128g, 128g+128) (padding +inf) and the
-// group runs a full bitonic sort over N = 128 L elements, element e = 128g + i
-// in register i of lane g: stages with j < 128 compare registers of one lane
-// (direction known at compile time while k <= 128, per lane above), stages with
-// j >= 128 exchange register i with lane g ^ (j/128).  Rank e then sits in lane
-// e/128, register e%128.  Trimmed sums are per-lane sequential in rank order,
-// combined in lane order (deterministic; 1e-5 vs torch, not bit-exact).
-template <int K2, int J>
-__device__ __forceinline__ void bitonic_reg_stage(float* v, bool asc_lane) {
-  // k = K2, j = J < 128: pairs (i, i ^ J) inside the lane
+// Lane g of the group holds clients [128g, 128g+128) (padding +inf).  Each lane
+// first sorts its 128 registers with the same odd-even merge network as the
+// single-lane kernel (all directions compile-time, 2 VALU ops per compare).
+// Sorted lanes are then merged pairwise by bitonic merges:
+//   flip step: lane g's register i meets register 127-i of the partner lane
+//              (DPP quad permutation), the lower lane keeps the min, the upper
+//              the max -- one v_med3_f32 against a lane-constant -inf / +inf;
+//   (L = 4) a cross-lane half-cleaner between lanes g and g^1, same register;
+//   then a 7-stage in-lane half-cleaner (j = 64..1, ascending everywhere).
+// Rank e then sits in lane e/128, register e%128.  About half the VALU work of a
+// full 512-wide bitonic sort.  Trimmed sums are per-lane sequential in rank
+// order, combined in lane order (deterministic; 1e-5 vs torch, not bit-exact).
+template <int CTRL>
+__device__ __forceinline__ float dpp_swap(float x) {
+  // all lanes valid (quad permutation, full masks): no "old" operand to initialise
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+
+// med3(a, b, -inf) = min(a, b); med3(a, b, +inf) = max(a, b)
+template <int CTRL>
+__device__ __forceinline__ void merge_flip(float* v, float bound) {
 #pragma unroll
-  for (int i = 0; i < 128; ++i) {
-    const int p = i ^ J;
-    if (p > i) {
-      const float a = v[i], b = v[p];
-      const float lo = fminf(a, b), hi = fmaxf(a, b);
-      bool asc;
-      if constexpr (K2 < 128) asc = (i & K2) == 0;  // (128g + i) & K2 == i & K2
-      else asc = asc_lane;                          // K2 >= 128: set by the lane index
-      v[i] = asc ? lo : hi;
-      v[p] = asc ? hi : lo;
-    }
+  for (int i = 0; i < 64; ++i) {
+    const float wa = dpp_swap<CTRL>(v[127 - i]);
+    const float wb = dpp_swap<CTRL>(v[i]);
+    v[i] = __builtin_amdgcn_fmed3f(v[i], wa, bound);
+    v[127 - i] = __builtin_amdgcn_fmed3f(v[127 - i], wb, bound);
   }
 }
 
-template <int K2, int J>
-__device__ __forceinline__ void bitonic_lane_stage(float* v, int g) {
-  constexpr int JL = J / 128;
-  const bool lower = (g & JL) == 0;
-  const bool asc = ((g * 128) & K2) == 0;
-  const bool keep_min = lower == asc;
-  // partner lane = lane ^ JL (JL = 1 or 2): a DPP quad permutation, so the
-  // exchange is one VALU op per register (no LDS round trip, short live range)
-  constexpr int CTRL = JL == 1 ? 0xB1 : 0x4E;
+template <int CTRL>
+__device__ __forceinline__ void merge_cross(float* v, float bound) {
 #pragma unroll
-  for (int i = 0; i < 128; ++i) {
-    const float w = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[i]), CTRL, 0xF, 0xF, false));
-    v[i] = keep_min ? fminf(v[i], w) : fmaxf(v[i], w);
-  }
+  for (int i = 0; i < 128; ++i) v[i] = __builtin_amdgcn_fmed3f(v[i], dpp_swap<CTRL>(v[i]), bound);
 }
 
-template <int K2, int J, int N>
-__device__ __forceinline__ void bitonic_stages_j(float* v, int g) {
-  if constexpr (J >= 1) {
-    if constexpr (J >= 128) bitonic_lane_stage<K2, J>(v, g);
-    else bitonic_reg_stage<K2, J>(v, ((g * 128) & K2) == 0);
-    bitonic_stages_j<K2, J / 2, N>(v, g);
-  }
-}
-
-template <int K2, int N>
-__device__ __forceinline__ void bitonic_sort_all(float* v, int g) {
-  if constexpr (K2 <= N) {
-    bitonic_stages_j<K2, K2 / 2, N>(v, g);
-    bitonic_sort_all<K2 * 2, N>(v, g);
+__device__ __forceinline__ void half_clean_lane(float* v) {
+#pragma unroll
+  for (int j = 64; j >= 1; j >>= 1) {
+#pragma unroll
+    for (int i = 0; i < 128; ++i)
+      if ((i & j) == 0) cas(v[i], v[i + j]);
   }
 }
 
@@ -170,15 +152,28 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
   const int64_t gidx = (int64_t)blockIdx.x * THREADS + threadIdx.x;
   const int64_t p = gidx / L;
   const int g = (int)(gidx % L);
-  const bool active = p < P;  // inactive lanes still join the shuffles
+  const bool active = p < P;  // inactive lanes still join the exchanges
   const int64_t pc = active ? p : 0;
   float v[128];
+  const float* __restrict__ base = X + (int64_t)(128 * g) * ldx + pc;
+  if (K >= 128 * L) {  // wave-uniform: every register holds a client (K = 256, 512)
 #pragma unroll
-  for (int i = 0; i < 128; ++i) {
-    const int k = 128 * g + i;
-    v[i] = k < K ? X[(int64_t)k * ldx + pc] : __builtin_huge_valf();
+    for (int i = 0; i < 128; ++i) v[i] = base[(int64_t)i * ldx];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 128; ++i) v[i] = 128 * g + i < K ? base[(int64_t)i * ldx] : __builtin_huge_valf();
   }
-  bitonic_sort_all<2, 128 * L>(v, g);
+  oem_sort<0, 128>(v);
+  const float inf = __builtin_huge_valf();
+  // pairs (0,1), (2,3): quad permutation [1,0,3,2]
+  merge_flip<0xB1>(v, (g & 1) ? inf : -inf);
+  half_clean_lane(v);
+  if constexpr (L == 4) {
+    // (0,1) against (2,3): flip partners g^3 = quad permutation [3,2,1,0]
+    merge_flip<0x1B>(v, g < 2 ? -inf : inf);
+    merge_cross<0xB1>(v, (g & 1) ? inf : -inf);
+    half_clean_lane(v);
+  }
   __builtin_amdgcn_sched_barrier(0);
   float r = 0.f;
   if constexpr (MODE == 1) {
