@@ -169,7 +169,8 @@ __host__ __device__ inline int64_t slice_chunk(int64_t nch, int q) { return nch 
 template <int NL, bool CROSS, int TERMS, int ABLATE = 0>
 __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
     const float* __restrict__ X, int K, int64_t ldx, int64_t nch_total, int q_base, int64_t chunk0,
-    int group_base, int ngroups, const int* __restrict__ pivot_ptr, float* __restrict__ partials, int nseg) {
+    int group_base, int ngroups, const int* __restrict__ pivot_ptr, float* __restrict__ partials, int nseg,
+    int seg_stride) {
   using TS = TileSet<NL, CROSS>;
   constexpr int NT = TS::N;
   constexpr int ROWS = 32 * NL;
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
   }
 
   // ---- epilogue: reduce the 4 waves in fixed order, write the record ----
-  float* rec = partials + (((int64_t)blockIdx.z * ngroups + g) * nseg + seg) * REC;
+  float* rec = partials + (((int64_t)blockIdx.z * ngroups + g) * seg_stride + seg) * REC;
   float* red = lds;
   static_for<0, NT>([&](auto tc) {
     constexpr int t = decltype(tc)::value;
@@ -348,15 +349,18 @@ __global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
 // split with 4 waves x 4 independent accumulators; stage 2 adds the splits.
 constexpr int RSPLIT = 8;
 __global__ __launch_bounds__(256) void reduce_records_kernel(const float* __restrict__ partials,
-                                                              int nseg, double* __restrict__ stage1) {
+                                                              int seg_stride, int ngroups, int ngroups_diag,
+                                                              int nseg_diag, int nseg_cross,
+                                                              double* __restrict__ stage1) {
   __shared__ double red[4][64];
   const int g = blockIdx.y, z = blockIdx.z;
+  const int nseg = (g % ngroups) < ngroups_diag ? nseg_diag : nseg_cross;
   const int e = blockIdx.x * 64 + (threadIdx.x & 63);
   const int w = threadIdx.x >> 6;
   const int s0 = (int)((int64_t)nseg * z / RSPLIT), s1 = (int)((int64_t)nseg * (z + 1) / RSPLIT);
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   if (e < REC) {
-    const float* p = partials + (int64_t)g * nseg * REC + e;
+    const float* p = partials + (int64_t)g * seg_stride * REC + e;
     int k = s0 + w;
     for (; k + 12 < s1; k += 16) {
       a0 += (double)p[(int64_t)k * REC];
@@ -509,7 +513,9 @@ __global__ __launch_bounds__(256) void pivot_kernel(const double* __restrict__ D
 
 struct Plan {
   int64_t nchunks;   // full 64-coordinate chunks of the whole vector
-  int nseg;          // segments per (slice, group)
+  int nseg;          // record stride per (slice, group) = max(nseg_diag, nseg_cross)
+  int nseg_diag;     // segments per (slice, DIAG group)
+  int nseg_cross;    // segments per (slice, CROSS group)
   int ngroups_diag;  // groups launched with the DIAG kernel
   int ngroups_cross; // groups launched with the CROSS kernel
   int nl_diag;       // loaded blocks per DIAG group
@@ -532,8 +538,29 @@ inline Plan make_plan(int64_t K, int64_t P) {
     p.nl_diag = 4;
   }
   const int64_t min_slice = p.nchunks / FLR_PW_SLICES;
-  const int target = std::max(1, TARGET_BLOCKS / (FLR_PW_SLICES * p.ngroups()));
-  p.nseg = (int)std::max<int64_t>(1, std::min<int64_t>(min_slice, std::min(MAX_SEG, target)));
+  const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(min_slice, MAX_SEG));
+  if (K <= SUPER) {
+    const int target = std::max(1, TARGET_BLOCKS / (FLR_PW_SLICES * p.ngroups()));
+    p.nseg = p.nseg_diag = (int)std::min<int64_t>(cap, target);
+    p.nseg_cross = 0;
+    return p;
+  }
+  // K > 128: the DIAG and CROSS groups are separate launches, so each gets its
+  // own segment count, chosen to minimise the number of residency rounds per
+  // unit of work: ceil(units * n / slots) / n (units = groups x slices; slots =
+  // 2 workgroups per CU for the 64 KB DIAG stage, 1 for the 96 KB CROSS stage).
+  auto pick = [&](int units, int slots) {
+    int best = 1;
+    for (int n = 2; n <= std::min<int64_t>(cap, 64); ++n) {
+      // rounds(n) / n < rounds(best) / best
+      const int64_t rn = ((int64_t)units * n + slots - 1) / slots, rb = ((int64_t)units * best + slots - 1) / slots;
+      if (rn * best < rb * n) best = n;
+    }
+    return best;
+  };
+  p.nseg_diag = pick(p.ngroups_diag * FLR_PW_SLICES, 2 * 256);
+  p.nseg_cross = pick(p.ngroups_cross * FLR_PW_SLICES, 256);
+  p.nseg = std::max(p.nseg_diag, p.nseg_cross);
   return p;
 }
 
@@ -599,10 +626,11 @@ struct GramArgs {
 template <int NL, bool CROSS>
 int launch_gram(const GramArgs& a, const Plan& p, int group_base, int ngroups, hipStream_t st) {
   const size_t lds = (size_t)2 * 32 * NL * CW * sizeof(float);
-  dim3 grid(p.nseg, ngroups, a.nsl);
+  const int nseg = CROSS ? p.nseg_cross : p.nseg_diag;
+  dim3 grid(nseg, ngroups, a.nsl);
 #define FLR_GRAM_LAUNCH(T, AB)                                                                              \
   hipLaunchKernelGGL((gram_partials_kernel<NL, CROSS, T, AB>), grid, dim3(THREADS), lds, st, a.X, a.K, a.ldx, \
-                     p.nchunks, a.q0, a.chunk0, group_base, p.ngroups(), a.pivot, a.partials, p.nseg)
+                     p.nchunks, a.q0, a.chunk0, group_base, p.ngroups(), a.pivot, a.partials, nseg, p.nseg)
   if (gram_terms(a.P) == 3) {
     FLR_GRAM_LAUNCH(3, 0);
     return launch_status("gram_partials_kernel");
@@ -744,7 +772,7 @@ int gram_phase(const GramArgs& a, double* stage1, double* gsum, hipStream_t st, 
   if (ev_end && hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), st) != hipSuccess) return FLR_ERR_HIP;
   const int nrec = a.nsl * p.ngroups();  // (slice, group) pairs, slice-major
   hipLaunchKernelGGL(reduce_records_kernel, dim3(cdiv(REC, 64), nrec, RSPLIT), dim3(256), 0, st, a.partials,
-                     p.nseg, stage1);
+                     p.nseg, p.ngroups(), p.ngroups_diag, p.nseg_diag, p.nseg_cross, stage1);
   if ((rc = launch_status("reduce_records_kernel")) != FLR_OK) return rc;
   hipLaunchKernelGGL(reduce_splits_kernel, dim3(cdiv(nrec * REC, 256)), dim3(256), 0, st, stage1, nrec, gsum);
   return launch_status("reduce_splits_kernel");
