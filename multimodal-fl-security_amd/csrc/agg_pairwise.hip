@@ -167,7 +167,9 @@ __device__ __forceinline__ GroupDesc group_desc(int g, int K, bool cross) {
 __host__ __device__ inline int64_t slice_chunk(int64_t nch, int q) { return nch * q / FLR_PW_SLICES; }
 
 template <int NL, bool CROSS, int TERMS, int ABLATE = 0>
-__global__ __launch_bounds__(THREADS, 2) void gram_partials_kernel(
+// CROSS (96 KB of LDS) is limited to one workgroup per CU: give it the whole
+// register file (with the 2-per-CU bound it spilled to scratch).
+__global__ __launch_bounds__(THREADS, CROSS ? 1 : 2) void gram_partials_kernel(
     const float* __restrict__ X, int K, int64_t ldx, int64_t nch_total, int q_base, int64_t chunk0,
     int group_base, int ngroups, const int* __restrict__ pivot_ptr, float* __restrict__ partials, int nseg,
     int seg_stride) {
