@@ -55,13 +55,22 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// K > 128 cross groups: 2 blocks of super-block I against CROSS_NJ blocks of J.
+// CROSS_NJ = 4 (NL = 6, 96 KB of LDS, one workgroup per CU): 56 ms at K = 512,
+// P = 3.3e7.  CROSS_NJ = 2 (NL = 4, 64 KB, two per CU, so one wave's bf16 split
+// can overlap the other's MFMAs) measured 67 ms: the extra split work (one block
+// per tile instead of 0.75) costs more than the overlap gains.
+constexpr int CROSS_NJ = 4;
+constexpr int CROSS_NL = 2 + CROSS_NJ;
+constexpr int CROSS_PER_PAIR = 2 * (4 / CROSS_NJ);  // cross groups per super-block pair
+
 // Tile enumeration.  DIAG: every (a <= b) over NL loaded blocks, a-major.
-// CROSS (NL = 6): a in {0,1} (rows of super-block I), b in {2..5} (rows of J).
+// CROSS: a in {0,1} (rows of super-block I), b in {2..NL-1} (rows of J).
 template <int NL, bool CROSS>
 struct TileSet {
-  static constexpr int N = CROSS ? 8 : NL * (NL + 1) / 2;
+  static constexpr int N = CROSS ? 2 * (NL - 2) : NL * (NL + 1) / 2;
   __host__ __device__ static constexpr int a(int t) {
-    if (CROSS) return t / 4;
+    if (CROSS) return t / (NL - 2);
     int r = t;
     for (int i = 0; i < NL; ++i) {
       if (r < NL - i) return i;
@@ -70,7 +79,7 @@ struct TileSet {
     return -1;
   }
   __host__ __device__ static constexpr int b(int t) {
-    if (CROSS) return 2 + t % 4;
+    if (CROSS) return 2 + t % (NL - 2);
     int r = t;
     for (int i = 0; i < NL; ++i) {
       if (r < NL - i) return i + r;
@@ -148,13 +157,14 @@ __device__ __forceinline__ GroupDesc group_desc(int g, int K, bool cross) {
     for (int i = 0; i < 6; ++i) d.blk[i] = 4 * g + i;
     return d;
   }
-  const int q = (g - nsb) >> 1, h = (g - nsb) & 1;
+  const int q = (g - nsb) / CROSS_PER_PAIR, w = (g - nsb) % CROSS_PER_PAIR;
+  const int hi = w / (4 / CROSS_NJ), hj = w % (4 / CROSS_NJ);
   int I = 0, rem = q;
   while (rem >= nsb - 1 - I) { rem -= nsb - 1 - I; ++I; }
   const int J = I + 1 + rem;
-  d.blk[0] = 4 * I + 2 * h;
-  d.blk[1] = 4 * I + 2 * h + 1;
-  for (int i = 0; i < 4; ++i) d.blk[2 + i] = 4 * J + i;
+  d.blk[0] = 4 * I + 2 * hi;
+  d.blk[1] = 4 * I + 2 * hi + 1;
+  for (int i = 0; i < CROSS_NJ; ++i) d.blk[2 + i] = 4 * J + CROSS_NJ * hj + i;
   return d;
 }
 
@@ -167,9 +177,9 @@ __device__ __forceinline__ GroupDesc group_desc(int g, int K, bool cross) {
 __host__ __device__ inline int64_t slice_chunk(int64_t nch, int q) { return nch * q / FLR_PW_SLICES; }
 
 template <int NL, bool CROSS, int TERMS, int ABLATE = 0>
-// CROSS (96 KB of LDS) is limited to one workgroup per CU: give it the whole
+// NL = 6 (96 KB of LDS) is limited to one workgroup per CU: give it the whole
 // register file (with the 2-per-CU bound it spilled to scratch).
-__global__ __launch_bounds__(THREADS, CROSS ? 1 : 2) void gram_partials_kernel(
+__global__ __launch_bounds__(THREADS, NL >= 6 ? 1 : 2) void gram_partials_kernel(
     const float* __restrict__ X, int K, int64_t ldx, int64_t nch_total, int q_base, int64_t chunk0,
     int group_base, int ngroups, const int* __restrict__ pivot_ptr, float* __restrict__ partials, int nseg,
     int seg_stride) {
@@ -447,10 +457,10 @@ __global__ void assemble_kernel(const double* __restrict__ gsum, int ngroups, co
       int q = 0;
       for (int a = 0; a < I; ++a) q += nsb - 1 - a;
       q += J - I - 1;
-      g = nsb + 2 * q + (bi >> 1);
+      g = nsb + CROSS_PER_PAIR * q + (bi >> 1) * (4 / CROSS_NJ) + bj / CROSS_NJ;
       lb_i = bi & 1;
-      lb_j = 2 + bj;
-      t = lb_i * 4 + bj;
+      lb_j = 2 + bj % CROSS_NJ;
+      t = lb_i * CROSS_NJ + bj % CROSS_NJ;
     }
   }
   double gij = 0.0, gii = 0.0, gjj = 0.0;
@@ -536,7 +546,7 @@ inline Plan make_plan(int64_t K, int64_t P) {
   } else {
     const int nsb = cdiv((int)K, SUPER);
     p.ngroups_diag = nsb;
-    p.ngroups_cross = nsb * (nsb - 1);  // two half-groups per super-block pair
+    p.ngroups_cross = nsb * (nsb - 1) / 2 * CROSS_PER_PAIR;
     p.nl_diag = 4;
   }
   const int64_t min_slice = p.nchunks / FLR_PW_SLICES;
@@ -550,7 +560,7 @@ inline Plan make_plan(int64_t K, int64_t P) {
   // K > 128: the DIAG and CROSS groups are separate launches, so each gets its
   // own segment count, chosen to minimise the number of residency rounds per
   // unit of work: ceil(units * n / slots) / n (units = groups x slices; slots =
-  // 2 workgroups per CU for the 64 KB DIAG stage, 1 for the 96 KB CROSS stage).
+  // 2 workgroups per CU for the 64 KB stages, 1 for the 96 KB NL = 6 cross stage).
   auto pick = [&](int units, int slots) {
     int best = 1;
     for (int n = 2; n <= std::min<int64_t>(cap, 64); ++n) {
@@ -561,7 +571,7 @@ inline Plan make_plan(int64_t K, int64_t P) {
     return best;
   };
   p.nseg_diag = pick(p.ngroups_diag * FLR_PW_SLICES, 2 * 256);
-  p.nseg_cross = pick(p.ngroups_cross * FLR_PW_SLICES, 256);
+  p.nseg_cross = pick(p.ngroups_cross * FLR_PW_SLICES, CROSS_NL >= 6 ? 256 : 512);
   p.nseg = std::max(p.nseg_diag, p.nseg_cross);
   return p;
 }
@@ -768,7 +778,7 @@ int gram_phase(const GramArgs& a, double* stage1, double* gsum, hipStream_t st, 
     }
   } else {
     rc = launch_gram<4, false>(a, p, 0, p.ngroups_diag, st);
-    if (rc == FLR_OK) rc = launch_gram<6, true>(a, p, p.ngroups_diag, p.ngroups_cross, st);
+    if (rc == FLR_OK) rc = launch_gram<CROSS_NL, true>(a, p, p.ngroups_diag, p.ngroups_cross, st);
   }
   if (rc != FLR_OK) return rc;
   if (ev_end && hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), st) != hipSuccess) return FLR_ERR_HIP;
