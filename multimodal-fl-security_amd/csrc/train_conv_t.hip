@@ -897,18 +897,34 @@ __global__ void zero_taps_kernel(float* __restrict__ dw, int KK, int64_t slab, u
 // a client's reduction order — and so its trained weights — must not depend
 // on how many clients share its GPU (bit-identical results at 1/2/4/8 GPUs).
 // 16 tiles per client = the 2048-workgroup target at the nominal 128 clients.
-inline int choose_splits(int M, int N, int R, int /*K*/, int sub = 1) {
+// min_kt: fewest K-tiles a split may keep (8 for the convolutions; the batched
+// GEMMs read FLR_BGEMM_MINKT, default 8, for A/B runs of the GRU recurrence).
+inline int choose_splits(int M, int N, int R, int /*K*/, int sub = 1, int min_kt = 8) {
   const int tiles = cdiv(M, BM) * cdiv(N, BN) / sub;
   const int ktiles = cdiv(R, BK);
   int S = 1;
-  while (S < 16 && tiles * S < 16 && ktiles / (2 * S) >= 8) S *= 2;
+  while (S < 16 && tiles * S < 16 && ktiles / (2 * S) >= min_kt) S *= 2;
   return S;
+}
+
+inline int bgemm_min_kt() {
+  static const int v = [] {
+    const char* e = getenv("FLR_BGEMM_MINKT");
+    const int x = e ? atoi(e) : 0;
+    return x >= 1 && x <= 64 ? x : 8;
+  }();
+  return v;
+}
+
+template <class Plan>
+inline int plan_min_kt() {
+  return std::is_base_of<BGemmArgs, Plan>::value ? bgemm_min_kt() : 8;
 }
 
 template <class Plan>
 size_t splits_bytes(const Plan& pl) {  // enough for any sub-tile shape
-  const int S = std::max(choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 1),
-                         choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 2));
+  const int S = std::max(choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 1, plan_min_kt<Plan>()),
+                         choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 2, plan_min_kt<Plan>()));
   return S > 1 ? (size_t)S * pl.g.Kc * pl.M() * pl.N() * sizeof(float) : 0;
 }
 
@@ -934,7 +950,7 @@ inline int tile_choice(int M, int N, int R) {
 template <class Plan, int MS, int NS>
 int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   const int M = pl.M(), N = pl.N(), R = pl.R(), K = pl.g.Kc;
-  int S = choose_splits(M, N, R, K, MS * NS);
+  int S = choose_splits(M, N, R, K, MS * NS, plan_min_kt<Plan>());
   if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) S = 1;
   const dim3 grid((unsigned)cdiv(N, BN * NS), (unsigned)cdiv(M, BM * MS), (unsigned)(K * S));
   if (gemm_x6())
@@ -1151,7 +1167,7 @@ int bgemm_b(int bm, const convt::BGemmArgs& args, void* ws, size_t wsb, hipStrea
 
 extern "C" size_t flr_bgemm_workspace(int64_t batch, int64_t M, int64_t N, int64_t R) {
   if (batch < 1 || M < 1 || N < 1 || R < 0 || M > INT32_MAX || N > INT32_MAX || R > INT32_MAX) return 0;
-  const int S = convt::choose_splits((int)M, (int)N, (int)R, (int)batch);
+  const int S = convt::choose_splits((int)M, (int)N, (int)R, (int)batch, 1, convt::bgemm_min_kt());
   return S > 1 ? (size_t)S * batch * M * N * sizeof(float) : 0;
 }
 
