@@ -47,6 +47,39 @@ def gram_traffic(K: int, P: int):
     return (2.0 * t["fetch_kib"] + t["write_kib"]) * 1024.0
 
 
+def cpu_model() -> str:
+    """`lscpu` model name (from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def round_roofline(K: int, P: int, P_live: int, steps: int, ms_per_round: float, world: int):
+    """SURVEY §8(d) round bytes: each client-step of the fused ideal moves 36 B
+    per parameter (forward W read 4, backward W read 4 + grad write 4, norm read
+    4, SGD read p, g, buf + write p, buf 20), plus 8 B per parameter per client
+    per round for the global copy in and the update out:
+        bytes = K (steps 36 P + 8 P).
+    The engine trains only the live parameters (taps that read real pixels at
+    32x32; dead taps have exactly zero gradient), so the achievable bound uses
+    P_live for the per-step term.  Aggregated over all GPUs of the job."""
+    full = K * (steps * 36.0 * P + 8.0 * P)
+    live = K * (steps * 36.0 * P_live + 8.0 * P)
+    sec = ms_per_round * 1e-3
+    peak = HBM_PEAK_GBS * world
+    return {
+        "bound": "hbm", "unit": "GB/s", "peak": peak,
+        "bytes_per_round": full, "achieved": full / sec / 1e9, "frac": full / sec / 1e9 / peak,
+        "bytes_per_round_live": live, "achieved_live": live / sec / 1e9, "frac_live": live / sec / 1e9 / peak,
+        "P": P, "P_live": P_live, "formula": "K*(steps*36*P + 8*P) (SURVEY 8d)",
+    }
+
+
 def cpu_baseline(spec, P, K, f, multi_k, steps, batch, budget_s: float = 20.0):
     """Time the oracle (the reference's CPU path restated) on a bounded sample
     and extrapolate one round: K clients x local update + K(K-1)/2 pair norms +
@@ -56,7 +89,11 @@ def cpu_baseline(spec, P, K, f, multi_k, steps, batch, budget_s: float = 20.0):
     from oracle import training as otrain
     from flr.models.multimodal import MultimodalNet
 
-    threads = torch.get_num_threads()
+    # the box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool; os.cpu_count()
+    # reports the whole host there, whose other cores belong to other jobs)
+    host_cpus = os.cpu_count() or 1
+    threads = min(host_cpus, int(os.environ.get("OMP_NUM_THREADS", host_cpus)))
+    torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(1000)
     batches = [(torch.randn(batch, spec.in_channels, spec.image_size, spec.image_size, generator=g),
                 torch.randint(0, spec.vocab, (batch, spec.seq_len), generator=g),
@@ -91,6 +128,7 @@ def cpu_baseline(spec, P, K, f, multi_k, steps, batch, budget_s: float = 20.0):
     round_s = K * t_client + K * (K - 1) / 2 * t_pair + t_mean
     return {
         "value": 1.0 / round_s, "unit": "rounds/s", "cores": threads, "kind": "port",
+        "cpu_model": cpu_model(), "host_cpus": host_cpus,
         "sample": (f"oracle (reference loop restated, torch CPU fp32, {threads} threads): {n_clients} client "
                    f"local update(s) x {steps} steps timed ({t_client:.3f} s/client), {n_pairs} Krum pair "
                    f"norms at P={P} ({t_pair * 1e3:.1f} ms/pair), 4-row mean ({t_mean / multi_k * 1e3:.1f} "
@@ -203,7 +241,7 @@ def main() -> None:
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32 (bf16x6-split MFMA conv/GEMM = fp32 operands; Krum Gram bf16x4 hi/lo split, fp32 accumulate)",
         "data": "synthetic (SURVEY §8d: N(0,1) 3x32x32 images, U{0..999} 16-token texts, 10 classes; "
                 "random-init weights, seed 42)",
         "config": {
@@ -221,6 +259,8 @@ def main() -> None:
         "aggregate_ms": aggregate_ms,
         "train_ms_per_round": train_ms,
         "attackers_selected": attackers_selected,
+        "round_roofline": round_roofline(K, P, sum(c for _, _, c, _ in eng.trainer.blocks), args.local_steps,
+                                         elapsed / args.steps * 1e3, world),
         "roofline": {
             "kernel": "gram_partials_kernel (Krum pairwise, centred Gram on MFMA)",
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -14,6 +14,14 @@
 // trimmed sum restates torch's CPU outer-reduction order (cascade_sum:
 // 16-row blocks folded through 4 levels, then divided by R), which makes it
 // bit-identical to torch on the vectorised columns.
+//
+// NaN: torch.sort orders NaN after +inf and torch.median(dim=0) returns NaN
+// for a column holding any NaN.  The min/max compare-exchanges below would
+// instead drop a NaN (fminf/fmaxf return the other operand), so a wave that
+// loaded any NaN (one ballot; never in practice) maps each NaN to +inf and
+// counts them: the top n_nan ranks of torch's order are then exactly the
+// NaN, the median is NaN when n_nan > 0, and the trimmed mean is NaN when
+// n_nan > t (a NaN survives the trim).
 #include "flr_common.h"
 
 #include <type_traits>
@@ -52,6 +60,25 @@ __device__ __forceinline__ void oem_sort(float* v) {
   }
 }
 
+// Maps NaN to +inf in place and returns this lane's NaN count; the scan runs
+// only in a wave that loaded a NaN (wave-uniform branch).
+template <int N>
+__device__ __forceinline__ int nan_to_inf(float* v) {
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < N; ++k) any |= __builtin_isnan(v[k]);
+  int n = 0;
+  if (__any(any)) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const bool isn = __builtin_isnan(v[k]);
+      n += isn ? 1 : 0;
+      v[k] = isn ? __builtin_huge_valf() : v[k];
+    }
+  }
+  return n;
+}
+
 // MODE 0: trimmed mean over ranks [t, K-t); MODE 1: lower median.
 template <int NP, int MODE>
 // 3 waves/SIMD: the NP=128 network needs ~150 VGPRs; the bound stops the
@@ -63,6 +90,7 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
   float v[NP];
 #pragma unroll
   for (int k = 0; k < NP; ++k) v[k] = k < K ? X[(int64_t)k * ldx + p] : __builtin_huge_valf();
+  const int nnan = nan_to_inf<NP>(v);
   oem_sort<0, NP>(v);
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (MODE == 1) {
@@ -70,7 +98,7 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
     float r = v[0];
 #pragma unroll
     for (int k = 1; k < NP; ++k) r = (k == med) ? v[k] : r;
-    out[p] = r;
+    out[p] = nnan > 0 ? __builtin_nanf("") : r;
   } else {
     const int R = K - 2 * t;
     const int nfull = R & ~15;
@@ -83,7 +111,6 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
       const float n0 = add_rn(a0, v[k]);
       a0 = in ? n0 : a0;
       const bool blk = in && pos < nfull && ((pos + 1) & 15) == 0;
-      const int i = pos + 1;
       const float n1 = add_rn(a1, a0);
       a1 = blk ? n1 : a1;
       a0 = blk ? 0.f : a0;
@@ -94,7 +121,7 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
     a0 = add_rn(a0, a1);
     a0 = add_rn(a0, a2);
     a0 = add_rn(a0, a3);
-    out[p] = div_rn(a0, (float)R);
+    out[p] = nnan > t ? __builtin_nanf("") : div_rn(a0, (float)R);
   }
 }
 
@@ -163,6 +190,11 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
 #pragma unroll
     for (int i = 0; i < 128; ++i) v[i] = 128 * g + i < K ? base[(int64_t)i * ldx] : __builtin_huge_valf();
   }
+  int nnan = nan_to_inf<128>(v);
+  if (__any(nnan > 0)) {  // the coordinate's total over its L lanes (adjacent lanes)
+    nnan += __shfl_xor(nnan, 1, 64);
+    if constexpr (L == 4) nnan += __shfl_xor(nnan, 2, 64);
+  }
   oem_sort<0, 128>(v);
   const float inf = __builtin_huge_valf();
   // pairs (0,1), (2,3): quad permutation [1,0,3,2]
@@ -181,7 +213,7 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
     const int loc = med - 128 * g;
 #pragma unroll
     for (int i = 0; i < 128; ++i) r = (i == loc) ? v[i] : r;
-    if (active && g == med / 128) out[p] = r;  // the lane that owns rank med
+    if (active && g == med / 128) out[p] = nnan > 0 ? __builtin_nanf("") : r;  // the lane that owns rank med
   } else {
     const int lo = t, hi = K - t;
     float acc = 0.f;
@@ -200,7 +232,7 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
         tot = add_rn(tot, t2);
       }
     }
-    if (active && g == 0) out[p] = div_rn(tot, (float)(K - 2 * t));
+    if (active && g == 0) out[p] = nnan > t ? __builtin_nanf("") : div_rn(tot, (float)(K - 2 * t));
   }
 }
 

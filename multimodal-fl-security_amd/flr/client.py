@@ -8,6 +8,10 @@ client-batched trainer with K = 1 (the round engine trains all of a GPU's
 clients in one batch instead).  Differences from the reference, by design:
 parameters() only (the simulation path, run_experiments.py:238), fixed
 batches instead of a shuffling DataLoader, explicit dropout masks.
+
+No gradient clipping by default (clip = 0.0), as FLClient._train
+(fl_client.py:130-141: zero_grad, forward, loss, backward, step); pass
+clip = 1.0 for the simulation loop's clip_grad_norm_ (run_experiments.py:234).
 """
 from __future__ import annotations
 
@@ -22,7 +26,7 @@ from .train import ClientBatchTrainer, TrainConfig
 
 class Client:
     def __init__(self, client_id: int, batches: Sequence, spec: ModelSpec = ModelSpec(), device="cuda",
-                 local_epochs: int = 1, learning_rate: float = 0.01, clip: float = 1.0, momentum: float = 0.9,
+                 local_epochs: int = 1, learning_rate: float = 0.01, clip: float = 0.0, momentum: float = 0.9,
                  weight_decay: float = 0.0, dropout_masks: Optional[Sequence] = None, malicious: bool = False):
         self.client_id = client_id
         self.batches = list(batches)  # [(images [B,...], tokens [B,T], labels [B])]

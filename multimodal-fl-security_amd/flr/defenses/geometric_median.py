@@ -39,10 +39,19 @@ def _weights(dist64: np.ndarray):
     return w, W
 
 
+# dist2_i = (D2 a)_i - a^T D2 a / 2 cancels when the iterate nears client i
+# (duplicate or colluding clients): its relative error is the distances'
+# relative error (Gram kernel: up to ~1e-5) times (D2 a)_i / dist2_i.  Past
+# this cancellation factor the identity is not trusted and the caller runs the
+# reference's direct passes instead.
+CANCEL_LIMIT = 8.0
+
+
 def weiszfeld_pairwise(D: np.ndarray, d0: np.ndarray, max_iters: int, tolerance: float):
     """Weiszfeld in coefficient space.  D: K x K pairwise distances, d0: the
     rows' distances to the coordinate median.  Returns (w fp32 [K], W fp32,
-    num_iters) such that the estimate is (sum_j w_j U_j) / W."""
+    num_iters) such that the estimate is (sum_j w_j U_j) / W, or None when a
+    distance cancels past CANCEL_LIMIT (use the direct method)."""
     D2 = D.astype(np.float64) ** 2
     tol = np.float32(tolerance)
     w, W = _weights(d0)
@@ -53,6 +62,8 @@ def weiszfeld_pairwise(D: np.ndarray, d0: np.ndarray, max_iters: int, tolerance:
     for it in range(1, max_iters):
         D2a = D2 @ a
         dist2 = D2a - 0.5 * float(a @ D2a)
+        if np.any(dist2 * CANCEL_LIMIT < D2a):
+            return None
         w, W = _weights(np.sqrt(np.maximum(dist2, 0.0)))
         a_new = w.astype(np.float64) / float(W)
         b = a_new - a
@@ -74,6 +85,7 @@ class GeometricMedianDefense(BaseDefense):
 
     def aggregate_flat(self, cm: ClientMatrix, num_examples: List[int]) -> torch.Tensor:
         X = cm.X
+        self.used_direct = self.method == "direct"
         med = ops.median_lower(X)
         if self.max_iters <= 0:
             self.num_iters = 0
@@ -87,7 +99,11 @@ class GeometricMedianDefense(BaseDefense):
     def _pairwise(self, X: torch.Tensor, med: torch.Tensor) -> torch.Tensor:
         D = ops.pairwise_l2(X).cpu().numpy()
         d0 = ops.row_norms(X, center=med).cpu().numpy()
-        w, W, self.num_iters = weiszfeld_pairwise(D, d0, self.max_iters, self.tolerance)
+        res = weiszfeld_pairwise(D, d0, self.max_iters, self.tolerance)
+        if res is None:  # an iterate close to a client: the identity cancels
+            self.used_direct = True
+            return self._direct(X, med)
+        w, W, self.num_iters = res
         return ops.weighted_rows(X, w, float(W))
 
     def _direct(self, X: torch.Tensor, med: torch.Tensor) -> torch.Tensor:

@@ -49,6 +49,13 @@ def allgather_rows(local: torch.Tensor, full: torch.Tensor, group: Optional[dist
         if full.data_ptr() != local.data_ptr():
             full.copy_(local)
         return
+    if dist.get_backend(group) == "gloo" and full.is_cuda:
+        # gloo has no device collectives: stage through host memory (the
+        # world_size > 1 rehearsal on one GPU); RCCL takes the device tensors
+        hf = full.cpu()
+        dist.all_gather_into_tensor(hf, local.contiguous().cpu(), group=group)
+        full.copy_(hf)
+        return
     dist.all_gather_into_tensor(full, local.contiguous(), group=group)
 
 

@@ -18,6 +18,8 @@ Both give the bit-identical global model at every GPU count.
 """
 from __future__ import annotations
 
+import inspect
+import logging
 import os
 from dataclasses import dataclass, field
 from typing import Dict, Optional
@@ -25,6 +27,7 @@ from typing import Dict, Optional
 import torch
 
 from . import dist as fdist
+from . import ops
 from .attacks import Backdoor, poison_batches_
 from .defenses import get_defense
 from .matrix import ClientMatrix
@@ -44,6 +47,7 @@ class RoundConfig:
     seed: int = 42                       # run_experiments.py:43
     exchange: str = "auto"               # "alltoall" | "allgather" | "auto" (alltoall when the defense shards)
     graph: bool = True                   # replay the training phase as one captured HIP graph (FLR_GRAPH=0: eager)
+    fallback_fedavg: bool = False        # defense raises -> FedAvg of the round (robust_server.py:120-122)
 
 
 def initial_global(spec: ModelSpec, seed: int, device) -> torch.Tensor:
@@ -96,6 +100,9 @@ class RoundEngine:
         self.use_graph = (rcfg.graph and self.device.type == "cuda" and os.environ.get("FLR_GRAPH", "1") != "0")
         self._graph = None
         self._graph_losses: Optional[torch.Tensor] = None
+        self._wants_global = "global_flat" in inspect.signature(self.defense.aggregate_flat).parameters
+        self.round_index = 0
+        self.fell_back = False
 
     def _poison(self) -> None:
         f = self.rcfg.num_attackers if self.rcfg.attack == "sign_flip" else 0
@@ -136,15 +143,67 @@ class RoundEngine:
         else:
             self.losses = self._train_phase()
         kw = {"publish": False} if hasattr(self.defense, "publish") else {}
+        self.fell_back = False
         if self.exchange == "alltoall":
             self.slice = self.xchg.exchange(self.trainer.X.data)
-            part = self.defense.aggregate_sharded(self.slice, self.num_examples, **kw)
+            try:
+                part = self.defense.aggregate_sharded(self.slice, self.num_examples, **kw)
+            except Exception as e:  # noqa: BLE001 - the reference catches any exception
+                part = self._fallback(e, self.slice.X)
             self.slice.gather_vector(part, self.global_flat)
+            self.round_index += 1
             return self.global_flat
         fdist.allgather_rows(self.trainer.X.data, self.full.data)
-        agg = self.defense.aggregate_flat(self.full, self.num_examples, **kw)
+        if self._wants_global:  # FLTrust: the server update starts from this round's global model
+            kw["global_flat"] = self.global_flat.clone()  # global_flat is overwritten below
+        try:
+            agg = self.defense.aggregate_flat(self.full, self.num_examples, **kw)
+        except Exception as e:  # noqa: BLE001
+            agg = self._fallback(e, self.full.X)
         self.global_flat.copy_(agg)
+        self.round_index += 1
         return self.global_flat
+
+    def _fallback(self, err: Exception, X: torch.Tensor) -> torch.Tensor:
+        """robust_server.py:120-122: a failing defense falls back to FedAvg
+        (only with RoundConfig.fallback_fedavg; otherwise the error propagates)."""
+        if not self.rcfg.fallback_fedavg:
+            raise err
+        logging.getLogger(__name__).error("Defense aggregation failed: %s, falling back to FedAvg", err)
+        self.fell_back = True
+        return ops.fedavg(X, self.num_examples)
+
+    # ---- checkpoint / resume (run_experiments.py:268-279) ----------------------
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """The global model's state_dict: parameters() from the global vector,
+        buffers (BatchNorm running statistics) at their initial values — the
+        simulation never updates the global model's buffers (:257-259)."""
+        m = model_class(self.spec)(self.spec)
+        flat = self.global_flat.detach().cpu()
+        off = 0
+        with torch.no_grad():
+            for p in m.parameters():
+                n = p.numel()
+                p.copy_(flat[off:off + n].view(p.shape))
+                off += n
+        return m.state_dict()
+
+    def save_checkpoint(self, path: str, accuracy: Optional[float] = None, loss: Optional[float] = None) -> None:
+        """torch.save({'round', 'model_state_dict', 'accuracy', 'loss'}) — the
+        reference's checkpoint dict (run_experiments.py:273-279)."""
+        torch.save({"round": self.round_index, "model_state_dict": self.state_dict(), "accuracy": accuracy,
+                    "loss": loss}, path)
+
+    def load_checkpoint(self, path: str) -> int:
+        """Resume: the global vector and round index from save_checkpoint's file
+        (weights_only load: nothing in the file is executed)."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        names = [n for n, _ in param_layout(self.spec)]
+        sd = ck["model_state_dict"]
+        flat = torch.cat([sd[n].reshape(-1).float() for n in names])
+        self.global_flat.copy_(flat.to(self.global_flat.device))
+        self.round_index = int(ck["round"])
+        return self.round_index
 
     # ---- per-round evaluation (run_experiments.py:261-266, 281-291) ------------
     def evaluator(self):

@@ -69,3 +69,13 @@ def local_update(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, 
         losses.append(loss.item())
     update = [p.data.clone() for p in model.parameters()]  # :238
     return update, sum(losses) / len(losses)
+
+
+def fl_client_train(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, learning_rate: float = 0.01,
+                    masks: Optional[Sequence[torch.Tensor]] = None) -> Tuple[List[torch.Tensor], float]:
+    """FLClient._train (src/client/fl_client.py:109-149): SGD(lr, momentum=0.9),
+    no weight decay and NO gradient clipping (only the simulation loop clips,
+    run_experiments.py:234); loss = sum of batch losses / number of batches.
+    clip_grad_norm_ with max_norm = inf scales by exactly 1, i.e. no clip."""
+    return local_update(model_cls, spec, global_flat, batches, lr=learning_rate, momentum=0.9, weight_decay=0.0,
+                        max_norm=float("inf"), masks=masks)

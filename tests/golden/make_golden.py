@@ -68,6 +68,58 @@ def stat_case(name, X, shapes, trim_ratio, num_examples):
         num_examples=np.array(num_examples, dtype=np.int64), fedavg=cat(fa), **META)
 
 
+def x_checksum(X: torch.Tensor):
+    """(sum, sum of squares) in fp64 — pins the CPU generator stream the test
+    regenerates X from (the fixture stores the seed, not X)."""
+    Xd = X.double()
+    return float(Xd.sum()), float((Xd * Xd).sum())
+
+
+def exact_distances(X: torch.Tensor) -> np.ndarray:
+    """fp64 distances through a centred fp64 Gram matrix (no cancellation at
+    fp64 for these magnitudes), the yardstick both the reference's fp32
+    torch.norm and the GPU kernels are measured against."""
+    Xd = X.double()
+    Y = Xd - Xd.mean(dim=0, keepdim=True)
+    G = Y @ Y.T
+    d = torch.diag(G)
+    D2 = (d[:, None] + d[None, :] - 2 * G).clamp_min(0)
+    D = D2.sqrt().numpy()
+    np.fill_diagonal(D, 0.0)
+    return D
+
+
+def krum_c3_case(name, K, P, f, multi_k, seed):
+    """C3-shaped Krum case: K clients, f sign-flipped, the
+    §8d heteroscedastic generator, run through the oracle (krum.py:73-192 with
+    the simulation's multi_k, run_experiments.py:155-162).  Only the seed,
+    the outputs and a checksum are stored; the test regenerates X on the CPU
+    (flr.workload.update_matrix, torch CPU generator) so the .npz stays small."""
+    import hashlib
+    X = update_matrix(K, P, f=f, seed=seed, device="cpu")[:, :P].contiguous()
+    ups = split_rows(X, P, [(P,)])
+    agg, scores, sel, rej, dist = orc.krum(ups, f, multi_k)
+    flat_agg = torch.cat([a.reshape(-1) for a in agg]).numpy()
+    exact = exact_distances(X)
+    off = ~np.eye(K, dtype=bool)
+    ref_err = float((np.abs(dist - exact)[off] / exact[off]).max())  # the reference's own fp32 error
+    s, s2 = x_checksum(X)
+    np.savez_compressed(
+        os.path.join(HERE, f"c3krum_{name}.npz"), K=K, P=P, f=f, multi_k=multi_k, seed=seed, x_sum=s, x_sumsq=s2,
+        dist=dist, exact=exact, scores=np.array(scores), selected=np.array(sel), rejected=np.array(rej),
+        agg_sha256=hashlib.sha256(flat_agg.tobytes()).hexdigest(), agg_head=flat_agg[:4096],
+        margin=margin(scores, multi_k), ref_err=ref_err, **META)
+    print(f"c3krum_{name}: margin {margin(scores, multi_k):.3e}, reference fp32 error {ref_err:.3e}")
+
+
+def main_c3():
+    # C3: K = 128, f = int(0.2 K) = 25 (experiment_matrix.py:67), multi_k = K // 2 = 64
+    # (run_experiments.py:161); P = 65,537 runs the 3-term Gram split, P = 1,048,640
+    # (>= 2^20) the 2-term split every BASELINE config runs.
+    krum_c3_case("K128_P65537", 128, 65537, 25, 64, seed=2024)
+    krum_c3_case("K128_P1048640", 128, 1_048_640, 25, 64, seed=2025)
+
+
 def main():
     torch.manual_seed(0)
     # reference demo construction (krum.py:244-263): 5 benign base+0.1N, 2 malicious 10*base+5N
@@ -96,4 +148,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "c3":
+        main_c3()
+    else:
+        main()
+        main_c3()

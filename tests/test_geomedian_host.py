@@ -41,3 +41,17 @@ def test_zero_iters_case_returns_median_weights_shape():
     D = torch.cdist(U, U).numpy()
     w, W, n = weiszfeld_pairwise(D, np.ones(4), 1, 1e-5)
     assert w.shape == (4,) and n == 1
+
+
+def test_duplicate_clients_trigger_direct_fallback():
+    """Colluding clients sending the same vector: the Weiszfeld iterate moves
+    onto their point, dist2 = (D2 a)_i - a^T D2 a / 2 cancels, and the
+    pairwise form declines (None -> the defense runs the direct passes)."""
+    ups = _case(9, 500, 6)
+    for i in range(1, 4):  # 4 of 9 identical: the iterate converges onto their point (44 iterations)
+        ups[i] = [t.clone() for t in ups[0]]
+    U = torch.stack([torch.cat([p.flatten() for p in u]) for u in ups]).double()
+    D = torch.cdist(U, U).numpy()
+    med = torch.median(U.float(), dim=0)[0].double()
+    d0 = torch.norm((U.float() - med.float()).double(), dim=1).numpy()
+    assert weiszfeld_pairwise(D, d0, 100, 1e-5) is None

@@ -174,6 +174,31 @@ def test_order_stats_vs_torch(cuda, K):
     del ref_sorted
 
 
+@pytest.mark.parametrize("K", [5, 16, 100, 128, 200, 512])
+def test_order_stats_nan_like_torch(cuda, K):
+    """A Byzantine client sending NaN: torch.sort orders NaN last, torch.median
+    returns NaN for a column with any NaN, and the trimmed mean is NaN only
+    when more NaN than t survive the trim (trimmed_mean.py:74-101)."""
+    P = 3001
+    X = torch.randn(K, P, device=cuda)
+    nan = float("nan")
+    X[0, :700] = nan                      # one NaN per column: trimmed away when t >= 1
+    X[1 % K, 100:200] = nan               # two NaN in these columns
+    X[2 % K, 200:300] = float("inf")      # NaN / +inf ties
+    X[3 % K, 300:400] = -nan              # negative-signed NaN sorts last too
+    t = max(1, int(K * 0.1))
+    cpu = X.cpu()
+    med_ref = torch.median(cpu, dim=0)[0]
+    med = ops.median_lower(X).cpu()
+    np.testing.assert_array_equal(med.numpy(), med_ref.numpy())  # NaN == NaN positions, bit-exact elsewhere
+    if K - 2 * t >= 1:
+        ref = torch.sort(cpu, dim=0)[0][t:K - t].mean(dim=0)
+        got = ops.trimmed_mean(X, t).cpu()
+        assert torch.equal(torch.isnan(got), torch.isnan(ref))
+        fin = ~torch.isnan(ref)
+        torch.testing.assert_close(got[fin], ref[fin], rtol=1e-5, atol=1e-6)
+
+
 def test_trimmed_falls_back_to_median(cuda):
     ups = [[torch.randn(7, device=cuda)] for _ in range(3)]
     d = get_defense("trimmed_mean", {"trim_ratio": 0.5})

@@ -133,3 +133,22 @@ def test_geometric_median_vs_oracle(cuda, K, P, tol, method):
     got = d.aggregate([[t.to(cuda) for t in u] for u in ups], [1] * K)
     assert abs(d.num_iters - iters) <= 1, (d.num_iters, iters)
     _close(_flat(got), want)
+
+
+def test_geometric_median_duplicate_clients(cuda):
+    """Duplicated / colluding client rows: the pairwise identity cancels near
+    the shared point, so the defense falls back to the direct passes and
+    matches the oracle (trimmed_mean.py:216-251)."""
+    K, P = 9, 500
+    g = torch.Generator().manual_seed(6)
+    base = torch.randn(P, generator=g) * 0.05
+    rows = [base + torch.randn(P, generator=g) * 0.01 * (1 + 0.5 * i / K) for i in range(K)]
+    ups = [[r[: P // 2].clone(), r[P // 2:].clone()] for r in rows]
+    for i in range(1, 4):  # 4 of 9 identical: the iterate converges onto their point
+        ups[i] = [t.clone() for t in ups[0]]
+    want, iters = orc.geometric_median(ups, 100, 1e-5)
+    d = get_defense("geometric_median", {"tolerance": 1e-5})
+    got = d.aggregate([[t.to(cuda) for t in u] for u in ups], [1] * K)
+    assert d.used_direct
+    assert abs(d.num_iters - iters) <= 1, (d.num_iters, iters)
+    _close(_flat(got), want)

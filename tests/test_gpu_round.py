@@ -1,0 +1,81 @@
+"""GPU: the round engine's auxiliary paths.
+
+* checkpoint / resume — the reference's dict {'round', 'model_state_dict',
+  'accuracy', 'loss'} (run_experiments.py:268-279), loadable into the
+  reference-structured module, and a resumed engine continues bit-identically;
+* FedAvg fallback when the defense raises (robust_server.py:120-122);
+* FLTrust through the round engine (the global_params plumbing the
+  reference's simulation lacks, fltrust.py:235-238).
+"""
+import pytest
+import torch
+
+from oracle import aggregation as orc
+from flr.models.multimodal import TINY, MultimodalNet
+from flr.round import RoundConfig, RoundEngine
+from flr.train import TrainConfig
+
+pytestmark = pytest.mark.gpu
+
+
+def test_checkpoint_resume_bit_identical(cuda, tmp_path):
+    rc = RoundConfig(num_clients=4, batch=4, defense="fedavg", attack="none", num_attackers=0, graph=False)
+    eng = RoundEngine(TINY, rc, TrainConfig(local_steps=2), cuda)
+    eng.run_round()
+    path = str(tmp_path / "ck.pt")
+    eng.save_checkpoint(path, accuracy=0.25, loss=2.0)
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    assert set(ck) == {"round", "model_state_dict", "accuracy", "loss"} and ck["round"] == 1
+    m = MultimodalNet(TINY)
+    m.load_state_dict(ck["model_state_dict"])  # strict: every parameter and buffer
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    assert torch.equal(flat, eng.global_flat.cpu())
+    eng2 = RoundEngine(TINY, rc, TrainConfig(local_steps=2), cuda)
+    assert eng2.load_checkpoint(path) == 1
+    assert torch.equal(eng.run_round(), eng2.run_round())
+    assert eng2.round_index == 2
+
+
+def test_fedavg_fallback_when_defense_raises(cuda):
+    # Krum with f = 1 needs n >= 5: at n = 4 it raises (krum.py:153-157)
+    kw = dict(num_clients=4, batch=4, attack="sign_flip", num_attackers=1, graph=False)
+    eng = RoundEngine(TINY, RoundConfig(defense="krum", fallback_fedavg=True, **kw), TrainConfig(local_steps=1), cuda)
+    out = eng.run_round().clone()
+    assert eng.fell_back
+    ref = RoundEngine(TINY, RoundConfig(defense="fedavg", **kw), TrainConfig(local_steps=1), cuda).run_round()
+    assert torch.equal(out, ref)
+    strict = RoundEngine(TINY, RoundConfig(defense="krum", **kw), TrainConfig(local_steps=1), cuda)
+    with pytest.raises(ValueError):
+        strict.run_round()
+
+
+def test_fltrust_round(cuda):
+    """FLTrust in the round loop: the engine hands the defense a copy of the
+    round's global vector; the result equals the oracle's trust-weighted
+    aggregate of the same client rows given the same server update."""
+    spec = TINY
+    g = torch.Generator().manual_seed(5)
+    N = 24
+    root = (torch.randn(N, spec.in_channels, spec.image_size, spec.image_size, generator=g),
+            torch.randint(0, spec.vocab, (N, spec.seq_len), generator=g),
+            torch.randint(0, spec.num_classes, (N,), generator=g))
+    rc = RoundConfig(num_clients=6, batch=4, defense="fltrust", attack="sign_flip", num_attackers=1,
+                     defense_cfg={"batch_size": 8, "shuffle": False}, graph=False)
+    eng = RoundEngine(spec, rc, TrainConfig(local_steps=2), cuda)
+    eng.defense.set_root_dataset(*root)
+    eng.defense.set_model(spec)
+    assert eng.exchange == "allgather"
+    before = eng.global_flat.clone()
+    out = eng.run_round().clone()
+    assert not torch.equal(out, before)
+    X = eng.full.X.cpu()
+    ups = [[X[i]] for i in range(X.shape[0])]
+    want, trust = orc.fltrust(ups, [eng.defense.server_gradient.cpu()])
+    # every client's trust score matches the oracle's (fltrust.py:158-214); the
+    # simulation's updates are weights, so the sign-flipped row's cosine against
+    # the server delta has no fixed sign and is checked like the others
+    assert len(eng.defense.trust_scores) == len(trust) == 6
+    for got_t, want_t in zip(eng.defense.trust_scores, trust):
+        assert abs(got_t - want_t) <= 1e-4 * max(1.0, abs(want_t)) + 1e-6
+    err = (out.cpu().double() - want[0].double()).abs().max().item()
+    assert err <= 1e-5 * max(1.0, want[0].abs().max().item()), err

@@ -113,7 +113,7 @@ def _free_port():
     return p
 
 
-def _round_worker(rank, world, port, defense, q):
+def _round_worker(rank, world, port, defense, q, exchange="alltoall"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
@@ -122,7 +122,7 @@ def _round_worker(rank, world, port, defense, q):
     from flr.models.multimodal import TINY
     from flr.round import RoundConfig, RoundEngine
     from flr.train import TrainConfig
-    rc = RoundConfig(num_clients=8, batch=4, defense=defense, num_attackers=1, exchange="alltoall",
+    rc = RoundConfig(num_clients=8, batch=4, defense=defense, num_attackers=1, exchange=exchange,
                      defense_cfg={"trim_ratio": 0.2} if defense == "trimmed_mean" else {})
     eng = RoundEngine(TINY, rc, TrainConfig(local_steps=2), torch.device("cuda:0"), rank, world)
     for _ in range(2):
@@ -138,12 +138,12 @@ def _round_worker(rank, world, port, defense, q):
         dist.destroy_process_group()
 
 
-def _run(world, defense):
+def _run(world, defense, exchange="alltoall"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_round_worker, args=(r, world, port, defense, q)) for r in range(world)]
+    procs = [ctx.Process(target=_round_worker, args=(r, world, port, defense, q, exchange)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in procs], key=lambda r: r[0])
@@ -153,9 +153,12 @@ def _run(world, defense):
     return res
 
 
-@pytest.mark.parametrize("defense", ["krum", "trimmed_mean"])
-def test_sharded_round_two_ranks_equals_one(cuda, defense):
-    one = _run(1, defense)
-    two = _run(2, defense)
+@pytest.mark.parametrize("defense,exchange", [("krum", "alltoall"), ("trimmed_mean", "alltoall"),
+                                              ("krum", "allgather"), ("norm_bounding", "allgather")])
+def test_sharded_round_two_ranks_equals_one(cuda, defense, exchange):
+    """Both exchanges; 'allgather' is the path of every defense without a
+    coordinate-sharded form (norm_bounding here), gloo-staged through the host."""
+    one = _run(1, defense, exchange)
+    two = _run(2, defense, exchange)
     assert np.array_equal(one[0][1], two[0][1]) and np.array_equal(two[0][1], two[1][1])
     assert one[0][2] == two[0][2] == two[1][2]

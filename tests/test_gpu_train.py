@@ -57,10 +57,21 @@ def test_client_api_mirror(cuda):
     params, n, metrics = c.local_update(parts, {"local_epochs": 1, "learning_rate": 0.01})
     assert n == 16 and metrics["client_id"] == 7 and isinstance(metrics["loss"], float)
     assert [p.shape for p in params] == shapes
-    upd, ref_loss = otrain.local_update(MultimodalNet, spec, glob.cpu(), [(a.cpu(), b.cpu(), y.cpu()) for a, b, y in batches])
+    cpu_b = [(a.cpu(), b.cpu(), y.cpu()) for a, b, y in batches]
+    upd, ref_loss = otrain.fl_client_train(MultimodalNet, spec, glob.cpu(), cpu_b)  # fl_client.py:109-149, no clip
     assert abs(metrics["loss"] - ref_loss) < 1e-5
+    ref = torch.cat([u.reshape(-1) for u in upd])
+    got = torch.cat([p.reshape(-1) for p in params]).cpu()
+    assert _rel(got, ref) < 1e-5, _rel(got, ref)
     nd, _, _ = c.fit([p.cpu().numpy() for p in parts], {})
     assert len(nd) == len(shapes)
+    # clip = 1.0: the simulation loop's clip_grad_norm_ (run_experiments.py:234)
+    c1 = Client(7, batches, spec, cuda, clip=1.0, learning_rate=0.5)
+    params1, _, m1 = c1.local_update(parts, {"local_epochs": 1})
+    upd1, loss1 = otrain.local_update(MultimodalNet, spec, glob.cpu(), cpu_b, lr=0.5, max_norm=1.0)
+    assert abs(m1["loss"] - loss1) < 1e-5
+    ref1 = torch.cat([u.reshape(-1) for u in upd1])
+    assert _rel(torch.cat([p.reshape(-1) for p in params1]).cpu(), ref1) < 1e-5
 
 
 def test_full_model_single_step_runs(cuda):

@@ -116,6 +116,32 @@ def test_golden_stats_reproduce(path):
     np.testing.assert_array_equal(cat(orc.fedavg(ups, fx["num_examples"].tolist())), fx["fedavg"])
 
 
+@pytest.mark.parametrize("path", golden_files("c3krum"), ids=lambda p: p.split("/")[-1])
+def test_golden_c3_krum_regenerates(path):
+    """The C3-shaped fixtures store the seed, not X: the CPU generator must
+    reproduce X exactly (checksums), and — at the smaller P — the oracle must
+    reproduce the stored distances, scores and selection bit for bit."""
+    import hashlib
+    from flr.workload import update_matrix
+    fx = load_golden(path)
+    K, P, f, mk = (int(fx[k]) for k in ("K", "P", "f", "multi_k"))
+    X = update_matrix(K, P, f=f, seed=int(fx["seed"]), device="cpu")[:, :P].contiguous()
+    Xd = X.double()
+    assert float(Xd.sum()) == float(fx["x_sum"]) and float((Xd * Xd).sum()) == float(fx["x_sumsq"])
+    # selection from the stored D (krum.py:101-131, 174)
+    scores = orc.krum_scores(fx["dist"], K - f - 2)
+    np.testing.assert_array_equal(np.asarray(scores), fx["scores"])
+    order = np.argsort(scores)
+    assert order[:mk].tolist() == fx["selected"].tolist() and order[mk:].tolist() == fx["rejected"].tolist()
+    assert not set(fx["selected"].tolist()) & set(range(f))  # every sign-flipped client rejected
+    if P < 100_000:
+        agg, sc, sel, rej, dist = orc.krum(split_rows(X, P, [(P,)]), f, mk)
+        np.testing.assert_array_equal(dist, fx["dist"])
+        assert sel == fx["selected"].tolist()
+        flat = torch.cat([a.reshape(-1) for a in agg]).numpy()
+        assert hashlib.sha256(flat.tobytes()).hexdigest() == str(fx["agg_sha256"])
+
+
 def test_golden_krum_margins_recorded():
     for path in golden_files("krum"):
         fx = load_golden(path)
