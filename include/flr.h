@@ -162,7 +162,7 @@ int flr_clip_sgd_step(float* X, const float* G, float* M, int64_t K, int64_t P,
 /* Same step on the parameter-major training layout: block j holds block_numel[j]
  * elements per client at client stride block_client_stride[j] (NULL: the
  * blocks are whole parameters, stride = numel); x/g/m_blocks are host arrays
- * of nblocks device pointers (nblocks <= 96).  Client k's element e of block j
+ * of nblocks device pointers (nblocks <= 768, run as launches of <= 96 blocks).  Client k's element e of block j
  * is at ptr_j + k*stride_j + e.  Elements not covered by any block (dead
  * kernel taps, whose gradient is identically zero) are neither read nor
  * updated; with weight_decay == 0 that is exactly the reference's update.
@@ -347,6 +347,27 @@ int flr_batchnorm_bwd(const float* dy, const float* x, const float* y,
  * flr_sum_rows: out[k][n] = sum_m X[k][m][n] (bias gradients; eight interleaved
  * partial sums in a fixed order, deterministic). */
 size_t flr_bgemm_workspace(int64_t batch, int64_t M, int64_t N, int64_t R);
+/* flr_bgemm with a fused epilogue, applied per output element after the
+ * bias / addend (and after the split-K reduction):
+ *   pre (optional, C-shaped) <- v;  v <- act(v);  v <- v * mul (optional);  C <- v
+ * act: FLR_ACT_NONE, _RELU, _GELU (exact erf, torch's nn.GELU()), _TANH; the
+ * backward modes multiply the incoming gradient v by the activation's
+ * derivative at aux (C-shaped, required): _DRELU (aux > 0, aux = the ReLU
+ * input or output), _DGELU (aux = the GELU input), _DTANH (aux = the tanh
+ * output).  mul / aux / pre share C's strides.  The late-fusion head's
+ * ReLU + dropout mask, the transformer MLP's GELU and BERT's pooler tanh run
+ * here instead of as separate elementwise passes. */
+#define FLR_ACT_NONE 0
+#define FLR_ACT_RELU 1
+#define FLR_ACT_GELU 2
+#define FLR_ACT_TANH 3
+#define FLR_ACT_DRELU 4
+#define FLR_ACT_DGELU 5
+#define FLR_ACT_DTANH 6
+int flr_bgemm_ex(const float* A, int64_t a_k, int64_t a_m, int64_t a_r, const float* B, int64_t b_k, int64_t b_n,
+                 int64_t b_r, float* C, int64_t c_k, int64_t c_m, int64_t c_n, const float* bias, int64_t bias_k,
+                 const float* add, int act, const float* mul, const float* aux, float* pre, int64_t batch,
+                 int64_t M, int64_t N, int64_t R, void* workspace, size_t workspace_bytes, void* stream);
 int flr_bgemm(const float* A, int64_t a_k, int64_t a_m, int64_t a_r, const float* B,
               int64_t b_k, int64_t b_n, int64_t b_r, float* C, int64_t c_k, int64_t c_m,
               int64_t c_n, const float* bias, int64_t bias_k, const float* add,
@@ -388,6 +409,75 @@ int flr_batchnorm_infer(const float* x, const float* gamma, const float* beta,
 int flr_classify_rows(const float* logits, const int64_t* labels, int64_t R, int64_t C,
                       int64_t target, int64_t source, int32_t* pred, float* loss_rows,
                       int64_t* counts, void* stream);
+
+/* ---- a3 + C4/C5 encoders: embedding, LayerNorm, self-attention -------------
+ * (csrc/train_xfmr.hip).  Every op is batched over the clients of a GPU;
+ * client k's rows are the k-th run of rows_per_client rows (or N positions).
+ *
+ * flr_fill: p[0..n) = value (a kernel, so it replays inside HIP graphs).
+ *
+ * flr_embedding_fwd replaces nn.Embedding (the GRU branch's token embedding,
+ * BERT's word / token-type / position embeddings summed in that order):
+ *   out[k][n] = ((w0[k][ids0[k][n]] + w1[k][ids1[k][n]]) + w2[k][ids2[k][n]])
+ * wj at wj + k*wj_k (row-major [Vj][E]), idsj at idsj + k*idsj_k (stride 0 =
+ * the same ids for every client); w1 / w2 may be NULL.  An id outside
+ * [0, Vj) yields a NaN row (the caller validates; nothing faults).
+ * flr_embedding_bwd: dtable[k][v] = sum of dout[k][n] over the n with
+ * ids[k][n] == v, in increasing n, from 0 — torch's CPU embedding backward
+ * (index_add in index order), bit for bit.  zero_fill != 0 first zeroes the
+ * whole [V][E] table of every client; rows no id touches are otherwise left
+ * as they are.  N <= 4096; workspace flr_embedding_bwd_workspace(K, N).
+ */
+int flr_fill(float* p, int64_t n, float value, void* stream);
+/* out[i] = dy[i] * act'(aux[i]) [* mul[i]] for the FLR_ACT_D* modes (the
+ * activation backward where no GEMM epilogue can take it). */
+int flr_act_bwd(const float* dy, const float* aux, const float* mul, int act, float* out, int64_t n, void* stream);
+int flr_embedding_fwd(const float* w0, int64_t w0_k, int64_t V0, const int64_t* ids0, int64_t ids0_k,
+                      const float* w1, int64_t w1_k, int64_t V1, const int64_t* ids1, int64_t ids1_k,
+                      const float* w2, int64_t w2_k, int64_t V2, const int64_t* ids2, int64_t ids2_k,
+                      int64_t K, int64_t N, int64_t E, float* out, void* stream);
+size_t flr_embedding_bwd_workspace(int64_t K, int64_t N);
+int flr_embedding_bwd(const float* dout, const int64_t* ids, int64_t ids_k, int64_t K, int64_t N, int64_t V,
+                      int64_t E, float* dtable, int64_t dtable_k, int zero_fill, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
+/* flr_layernorm_fwd replaces nn.LayerNorm(D, eps) over `rows` rows (row i at
+ * x + i*ldx, gamma / beta [K][D] for client i / rows_per_client), with the
+ * residual add of the encoder block fused in front:
+ *   s = x [+ residual];  y = (s - mean) rstd gamma + beta,  rstd = 1/sqrt(var + eps)
+ * (biased variance).  s_out (optional, needs residual) receives s; mean / rstd
+ * [rows] are saved for the backward.  D % 4 == 0, D <= 1024.
+ * flr_layernorm_bwd: ds = rstd (g dy - mean(g dy) - xh mean(g dy xh)) [+ dskip],
+ * xh = (s - mean) rstd, written to dx; dgamma / dbeta [K][D] = the per-client
+ * sums over rows of dy xh / dy (fixed-order partials over 64-row chunks).
+ * Workspace flr_layernorm_bwd_workspace(K, rows_per_client, D). */
+int flr_layernorm_fwd(const float* x, int64_t ldx, const float* residual, int64_t ldr, const float* gamma,
+                      const float* beta, float* y, int64_t ldy, float* s_out, int64_t lds, float* mean, float* rstd,
+                      int64_t rows, int64_t D, int64_t rows_per_client, float eps, void* stream);
+size_t flr_layernorm_bwd_workspace(int64_t K, int64_t rows_per_client, int64_t D);
+int flr_layernorm_bwd(const float* dy, int64_t lddy, const float* s, int64_t lds, const float* gamma,
+                      const float* mean, const float* rstd, const float* dskip, int64_t ldk, float* dx, int64_t lddx,
+                      float* dgamma, float* dbeta, int64_t K, int64_t rows_per_client, int64_t D, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
+/* ViT token sequence: x0 [K][B][P+1][D], row t of sequence (k, b) =
+ * (t == 0 ? cls[k] : tok[k][b*P + t - 1]) + pos[k][t]  (the class token and
+ * the patch projections plus the learned position embedding).  D % 4 == 0,
+ * 16-B aligned operands. */
+int flr_vit_tokens(const float* tok, const float* cls, const float* pos, int64_t K, int64_t B, int64_t P, int64_t D,
+                   float* x0, void* stream);
+
+/* Multi-head self-attention core (no mask) for KB = clients x batch
+ * sequences of T <= 96 tokens, H heads of width head_dim = 64:
+ *   qkv [KB*T][3*H*64] = the fused in-projection's output (q | k | v, heads
+ *   concatenated inside each);  S = q k^T / 8;  P = softmax(S);  ctx = P v
+ *   ctx [KB*T][H*64];  lse [KB][H][T] = the softmax log-normalisers (saved).
+ * flr_attention_bwd recomputes P from lse and writes dqkv [KB*T][3*H*64]
+ * (dq | dk | dv).  fp32 on the VALU, one workgroup per (sequence, head). */
+int flr_attention_fwd(const float* qkv, int64_t KB, int64_t T, int64_t H, int64_t head_dim, float* ctx, float* lse,
+                      void* stream);
+int flr_attention_bwd(const float* qkv, const float* ctx, const float* dctx, const float* lse, int64_t KB, int64_t T,
+                      int64_t H, int64_t head_dim, float* dqkv, void* stream);
 
 #ifdef __cplusplus
 }

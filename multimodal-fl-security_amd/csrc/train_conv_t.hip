@@ -569,7 +569,35 @@ struct BGemmArgs {
   const float* bias;  // bias[k * bias_k + n]
   int64_t bias_k;
   const float* add;   // add[k*c_k + m*c_m + n*c_n] (may alias c)
+  // epilogue (flr_bgemm_ex): pre <- v; v <- act(v [, aux]); v <- v * mul
+  int act;            // FLR_ACT_*
+  const float* mul;   // indexed like c (may be NULL)
+  const float* aux;   // indexed like c: the saved activation input/output of the D* modes
+  float* pre;         // indexed like c: the pre-activation value (may be NULL)
 };
+
+// exact-erf GELU as torch's CPU kernel: x * 0.5 * (1 + erf(x * M_SQRT1_2))
+__device__ __forceinline__ float gelu_erf(float x) {
+  return __fmul_rn(__fmul_rn(x, 0.5f), __fadd_rn(1.f, erff(__fmul_rn(x, 0.70710678118654752440f))));
+}
+// d/dx GELU: 0.5 (1 + erf(x / sqrt 2)) + x exp(-x^2 / 2) / sqrt(2 pi)
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752440f));
+  const float pdf = expf(-0.5f * x * x) * 0.39894228040143267794f;
+  return cdf + x * pdf;
+}
+
+__device__ __forceinline__ float apply_act(int act, float v, const float* aux, int64_t i) {
+  switch (act) {
+    case FLR_ACT_RELU: return v > 0.f ? v : 0.f;
+    case FLR_ACT_GELU: return gelu_erf(v);
+    case FLR_ACT_TANH: return tanhf(v);
+    case FLR_ACT_DRELU: return aux[i] > 0.f ? v : 0.f;
+    case FLR_ACT_DGELU: return v * gelu_erf_grad(aux[i]);
+    case FLR_ACT_DTANH: { const float y = aux[i]; return v * (1.f - y * y); }
+    default: return v;
+  }
+}
 
 template <int AM, int BMD>
 struct BGemm : BGemmArgs {
@@ -635,9 +663,12 @@ struct BGemm : BGemmArgs {
     const int64_t i = k * c_k + mm * c_m + nn * c_n;
     if (bias) v = bias[k * bias_k + nn] + v;
     if (add) v = add[i] + v;
+    if (pre) pre[i] = v;
+    if (act) v = apply_act(act, v, aux, i);
+    if (mul) v = v * mul[i];
     c[i] = v;
   }
-  __device__ bool linear() const { return c_n == 1 && !bias && !add; }
+  __device__ bool linear() const { return c_n == 1 && !bias && !add && !act && !mul && !pre; }
   __device__ float* out() const { return c; }
   __device__ int64_t tile_base(int k, int m0, int n0) const { return k * c_k + m0 * c_m + n0; }
   __device__ int64_t ldm() const { return c_m; }
@@ -1175,7 +1206,18 @@ extern "C" int flr_bgemm(const float* A, int64_t a_k, int64_t a_m, int64_t a_r, 
                          int64_t b_n, int64_t b_r, float* C, int64_t c_k, int64_t c_m, int64_t c_n, const float* bias,
                          int64_t bias_k, const float* add, int64_t batch, int64_t M, int64_t N, int64_t R, void* ws,
                          size_t ws_bytes, void* stream) {
+  return flr_bgemm_ex(A, a_k, a_m, a_r, B, b_k, b_n, b_r, C, c_k, c_m, c_n, bias, bias_k, add, FLR_ACT_NONE, nullptr,
+                      nullptr, nullptr, batch, M, N, R, ws, ws_bytes, stream);
+}
+
+extern "C" int flr_bgemm_ex(const float* A, int64_t a_k, int64_t a_m, int64_t a_r, const float* B, int64_t b_k,
+                            int64_t b_n, int64_t b_r, float* C, int64_t c_k, int64_t c_m, int64_t c_n,
+                            const float* bias, int64_t bias_k, const float* add, int act, const float* mul,
+                            const float* aux, float* pre, int64_t batch, int64_t M, int64_t N, int64_t R, void* ws,
+                            size_t ws_bytes, void* stream) {
   if (!A || !B || !C || batch < 1 || batch > 65535 || M < 1 || N < 1 || R < 1) return FLR_ERR_ARG;
+  if (act < FLR_ACT_NONE || act > FLR_ACT_DTANH) return FLR_ERR_ARG;
+  if (act >= FLR_ACT_DRELU && !aux) return FLR_ERR_ARG;
   if (a_k < 0 || a_m < 0 || a_r < 0 || b_k < 0 || b_n < 0 || b_r < 0 || c_k < 0 || c_m < 0 || c_n < 0)
     return FLR_ERR_ARG;
   const int64_t a_ext = (M - 1) * a_m + (R - 1) * a_r + 1;
@@ -1190,6 +1232,7 @@ extern "C" int flr_bgemm(const float* A, int64_t a_k, int64_t a_m, int64_t a_r, 
   p.b = B; p.b_k = b_k; p.b_n = b_n; p.b_r = b_r; p.b_ext = b_ext;
   p.c = C; p.c_k = c_k; p.c_m = c_m; p.c_n = c_n;
   p.bias = bias; p.bias_k = bias_k; p.add = add;
+  p.act = act; p.mul = mul; p.aux = aux; p.pre = pre;
   hipStream_t st = as_stream(stream);
   const int am = bgemm_mode(A, a_k, a_m, a_r, M, R), bm = bgemm_mode(B, b_k, b_n, b_r, N, R);
   switch (am) {

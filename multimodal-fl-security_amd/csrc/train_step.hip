@@ -11,6 +11,8 @@
 // coef = min(1, max_norm / (total + 1e-6)), g *= coef.
 #include "flr_common.h"
 
+#include <algorithm>
+
 namespace flr {
 namespace train {
 
@@ -44,12 +46,15 @@ __global__ __launch_bounds__(THREADS) void sumsq_kernel(const float* __restrict_
 
 // coef[k] = min(1, max_norm / (||g_k|| + 1e-6)) in fp32 (torch computes it in
 // the gradient dtype); norms_out[k] = ||g_k||.
+// partial [nparts][K][NBLK] (the blocked step's launches over block chunks),
+// summed part by part in fixed order.
 __global__ void clip_coef_kernel(const double* __restrict__ partial, int K, float max_norm,
-                                 float* __restrict__ coef, float* __restrict__ norms_out) {
+                                 float* __restrict__ coef, float* __restrict__ norms_out, int nparts = 1) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
   double s = 0.0;
-  for (int b = 0; b < NBLK; ++b) s += partial[(int64_t)k * NBLK + b];
+  for (int c = 0; c < nparts; ++c)
+    for (int b = 0; b < NBLK; ++b) s += partial[((int64_t)c * K + k) * NBLK + b];
   const float total = (float)sqrt(s);
   float c = __fdiv_rn(max_norm, __fadd_rn(total, 1e-6f));
   coef[k] = c < 1.0f ? c : 1.0f;
@@ -129,7 +134,8 @@ __global__ void scale_rows_kernel(float* __restrict__ d, const float* __restrict
 // client stride cs[j] is n[j] for a whole parameter and larger for a sub-slab
 // (the live kernel taps of a tap-major conv weight; the dead taps' slabs are
 // left out of the step altogether).
-constexpr int MAXB = 96;
+constexpr int MAXB = 96;        // blocks per launch (the table is a kernel argument)
+constexpr int MAX_PARTS = 8;    // launches per step: up to 768 parameter blocks
 struct BlockTable {
   float* x[MAXB];
   const float* g[MAXB];
@@ -272,7 +278,8 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
 using namespace flr;
 
 extern "C" size_t flr_clip_sgd_workspace(int64_t K) {
-  return align_up((size_t)K * train::NBLK * sizeof(double), 256) + align_up((size_t)K * sizeof(float), 256);
+  return align_up((size_t)train::MAX_PARTS * K * train::NBLK * sizeof(double), 256) +
+         align_up((size_t)K * sizeof(float), 256);
 }
 
 extern "C" int flr_clip_sgd_step(float* X, const float* G, float* M, int64_t K, int64_t P, int64_t ld, float lr,
@@ -287,7 +294,7 @@ extern "C" int flr_clip_sgd_step(float* X, const float* G, float* M, int64_t K, 
   if (max_norm > 0) {
     double* partial = static_cast<double*>(workspace);
     coef = reinterpret_cast<float*>(static_cast<char*>(workspace) +
-                                    align_up((size_t)K * train::NBLK * sizeof(double), 256));
+                                    align_up((size_t)train::MAX_PARTS * K * train::NBLK * sizeof(double), 256));
     hipLaunchKernelGGL(train::sumsq_kernel, dim3(train::NBLK, (unsigned)K), dim3(train::THREADS), 0, st, G, P, ld,
                        partial);
     if ((rc = launch_status("sumsq_kernel")) != FLR_OK) return rc;
@@ -328,26 +335,35 @@ extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* co
                                          int64_t nblocks, int64_t K, float lr,
                                          float momentum, float weight_decay, float max_norm, int first_step,
                                          float* norms_out, void* workspace, size_t workspace_bytes, void* stream) {
-  if (K < 1 || nblocks < 1 || nblocks > train::MAXB || !x_blocks || !g_blocks || !m_blocks || !block_numel)
+  if (K < 1 || nblocks < 1 || nblocks > (int64_t)train::MAXB * train::MAX_PARTS || !x_blocks || !g_blocks ||
+      !m_blocks || !block_numel)
     return FLR_ERR_ARG;
   if (max_norm > 0 && (!workspace || workspace_bytes < flr_clip_sgd_workspace(K))) return FLR_ERR_WORKSPACE;
-  train::BlockTable tb;
-  tb.nb = (int)nblocks;
-  tb.pre[0] = 0;
-  for (int j = 0; j < tb.nb; ++j) {
-    if (!x_blocks[j] || !g_blocks[j] || !m_blocks[j] || block_numel[j] < 0) return FLR_ERR_ARG;
-    tb.x[j] = x_blocks[j];
-    tb.g[j] = g_blocks[j];
-    tb.m[j] = m_blocks[j];
-    tb.pre[j + 1] = tb.pre[j] + block_numel[j];
-    const int64_t cs = block_client_stride ? block_client_stride[j] : block_numel[j];
-    if (cs < block_numel[j] || cs >= ((int64_t)1 << 31)) return FLR_ERR_ARG;
-    tb.cs[j] = (int32_t)cs;
-    const uintptr_t al = reinterpret_cast<uintptr_t>(x_blocks[j]) | reinterpret_cast<uintptr_t>(g_blocks[j]) |
-                         reinterpret_cast<uintptr_t>(m_blocks[j]);
-    tb.vec[j] = (block_numel[j] % 4 == 0 && cs % 4 == 0 && (al & 15) == 0) ? 1 : 0;
+  // the blocks in launches of at most MAXB (the table travels as a kernel argument)
+  const int nparts = (int)((nblocks + train::MAXB - 1) / train::MAXB);
+  train::BlockTable tbs[train::MAX_PARTS];
+  int64_t P = 0;
+  for (int c = 0; c < nparts; ++c) {
+    train::BlockTable& tb = tbs[c];
+    const int j0 = c * train::MAXB, j1 = (int)std::min<int64_t>(nblocks, (int64_t)j0 + train::MAXB);
+    tb.nb = j1 - j0;
+    tb.pre[0] = 0;
+    for (int q = 0; q < tb.nb; ++q) {
+      const int j = j0 + q;
+      if (!x_blocks[j] || !g_blocks[j] || !m_blocks[j] || block_numel[j] < 0) return FLR_ERR_ARG;
+      tb.x[q] = x_blocks[j];
+      tb.g[q] = g_blocks[j];
+      tb.m[q] = m_blocks[j];
+      tb.pre[q + 1] = tb.pre[q] + block_numel[j];
+      const int64_t cs = block_client_stride ? block_client_stride[j] : block_numel[j];
+      if (cs < block_numel[j] || cs >= ((int64_t)1 << 31)) return FLR_ERR_ARG;
+      tb.cs[q] = (int32_t)cs;
+      const uintptr_t al = reinterpret_cast<uintptr_t>(x_blocks[j]) | reinterpret_cast<uintptr_t>(g_blocks[j]) |
+                           reinterpret_cast<uintptr_t>(m_blocks[j]);
+      tb.vec[q] = (block_numel[j] % 4 == 0 && cs % 4 == 0 && (al & 15) == 0) ? 1 : 0;
+    }
+    P += tb.pre[tb.nb];
   }
-  const int64_t P = tb.pre[tb.nb];
   if (P == 0) return FLR_OK;
   hipStream_t st = as_stream(stream);
   float* coef = nullptr;
@@ -355,15 +371,20 @@ extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* co
   if (max_norm > 0) {
     double* partial = static_cast<double*>(workspace);
     coef = reinterpret_cast<float*>(static_cast<char*>(workspace) +
-                                    align_up((size_t)K * train::NBLK * sizeof(double), 256));
-    hipLaunchKernelGGL(train::sumsq_blocked_kernel, dim3(train::NBLK, (unsigned)K), dim3(train::THREADS), 0, st, tb,
-                       P, partial);
-    if ((rc = launch_status("sumsq_blocked_kernel")) != FLR_OK) return rc;
+                                    align_up((size_t)train::MAX_PARTS * K * train::NBLK * sizeof(double), 256));
+    for (int c = 0; c < nparts; ++c) {
+      hipLaunchKernelGGL(train::sumsq_blocked_kernel, dim3(train::NBLK, (unsigned)K), dim3(train::THREADS), 0, st,
+                         tbs[c], tbs[c].pre[tbs[c].nb], partial + (int64_t)c * K * train::NBLK);
+      if ((rc = launch_status("sumsq_blocked_kernel")) != FLR_OK) return rc;
+    }
     hipLaunchKernelGGL(train::clip_coef_kernel, dim3(cdiv((int)K, 64)), dim3(64), 0, st, partial, (int)K, max_norm,
-                       coef, norms_out);
+                       coef, norms_out, nparts);
     if ((rc = launch_status("clip_coef_kernel")) != FLR_OK) return rc;
   }
-  hipLaunchKernelGGL(train::sgd_blocked_kernel, dim3(train::NSGD, (unsigned)K), dim3(train::THREADS), 0, st, tb, P,
-                     coef, lr, momentum, weight_decay, first_step & 3);
-  return launch_status("sgd_blocked_kernel");
+  for (int c = 0; c < nparts; ++c) {
+    hipLaunchKernelGGL(train::sgd_blocked_kernel, dim3(train::NSGD, (unsigned)K), dim3(train::THREADS), 0, st, tbs[c],
+                       tbs[c].pre[tbs[c].nb], coef, lr, momentum, weight_decay, first_step & 3);
+    if ((rc = launch_status("sgd_blocked_kernel")) != FLR_OK) return rc;
+  }
+  return FLR_OK;
 }

@@ -87,6 +87,26 @@ SIGNATURES = {
     "flr_bgemm_workspace": (_size_t, [_i64] * 4),
     "flr_bgemm": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _i64, _i64,
                          _c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _size_t, _c_void_p]),
+    "flr_bgemm_ex": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _i64, _i64,
+                            _c_void_p, _i64, _c_void_p, _int, _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64, _i64,
+                            _c_void_p, _size_t, _c_void_p]),
+    "flr_fill": (_int, [_c_void_p, _i64, ctypes.c_float, _c_void_p]),
+    "flr_act_bwd": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _c_void_p]),
+    "flr_embedding_fwd": (_int, [_c_void_p, _i64, _i64, _c_void_p, _i64] * 3 + [_i64, _i64, _i64, _c_void_p,
+                                                                                _c_void_p]),
+    "flr_embedding_bwd_workspace": (_size_t, [_i64, _i64]),
+    "flr_embedding_bwd": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _i64, _i64, _c_void_p, _i64, _int,
+                                 _c_void_p, _size_t, _c_void_p]),
+    "flr_layernorm_fwd": (_int, [_c_void_p, _i64, _c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
+                                 _i64, _c_void_p, _c_void_p, _i64, _i64, _i64, ctypes.c_float, _c_void_p]),
+    "flr_layernorm_bwd_workspace": (_size_t, [_i64, _i64, _i64]),
+    "flr_layernorm_bwd": (_int, [_c_void_p, _i64, _c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64,
+                                 _c_void_p, _i64, _c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p, _size_t,
+                                 _c_void_p]),
+    "flr_vit_tokens": (_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p]),
+    "flr_attention_fwd": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),
+    "flr_attention_bwd": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64, _i64, _c_void_p,
+                                 _c_void_p]),
     "flr_sum_rows": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p]),
     "flr_maxpool2d_fwd": (_int, [_c_void_p] * 3 + [_i64] * 7 + [_c_void_p]),
     "flr_maxpool2d_bwd": (_int, [_c_void_p] * 3 + [_i64] * 7 + [_c_void_p]),

@@ -49,12 +49,26 @@ class ModelSpec:
     hidden: int = 256
     fusion: int = 256
     dropout: float = 0.5
-    family: str = "resnet_gru"  # "resnet_gru" (C2/C3) | "cub" (C1)
+    family: str = "resnet_gru"  # "resnet_gru" (C2/C3) | "cub" (C1) | "vit_bert" (C4/C5)
+    # vit_bert (flr.models.transformer): ViT-S/4 image encoder + BERT-mini text encoder
+    patch: int = 4
+    vit_dim: int = 384
+    vit_depth: int = 12
+    vit_heads: int = 6
+    vit_mlp: int = 1536
+    bert_dim: int = 256
+    bert_depth: int = 4
+    bert_heads: int = 4
+    bert_ffn: int = 1024
+    bert_max_pos: int = 512
 
     @property
     def name(self) -> str:
         if self.family == "cub":
             return "cub200-multimodal-cnn (conv img + attribute MLP) late-fusion"
+        if self.family == "vit_bert":
+            return (f"vit-s/{self.patch}(d{self.vit_dim}x{self.vit_depth})-img+bert-mini(d{self.bert_dim}x"
+                    f"{self.bert_depth})-text late-fusion")
         return "resnet18-img+gru1-text late-fusion"
 
 
@@ -67,6 +81,14 @@ TINY = ModelSpec(widths=(8, 16, 16, 32), blocks=(1, 1, 1, 1), vocab=50, embed=8,
 # attribute MLP's widths (cub200_cnn.py:71-93).
 CUB = ModelSpec(family="cub", num_classes=10, widths=(32, 64, 128), blocks=(), vocab=312, embed=128,
                 hidden=256, fusion=256, dropout=0.5)
+
+# C4/C5: ViT-S/4 (384 x 12, 6 heads, MLP 1536) + BERT-mini (256 x 4, 4 heads, FFN
+# 1024, WordPiece vocabulary 30522), fusion 640 -> 256 -> 10 (flr.models.transformer)
+VIT_BERT = ModelSpec(family="vit_bert", num_classes=10, vocab=30522, seq_len=16, fusion=256, dropout=0.5)
+# the same structure at test size (every layer kind, a few hundred thousand parameters)
+VIT_BERT_TINY = ModelSpec(family="vit_bert", num_classes=10, vocab=97, seq_len=16, fusion=32, dropout=0.0,
+                          patch=8, vit_dim=64, vit_depth=2, vit_heads=1, vit_mlp=128, bert_dim=128, bert_depth=2,
+                          bert_heads=2, bert_ffn=256, bert_max_pos=32)
 
 
 class BasicBlock(nn.Module):
@@ -154,6 +176,9 @@ class CubMultimodalNet(nn.Module):
 
 def model_class(spec: ModelSpec):
     """The nn.Module of one client for this spec's family."""
+    if spec.family == "vit_bert":
+        from .transformer import ViTBertNet
+        return ViTBertNet
     return CubMultimodalNet if spec.family == "cub" else MultimodalNet
 
 
@@ -200,6 +225,8 @@ def conv_geometry(spec: ModelSpec) -> Dict[str, Tuple[int, int, int, int, int]]:
     """name -> (H_in, kernel, stride, pad, H_out) of every conv weight (square maps)."""
     out = {}
     H = spec.image_size
+    if spec.family == "vit_bert":  # no convolutions (the patch embedding is a Linear)
+        return out
     if spec.family == "cub":
         for idx in (0, 4, 8):
             out[f"image_conv.{idx}.weight"] = (H, 3, 1, 1, H)
@@ -337,6 +364,10 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     """
     if spec.family == "cub":
         return _cub_forward(p, images, tokens, spec, dropout_mask, tap_major, bn_stats)
+    if spec.family == "vit_bert":
+        from .transformer import patchify, vit_bert_forward
+        patches = patchify(images, spec.patch) if images.dim() == 5 else images
+        return vit_bert_forward(p, patches, tokens, spec, dropout_mask, native=_LAYERS == "native" and images.is_cuda)
 
     def st(bn):
         return _eval_stats(bn_stats, bn, p[bn + ".weight"])
@@ -370,7 +401,10 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
             x = _bn_act(conv(pre + "conv2.weight", y, 1, 1), p[pre + "bn2.weight"], p[pre + "bn2.bias"],
                         residual=idt, stats=st(pre + "bn2"))
     if native:
-        img = x.mean(dim=(2, 3)).view(K, w[-1], B).transpose(1, 2)  # [K, B, 512]
+        # global average pool: at 32x32 input layer4's map is 1x1, where the mean
+        # is the value itself (exact) and the pooled features are a free view
+        gap = x.view(K, w[-1], B) if x.shape[2] * x.shape[3] == 1 else x.mean(dim=(2, 3)).view(K, w[-1], B)
+        img = gap.transpose(1, 2)  # [K, B, 512]
     else:
         img = x.mean(dim=(2, 3)).view(B, K, w[-1]).transpose(0, 1)
 
@@ -378,8 +412,12 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     V, E, H = spec.vocab, spec.embed, spec.hidden
     table = p["embedding.weight"]  # [K, V, E]
     T = tokens.shape[2]
-    kofs = (torch.arange(K, device=tokens.device) * V).view(K, 1, 1)
-    emb = table.reshape(K * V, E)[(tokens + kofs).reshape(-1)].view(K, B * T, E)
+    if native:  # flr_embedding_fwd / _bwd (deterministic index_add order)
+        from ..nn import client_embedding
+        emb = client_embedding(table, tokens.reshape(K, B * T))
+    else:
+        kofs = (torch.arange(K, device=tokens.device) * V).view(K, 1, 1)
+        emb = table.reshape(K * V, E)[(tokens + kofs).reshape(-1)].view(K, B * T, E)
     if native:  # flr_bgemm (MFMA) for every matrix product of the text branch and the head
         from ..nn import client_linear as _lin
     else:
@@ -393,6 +431,10 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     else:
         h = _gru_torch(gi, p["gru.weight_hh_l0"], p["gru.bias_hh_l0"])
 
+    if native:  # fusion head: [img | h] never concatenated; ReLU + dropout mask in the GEMM epilogues
+        from ..nn import client_mlp
+        return client_mlp((img, h), p["fc1.weight"], p["fc1.bias"], p["fc2.weight"], p["fc2.bias"], "relu",
+                          mask=dropout_mask)
     f = torch.cat([img, h], dim=2)  # [K, B, 512 + H]
     f = F.relu(_lin(f, p["fc1.weight"], p["fc1.bias"]))
     if dropout_mask is not None:

@@ -337,3 +337,327 @@ class ClientMaxPool2d(torch.autograd.Function):
 
 def client_maxpool2d(x, k: int, stride: int, pad: int):
     return ClientMaxPool2d.apply(x, k, stride, pad)
+
+
+# ---------------------------------------------------------------------------
+# a3 / a4 / C4-C5 encoders: embedding, fused-epilogue GEMM, LayerNorm, attention
+# ---------------------------------------------------------------------------
+
+ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3, "drelu": 4, "dgelu": 5, "dtanh": 6}
+
+
+def fill_(t: torch.Tensor, value: float = 0.0) -> torch.Tensor:
+    """t[...] = value on the flr_fill kernel (contiguous t)."""
+    assert t.is_contiguous()
+    _capi.call("flr_fill", t.data_ptr(), t.numel(), float(value), _stream(t))
+    return t
+
+
+def bgemm_ex(A: torch.Tensor, B: torch.Tensor, bias=None, add=None, act: str = "none", mul=None, aux=None,
+             pre=None, out=None) -> torch.Tensor:
+    """bgemm with the fused epilogue of flr_bgemm_ex: pre <- v; v <- act(v, aux);
+    v <- v * mul.  add / mul / aux / pre share out's strides."""
+    K, M, R = A.shape
+    N = B.shape[1]
+    if B.shape[0] != K or B.shape[2] != R:
+        raise ValueError(f"bgemm operand shapes {tuple(A.shape)} / {tuple(B.shape)}")
+    if out is None:
+        out = torch.empty(K, M, N, dtype=A.dtype, device=A.device)
+    for name, t in (("add", add), ("mul", mul), ("aux", aux), ("pre", pre)):
+        if t is not None and (t.shape != out.shape or t.stride() != out.stride()):
+            raise ValueError(f"bgemm_ex {name} must share the output's shape and strides")
+    if bias is not None and (bias.shape != (K, N) or bias.stride(1) != 1):
+        raise ValueError("bgemm bias must be [K, N] with unit row stride")
+    n = int(_capi.lib().flr_bgemm_workspace(K, M, N, R))
+    ws = torch.empty(n, dtype=torch.uint8, device=A.device) if n else None
+    _capi.call("flr_bgemm_ex", A.data_ptr(), *A.stride(), B.data_ptr(), *B.stride(), out.data_ptr(), *out.stride(),
+               _ptr(bias), 0 if bias is None else bias.stride(0), _ptr(add), ACT[act], _ptr(mul), _ptr(aux),
+               _ptr(pre), K, M, N, R, None if ws is None else ws.data_ptr(), n, _stream(A))
+    return out
+
+
+class ClientEmbedding(torch.autograd.Function):
+    """out[K, N, E] = table[K, V, E][ids[K, N]] (nn.Embedding per client) on
+    flr_embedding_fwd; backward: flr_embedding_bwd, torch's index_add order."""
+
+    @staticmethod
+    def forward(ctx, table, ids):
+        K, V, E = table.shape
+        table = table.contiguous()
+        ids = ids.reshape(K, -1).contiguous()
+        N = ids.shape[1]
+        out = torch.empty(K, N, E, dtype=table.dtype, device=table.device)
+        _capi.call("flr_embedding_fwd", table.data_ptr(), V * E, V, ids.data_ptr(), N, None, 0, 0, None, 0, None, 0, 0,
+                   None, 0, K, N, E, out.data_ptr(), _stream(table))
+        ctx.save_for_backward(ids)
+        ctx.shape = (K, V, E, N)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (ids,) = ctx.saved_tensors
+        K, V, E, N = ctx.shape
+        dout = dout.contiguous()
+        dtab = torch.empty(K, V, E, dtype=dout.dtype, device=dout.device)
+        n = int(_capi.lib().flr_embedding_bwd_workspace(K, N))
+        ws = torch.empty(n, dtype=torch.uint8, device=dout.device)
+        _capi.call("flr_embedding_bwd", dout.data_ptr(), ids.data_ptr(), N, K, N, V, E, dtab.data_ptr(), V * E, 1,
+                   ws.data_ptr(), n, _stream(dout))
+        return dtab, None
+
+
+def client_embedding(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    return ClientEmbedding.apply(table, ids)
+
+
+class ClientEmbeddingSum(torch.autograd.Function):
+    """BERT embeddings before the LayerNorm: (word[ids] + type[type_ids]) +
+    pos[pos_ids] per client (one flr_embedding_fwd); each table's gradient is
+    its own flr_embedding_bwd.  ids [K, N]; type_ids / pos_ids [N] shared by
+    every client (client stride 0)."""
+
+    @staticmethod
+    def forward(ctx, word, typ, pos, ids, type_ids, pos_ids):
+        K, V, E = word.shape
+        word, typ, pos = word.contiguous(), typ.contiguous(), pos.contiguous()
+        ids = ids.reshape(K, -1).contiguous()
+        N = ids.shape[1]
+        Vt, Vp = typ.shape[1], pos.shape[1]
+        out = torch.empty(K, N, E, dtype=word.dtype, device=word.device)
+        _capi.call("flr_embedding_fwd", word.data_ptr(), V * E, V, ids.data_ptr(), N,
+                   typ.data_ptr(), Vt * E, Vt, type_ids.data_ptr(), 0,
+                   pos.data_ptr(), Vp * E, Vp, pos_ids.data_ptr(), 0, K, N, E, out.data_ptr(), _stream(word))
+        ctx.save_for_backward(ids, type_ids, pos_ids)
+        ctx.shape = (K, E, N, V, Vt, Vp)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ids, type_ids, pos_ids = ctx.saved_tensors
+        K, E, N, V, Vt, Vp = ctx.shape
+        dout = dout.contiguous()
+        n = int(_capi.lib().flr_embedding_bwd_workspace(K, N))
+        ws = torch.empty(n, dtype=torch.uint8, device=dout.device)
+        grads = []
+        for idv, ik, rows in ((ids, N, V), (type_ids, 0, Vt), (pos_ids, 0, Vp)):
+            d = torch.empty(K, rows, E, dtype=dout.dtype, device=dout.device)
+            _capi.call("flr_embedding_bwd", dout.data_ptr(), idv.data_ptr(), ik, K, N, rows, E, d.data_ptr(),
+                       rows * E, 1, ws.data_ptr(), n, _stream(dout))
+            grads.append(d)
+        return grads[0], grads[1], grads[2], None, None, None
+
+
+def client_embedding_sum(word, typ, pos, ids, type_ids, pos_ids):
+    return ClientEmbeddingSum.apply(word, typ, pos, ids, type_ids, pos_ids)
+
+
+class ClientLayerNorm(torch.autograd.Function):
+    """y = LayerNorm(x [+ residual]) per client over rows of width D; with a
+    residual it also returns s = x + residual (the encoder's residual stream)
+    so the skip path's gradient can be handed back as the backward's addend.
+    x / residual [K, R, D] contiguous, gamma / beta [K, D]."""
+
+    @staticmethod
+    def forward(ctx, x, residual, gamma, beta, eps: float):
+        x = x.contiguous()
+        K, R, D = x.shape
+        y = torch.empty_like(x)
+        mean = torch.empty(K * R, dtype=x.dtype, device=x.device)
+        rstd = torch.empty_like(mean)
+        s = None
+        if residual is not None:
+            residual = residual.contiguous()
+            s = torch.empty_like(x)
+        g, b = gamma.contiguous(), beta.contiguous()
+        _capi.call("flr_layernorm_fwd", x.data_ptr(), D, _ptr(residual), D, g.data_ptr(), b.data_ptr(), y.data_ptr(),
+                   D, _ptr(s), D, mean.data_ptr(), rstd.data_ptr(), K * R, D, R, eps, _stream(x))
+        ctx.save_for_backward(x if s is None else s, g, mean, rstd)
+        ctx.has_res = residual is not None
+        return y, s
+
+    @staticmethod
+    def backward(ctx, dy, ds):
+        s, g, mean, rstd = ctx.saved_tensors
+        K, R, D = s.shape
+        dy = dy.contiguous()
+        dx = torch.empty_like(s)
+        dg = torch.empty_like(g)
+        db = torch.empty_like(g)
+        dskip = None if ds is None else ds.contiguous()
+        n = int(_capi.lib().flr_layernorm_bwd_workspace(K, R, D))
+        ws = torch.empty(n, dtype=torch.uint8, device=dy.device)
+        _capi.call("flr_layernorm_bwd", dy.data_ptr(), D, s.data_ptr(), D, g.data_ptr(), mean.data_ptr(),
+                   rstd.data_ptr(), _ptr(dskip), D, dx.data_ptr(), D, dg.data_ptr(), db.data_ptr(), K, R, D,
+                   ws.data_ptr(), n, _stream(dy))
+        return dx, (dx if ctx.has_res else None), dg, db, None
+
+
+def client_layernorm(x, gamma, beta, residual=None, eps: float = 1e-5):
+    """Returns y (residual None) or (y, s = x + residual)."""
+    y, s = ClientLayerNorm.apply(x, residual, gamma, beta, eps)
+    return y if residual is None else (y, s)
+
+
+class ClientAttention(torch.autograd.Function):
+    """ctx [K, B, T, D] = softmax(q k^T / sqrt(64)) v per (client, batch row,
+    head) from the fused projection qkv [K, B, T, 3D] (flr_attention_fwd/_bwd)."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads: int):
+        qkv = qkv.contiguous()
+        K, B, T, D3 = qkv.shape
+        D = D3 // 3
+        out = torch.empty(K, B, T, D, dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty(K * B * heads * T, dtype=qkv.dtype, device=qkv.device)
+        _capi.call("flr_attention_fwd", qkv.data_ptr(), K * B, T, heads, D // heads, out.data_ptr(), lse.data_ptr(),
+                   _stream(qkv))
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.heads = heads
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        K, B, T, D3 = qkv.shape
+        dout = dout.contiguous()
+        dqkv = torch.empty_like(qkv)
+        _capi.call("flr_attention_bwd", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), K * B, T,
+                   ctx.heads, D3 // 3 // ctx.heads, dqkv.data_ptr(), _stream(dout))
+        return dqkv, None
+
+
+def client_attention(qkv: torch.Tensor, heads: int) -> torch.Tensor:
+    return ClientAttention.apply(qkv, heads)
+
+
+def _act_bwd(dy: torch.Tensor, aux: torch.Tensor, mask, act: str) -> torch.Tensor:
+    """d(pre) = dy * act'(aux) [* mask] on flr_act_bwd (contiguous operands)."""
+    out = torch.empty_like(dy)
+    _capi.call("flr_act_bwd", dy.data_ptr(), aux.data_ptr(), _ptr(mask), ACT["d" + act], out.data_ptr(), dy.numel(),
+               _stream(dy))
+    return out
+
+
+class ClientLinearAct(torch.autograd.Function):
+    """y = act(x W^T + b) per client on flr_bgemm_ex (act in relu / gelu / tanh,
+    fused in the GEMM epilogue); the backward's activation derivative is one
+    flr_act_bwd pass.  BERT's pooler (tanh) and the CUB attribute MLP use it.
+    x [K, M, in] (any strides), W [K, out, in], b [K, out]."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, act: str):
+        pre = torch.empty(x.shape[0], x.shape[1], W.shape[1], dtype=x.dtype, device=x.device) \
+            if act == "gelu" else None
+        y = bgemm_ex(x, W, bias=b, act=act, pre=pre)
+        ctx.save_for_backward(x, W, pre if act == "gelu" else y)  # relu: y > 0 <=> pre > 0; tanh': 1 - y^2
+        ctx.act = act
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W, aux = ctx.saved_tensors
+        dpre = _act_bwd(dy.contiguous(), aux, None, ctx.act)
+        dx = bgemm(dpre, W.transpose(1, 2)) if ctx.needs_input_grad[0] else None
+        dW = bgemm(dpre.transpose(1, 2), x.transpose(1, 2)) if ctx.needs_input_grad[1] else None
+        db = sum_rows(dpre) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        return dx, dW, db, None
+
+
+def client_linear_act(x, W, b, act: str):
+    return ClientLinearAct.apply(x, W, b, act)
+
+
+class ClientMLP(torch.autograd.Function):
+    """y = act(x W1^T + b1) [* mask] W2^T + b2 [+ residual] — the encoder MLP
+    (GELU) and the late-fusion head (ReLU + dropout mask, cub200_cnn.py:88-93).
+    x is one operand [K, M, in] or a tuple of column blocks (the head's
+    [img | text] concat, never materialised: fc1 runs as one GEMM per block
+    accumulating through the addend).  Fused epilogues: act (+ mask, + the
+    saved GELU input) in fc1's, act' (and the mask) in the dy W2 GEMM's."""
+
+    @staticmethod
+    def forward(ctx, W1, b1, W2, b2, mask, residual, act: str, *xs):
+        K, M = xs[0].shape[:2]
+        F = W1.shape[1]
+        pre = torch.empty(K, M, F, dtype=W1.dtype, device=W1.device) if act == "gelu" else None
+        mask = None if mask is None else mask.contiguous()
+        h = None
+        c0 = 0
+        for i, x in enumerate(xs):
+            w = W1[:, :, c0:c0 + x.shape[2]]
+            c0 += x.shape[2]
+            last = i == len(xs) - 1
+            h = bgemm_ex(x, w, bias=b1 if i == 0 else None, add=h, act=act if last else "none",
+                         mul=mask if last else None, pre=pre if last else None, out=h)
+        y = bgemm(h, W2, bias=b2, add=None if residual is None else residual.contiguous())
+        ctx.save_for_backward(W1, W2, h, pre, mask, *xs)
+        ctx.act = act
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        W1, W2, h, pre, mask, *xs = ctx.saved_tensors
+        dy = dy.contiguous()
+        aux = pre if ctx.act == "gelu" else h  # relu: h > 0 <=> kept and pre > 0
+        dpre = bgemm_ex(dy, W2.transpose(1, 2), act="d" + ctx.act, aux=aux, mul=mask)
+        dW2 = bgemm(dy.transpose(1, 2), h.transpose(1, 2))
+        db2 = sum_rows(dy)
+        K, F, Din = W1.shape
+        dW1 = torch.empty(K, F, Din, dtype=W1.dtype, device=W1.device)
+        dxs = []
+        c0 = 0
+        for i, x in enumerate(xs):
+            w = x.shape[2]
+            if ctx.needs_input_grad[7 + i]:
+                dxs.append(bgemm(dpre, W1[:, :, c0:c0 + w].transpose(1, 2)))
+            else:
+                dxs.append(None)
+            bgemm(dpre.transpose(1, 2), x.transpose(1, 2), out=dW1[:, :, c0:c0 + w])
+            c0 += w
+        db1 = sum_rows(dpre)
+        return (dW1, db1, dW2, db2, None, dy if ctx.has_res else None, None, *dxs)
+
+
+def client_mlp(x, W1, b1, W2, b2, act: str, mask=None, residual=None):
+    """x: a [K, M, in] tensor or a tuple of column blocks (see ClientMLP)."""
+    xs = tuple(x) if isinstance(x, (tuple, list)) else (x,)
+    return ClientMLP.apply(W1, b1, W2, b2, mask, residual, act, *xs)
+
+
+class ClientViTTokens(torch.autograd.Function):
+    """x0 [K, B, P+1, D]: the class token and the patch projections tok
+    [K, B*P, D], plus the position embedding pos [K, P+1, D] (flr_vit_tokens).
+    Backward: dpos / dcls = per-client sums over the batch rows (flr_sum_rows),
+    dtok = rows 1..P of every sequence (flr_copy_rows)."""
+
+    @staticmethod
+    def forward(ctx, tok, cls, pos, B: int):
+        K, BP, D = tok.shape
+        P = BP // B
+        tok, cls, pos = tok.contiguous(), cls.contiguous(), pos.contiguous()
+        x0 = torch.empty(K, B, P + 1, D, dtype=tok.dtype, device=tok.device)
+        _capi.call("flr_vit_tokens", tok.data_ptr(), cls.data_ptr(), pos.data_ptr(), K, B, P, D, x0.data_ptr(),
+                   _stream(tok))
+        ctx.dims = (K, B, P, D)
+        ctx.cls_shape = cls.shape
+        return x0
+
+    @staticmethod
+    def backward(ctx, dx0):
+        K, B, P, D = ctx.dims
+        dx0 = dx0.contiguous()
+        T = P + 1
+        st = _stream(dx0)
+        dpos = torch.empty(K, T, D, dtype=dx0.dtype, device=dx0.device)
+        _capi.call("flr_sum_rows", dx0.data_ptr(), B * T * D, T * D, K, B, T * D, dpos.data_ptr(), T * D, st)
+        dcls = torch.empty(K, D, dtype=dx0.dtype, device=dx0.device)
+        _capi.call("flr_sum_rows", dx0.data_ptr(), B * T * D, T * D, K, B, D, dcls.data_ptr(), D, st)
+        dtok = torch.empty(K, B * P, D, dtype=dx0.dtype, device=dx0.device)
+        _capi.call("flr_copy_rows", dx0.data_ptr() + 4 * D, T * D, P * D, dtok.data_ptr(), P * D, K * B, st)
+        return dtok, dcls.view(ctx.cls_shape), dpos, None
+
+
+def client_vit_tokens(tok, cls, pos, B: int):
+    return ClientViTTokens.apply(tok, cls, pos, B)

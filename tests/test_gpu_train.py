@@ -174,3 +174,48 @@ def test_c1_round_fedavg_matches_reference(cuda):
         ups.append(upd)
     ref = torch.cat([t.reshape(-1) for t in orc.fedavg(ups, [steps * B] * K)])
     assert _rel(new, ref) < 1e-5, _rel(new, ref)
+
+
+def test_vit_bert_tiny_matches_reference_loop(cuda):
+    """The C4/C5 family (ViT + BERT encoders, every kernel of train_xfmr.hip
+    and the fused GEMM epilogues) at test size: 3 clients x 3 steps with
+    dropout masks vs the oracle loop on one ViTBertNet per client."""
+    from flr.models.multimodal import VIT_BERT_TINY
+    spec = VIT_BERT_TINY.__class__(**{**VIT_BERT_TINY.__dict__, "dropout": 0.5})
+    K, B, steps = 3, 8, 3
+    glob = initial_global(spec, 42, cuda)
+    tr = ClientBatchTrainer(spec, K, cuda, TrainConfig(local_steps=steps))
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    masks = make_dropout_masks(spec, steps, K, B, cuda, seed=4)
+    tr.load_global(glob)
+    loss = tr.local_update(batches, masks).cpu()
+    for k in range(K):
+        cb = [(im[k].cpu(), tk[k].cpu(), lb[k].cpu()) for im, tk, lb in batches]
+        upd, ref_loss = otrain.local_update(model_class(spec), spec, glob.cpu(), cb, masks=[m[k].cpu() for m in masks])
+        ref = torch.cat([u.reshape(-1) for u in upd])
+        got = tr.X.data[k, : tr.P].cpu()
+        assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+        assert _rel(got, ref) < 1e-5, _rel(got, ref)
+
+
+def test_vit_bert_full_model_matches_reference_loop(cuda):
+    """The C4/C5 model itself (ViT-S/4 + BERT-mini, P = 32,675,722): 2 clients
+    x 2 steps vs the oracle loop."""
+    from flr.models.multimodal import VIT_BERT
+    spec = VIT_BERT
+    assert num_params(spec) == 32_675_722
+    K, B, steps = 2, 4, 2
+    glob = initial_global(spec, 42, cuda)
+    tr = ClientBatchTrainer(spec, K, cuda, TrainConfig(local_steps=steps))
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    masks = make_dropout_masks(spec, steps, K, B, cuda, seed=6)
+    tr.load_global(glob)
+    loss = tr.local_update(batches, masks).cpu()
+    assert torch.isfinite(loss).all()
+    for k in range(K):
+        cb = [(im[k].cpu(), tk[k].cpu(), lb[k].cpu()) for im, tk, lb in batches]
+        upd, ref_loss = otrain.local_update(model_class(spec), spec, glob.cpu(), cb, masks=[m[k].cpu() for m in masks])
+        ref = torch.cat([u.reshape(-1) for u in upd])
+        got = tr.X.data[k, : tr.P].cpu()
+        assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+        assert _rel(got, ref) < 1e-5, _rel(got, ref)
