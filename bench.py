@@ -137,24 +137,43 @@ def cpu_baseline(spec, P, K, f, multi_k, steps, batch, budget_s: float = 20.0):
     }
 
 
+# BASELINE.json configs as presets: (model, clients, defense, defense_cfg, attack, attacker fraction)
+PRESETS = {
+    "C1": ("cub", 4, "fedavg", {}, "none", 0.0),
+    "C2": ("resnet_gru", 32, "fedavg", {}, "none", 0.0),
+    "C3": ("resnet_gru", 128, "krum", {}, "sign_flip", 0.2),
+    "C4": ("vit_bert", 256, "trimmed_mean", {"trim_ratio": 0.1}, "none", 0.0),
+    "C5": ("vit_bert", 512, "krum_trimmed_mean", {"trim_ratio": 0.1}, "backdoor", 0.2),
+}
+WORKLOAD = {
+    "C1": "C1: FedAvg K=4, CUB200MultimodalCNN structure (conv img + attribute MLP over the BoW text)",
+    "C2": "C2: FedAvg K=32, ResNet-18 img + 1-layer GRU text late fusion, 5 local SGD steps/round",
+    "C3": "C3: Multi-Krum K=128, 20% sign-flip, ResNet-18 img + 1-layer GRU text late fusion, 5 local SGD steps/round",
+    "C4": "C4: trimmed-mean K=256, ViT-S/4 img + BERT-mini text late fusion, 5 local SGD steps/round",
+    "C5": "C5: backdoor K=512 (20% trigger-patch clients), ViT-S/4 + BERT-mini, Multi-Krum then trimmed-mean",
+}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--clients", type=int, default=128)
+    ap.add_argument("--config", default="C3", choices=sorted(PRESETS),
+                    help="BASELINE.json config preset (C3 = the headline metric's workload)")
+    ap.add_argument("--clients", type=int, default=None)
     ap.add_argument("--local-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "allgather"])
-    ap.add_argument("--defense", default="krum", help="secondary configs: fedavg (C2), trimmed_mean, median")
-    ap.add_argument("--model", default="resnet_gru", choices=["resnet_gru", "cub"],
-                    help="cub = the C1 model (the reference's CUB200MultimodalCNN structure)")
+    ap.add_argument("--defense", default=None, help="override the preset's defense (fedavg, krum, trimmed_mean, median)")
+    ap.add_argument("--model", default=None, choices=["resnet_gru", "cub", "vit_bert"])
+    ap.add_argument("--client-chunk", type=int, default=0, help="clients per forward/backward pass (0: automatic)")
     args = ap.parse_args()
 
     import torch
     from flr import dist as fdist
-    from flr.models.multimodal import CUB, ModelSpec, num_params
+    from flr.models.multimodal import CUB, VIT_BERT, ModelSpec, num_params
     from flr.round import RoundConfig, RoundEngine
     from flr.timing import HipEventPair
     from flr.train import TrainConfig
@@ -163,16 +182,24 @@ def main() -> None:
     rank, world, local = fdist.init("nccl")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    spec = CUB if args.model == "cub" else ModelSpec()
+    model, K, defense, dcfg, attack, afrac = PRESETS[args.config]
+    custom = any(v is not None for v in (args.clients, args.defense, args.model))
+    model = args.model or model
+    K = args.clients or K
+    if args.defense:
+        defense, dcfg = args.defense, ({"trim_ratio": 0.1} if "trimmed" in args.defense else {})
+        attack, afrac = ("sign_flip", 0.2) if args.defense in ("krum", "multi_krum") else ("none", 0.0)
+    spec = {"cub": CUB, "vit_bert": VIT_BERT}.get(model, ModelSpec())
     P = num_params(spec)
-    K = args.clients
-    krum = args.defense in ("krum", "multi_krum")
-    f = int(0.2 * K) if krum else 0
-    rcfg = RoundConfig(num_clients=K, defense=args.defense, num_attackers=f, exchange=args.exchange,
-                       attack="sign_flip" if krum else "none")
-    tcfg = TrainConfig(local_steps=args.local_steps)
+    krum = defense in ("krum", "multi_krum", "krum_trimmed_mean")
+    f = int(afrac * K)
+    rcfg = RoundConfig(num_clients=K, defense=defense, defense_cfg=dict(dcfg), num_attackers=f,
+                       exchange=args.exchange, attack=attack)
+    tcfg = TrainConfig(local_steps=args.local_steps, client_chunk=args.client_chunk)
     eng = RoundEngine(spec, rcfg, tcfg, device, rank, world)
     multi_k = getattr(eng.defense, "multi_k", 0)
+    workload = (WORKLOAD[args.config] if not custom else
+                f"{defense} K={K}, {spec.name}, {args.local_steps} local SGD steps/round")
 
     for _ in range(args.warmup):
         eng.run_round()
@@ -245,11 +272,10 @@ def main() -> None:
         "data": "synthetic (SURVEY §8d: N(0,1) 3x32x32 images, U{0..999} 16-token texts, 10 classes; "
                 "random-init weights, seed 42)",
         "config": {
-            "workload": ("C3: Multi-Krum K=128, 20% sign-flip, ResNet-18 img + 1-layer GRU text late fusion, "
-                         "5 local SGD steps/round") if (krum and K == 128 and args.model == "resnet_gru") else
-                        f"{args.defense} K={K}, {spec.name}, {args.local_steps} local SGD steps/round",
+            "workload": workload, "preset": None if custom else args.config, "model": spec.name,
             "clients": K, "params": P, "local_steps": args.local_steps, "batch": rcfg.batch,
-            "defense": f"krum(f={f}, multi_k={multi_k})" if krum else args.defense, "attackers": f,
+            "defense": f"{defense}(f={f}, multi_k={multi_k})" if krum else defense, "attack": attack,
+            "attackers": f, "client_chunk": eng.trainer.chunks[0][1] - eng.trainer.chunks[0][0],
             "parallelism": (f"clients sharded {K // world}/GPU x {world}; " + (
                 "one all-to-all (client rows -> coordinate ranges), per-GPU aggregation of its range, "
                 "all-gather of the aggregated vector" if sharded else "one all-gather of the client matrix")),
@@ -268,7 +294,7 @@ def main() -> None:
             "kernel_ms": kernel_ms, "algorithmic_bytes": pair_bytes, "coords_per_gpu": n_coords,
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and krum and args.model == "resnet_gru":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and defense == "krum" and model == "resnet_gru":
         out["cpu_baseline"] = cpu_baseline(spec, P, K, f, multi_k, args.local_steps, rcfg.batch, args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)

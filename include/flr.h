@@ -144,6 +144,14 @@ int flr_trimmed_mean(const float* X, int64_t K, int64_t P, int64_t ldx,
 int flr_median_lower(const float* X, int64_t K, int64_t P, int64_t ldx,
                      float* out, void* stream);
 
+/* The same two order statistics over the row subset rows[0..m) of X (device
+ * int32 indices, m <= K <= 512): the coordinate-wise trimmed mean of the
+ * Multi-Krum selection ("Krum + trimmed-mean", BASELINE.json configs[4]). */
+int flr_trimmed_mean_rows(const float* X, int64_t K, int64_t P, int64_t ldx, const int32_t* rows, int64_t m,
+                          int64_t t, float* out, void* stream);
+int flr_median_lower_rows(const float* X, int64_t K, int64_t P, int64_t ldx, const int32_t* rows, int64_t m,
+                          float* out, void* stream);
+
 /* ---- a6 + a7: fused gradient clip + SGD-momentum step -----------------
  * Replaces, for every client row at once, clip_grad_norm_(params, max_norm)
  * + torch.optim.SGD(lr, momentum, weight_decay).step()
@@ -375,6 +383,12 @@ int flr_bgemm(const float* A, int64_t a_k, int64_t a_m, int64_t a_r, const float
               size_t workspace_bytes, void* stream);
 int flr_sum_rows(const float* X, int64_t x_k, int64_t x_m, int64_t batch, int64_t M,
                  int64_t N, float* out, int64_t out_k, void* stream);
+/* The same sum over M > 256 rows as fixed 256-row chunks reduced in chunk order
+ * (a chunking that depends on M alone); workspace flr_sum_rows_workspace (0:
+ * one pass, as flr_sum_rows). */
+size_t flr_sum_rows_workspace(int64_t batch, int64_t M, int64_t N);
+int flr_sum_rows_ex(const float* X, int64_t x_k, int64_t x_m, int64_t batch, int64_t M, int64_t N, float* out,
+                    int64_t out_k, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- a2: max pooling of the image branch (the stem's 3x3/2 pad-1 pool) ----
  * Replaces nn.MaxPool2d / F.max_pool2d on x [nplanes][H][W] (planes = B*K*C of

@@ -84,12 +84,18 @@ template <int NP, int MODE>
 // 3 waves/SIMD: the NP=128 network needs ~150 VGPRs; the bound stops the
 // trimmed sum from pushing the kernel over the 168-VGPR occupancy step.
 __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __restrict__ X, int K, int64_t P,
-                                                            int64_t ldx, int t, float* __restrict__ out) {
+                                                            int64_t ldx, int t, float* __restrict__ out,
+                                                            const int32_t* __restrict__ rows) {
   const int64_t p = (int64_t)blockIdx.x * THREADS + threadIdx.x;
   if (p >= P) return;
   float v[NP];
+  if (rows) {  // a row subset (e.g. the Multi-Krum selection); the index loads are wave-uniform
 #pragma unroll
-  for (int k = 0; k < NP; ++k) v[k] = k < K ? X[(int64_t)k * ldx + p] : __builtin_huge_valf();
+    for (int k = 0; k < NP; ++k) v[k] = k < K ? X[(int64_t)rows[k] * ldx + p] : __builtin_huge_valf();
+  } else {
+#pragma unroll
+    for (int k = 0; k < NP; ++k) v[k] = k < K ? X[(int64_t)k * ldx + p] : __builtin_huge_valf();
+  }
   const int nnan = nan_to_inf<NP>(v);
   oem_sort<0, NP>(v);
   __builtin_amdgcn_sched_barrier(0);
@@ -175,20 +181,27 @@ __device__ __forceinline__ void half_clean_lane(float* v) {
 template <int L, int MODE>
 __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const float* __restrict__ X, int K,
                                                                          int64_t P, int64_t ldx, int t,
-                                                                         float* __restrict__ out) {
+                                                                         float* __restrict__ out,
+                                                                         const int32_t* __restrict__ rows) {
   const int64_t gidx = (int64_t)blockIdx.x * THREADS + threadIdx.x;
   const int64_t p = gidx / L;
   const int g = (int)(gidx % L);
   const bool active = p < P;  // inactive lanes still join the exchanges
   const int64_t pc = active ? p : 0;
   float v[128];
-  const float* __restrict__ base = X + (int64_t)(128 * g) * ldx + pc;
-  if (K >= 128 * L) {  // wave-uniform: every register holds a client (K = 256, 512)
+  if (rows) {  // a row subset (e.g. the Multi-Krum selection)
+    const int32_t* rg = rows + 128 * g;
 #pragma unroll
-    for (int i = 0; i < 128; ++i) v[i] = base[(int64_t)i * ldx];
+    for (int i = 0; i < 128; ++i) v[i] = 128 * g + i < K ? X[(int64_t)rg[i] * ldx + pc] : __builtin_huge_valf();
   } else {
+    const float* __restrict__ base = X + (int64_t)(128 * g) * ldx + pc;
+    if (K >= 128 * L) {  // wave-uniform: every register holds a client (K = 256, 512)
 #pragma unroll
-    for (int i = 0; i < 128; ++i) v[i] = 128 * g + i < K ? base[(int64_t)i * ldx] : __builtin_huge_valf();
+      for (int i = 0; i < 128; ++i) v[i] = base[(int64_t)i * ldx];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 128; ++i) v[i] = 128 * g + i < K ? base[(int64_t)i * ldx] : __builtin_huge_valf();
+    }
   }
   int nnan = nan_to_inf<128>(v);
   if (__any(nnan > 0)) {  // the coordinate's total over its L lanes (adjacent lanes)
@@ -237,24 +250,25 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
 }
 
 template <int MODE>
-int launch(const float* X, int K, int64_t P, int64_t ldx, int t, float* out, hipStream_t st) {
+int launch(const float* X, int K, int64_t P, int64_t ldx, int t, float* out, hipStream_t st,
+           const int32_t* rows = nullptr) {
   const dim3 grid((unsigned)((P + THREADS - 1) / THREADS));
   if (K <= 8)
-    hipLaunchKernelGGL((orderstat_kernel<8, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out);
+    hipLaunchKernelGGL((orderstat_kernel<8, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
   else if (K <= 16)
-    hipLaunchKernelGGL((orderstat_kernel<16, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out);
+    hipLaunchKernelGGL((orderstat_kernel<16, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
   else if (K <= 32)
-    hipLaunchKernelGGL((orderstat_kernel<32, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out);
+    hipLaunchKernelGGL((orderstat_kernel<32, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
   else if (K <= 64)
-    hipLaunchKernelGGL((orderstat_kernel<64, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out);
+    hipLaunchKernelGGL((orderstat_kernel<64, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
   else if (K <= 128)
-    hipLaunchKernelGGL((orderstat_kernel<128, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out);
+    hipLaunchKernelGGL((orderstat_kernel<128, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
   else if (K <= 256)
     hipLaunchKernelGGL((orderstat_multilane_kernel<2, MODE>), dim3((unsigned)((2 * P + THREADS - 1) / THREADS)),
-                       dim3(THREADS), 0, st, X, K, P, ldx, t, out);
+                       dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
   else if (K <= 512)
     hipLaunchKernelGGL((orderstat_multilane_kernel<4, MODE>), dim3((unsigned)((4 * P + THREADS - 1) / THREADS)),
-                       dim3(THREADS), 0, st, X, K, P, ldx, t, out);
+                       dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
   else
     return FLR_ERR_UNSUPPORTED;
   return launch_status("orderstat_kernel");
@@ -276,4 +290,19 @@ extern "C" int flr_median_lower(const float* X, int64_t K, int64_t P, int64_t ld
   if (K < 1 || P < 0 || ldx < P || !X || !out) return FLR_ERR_ARG;
   if (P == 0) return FLR_OK;
   return ostat::launch<1>(X, (int)K, P, ldx, 0, out, as_stream(stream));
+}
+
+extern "C" int flr_trimmed_mean_rows(const float* X, int64_t K, int64_t P, int64_t ldx, const int32_t* rows,
+                                     int64_t m, int64_t t, float* out, void* stream) {
+  if (K < 1 || m < 1 || m > K || P < 0 || ldx < P || t < 0 || m - 2 * t < 1 || !X || !out || !rows)
+    return FLR_ERR_ARG;
+  if (P == 0) return FLR_OK;
+  return ostat::launch<0>(X, (int)m, P, ldx, (int)t, out, as_stream(stream), rows);
+}
+
+extern "C" int flr_median_lower_rows(const float* X, int64_t K, int64_t P, int64_t ldx, const int32_t* rows,
+                                     int64_t m, float* out, void* stream) {
+  if (K < 1 || m < 1 || m > K || P < 0 || ldx < P || !X || !out || !rows) return FLR_ERR_ARG;
+  if (P == 0) return FLR_OK;
+  return ostat::launch<1>(X, (int)m, P, ldx, 0, out, as_stream(stream), rows);
 }

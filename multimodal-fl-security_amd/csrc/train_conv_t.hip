@@ -146,15 +146,21 @@ inline int xcd_remap() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 
-// FLR_PRIO=1: raise the wave priority around each MFMA cluster (A/B only).
-inline int mfma_prio() {
+// Wave priority raised around each MFMA cluster (FLR_PRIO=0: off, for A/B).
+inline int mfma_prio() {  // measured +0-5 % on the encoder GEMMs and the 3x3 convs (FLR_PRIO=0 turns it off)
   const char* e = getenv("FLR_PRIO");
-  return (e && e[0] == '1') ? 1 : 0;
+  return (e && e[0] == '0') ? 0 : 1;
 }
 
-inline bool gemm_x6() {
+// 0: exact f32 MFMA; 1: bf16x6, accumulator-chain order (each output tile's six
+// products back to back); 2: bf16x6, product-major order (the tiles' chains
+// interleave; the default).  FLR_GEMM=f32 | chain | (unset).
+inline int gemm_form() {
   const char* e = getenv("FLR_GEMM");
-  return !(e && e[0] == 'f');
+  if (e && e[0] == 'f') return 0;
+  if (e && e[0] == 'c') return 1;
+  if (e && e[0] == 'A') return 3;  // ablation (timing only, wrong results): one bf16 term, no split
+  return 2;
 }
 
 // ---- load plans ---------------------------------------------------------------
@@ -761,7 +767,7 @@ __device__ __forceinline__ void xcd_tile(int& bx, int& by, int& bz) {
   bz = t / (gx * gy);
 }
 
-template <class Plan, int MS, int NS, bool X6>
+template <class Plan, int MS, int NS, int X6>
 __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S, float* __restrict__ part, int remap,
                                                            int prio) {
   __shared__ __attribute__((aligned(16))) float As[2][MS][TILE];
@@ -813,7 +819,7 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
   for (int r0 = rbeg; r0 < rend; r0 += BK) {
     const bool more = r0 + BK < rend;
     if (more) load(r0 + BK);  // in flight during the MFMAs below
-    if constexpr (X6) {
+    if constexpr (X6 != 0) {
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
         bf16x8 ah[MS], am[MS], al[MS], bh[NS], bm[NS], bl[NS];
@@ -821,28 +827,53 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
         for (int i = 0; i < MS; ++i) {
           float v[8];
           frag8<Plan::LA>(As[cur][i], 32 * wm + l32, 16 * s + 8 * h, v);
-          split3(v, ah[i], am[i], al[i]);
+          if constexpr (X6 == 3) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ah[i][q] = am[i][q] = al[i][q] = (__bf16)v[q];
+          } else {
+            split3(v, ah[i], am[i], al[i]);
+          }
         }
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
           float v[8];
           frag8<Plan::LB>(Bs[cur][j], 32 * wn + l32, 16 * s + 8 * h, v);
-          split3(v, bh[j], bm[j], bl[j]);
+          if constexpr (X6 == 3) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) bh[j][q] = bm[j][q] = bl[j][q] = (__bf16)v[q];
+          } else {
+            split3(v, bh[j], bm[j], bl[j]);
+          }
         }
         if (prio) __builtin_amdgcn_s_setprio(1);
+        if constexpr (X6 >= 2) {
+          // product-major: the MS*NS accumulator chains interleave, so a chain's
+          // next MFMA never waits on its own previous one (small terms first)
+#define FLR_X6_STEP(AV, BV)                                                              \
+  _Pragma("unroll") for (int i = 0; i < MS; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(AV[i], BV[j], acc[i][j], 0, 0, 0);
+          FLR_X6_STEP(am, bm)
+          FLR_X6_STEP(ah, bl)
+          FLR_X6_STEP(al, bh)
+          FLR_X6_STEP(ah, bm)
+          FLR_X6_STEP(am, bh)
+          FLR_X6_STEP(ah, bh)
+#undef FLR_X6_STEP
+        } else {
 #pragma unroll
-        for (int i = 0; i < MS; ++i)
+          for (int i = 0; i < MS; ++i)
 #pragma unroll
-          for (int j = 0; j < NS; ++j) {  // small terms first
-            f32x16 c = acc[i][j];
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c, 0, 0, 0);
-            acc[i][j] = c;
-          }
+            for (int j = 0; j < NS; ++j) {  // small terms first
+              f32x16 c = acc[i][j];
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c, 0, 0, 0);
+              acc[i][j] = c;
+            }
+        }
         if (prio) __builtin_amdgcn_s_setprio(0);
       }
     } else {
@@ -984,12 +1015,23 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   int S = choose_splits(M, N, R, K, MS * NS, plan_min_kt<Plan>());
   if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) S = 1;
   const dim3 grid((unsigned)cdiv(N, BN * NS), (unsigned)cdiv(M, BM * MS), (unsigned)(K * S));
-  if (gemm_x6())
-    hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, true>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
-                       xcd_remap(), mfma_prio());
-  else
-    hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, false>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
-                       xcd_remap(), mfma_prio());
+  switch (MS * NS == 1 && gemm_form() == 2 ? 1 : gemm_form()) {  // one tile: the two orders coincide
+    case 0:
+      hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 0>), grid, dim3(THREADS), 0, st, pl, S,
+                         static_cast<float*>(ws), xcd_remap(), mfma_prio());
+      break;
+    case 1:
+      hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 1>), grid, dim3(THREADS), 0, st, pl, S,
+                         static_cast<float*>(ws), xcd_remap(), mfma_prio());
+      break;
+    case 3:
+      hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 3>), grid, dim3(THREADS), 0, st, pl, S,
+                         static_cast<float*>(ws), xcd_remap(), mfma_prio());
+      break;
+    default:
+      hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 2>), grid, dim3(THREADS), 0, st, pl, S,
+                         static_cast<float*>(ws), xcd_remap(), mfma_prio());
+  }
   int rc = launch_status(name);
   if (rc != FLR_OK || S == 1) return rc;
   const int64_t mn = (int64_t)M * N;
@@ -1180,10 +1222,23 @@ int bgemm_mode(const float* p, int64_t s_k, int64_t s_row, int64_t s_r, int64_t 
   if (s_row == 1 && al && s_r % 4 == 0 && rows % 4 == 0) return convt::BM_KR;
   return convt::BM_G;
 }
+// Workgroup tile of the batched GEMM: 128 x 128 (each wave 64 x 64, its
+// fragments and bf16 splits reused twice) for the encoder-sized products
+// (M, N >= 128 and a long reduction or many outputs), 64 x 64 for the small
+// ones (the GRU recurrence and the head, M = batch = 32).  Partial edge tiles
+// are bounds-checked in the loads and stores.  FLR_BGEMM_TILE=11|22 forces it.
+inline int bgemm_tile(int M, int N, int R) {
+  const char* e = getenv("FLR_BGEMM_TILE");
+  const int forced = e ? atoi(e) : 0;
+  if (forced == 11 || forced == 22) return forced;
+  return (M >= 128 && N >= 128 && (R >= 256 || (int64_t)M * N >= 128 * 512)) ? 22 : 11;
+}
 template <int AM, int BMD>
 int bgemm_run(const convt::BGemmArgs& args, void* ws, size_t ws_bytes, hipStream_t st) {
   convt::BGemm<AM, BMD> pl;
   static_cast<convt::BGemmArgs&>(pl) = args;
+  if (bgemm_tile(args.m, args.n, args.r) == 22)
+    return convt::launch_tiles<convt::BGemm<AM, BMD>, 2, 2>(pl, ws, ws_bytes, st, "batched gemm");
   return convt::launch_tiles<convt::BGemm<AM, BMD>, 1, 1>(pl, ws, ws_bytes, st, "batched gemm");
 }
 template <int AM>
@@ -1198,7 +1253,9 @@ int bgemm_b(int bm, const convt::BGemmArgs& args, void* ws, size_t wsb, hipStrea
 
 extern "C" size_t flr_bgemm_workspace(int64_t batch, int64_t M, int64_t N, int64_t R) {
   if (batch < 1 || M < 1 || N < 1 || R < 0 || M > INT32_MAX || N > INT32_MAX || R > INT32_MAX) return 0;
-  const int S = convt::choose_splits((int)M, (int)N, (int)R, (int)batch, 1, convt::bgemm_min_kt());
+  // the larger of the two tile shapes' split counts (sub-tile count 1 or 4)
+  const int S = std::max(convt::choose_splits((int)M, (int)N, (int)R, (int)batch, 1, convt::bgemm_min_kt()),
+                         convt::choose_splits((int)M, (int)N, (int)R, (int)batch, 4, convt::bgemm_min_kt()));
   return S > 1 ? (size_t)S * batch * M * N * sizeof(float) : 0;
 }
 
@@ -1242,10 +1299,75 @@ extern "C" int flr_bgemm_ex(const float* A, int64_t a_k, int64_t a_m, int64_t a_
   }
 }
 
+namespace flr {
+namespace convt {
+// Long reductions (the encoders' bias gradients sum M = 2080 rows) are cut
+// into fixed 256-row chunks: stage 1 sums each chunk with the 8-accumulator
+// kernel into a partial row, stage 2 adds the partials in chunk order.  The
+// chunking depends on M alone, so a client's sum never depends on the launch.
+constexpr int SR_CHUNK = 256;
+constexpr int SR_MAXCHUNK = 64;
+
+__global__ void sum_rows_chunks_kernel(const float* __restrict__ x, int64_t x_k, int64_t x_m, int M, int N,
+                                       float* __restrict__ part, int nch) {
+  const int k = blockIdx.z, c = blockIdx.y;
+  const int nn = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nn >= N) return;
+  const int m0 = c * SR_CHUNK, m1 = min(M, m0 + SR_CHUNK);
+  const float* p = x + k * x_k + (int64_t)m0 * x_m + nn;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int mm = 0;
+  const int R = m1 - m0;
+  for (; mm + 8 <= R; mm += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += p[(int64_t)(mm + j) * x_m];
+  }
+  for (int j = 0; mm < R; ++mm, ++j) a[j] += p[(int64_t)mm * x_m];
+  part[((int64_t)k * nch + c) * N + nn] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+__global__ void sum_rows_finish_kernel(const float* __restrict__ part, int nch, int N, float* __restrict__ out,
+                                       int64_t out_k) {
+  const int k = blockIdx.y;
+  const int nn = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nn >= N) return;
+  const float* p = part + (int64_t)k * nch * N + nn;
+  float s = p[0];
+  for (int c = 1; c < nch; ++c) s += p[(int64_t)c * N];
+  out[k * out_k + nn] = s;
+}
+}  // namespace convt
+}  // namespace flr
+
+extern "C" size_t flr_sum_rows_workspace(int64_t batch, int64_t M, int64_t N) {
+  if (batch < 1 || M <= convt::SR_CHUNK || N < 1) return 0;
+  const int64_t nch = std::min<int64_t>((M + convt::SR_CHUNK - 1) / convt::SR_CHUNK, convt::SR_MAXCHUNK);
+  return align_up((size_t)batch * nch * N * sizeof(float), 256);
+}
+
 extern "C" int flr_sum_rows(const float* X, int64_t x_k, int64_t x_m, int64_t batch, int64_t M, int64_t N, float* out,
                             int64_t out_k, void* stream) {
+  return flr_sum_rows_ex(X, x_k, x_m, batch, M, N, out, out_k, nullptr, 0, stream);
+}
+
+extern "C" int flr_sum_rows_ex(const float* X, int64_t x_k, int64_t x_m, int64_t batch, int64_t M, int64_t N,
+                               float* out, int64_t out_k, void* workspace, size_t workspace_bytes, void* stream) {
   if (!X || !out || batch < 1 || batch > 65535 || M < 0 || N < 1) return FLR_ERR_ARG;
-  hipLaunchKernelGGL(convt::sum_rows_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)batch), dim3(256), 0,
-                     as_stream(stream), X, x_k, x_m, (int)M, (int)N, out, out_k);
-  return launch_status("sum_rows");
+  const size_t need = flr_sum_rows_workspace(batch, M, N);
+  if (need == 0 || !workspace || workspace_bytes < need ||
+      (M + convt::SR_CHUNK - 1) / convt::SR_CHUNK > convt::SR_MAXCHUNK) {
+    hipLaunchKernelGGL(convt::sum_rows_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)batch), dim3(256), 0,
+                       as_stream(stream), X, x_k, x_m, (int)M, (int)N, out, out_k);
+    return launch_status("sum_rows");
+  }
+  const int nch = (int)((M + convt::SR_CHUNK - 1) / convt::SR_CHUNK);
+  float* part = static_cast<float*>(workspace);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(convt::sum_rows_chunks_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)nch, (unsigned)batch),
+                     dim3(256), 0, st, X, x_k, x_m, (int)M, (int)N, part, nch);
+  int rc = launch_status("sum_rows_chunks");
+  if (rc != FLR_OK) return rc;
+  hipLaunchKernelGGL(convt::sum_rows_finish_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)batch), dim3(256), 0,
+                     st, part, nch, (int)N, out, out_k);
+  return launch_status("sum_rows_finish");
 }

@@ -339,37 +339,67 @@ __global__ void ln_reduce_kernel(const float* __restrict__ part, int nchunk, int
 // in-projection's output).  ctx rows [rows][D] (heads concatenated),
 // lse [(kb * H + h) * T + i].
 //   S = Q K^T / 8,  P = softmax_row(S),  O = P V
-// Thread (ti, tj) = (tid / 16, tid % 16) owns S rows ti + 16a, columns
-// tj + 16c; LDS rows are padded to 65 floats (conflict-free column walks).
+// LDS regions of T4 = roundup(T, 4) rows x LDR floats (LDR >= max(64, T4),
+// LDR / 4 odd: 16-B rows, conflict-free ds_read_b128 for 16 distinct rows);
+// rows T..T4-1 hold zeros, so the 4-deep inner loops need no bounds.
+// Thread (ti, tj) = (tid / 16, tid % 16): score rows ti + 16a, columns
+// tj + 16c (a, c < NT); output rows ti + 16a, columns 4 tj .. 4 tj + 3.
+// Rows >= T are clamped to T - 1 on read and never written.
 // ---------------------------------------------------------------------------
 constexpr int DH = 64;
-constexpr int LDH = DH + 1;
 constexpr int ATT_MAXT = 96;
 
+__host__ __device__ inline int att_t4(int T) { return (T + 3) & ~3; }
+// row stride 4m with m odd: 16 lanes reading 16 distinct rows with ds_read_b128
+// hit 16 distinct 4-bank groups of the 64 banks (conflict-free)
+__host__ __device__ inline int att_ldr(int T) {
+  const int x = att_t4(T) > DH ? att_t4(T) : DH;
+  return ((x / 4) & 1) ? x : x + 4;
+}
+
+// s[a][c] = sum_d A[ra][d] * B[rc][d] over d < 64 (16-B LDS reads)
 template <int NT>
-__device__ __forceinline__ void att_scores(const float* A, const float* Bm, int T, int ti, int tj,
-                                           float (&s)[NT][NT]) {
-  // s[a][c] = sum_d A[ti + 16a][d] * Bm[tj + 16c][d]
+__device__ __forceinline__ void att_dot(const float* A, const float* Bm, int ldr, const int (&ra)[NT],
+                                        const int (&rc)[NT], float (&s)[NT][NT]) {
 #pragma unroll
   for (int a = 0; a < NT; ++a)
 #pragma unroll
     for (int c = 0; c < NT; ++c) s[a][c] = 0.f;
-  for (int d = 0; d < DH; ++d) {
-    float av[NT], bv[NT];
+#pragma unroll 2
+  for (int d = 0; d < DH; d += 4) {
+    f32x4 av[NT], bv[NT];
 #pragma unroll
-    for (int a = 0; a < NT; ++a) {
-      const int i = ti + 16 * a;
-      av[a] = i < T ? A[i * LDH + d] : 0.f;
-    }
+    for (int a = 0; a < NT; ++a) av[a] = *reinterpret_cast<const f32x4*>(A + ra[a] * ldr + d);
 #pragma unroll
-    for (int c = 0; c < NT; ++c) {
-      const int j = tj + 16 * c;
-      bv[c] = j < T ? Bm[j * LDH + d] : 0.f;
-    }
+    for (int c = 0; c < NT; ++c) bv[c] = *reinterpret_cast<const f32x4*>(Bm + rc[c] * ldr + d);
 #pragma unroll
     for (int a = 0; a < NT; ++a)
 #pragma unroll
-      for (int c = 0; c < NT; ++c) s[a][c] = __builtin_fmaf(av[a], bv[c], s[a][c]);
+      for (int c = 0; c < NT; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[a][c] = __builtin_fmaf(av[a][e], bv[c][e], s[a][c]);
+  }
+}
+
+// o[a][0..3] = sum_j L[ra][j] * R[j][4 tj .. 4 tj + 3] over j < T4 (L's columns
+// j >= T and R's rows j >= T are zero)
+template <int NT>
+__device__ __forceinline__ void att_mat(const float* L, const float* R, int ldr, int T4, const int (&ra)[NT], int tj,
+                                        f32x4 (&o)[NT]) {
+#pragma unroll
+  for (int a = 0; a < NT; ++a) o[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < T4; j += 4) {
+    f32x4 lv[NT], rv[4];
+#pragma unroll
+    for (int a = 0; a < NT; ++a) lv[a] = *reinterpret_cast<const f32x4*>(L + ra[a] * ldr + j);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rv[q] = *reinterpret_cast<const f32x4*>(R + (j + q) * ldr + 4 * tj);
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[a][e] = __builtin_fmaf(lv[a][q], rv[q][e], o[a][e]);
   }
 }
 
@@ -384,36 +414,69 @@ __device__ __forceinline__ float group16_sum(float v) {
   return v;
 }
 
-// rows [T][64] of one head from rows of stride ld at column col into LDS [T][65]
-__device__ __forceinline__ void att_load(float* dst, const float* src, int64_t ld, int T) {
-  for (int e = threadIdx.x; e < T * 16; e += 256) {
-    const int i = e / 16, q = e % 16;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(src + i * ld + 4 * q);
+// NS heads' [T][64] row blocks (row stride ld[s], column offset folded into
+// src[s]) into LDS regions [T4][ldr]; rows T..T4-1 zeroed.  Every global load
+// is issued before the first LDS store: at two workgroups per CU nothing else
+// hides a serial chain of HBM latencies.
+constexpr int ATT_LOAD_IT = (((ATT_MAXT + 3) & ~3) * 16 + 255) / 256;
+template <int NS>
+__device__ __forceinline__ void att_load(float* const (&dst)[NS], const float* const (&src)[NS],
+                                         const int64_t (&ld)[NS], int T, int ldr) {
+  const int T4 = att_t4(T);
+  f32x4 v[NS][ATT_LOAD_IT];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) dst[i * LDH + 4 * q + u] = v[u];
+  for (int it = 0; it < ATT_LOAD_IT; ++it) {
+    const int e = threadIdx.x + 256 * it;
+    const int i = e >> 4, q = e & 15;
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      v[k][it] = i < T ? *reinterpret_cast<const f32x4*>(src[k] + i * ld[k] + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+#pragma unroll
+  for (int it = 0; it < ATT_LOAD_IT; ++it) {
+    const int e = threadIdx.x + 256 * it;
+    const int i = e >> 4, q = e & 15;
+    if (e < T4 * 16) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) *reinterpret_cast<f32x4*>(dst[k] + i * ldr + 4 * q) = v[k][it];
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void att_rows(int T, int t, int (&r)[NT]) {
+#pragma unroll
+  for (int a = 0; a < NT; ++a) r[a] = min(t + 16 * a, T - 1);
 }
 
 template <int NT>
 __global__ __launch_bounds__(256) void att_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
                                                       float* __restrict__ lse, int T, int H) {
-  extern __shared__ float sm[];
-  float* Qs = sm;
-  float* Ks = Qs + T * LDH;
-  float* Vs = Ks + T * LDH;
-  float* Ps = Vs + T * LDH;  // [T][T + 1]
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int ldr = att_ldr(T), T4 = att_t4(T);
+  const int region = T4 * ldr;
+  float* Qs = sm;  // later: P [T4][ldr]
+  float* Ks = Qs + region;
+  float* Vs = Ks + region;
   const int h = blockIdx.x, kb = blockIdx.y;
   const int D = H * DH;
   const int64_t row0 = (int64_t)kb * T;
   const float* base = qkv + row0 * 3 * D + h * DH;
-  att_load(Qs, base, 3 * D, T);
-  att_load(Ks, base + D, 3 * D, T);
-  att_load(Vs, base + 2 * D, 3 * D, T);
+  {
+    float* const dst[3] = {Qs, Ks, Vs};
+    const float* const src[3] = {base, base + D, base + 2 * D};
+    const int64_t ld[3] = {3 * D, 3 * D, 3 * D};
+    att_load<3>(dst, src, ld, T, ldr);
+  }
   __syncthreads();
   const int tid = threadIdx.x, ti = tid >> 4, tj = tid & 15;
+  int ra[NT], rc[NT];
+  att_rows<NT>(T, ti, ra);
+  att_rows<NT>(T, tj, rc);
   float s[NT][NT];
-  att_scores<NT>(Qs, Ks, T, ti, tj, s);
-  const int LP = T + 1;
+  att_dot<NT>(Qs, Ks, ldr, ra, rc, s);
+  __syncthreads();  // Q is dead: its region takes P
+  float* Ps = Qs;
 #pragma unroll
   for (int a = 0; a < NT; ++a) {
     const int i = ti + 16 * a;
@@ -437,169 +500,133 @@ __global__ __launch_bounds__(256) void att_fwd_kernel(const float* __restrict__ 
 #pragma unroll
       for (int c = 0; c < NT; ++c) {
         const int j = tj + 16 * c;
-        if (j < T) Ps[i * LP + j] = s[a][c] * inv;
+        if (j < T4) Ps[i * ldr + j] = s[a][c] * inv;  // columns T..T4-1: 0
       }
       if (tj == 0) lse[((int64_t)kb * H + h) * T + i] = m + logf(sum);
     }
   }
   __syncthreads();
-  // O[i][d] for rows ti + 16a, columns d = tj + 16u
-  float o[NT][4];
-#pragma unroll
-  for (int a = 0; a < NT; ++a)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) o[a][u] = 0.f;
-  for (int j = 0; j < T; ++j) {
-    float vv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) vv[u] = Vs[j * LDH + tj + 16 * u];
-#pragma unroll
-    for (int a = 0; a < NT; ++a) {
-      const int i = ti + 16 * a;
-      const float p = i < T ? Ps[i * LP + j] : 0.f;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) o[a][u] = __builtin_fmaf(p, vv[u], o[a][u]);
-    }
-  }
+  f32x4 o[NT];
+  att_mat<NT>(Ps, Vs, ldr, T4, ra, tj, o);
 #pragma unroll
   for (int a = 0; a < NT; ++a) {
     const int i = ti + 16 * a;
-    if (i < T) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) ctx[(row0 + i) * D + h * DH + tj + 16 * u] = o[a][u];
-    }
+    if (i < T) *reinterpret_cast<f32x4*>(ctx + (row0 + i) * D + h * DH + 4 * tj) = o[a];
   }
 }
 
 // backward: P = exp(S / 8 - lse); dV = P^T dO; dP = dO V^T;
 // Drow_i = sum_d dO[i][d] O[i][d]; dS = P (dP - Drow) / 8;
 // dQ = dS K; dK = dS^T Q.  dqkv rows [rows][3D] (overwritten).
+// Four LDS regions: Q, K, V (-> P^T -> dS), dO (-> dS^T).
 template <int NT>
 __global__ __launch_bounds__(256) void att_bwd_kernel(const float* __restrict__ qkv, const float* __restrict__ ctx,
                                                       const float* __restrict__ dctx, const float* __restrict__ lse,
                                                       float* __restrict__ dqkv, int T, int H) {
-  extern __shared__ float sm[];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int ldr = att_ldr(T), T4 = att_t4(T);
+  const int region = T4 * ldr;
   float* Qs = sm;
-  float* Ks = Qs + T * LDH;
-  float* Vs = Ks + T * LDH;
-  float* dOs = Vs + T * LDH;
-  float* Ps = dOs + T * LDH;  // [T][T + 1]: P, then dS
+  float* Ks = Qs + region;
+  float* Vs = Ks + region;
+  float* dOs = Vs + region;
   const int h = blockIdx.x, kb = blockIdx.y;
   const int D = H * DH;
   const int64_t row0 = (int64_t)kb * T;
   const float* base = qkv + row0 * 3 * D + h * DH;
-  att_load(Qs, base, 3 * D, T);
-  att_load(Ks, base + D, 3 * D, T);
-  att_load(Vs, base + 2 * D, 3 * D, T);
-  att_load(dOs, dctx + row0 * D + h * DH, D, T);
   const int tid = threadIdx.x, ti = tid >> 4, tj = tid & 15;
-  const int LP = T + 1;
-  // Drow for rows ti + 16a (this thread's S rows): 16 lanes split the 64 columns
+  int ra[NT], rc[NT];
+  att_rows<NT>(T, ti, ra);
+  att_rows<NT>(T, tj, rc);
+  // Drow for rows ti + 16a (16 lanes split the 64 columns, 4 each) and the
+  // rows' lse: loads issued ahead of the LDS fill
+  f32x4 gv[NT], ov[NT];
+  float lrow[NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+    const int64_t off = (row0 + ra[a]) * D + h * DH + 4 * tj;
+    gv[a] = *reinterpret_cast<const f32x4*>(dctx + off);
+    ov[a] = *reinterpret_cast<const f32x4*>(ctx + off);
+    lrow[a] = lse[((int64_t)kb * H + h) * T + ra[a]];
+  }
+  {
+    float* const dst[4] = {Qs, Ks, Vs, dOs};
+    const float* const src[4] = {base, base + D, base + 2 * D, dctx + row0 * D + h * DH};
+    const int64_t ld[4] = {3 * D, 3 * D, 3 * D, D};
+    att_load<4>(dst, src, ld, T, ldr);
+  }
   float drow[NT];
 #pragma unroll
   for (int a = 0; a < NT; ++a) {
-    const int i = ti + 16 * a;
     float acc = 0.f;
-    if (i < T) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t off = (row0 + i) * D + h * DH + tj + 16 * u;
-        acc = __builtin_fmaf(dctx[off], ctx[off], acc);
-      }
-    }
+    for (int e = 0; e < 4; ++e) acc = __builtin_fmaf(gv[a][e], ov[a][e], acc);
     drow[a] = group16_sum(acc);
   }
   __syncthreads();
   float p[NT][NT], dp[NT][NT];
-  att_scores<NT>(Qs, Ks, T, ti, tj, p);
-  att_scores<NT>(dOs, Vs, T, ti, tj, dp);
+  att_dot<NT>(Qs, Ks, ldr, ra, rc, p);
+  att_dot<NT>(dOs, Vs, ldr, ra, rc, dp);
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int c = 0; c < NT; ++c) p[a][c] = tj + 16 * c < T ? expf(p[a][c] * 0.125f - lrow[a]) : 0.f;
+  __syncthreads();  // V is dead: its region takes P^T
+  float* Pt = Vs;
+  for (int e = tid; e < T4 * ldr; e += 256) Pt[e] = 0.f;
+  __syncthreads();
 #pragma unroll
   for (int a = 0; a < NT; ++a) {
     const int i = ti + 16 * a;
-    const float l = i < T ? lse[((int64_t)kb * H + h) * T + i] : 0.f;
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
       const int j = tj + 16 * c;
-      p[a][c] = (i < T && j < T) ? expf(p[a][c] * 0.125f - l) : 0.f;
-      if (i < T && j < T) Ps[i * LP + j] = p[a][c];
+      if (i < T && j < T) Pt[j * ldr + i] = p[a][c];
     }
   }
   __syncthreads();
   float* dq = dqkv + row0 * 3 * D + h * DH;
-  // dV[j][d] = sum_i P[i][j] dO[i][d]; thread owns rows j = ti + 16a, d = tj + 16u
-  {
-    float acc[NT][4];
-#pragma unroll
-    for (int a = 0; a < NT; ++a)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[a][u] = 0.f;
-    for (int i = 0; i < T; ++i) {
-      float ov[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) ov[u] = dOs[i * LDH + tj + 16 * u];
-#pragma unroll
-      for (int a = 0; a < NT; ++a) {
-        const int j = ti + 16 * a;
-        const float pv = j < T ? Ps[i * LP + j] : 0.f;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc[a][u] = __builtin_fmaf(pv, ov[u], acc[a][u]);
-      }
-    }
+  {  // dV[j][4tj..] = sum_i P^T[j][i] dO[i][4tj..]
+    f32x4 o[NT];
+    att_mat<NT>(Pt, dOs, ldr, T4, ra, tj, o);
 #pragma unroll
     for (int a = 0; a < NT; ++a) {
       const int j = ti + 16 * a;
-      if (j < T) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) dq[(int64_t)j * 3 * D + 2 * D + tj + 16 * u] = acc[a][u];
-      }
+      if (j < T) *reinterpret_cast<f32x4*>(dq + (int64_t)j * 3 * D + 2 * D + 4 * tj) = o[a];
     }
   }
-  __syncthreads();  // everyone done reading P
+  __syncthreads();  // P^T and dO are dead: dS into V's region, dS^T into dO's
+  float* dS = Vs;
+  float* dSt = dOs;
+  for (int e = tid; e < T4 * ldr; e += 256) {
+    dS[e] = 0.f;
+    dSt[e] = 0.f;
+  }
+  __syncthreads();
 #pragma unroll
   for (int a = 0; a < NT; ++a) {
     const int i = ti + 16 * a;
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
       const int j = tj + 16 * c;
-      if (i < T && j < T) Ps[i * LP + j] = p[a][c] * (dp[a][c] - drow[a]) * 0.125f;
+      if (i < T && j < T) {
+        const float v = p[a][c] * (dp[a][c] - drow[a]) * 0.125f;
+        dS[i * ldr + j] = v;
+        dSt[j * ldr + i] = v;
+      }
     }
   }
   __syncthreads();
-  // dQ[i][d] = sum_j dS[i][j] K[j][d]; dK[j][d] = sum_i dS[i][j] Q[i][d]
   {
-    float aq[NT][4], ak[NT][4];
-#pragma unroll
-    for (int a = 0; a < NT; ++a)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) aq[a][u] = ak[a][u] = 0.f;
-    for (int j = 0; j < T; ++j) {
-      float kv[4], qv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        kv[u] = Ks[j * LDH + tj + 16 * u];
-        qv[u] = Qs[j * LDH + tj + 16 * u];
-      }
-#pragma unroll
-      for (int a = 0; a < NT; ++a) {
-        const int r = ti + 16 * a;
-        const float sq = r < T ? Ps[r * LP + j] : 0.f;  // dS[r][j]
-        const float sk = r < T ? Ps[j * LP + r] : 0.f;  // dS[j][r]
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          aq[a][u] = __builtin_fmaf(sq, kv[u], aq[a][u]);
-          ak[a][u] = __builtin_fmaf(sk, qv[u], ak[a][u]);
-        }
-      }
-    }
+    f32x4 oq[NT], ok[NT];
+    att_mat<NT>(dS, Ks, ldr, T4, ra, tj, oq);   // dQ[i] = sum_j dS[i][j] K[j]
+    att_mat<NT>(dSt, Qs, ldr, T4, ra, tj, ok);  // dK[j] = sum_i dS^T[j][i] Q[i]
 #pragma unroll
     for (int a = 0; a < NT; ++a) {
       const int r = ti + 16 * a;
       if (r < T) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          dq[(int64_t)r * 3 * D + tj + 16 * u] = aq[a][u];
-          dq[(int64_t)r * 3 * D + D + tj + 16 * u] = ak[a][u];
-        }
+        *reinterpret_cast<f32x4*>(dq + (int64_t)r * 3 * D + 4 * tj) = oq[a];
+        *reinterpret_cast<f32x4*>(dq + (int64_t)r * 3 * D + D + 4 * tj) = ok[a];
       }
     }
   }
@@ -626,8 +653,8 @@ __global__ void act_bwd_kernel(const float* __restrict__ dy, const float* __rest
   }
 }
 
-inline size_t att_fwd_lds(int T) { return (size_t)(3 * T * LDH + T * (T + 1)) * sizeof(float); }
-inline size_t att_bwd_lds(int T) { return (size_t)(4 * T * LDH + T * (T + 1)) * sizeof(float); }
+inline size_t att_fwd_lds(int T) { return (size_t)3 * att_t4(T) * att_ldr(T) * sizeof(float); }
+inline size_t att_bwd_lds(int T) { return (size_t)4 * att_t4(T) * att_ldr(T) * sizeof(float); }
 
 }  // namespace xf
 }  // namespace flr

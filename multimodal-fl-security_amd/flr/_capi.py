@@ -52,6 +52,8 @@ SIGNATURES = {
     "flr_fedavg": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),
     "flr_trimmed_mean": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p]),
     "flr_median_lower": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p]),
+    "flr_trimmed_mean_rows": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _i64, _c_void_p, _c_void_p]),
+    "flr_median_lower_rows": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p, _c_void_p]),
     "flr_clip_sgd_workspace": (_size_t, [_i64]),
     "flr_clip_sgd_step": (_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64, ctypes.c_float, ctypes.c_float,
                                  ctypes.c_float, ctypes.c_float, _int, _c_void_p, _c_void_p, _size_t, _c_void_p]),
@@ -108,6 +110,9 @@ SIGNATURES = {
     "flr_attention_bwd": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64, _i64, _c_void_p,
                                  _c_void_p]),
     "flr_sum_rows": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p]),
+    "flr_sum_rows_workspace": (_size_t, [_i64, _i64, _i64]),
+    "flr_sum_rows_ex": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p, _size_t,
+                               _c_void_p]),
     "flr_maxpool2d_fwd": (_int, [_c_void_p] * 3 + [_i64] * 7 + [_c_void_p]),
     "flr_maxpool2d_bwd": (_int, [_c_void_p] * 3 + [_i64] * 7 + [_c_void_p]),
     "flr_gru_fwd_step": (_int, [_c_void_p] * 4 + [_i64] * 5 + [_c_void_p]),

@@ -4,14 +4,14 @@ Every name of the reference factory is registered and runs on the HIP kernels
 (FLTrust's server update runs on the client-batched trainer).
 """
 from .base_defense import BaseDefense, NoDefense
-from .krum import KrumDefense, MultiKrumDefense
+from .krum import KrumDefense, KrumTrimmedMeanDefense, MultiKrumDefense
 from .fltrust import FLTrustDefense
 from .geometric_median import GeometricMedianDefense
 from .norm_based import DPSGDDefense, GradientClippingDefense, NormBoundingDefense
 from .trimmed_mean import MedianDefense, TrimmedMeanDefense
 
 __all__ = [
-    "BaseDefense", "NoDefense", "KrumDefense", "MultiKrumDefense",
+    "BaseDefense", "NoDefense", "KrumDefense", "MultiKrumDefense", "KrumTrimmedMeanDefense",
     "TrimmedMeanDefense", "MedianDefense", "GeometricMedianDefense",
     "GradientClippingDefense", "NormBoundingDefense", "DPSGDDefense", "FLTrustDefense", "get_defense",
 ]
@@ -28,6 +28,8 @@ _DEFENSES = {
     "gradient_clipping": GradientClippingDefense,
     "norm_bounding": NormBoundingDefense,
     "fltrust": FLTrustDefense,
+    # build extension: Multi-Krum selection then trimmed mean (BASELINE.json configs[4])
+    "krum_trimmed_mean": KrumTrimmedMeanDefense,
 }
 
 

@@ -114,3 +114,55 @@ class MultiKrumDefense(KrumDefense):
         if "multi_k" not in defense_config:
             defense_config["multi_k"] = defense_config.get("default_k", 3)
         super().__init__(defense_config)
+
+
+class KrumTrimmedMeanDefense(KrumDefense):
+    """"Krum + trimmed-mean" (BASELINE.json configs[4]): the Multi-Krum
+    selection (krum.py:149-176, multi_k rows by score) followed by the
+    coordinate-wise trimmed mean of the selected rows (trimmed_mean.py:63-90:
+    t = max(1, int(m * trim_ratio)), the median if m - 2t < 1) — the Bulyan
+    composition of the reference's two defenses.  The reference has no such
+    class; its two halves are the reference's own rules, each restated by the
+    oracle.  One extra pass over the selected rows (flr_trimmed_mean_rows),
+    no gather copy of the selection."""
+
+    def __init__(self, defense_config: Dict[str, Any]):
+        super().__init__(defense_config)
+        self.trim_ratio = defense_config.get("trim_ratio", 0.1)
+        self.num_trimmed_per_end = 0
+
+    def _combine(self, X: torch.Tensor, order: torch.Tensor) -> torch.Tensor:
+        m = min(self.multi_k, X.shape[0])
+        t = max(1, int(m * self.trim_ratio))
+        self.num_trimmed_per_end = t
+        sel = order[:m]
+        if m - 2 * t < 1:
+            return ops.median_lower(X, rows=sel)
+        return ops.trimmed_mean(X, t, rows=sel)
+
+    def aggregate_flat(self, cm: ClientMatrix, num_examples: List[int], publish: bool = True) -> torch.Tensor:
+        order = self.select(cm)
+        if publish:
+            self.publish()
+        return self._combine(cm.X, order)
+
+    def aggregate_sharded(self, cs, num_examples: List[int], publish: bool = True, events=None) -> torch.Tensor:
+        n, f = cs.K, self.num_malicious
+        if n < 2 * f + 3:  # krum.py:153-157
+            raise ValueError(
+                f"Krum requires n >= 2f + 3. Got n={n}, f={f}. Need at least {2 * f + 3} clients.")
+        self.distances = ops.pairwise_l2_sharded(cs, events=events)
+        self.scores_device, self.order_device = ops.krum_select(self.distances, f)
+        if publish:
+            self.publish()
+        return self._combine(cs.X, self.order_device)
+
+    def aggregate(self, client_updates: Updates, num_examples: List[int]) -> List[torch.Tensor]:
+        cm = as_matrix(client_updates)
+        return cm.unflatten(self.aggregate_flat(cm, num_examples), source_device(client_updates))
+
+    def get_metrics(self) -> Dict[str, Any]:
+        m = super().get_metrics()
+        m.update({"defense_type": "krum_trimmed_mean", "trim_ratio": self.trim_ratio,
+                  "num_trimmed_per_end": self.num_trimmed_per_end})
+        return m

@@ -159,7 +159,10 @@ def sum_rows(X: torch.Tensor) -> torch.Tensor:
     if X.stride(2) != 1:
         X = X.contiguous()
     out = torch.empty(K, N, dtype=X.dtype, device=X.device)
-    _capi.call("flr_sum_rows", X.data_ptr(), X.stride(0), X.stride(1), K, M, N, out.data_ptr(), N, _stream(X))
+    n = int(_capi.lib().flr_sum_rows_workspace(K, M, N))
+    ws = torch.empty(n, dtype=torch.uint8, device=X.device) if n else None
+    _capi.call("flr_sum_rows_ex", X.data_ptr(), X.stride(0), X.stride(1), K, M, N, out.data_ptr(), N,
+               None if ws is None else ws.data_ptr(), n, _stream(X))
     return out
 
 

@@ -96,21 +96,38 @@ def fedavg(X: torch.Tensor, num_examples, out: Optional[torch.Tensor] = None) ->
     return out
 
 
-def trimmed_mean(X: torch.Tensor, t: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Coordinate-wise mean of sorted ranks [t, K-t) (trimmed_mean.py:74-88)."""
+def _rows_arg(rows, device):
+    return rows.to(device=device, dtype=torch.int32).contiguous()
+
+
+def trimmed_mean(X: torch.Tensor, t: int, out: Optional[torch.Tensor] = None,
+                 rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Coordinate-wise mean of sorted ranks [t, m-t) (trimmed_mean.py:74-88)
+    over all K rows, or over the row subset `rows` (m = len(rows))."""
     K, P, ldx = _check_matrix(X)
     if out is None:
         out = torch.empty(P, dtype=torch.float32, device=X.device)
-    _capi.call("flr_trimmed_mean", X.data_ptr(), K, P, ldx, int(t), out.data_ptr(), _stream(X))
+    if rows is None:
+        _capi.call("flr_trimmed_mean", X.data_ptr(), K, P, ldx, int(t), out.data_ptr(), _stream(X))
+    else:
+        r = _rows_arg(rows, X.device)
+        _capi.call("flr_trimmed_mean_rows", X.data_ptr(), K, P, ldx, r.data_ptr(), r.numel(), int(t), out.data_ptr(),
+                   _stream(X))
     return out
 
 
-def median_lower(X: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Coordinate-wise lower median (trimmed_mean.py:101, 163)."""
+def median_lower(X: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Coordinate-wise lower median (trimmed_mean.py:101, 163), optionally of a row subset."""
     K, P, ldx = _check_matrix(X)
     if out is None:
         out = torch.empty(P, dtype=torch.float32, device=X.device)
-    _capi.call("flr_median_lower", X.data_ptr(), K, P, ldx, out.data_ptr(), _stream(X))
+    if rows is None:
+        _capi.call("flr_median_lower", X.data_ptr(), K, P, ldx, out.data_ptr(), _stream(X))
+    else:
+        r = _rows_arg(rows, X.device)
+        _capi.call("flr_median_lower_rows", X.data_ptr(), K, P, ldx, r.data_ptr(), r.numel(), out.data_ptr(),
+                   _stream(X))
     return out
 
 

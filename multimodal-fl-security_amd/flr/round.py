@@ -68,7 +68,7 @@ class RoundEngine:
         shapes = [s for _, s in param_layout(spec)]
         self.trainer = ClientBatchTrainer(spec, self.hi - self.lo, self.device, tcfg)
         cfg = dict(rcfg.defense_cfg)
-        if rcfg.defense in ("krum", "multi_krum"):  # run_experiments.py:155-162
+        if rcfg.defense in ("krum", "multi_krum", "krum_trimmed_mean"):  # run_experiments.py:155-162
             cfg.setdefault("num_malicious", rcfg.num_attackers)
             cfg.setdefault("multi_k", max(1, K // 2))
         self.defense = get_defense(rcfg.defense, cfg)

@@ -71,6 +71,10 @@ class TrainConfig:
     weight_decay: float = 0.0    # :210 (1e-4 only for cub200)
     clip: float = 1.0            # :227, :234
     local_steps: int = 5
+    # clients per forward/backward pass (0: automatic).  Activations scale with
+    # it, parameters and optimizer state do not; every kernel's per-client
+    # result is independent of it (split-K is chosen per client).
+    client_chunk: int = 0
 
 
 class ClientBatchTrainer:
@@ -149,10 +153,24 @@ class ClientBatchTrainer:
                 blocks.append((j, lo * slab, (hi - lo) * slab, n))
         self.blocks = blocks
         nb = len(blocks)
-        self._xp = (ctypes.c_void_p * nb)(*[self.W[j].data_ptr() + 4 * o for j, o, _, _ in blocks])
-        self._mp = (ctypes.c_void_p * nb)(*[self.Mb[j].data_ptr() + 4 * o for j, o, _, _ in blocks])
         self._np = (ctypes.c_int64 * nb)(*[c for _, _, c, _ in blocks])
         self._cs = (ctypes.c_int64 * nb)(*[cs for _, _, _, cs in blocks])
+        chunk = cfg.client_chunk if cfg.client_chunk > 0 else self.auto_chunk(spec, self.K)
+        self.chunks = [(c0, min(self.K, c0 + chunk)) for c0 in range(0, self.K, chunk)]
+        # per chunk: the optimizer's block pointers at the chunk's first client
+        self._xp, self._mp = [], []
+        for c0, _ in self.chunks:
+            self._xp.append((ctypes.c_void_p * nb)(*[self.W[j].data_ptr() + 4 * (o + c0 * cs)
+                                                     for j, o, _, cs in blocks]))
+            self._mp.append((ctypes.c_void_p * nb)(*[self.Mb[j].data_ptr() + 4 * (o + c0 * cs)
+                                                     for j, o, _, cs in blocks]))
+
+    @staticmethod
+    def auto_chunk(spec: ModelSpec, K: int) -> int:
+        """Clients per pass: the encoder family holds ~0.6 GB of activations per
+        client at batch 32 (ViT-S over 65 tokens x 12 blocks), so 32 clients per
+        pass; the convolutional families fit every client of a GPU at once."""
+        return min(K, 32) if spec.family == "vit_bert" else K
 
     def load_global(self, global_flat: torch.Tensor) -> None:
         """Every client starts from the global model (run_experiments.py:203)."""
@@ -180,18 +198,31 @@ class ClientBatchTrainer:
         return self.X
 
     # ---- one optimizer step for every client -----------------------------
-    def step(self, images, tokens, labels, first: bool, dropout_mask=None, last: bool = False) -> torch.Tensor:
-        leaves = [w.detach().requires_grad_(True) for w in self.W]
-        params: Dict[str, torch.Tensor] = dict(zip(self.names, leaves))
-        logits = batched_forward(params, images, tokens, self.spec, dropout_mask, self.tap_major, self.skip_dead)
-        loss_k = CrossEntropy.apply(logits, labels)
-        grads = [g.contiguous() for g in torch.autograd.grad(loss_k.sum(), leaves)]
-        gp = (ctypes.c_void_p * len(self.blocks))(*[grads[j].data_ptr() + 4 * o for j, o, _, _ in self.blocks])
+    def step(self, images, tokens, labels, first: bool, dropout_mask=None, last: bool = False,
+             loss_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One local step of every client (chunk by chunk); returns the [K] losses."""
+        if loss_out is None:
+            loss_out = torch.empty(self.K, dtype=torch.float32, device=self.device)
         c = self.cfg
-        _capi.call("flr_clip_sgd_step_blocked", self._xp, gp, self._mp, self._np, self._cs, len(self.blocks), self.K,
-                   c.lr, c.momentum, c.weight_decay, c.clip, int(first) | (int(last) << 1), self.norms.data_ptr(),
-                   self._ws.data_ptr() + self._ws_off, self._ws_bytes, _stream(self._wbuf))
-        return loss_k.detach()
+        for (c0, c1), xp, mp in zip(self.chunks, self._xp, self._mp):
+            whole = c0 == 0 and c1 == self.K
+            leaves = [(w if whole else w[c0:c1]).detach().requires_grad_(True) for w in self.W]
+            params: Dict[str, torch.Tensor] = dict(zip(self.names, leaves))
+            sl = (lambda t: t) if whole else (lambda t: None if t is None else t[c0:c1])
+            logits = batched_forward(params, sl(images), sl(tokens), self.spec, sl(dropout_mask), self.tap_major,
+                                     self.skip_dead)
+            loss_k = CrossEntropy.apply(logits, sl(labels))
+            grads = [g.contiguous() for g in torch.autograd.grad(loss_k.sum(), leaves)]
+            gp = (ctypes.c_void_p * len(self.blocks))(*[grads[j].data_ptr() + 4 * o for j, o, _, _ in self.blocks])
+            _capi.call("flr_clip_sgd_step_blocked", xp, gp, mp, self._np, self._cs, len(self.blocks), c1 - c0,
+                       c.lr, c.momentum, c.weight_decay, c.clip, int(first) | (int(last) << 1),
+                       self.norms.data_ptr() + 4 * c0, self._ws.data_ptr() + self._ws_off, self._ws_bytes,
+                       _stream(self._wbuf))
+            del grads, leaves, params, logits
+            if whole:
+                return loss_k.detach()
+            loss_out[c0:c1].copy_(loss_k.detach())
+        return loss_out
 
     def local_update(self, batches: Sequence, dropout_masks: Optional[Sequence] = None,
                      export: bool = True) -> torch.Tensor:

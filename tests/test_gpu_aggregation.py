@@ -239,3 +239,35 @@ def test_client_matrix_zero_copy_defense(cuda):
     out = d.aggregate(cm, [1] * K)
     assert out[0].shape == (P,)
     assert not set(d.selected_clients) & set(range(4))  # sign-flipped clients rejected
+
+
+@pytest.mark.parametrize("K,m", [(40, 20), (200, 100), (512, 256), (300, 7)])
+def test_order_stats_row_subset(cuda, K, m):
+    P = 2049
+    X = torch.randn(K, P, device=cuda)
+    g = torch.Generator().manual_seed(K)
+    rows = torch.randperm(K, generator=g)[:m].to(torch.int32)
+    sub = X.cpu()[rows.long()]
+    np.testing.assert_array_equal(ops.median_lower(X, rows=rows).cpu().numpy(),
+                                  torch.median(sub, dim=0)[0].numpy())
+    t = max(1, int(m * 0.1))
+    if m - 2 * t >= 1:
+        ref = torch.sort(sub, dim=0)[0][t:m - t].mean(dim=0)
+        torch.testing.assert_close(ops.trimmed_mean(X, t, rows=rows).cpu(), ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("K,P", [(40, 4099), (128, 20_011)])
+def test_krum_trimmed_mean_vs_oracle(cuda, K, P):
+    """Multi-Krum selection (krum.py:149-176) then the trimmed mean of the
+    selected updates (trimmed_mean.py:63-90), both halves on the oracle."""
+    f = int(0.2 * K)
+    mk = K // 2
+    X = update_matrix(K, P, f=f, seed=K, device=cuda)[:, :P]
+    ups = [[X[i].cpu()] for i in range(K)]
+    _, _, sel, rej, _ = orc.krum(ups, f, mk)
+    want, t = orc.trimmed_mean([ups[i] for i in sel], 0.1)
+    d = get_defense("krum_trimmed_mean", {"num_malicious": f, "multi_k": mk, "trim_ratio": 0.1})
+    got = d.aggregate(ClientMatrix(update_matrix(K, P, f=f, seed=K, device=cuda), P, [(P,)]), [1] * K)
+    assert d.selected_clients == sel and d.rejected_clients == rej
+    assert d.num_trimmed_per_end == t
+    torch.testing.assert_close(got[0].cpu(), want[0], rtol=1e-5, atol=1e-6)

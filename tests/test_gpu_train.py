@@ -219,3 +219,24 @@ def test_vit_bert_full_model_matches_reference_loop(cuda):
         got = tr.X.data[k, : tr.P].cpu()
         assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
         assert _rel(got, ref) < 1e-5, _rel(got, ref)
+
+
+@pytest.mark.parametrize("spec_name", ["wide", "vit_tiny"])
+def test_client_chunking_bit_identical(cuda, spec_name):
+    """Training the clients in chunks (TrainConfig.client_chunk) gives the
+    same bits as one pass: every kernel's per-client result is independent of
+    how many clients share its launch."""
+    from flr.models.multimodal import VIT_BERT_TINY
+    spec = SPEC_WIDE if spec_name == "wide" else VIT_BERT_TINY
+    K, B, steps = 5, 4, 2
+    glob = initial_global(spec, 42, cuda)
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    out = []
+    for chunk in (0 if spec_name == "wide" else K, 2):
+        tr = ClientBatchTrainer(spec, K, cuda, TrainConfig(local_steps=steps, client_chunk=chunk))
+        assert len(tr.chunks) == (1 if chunk in (0, K) else 3)
+        tr.load_global(glob)
+        loss = tr.local_update(batches)
+        out.append((loss.cpu(), tr.X.data[:, : tr.P].cpu()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
