@@ -239,6 +239,9 @@ int flr_conv2d_bwd_weight_reuse(const float* x, const float* dy, float* dw, int6
 int flr_cross_entropy(const float* logits, const int64_t* labels, int64_t K,
                       int64_t B, int64_t C, float* loss, float* dlogits,
                       float* loss_rows, void* stream);
+/* out[c] = (sum_r X[r][c]) / R, the sum sequential in fp64: each client's
+ * reported training loss, the mean of its per-step losses (fl_client.py:143-149). */
+int flr_mean_rows(const float* X, int64_t R, int64_t C, float* out, void* stream);
 /* d[k, b, c] *= gk[k]  (chain rule for a per-client upstream gradient). */
 int flr_scale_client_rows(float* d, const float* gk, int64_t K, int64_t B,
                           int64_t C, void* stream);
@@ -284,6 +287,13 @@ int flr_copy_rows(const float* src, int64_t src_stride, int64_t n, float* dst,
                   int64_t dst_stride, int64_t K, void* stream);
 int flr_tap_major_to_torch(const float* w_t, int64_t K, int64_t KK, int64_t Cin,
                            int64_t Cout, float* dst, int64_t dst_stride, void* stream);
+/* The same two exports with rows k < nneg written negated: the sign-flip
+ * attackers' submitted update (model_poisoning.py:274-276, applied after
+ * training as malicious_client.py:103-115) folded into the export pass. */
+int flr_copy_rows_neg(const float* src, int64_t src_stride, int64_t n, float* dst, int64_t dst_stride, int64_t K,
+                      int64_t nneg, void* stream);
+int flr_tap_major_to_torch_neg(const float* w_t, int64_t K, int64_t KK, int64_t Cin, int64_t Cout, float* dst,
+                               int64_t dst_stride, int64_t nneg, void* stream);
 
 /* ---- §8(f): per-client norms and weighted row combinations ---------------
  * Building blocks of GradientClippingDefense / NormBoundingDefense /

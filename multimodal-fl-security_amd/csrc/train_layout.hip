@@ -10,6 +10,8 @@
 // goes through a [taps][16][64] LDS tile so both sides are coalesced.
 #include "flr_common.h"
 
+#include <algorithm>
+
 namespace flr {
 namespace layout {
 
@@ -33,19 +35,23 @@ __global__ __launch_bounds__(THREADS) void broadcast_kernel(const float* __restr
 }
 
 // dst[k * dstride + i] = src[k * sstride + i]
+// rows k < nneg are written negated (the sign-flip attackers' submission,
+// model_poisoning.py:274-276, folded into the export pass)
 template <bool VEC>
 __global__ __launch_bounds__(THREADS) void copy_rows_kernel(const float* __restrict__ src, int64_t sstride,
-                                                            int64_t n, float* __restrict__ dst, int64_t dstride) {
+                                                            int64_t n, float* __restrict__ dst, int64_t dstride,
+                                                            int nneg) {
   const float* s = src + (int64_t)blockIdx.y * sstride;
   float* d = dst + (int64_t)blockIdx.y * dstride;
+  const float sg = (int)blockIdx.y < nneg ? -1.f : 1.f;
   if constexpr (VEC) {
     const int64_t nv = n / 4;
     for (int64_t i = (int64_t)blockIdx.x * THREADS + threadIdx.x; i < nv; i += (int64_t)gridDim.x * THREADS)
-      reinterpret_cast<f32x4*>(d)[i] = reinterpret_cast<const f32x4*>(s)[i];
-    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) d[4 * nv + threadIdx.x] = s[4 * nv + threadIdx.x];
+      reinterpret_cast<f32x4*>(d)[i] = reinterpret_cast<const f32x4*>(s)[i] * sg;
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) d[4 * nv + threadIdx.x] = s[4 * nv + threadIdx.x] * sg;
   } else {
     for (int64_t i = (int64_t)blockIdx.x * THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * THREADS)
-      d[i] = s[i];
+      d[i] = s[i] * sg;
   }
 }
 
@@ -56,9 +62,10 @@ __global__ __launch_bounds__(THREADS) void copy_rows_kernel(const float* __restr
 constexpr int TCI = 16, TCO = 64, MAXKK = 9;
 template <bool VEC>
 __global__ __launch_bounds__(THREADS) void tap_to_ref_kernel(const float* __restrict__ wt, int KK, int Cin, int Cout,
-                                                             float* __restrict__ dst, int64_t dstride) {
+                                                             float* __restrict__ dst, int64_t dstride, int nneg) {
   __shared__ float tile[MAXKK * TCI][TCO + 1];
   const int k = blockIdx.z;
+  const float sg = k < nneg ? -1.f : 1.f;
   const int ci0 = blockIdx.y * TCI, co0 = blockIdx.x * TCO;
   const float* src = wt + (int64_t)k * KK * Cin * Cout;
   float* out = dst + (int64_t)k * dstride;
@@ -69,7 +76,7 @@ __global__ __launch_bounds__(THREADS) void tap_to_ref_kernel(const float* __rest
       const int t = r / TCI, ci = r % TCI;
       const f32x4 v = *reinterpret_cast<const f32x4*>(src + ((int64_t)t * Cin + ci0 + ci) * Cout + co0 + 4 * c4);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) tile[r][4 * c4 + q] = v[q];
+      for (int q = 0; q < 4; ++q) tile[r][4 * c4 + q] = v[q] * sg;
     }
     __syncthreads();
     for (int e = threadIdx.x; e < TCO * (run / 4); e += THREADS) {
@@ -84,7 +91,7 @@ __global__ __launch_bounds__(THREADS) void tap_to_ref_kernel(const float* __rest
       const int co = e % TCO, r = e / TCO;
       const int t = r / TCI, ci = r % TCI;
       float v = 0.f;
-      if (ci0 + ci < Cin && co0 + co < Cout) v = src[((int64_t)t * Cin + ci0 + ci) * Cout + co0 + co];
+      if (ci0 + ci < Cin && co0 + co < Cout) v = src[((int64_t)t * Cin + ci0 + ci) * Cout + co0 + co] * sg;
       tile[r][co] = v;
     }
     __syncthreads();
@@ -126,32 +133,43 @@ extern "C" int flr_broadcast_rows(const float* src, int64_t n, float* dst, int64
 
 extern "C" int flr_copy_rows(const float* src, int64_t src_stride, int64_t n, float* dst, int64_t dst_stride,
                              int64_t K, void* stream) {
-  if (!src || !dst || n < 0 || K < 1 || K > 65535 || src_stride < n || dst_stride < n) return FLR_ERR_ARG;
+  return flr_copy_rows_neg(src, src_stride, n, dst, dst_stride, K, 0, stream);
+}
+
+extern "C" int flr_copy_rows_neg(const float* src, int64_t src_stride, int64_t n, float* dst, int64_t dst_stride,
+                                 int64_t K, int64_t nneg, void* stream) {
+  if (!src || !dst || n < 0 || K < 1 || K > 65535 || src_stride < n || dst_stride < n || nneg < 0) return FLR_ERR_ARG;
   if (n == 0) return FLR_OK;
   const bool vec = layout::al16(src) && layout::al16(dst) && src_stride % 4 == 0 && dst_stride % 4 == 0;
   const dim3 grid(layout::grid_x(vec ? n / 4 : n), (unsigned)K);
   if (vec)
     hipLaunchKernelGGL(layout::copy_rows_kernel<true>, grid, dim3(layout::THREADS), 0, as_stream(stream), src,
-                       src_stride, n, dst, dst_stride);
+                       src_stride, n, dst, dst_stride, (int)std::min<int64_t>(nneg, K));
   else
     hipLaunchKernelGGL(layout::copy_rows_kernel<false>, grid, dim3(layout::THREADS), 0, as_stream(stream), src,
-                       src_stride, n, dst, dst_stride);
+                       src_stride, n, dst, dst_stride, (int)std::min<int64_t>(nneg, K));
   return launch_status("copy_rows");
 }
 
 extern "C" int flr_tap_major_to_torch(const float* w_t, int64_t K, int64_t KK, int64_t Cin, int64_t Cout, float* dst,
                                       int64_t dst_stride, void* stream) {
+  return flr_tap_major_to_torch_neg(w_t, K, KK, Cin, Cout, dst, dst_stride, 0, stream);
+}
+
+extern "C" int flr_tap_major_to_torch_neg(const float* w_t, int64_t K, int64_t KK, int64_t Cin, int64_t Cout,
+                                          float* dst, int64_t dst_stride, int64_t nneg, void* stream) {
   if (!w_t || !dst || K < 1 || K > 65535 || KK < 1 || KK > layout::MAXKK || Cin < 1 || Cout < 1 ||
-      dst_stride < KK * Cin * Cout)
+      dst_stride < KK * Cin * Cout || nneg < 0)
     return FLR_ERR_ARG;
+  const int ng = (int)std::min<int64_t>(nneg, K);
   const dim3 grid((unsigned)cdiv((int)Cout, layout::TCO), (unsigned)cdiv((int)Cin, layout::TCI), (unsigned)K);
   const bool vec = Cin % layout::TCI == 0 && Cout % layout::TCO == 0 && layout::al16(w_t) && layout::al16(dst) &&
                    dst_stride % 4 == 0 && (layout::TCI * KK) % 4 == 0;
   if (vec)
     hipLaunchKernelGGL(layout::tap_to_ref_kernel<true>, grid, dim3(layout::THREADS), 0, as_stream(stream), w_t,
-                       (int)KK, (int)Cin, (int)Cout, dst, dst_stride);
+                       (int)KK, (int)Cin, (int)Cout, dst, dst_stride, ng);
   else
     hipLaunchKernelGGL(layout::tap_to_ref_kernel<false>, grid, dim3(layout::THREADS), 0, as_stream(stream), w_t,
-                       (int)KK, (int)Cin, (int)Cout, dst, dst_stride);
+                       (int)KK, (int)Cin, (int)Cout, dst, dst_stride, ng);
   return launch_status("tap_major_to_torch");
 }

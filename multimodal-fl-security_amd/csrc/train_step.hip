@@ -119,6 +119,16 @@ __global__ void ce_mean_kernel(const float* __restrict__ loss_row, int K, int B,
   loss[k] = s / (float)B;
 }
 
+// out[c] = (sum_r X[r][c]) / R with a sequential fp64 sum — the client's
+// reported loss, sum(loss.item() per batch) / len (fl_client.py:143-149).
+__global__ void mean_rows_kernel(const float* __restrict__ X, int R, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int r = 0; r < R; ++r) s += (double)X[(int64_t)r * C + c];
+  out[c] = (float)(s / (double)R);
+}
+
 __global__ void scale_rows_kernel(float* __restrict__ d, const float* __restrict__ gk, int K, int B, int C) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)K * B * C) return;
@@ -320,6 +330,13 @@ extern "C" int flr_cross_entropy(const float* logits, const int64_t* labels, int
   if (rc != FLR_OK) return rc;
   hipLaunchKernelGGL(train::ce_mean_kernel, dim3(cdiv((int)K, 64)), dim3(64), 0, st, loss_rows, (int)K, (int)B, loss);
   return launch_status("ce_mean_kernel");
+}
+
+extern "C" int flr_mean_rows(const float* X, int64_t R, int64_t C, float* out, void* stream) {
+  if (!X || !out || R < 1 || C < 1) return FLR_ERR_ARG;
+  hipLaunchKernelGGL(train::mean_rows_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, as_stream(stream), X,
+                     (int)R, (int)C, out);
+  return launch_status("mean_rows_kernel");
 }
 
 extern "C" int flr_scale_client_rows(float* d, const float* gk, int64_t K, int64_t B, int64_t C, void* stream) {

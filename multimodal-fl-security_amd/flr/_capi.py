@@ -74,10 +74,13 @@ SIGNATURES = {
     "flr_conv2d_bwd_weight_reuse": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t,
                                                                                             _c_void_p]),
     "flr_cross_entropy": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "flr_mean_rows": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p]),
     "flr_scale_client_rows": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p]),
     "flr_broadcast_rows": (_int, [_c_void_p, _i64, _c_void_p, _i64, _i64, _c_void_p]),
     "flr_copy_rows": (_int, [_c_void_p, _i64, _i64, _c_void_p, _i64, _i64, _c_void_p]),
     "flr_tap_major_to_torch": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p]),
+    "flr_copy_rows_neg": (_int, [_c_void_p, _i64, _i64, _c_void_p, _i64, _i64, _i64, _c_void_p]),
+    "flr_tap_major_to_torch_neg": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _i64, _i64, _c_void_p]),
     "flr_row_norms_workspace": (_size_t, [_i64]),
     "flr_row_norms": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _int, _c_void_p, _c_void_p, _size_t,
                              _c_void_p]),

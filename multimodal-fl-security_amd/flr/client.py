@@ -55,9 +55,9 @@ class Client:
         masks = None if self.masks is None else [m.unsqueeze(0) for m in self.masks] * epochs
         if masks is not None:
             masks = masks[: len(batches)]
-        loss = self.trainer.local_update(batches, masks)
-        if self.malicious:  # sign flip (model_poisoning.py:274-276)
-            self.trainer.X.data[0, : self.trainer.P].neg_()
+        # a malicious client's row is written negated by the export: the sign
+        # flip (model_poisoning.py:274-276) after training (malicious_client.py:103-115)
+        loss = self.trainer.local_update(batches, masks, negate_rows=1 if self.malicious else 0)
         params = [t.clone() for t in self.trainer.X.row(0)]
         return params, self.num_examples, {"loss": float(loss[0].item()), "client_id": self.client_id}
 

@@ -104,19 +104,18 @@ class RoundEngine:
         self.round_index = 0
         self.fell_back = False
 
-    def _poison(self) -> None:
+    def _num_flipped(self) -> int:
+        """Local rows of sign-flip attackers (clients 0..f-1): they submit
+        -update, the weights negated as the reference does (model_poisoning.py:
+        274-276 via malicious_client.py:103-115) — written negated by the export."""
         f = self.rcfg.num_attackers if self.rcfg.attack == "sign_flip" else 0
-        lo, hi = self.lo, min(self.hi, f)
-        if hi > lo:  # malicious rows submit -update (weights, as the reference negates)
-            self.trainer.X.data[: hi - lo, : self.trainer.P].neg_()
+        return max(0, min(self.hi, f) - self.lo)
 
     def _train_phase(self) -> torch.Tensor:
         """Every local client: global -> local SGD steps -> client-matrix rows
-        (run_experiments.py:193-240), then the attackers' poisoning."""
+        (run_experiments.py:193-240), the attackers' poisoning in the export."""
         self.trainer.load_global(self.global_flat)
-        losses = self.trainer.local_update(self.batches, self.masks)
-        self._poison()
-        return losses
+        return self.trainer.local_update(self.batches, self.masks, negate_rows=self._num_flipped())
 
     def _capture(self) -> None:
         """Capture the training phase (~2.4k kernel launches per round at C3)

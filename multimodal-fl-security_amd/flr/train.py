@@ -184,17 +184,19 @@ class ClientBatchTrainer:
                 src = src.contiguous()
             _capi.call("flr_broadcast_rows", src.data_ptr(), n, w.data_ptr(), self.K, n, st)
 
-    def export(self) -> ClientMatrix:
-        """Client-major client matrix for the server (row k = client k)."""
+    def export(self, negate_rows: int = 0) -> ClientMatrix:
+        """Client-major client matrix for the server (row k = client k); rows
+        k < negate_rows are written negated (the sign-flip attackers)."""
         st = _stream(self._wbuf)
         ld = self.X.data.stride(0)
         base = self.X.data.data_ptr()
         for name, w, off, n, shp in zip(self.names, self.W, self.offsets, self.numels, self.shapes):
             if name in self.tap_major:
                 cout, cin, kh, kw = shp
-                _capi.call("flr_tap_major_to_torch", w.data_ptr(), self.K, kh * kw, cin, cout, base + 4 * off, ld, st)
+                _capi.call("flr_tap_major_to_torch_neg", w.data_ptr(), self.K, kh * kw, cin, cout, base + 4 * off, ld,
+                           negate_rows, st)
             else:
-                _capi.call("flr_copy_rows", w.data_ptr(), n, n, base + 4 * off, ld, self.K, st)
+                _capi.call("flr_copy_rows_neg", w.data_ptr(), n, n, base + 4 * off, ld, self.K, negate_rows, st)
         return self.X
 
     # ---- one optimizer step for every client -----------------------------
@@ -219,22 +221,26 @@ class ClientBatchTrainer:
                        self.norms.data_ptr() + 4 * c0, self._ws.data_ptr() + self._ws_off, self._ws_bytes,
                        _stream(self._wbuf))
             del grads, leaves, params, logits
-            if whole:
-                return loss_k.detach()
-            loss_out[c0:c1].copy_(loss_k.detach())
+            _capi.call("flr_copy_rows", loss_k.data_ptr(), c1 - c0, c1 - c0, loss_out.data_ptr() + 4 * c0, c1 - c0, 1,
+                       _stream(loss_out))
         return loss_out
 
     def local_update(self, batches: Sequence, dropout_masks: Optional[Sequence] = None,
-                     export: bool = True) -> torch.Tensor:
-        """Runs len(batches) steps; returns each client's mean loss [K]."""
-        total = torch.zeros(self.K, dtype=torch.float32, device=self.device)
+                     export: bool = True, negate_rows: int = 0) -> torch.Tensor:
+        """Runs len(batches) steps; returns each client's mean loss [K]
+        (fl_client.py:143-149).  The per-step losses land in one [steps, K]
+        buffer and are averaged by one flr_sum_rows pass (sum in step order)."""
+        n = max(1, len(batches))
+        steps = torch.empty(n, self.K, dtype=torch.float32, device=self.device)
         for s, (images, tokens, labels) in enumerate(batches):
             mask = None if dropout_masks is None else dropout_masks[s]
-            total += self.step(images, tokens, labels, first=(s == 0), dropout_mask=mask,
-                               last=(s == len(batches) - 1))
+            self.step(images, tokens, labels, first=(s == 0), dropout_mask=mask, last=(s == len(batches) - 1),
+                      loss_out=steps[s])
         if export:
-            self.export()
-        return total / max(1, len(batches))
+            self.export(negate_rows)
+        total = torch.empty(1, self.K, dtype=torch.float32, device=self.device)
+        _capi.call("flr_mean_rows", steps.data_ptr(), len(batches), self.K, total.data_ptr(), _stream(total))
+        return total[0]
 
 
 def make_dropout_masks(spec: ModelSpec, steps: int, client_ids, B: int, device,

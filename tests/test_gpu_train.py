@@ -240,3 +240,69 @@ def test_client_chunking_bit_identical(cuda, spec_name):
         out.append((loss.cpu(), tr.X.data[:, : tr.P].cpu()))
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1], out[1][1])
+
+
+def test_c2_round_fedavg_matches_reference(cuda):
+    """Config C2 end to end: FedAvg over K = 32 clients of the ResNet-18 + GRU
+    model (2 local steps at the reference batch 32, dropout masks): the
+    engine's round vs the oracle's per-client loop (run_experiments.py:193-240)
+    + oracle.fedavg (base_defense.py:80-97) at 1e-5."""
+    from oracle import aggregation as orc
+    from flr.round import RoundConfig, RoundEngine
+    spec = ModelSpec()
+    K, steps, B = 32, 2, 32
+    rc = RoundConfig(num_clients=K, batch=B, defense="fedavg", attack="none", num_attackers=0)
+    eng = RoundEngine(spec, rc, TrainConfig(local_steps=steps), cuda)
+    glob = eng.global_flat.clone().cpu()
+    new = eng.run_round().cpu()
+    batches = synthetic_batches(spec, steps, range(K), B, "cpu")
+    masks = make_dropout_masks(spec, steps, range(K), B, "cpu", seed=rc.seed + 7919)
+    ups, losses = [], []
+    for k in range(K):
+        cb = [(im[k], tk[k], lb[k]) for im, tk, lb in batches]
+        upd, ref_loss = otrain.local_update(MultimodalNet, spec, glob, cb, masks=[m[k] for m in masks])
+        ups.append(upd)
+        losses.append(ref_loss)
+    ref = torch.cat([t.reshape(-1) for t in orc.fedavg(ups, [steps * B] * K)])
+    assert _rel(new, ref) < 1e-5, _rel(new, ref)
+    got_loss = eng.losses.cpu()
+    err = max(abs(got_loss[k].item() - losses[k]) / max(1.0, abs(losses[k])) for k in range(K))
+    print(f"\n[C2 round] weights rel err {_rel(new, ref):.2e}, max loss rel err {err:.2e}")
+    assert err <= 1e-5
+
+
+def test_c3_round_multikrum_signflip(cuda):
+    """Config C3's round: K = 128 clients (f = 25 sign-flipped, multi_k = 64),
+    1 local step.  Four sampled clients' trained rows (attackers and benign)
+    match the oracle loop at 1e-5 (before the sign flip the row is the
+    reference's local update; after it, its negation, model_poisoning.py:274-276);
+    the Krum selection equals the oracle's scores and argsort on the GPU's
+    distance matrix (krum.py:101-131, 174) and rejects every attacker."""
+    from oracle import aggregation as orc
+    from flr.round import RoundConfig, RoundEngine
+    spec = ModelSpec()
+    K, f, steps, B = 128, 25, 1, 8
+    rc = RoundConfig(num_clients=K, batch=B, defense="krum", attack="sign_flip", num_attackers=f)
+    eng = RoundEngine(spec, rc, TrainConfig(local_steps=steps), cuda)
+    assert eng.defense.multi_k == 64
+    glob = eng.global_flat.clone().cpu()
+    eng.run_round()
+    eng.defense.publish()
+    X = eng.trainer.X.data[:, : eng.trainer.P]
+    batches = synthetic_batches(spec, steps, [0, 24, 25, 127], B, "cpu")
+    masks = make_dropout_masks(spec, steps, [0, 24, 25, 127], B, "cpu", seed=rc.seed + 7919)
+    for j, k in enumerate([0, 24, 25, 127]):
+        cb = [(im[j], tk[j], lb[j]) for im, tk, lb in batches]
+        upd, _ = otrain.local_update(MultimodalNet, spec, glob, cb, masks=[m[j] for m in masks])
+        ref = torch.cat([u.reshape(-1) for u in upd])
+        if k < f:
+            ref = -ref
+        assert _rel(X[k].cpu(), ref) < 1e-5, (k, _rel(X[k].cpu(), ref))
+    D = eng.defense.distances.cpu().numpy()
+    scores = orc.krum_scores(D, K - f - 2)
+    import numpy as np
+    order = np.argsort(scores, kind="stable")
+    assert eng.defense.selected_clients == order[:64].tolist()
+    assert not set(eng.defense.selected_clients) & set(range(f))
+    s = np.sort(np.asarray(scores))
+    print(f"\n[C3 round] selection-boundary margin {(s[64] - s[63]) / s[64]:.3e}")
