@@ -333,6 +333,26 @@ int flr_gru_fwd_step(const float* gi, const float* gh, float* hseq, float* gates
 int flr_gru_bwd_step(const float* dh, const float* gates, const float* hseq,
                      float* dgh, float* dgi, float* dh_direct, int64_t K,
                      int64_t B, int64_t T, int64_t H, int64_t t, void* stream);
+/* Fused recurrence steps (B <= 32): one launch per time step instead of a
+ * batched GEMM plus a gate kernel.  flr_gru_fwd_fused: gh = h_t W_hh^T + b_hh
+ * (whhP = W_hh [K][3H][H] packed by flr_gru_pack(NG=3, C=H, trans=0), bhh
+ * [K][3H]) and the gate math of flr_gru_fwd_step in the GEMM's epilogue.
+ * flr_gru_bwd_fused (t >= 1): dh_t = dh_direct + dgh[:, t] W_hh (whhTP = W_hh^T
+ * packed by flr_gru_pack(NG=1, C=3H, trans=1)), then flr_gru_bwd_step's math
+ * for step t - 1 with dy = dh_t (dh_direct rewritten in place); dh0 (optional,
+ * [K][B][H]) receives dh_t.  Same products as the batched GEMM (bf16x6 on MFMA,
+ * fp32 accumulate), a different reduction order. */
+int flr_gru_fwd_fused(const float* gi, const float* whhP, const float* bhh, float* hseq, float* gates, int64_t K,
+                      int64_t B, int64_t T, int64_t H, int64_t t, void* stream);
+int flr_gru_bwd_fused(const float* whhTP, const float* gates, const float* hseq, float* dgh, float* dgi,
+                      float* dh_direct, float* dh0, int64_t K, int64_t B, int64_t T, int64_t H, int64_t t,
+                      void* stream);
+/* Pack a per-client weight into the fused kernels' MFMA-fragment order: the
+ * [NG*H][C] operand (trans = 0: w is [NG*H][C]; trans = 1, NG = 1: w is [C][H]
+ * and the operand is its transpose) in 32-row blocks x 16-deep k-steps, each
+ * (block, k-step) 512 floats (two 1 KB wave loads), zero-padded.  wp holds
+ * K * NG * ceil(H/32) * ceil(C/16) * 512 floats. */
+int flr_gru_pack(const float* w, int64_t K, int64_t NG, int64_t H, int64_t C, int trans, float* wp, void* stream);
 
 /* ---- a2: per-client BatchNorm (train mode) + fused residual add / ReLU ----
  * Replaces nn.BatchNorm2d(train) [+ identity add] [+ ReLU] of the conv blocks.

@@ -120,6 +120,9 @@ SIGNATURES = {
     "flr_maxpool2d_bwd": (_int, [_c_void_p] * 3 + [_i64] * 7 + [_c_void_p]),
     "flr_gru_fwd_step": (_int, [_c_void_p] * 4 + [_i64] * 5 + [_c_void_p]),
     "flr_gru_bwd_step": (_int, [_c_void_p] * 6 + [_i64] * 5 + [_c_void_p]),
+    "flr_gru_fwd_fused": (_int, [_c_void_p] * 5 + [_i64] * 5 + [_c_void_p]),
+    "flr_gru_bwd_fused": (_int, [_c_void_p] * 7 + [_i64] * 5 + [_c_void_p]),
+    "flr_gru_pack": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _int, _c_void_p, _c_void_p]),
     "flr_batchnorm_infer": (_int, [_c_void_p] * 7 + [_i64, _i64, ctypes.c_float, _int, _c_void_p]),
     "flr_classify_rows": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p,
                                  _c_void_p]),

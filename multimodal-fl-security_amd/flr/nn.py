@@ -1,6 +1,8 @@
 """Autograd wrappers over the client-batched HIP layer kernels."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _capi
@@ -191,15 +193,23 @@ def client_linear(x, W, b=None):
     return ClientLinear.apply(x, W, b)
 
 
+def _gru_packed(ng: int, h: int, c: int) -> int:
+    """Floats per client of a weight packed by flr_gru_pack: ng groups of
+    ceil(h/32) row blocks x ceil(c/16) k-steps x 512."""
+    return ng * ((h + 31) // 32) * ((c + 15) // 16) * 512
+
+
 class ClientGRU(torch.autograd.Function):
     """Final hidden state of a 1-layer GRU (h_0 = 0) for K clients at once.
 
     gi [K, B, T, 3H] = x W_ih^T + b_ih (computed by the caller, so autograd
     handles W_ih, b_ih and the embedding), whh [K, 3H, H], bhh [K, 3H] ->
-    h_T [K, B, H].  Per step: one flr_bgemm (h W_hh^T + b_hh) and one
-    flr_gru_fwd_step launch; backward: one flr_gru_bwd_step and one flr_bgemm
-    per step, then dW_hh / db_hh over all steps at once (flr_bgemm,
-    flr_sum_rows).
+    h_T [K, B, H].  B <= 32: W_hh is packed once into MFMA-fragment order
+    (flr_gru_pack) and each step is one flr_gru_fwd_fused launch (recurrence
+    GEMM + gate math); backward packs W_hh^T and runs one flr_gru_bwd_fused
+    per step.  Otherwise per step one flr_bgemm (h W_hh^T + b_hh) and one
+    flr_gru_fwd_step / flr_gru_bwd_step.  dW_hh / db_hh over all steps at once
+    (flr_bgemm, flr_sum_rows).
     """
 
     @staticmethod
@@ -209,16 +219,28 @@ class ClientGRU(torch.autograd.Function):
         H = H3 // 3
         dev = gi.device
         hseq = torch.empty(K, T + 1, B, H, dtype=gi.dtype, device=dev)
-        hseq[:, 0].zero_()
         gates = torch.empty(K, T, B, 4, H, dtype=gi.dtype, device=dev)
         bias = bhh.contiguous()
+        whh = whh.contiguous()
         st = _stream(gi)
-        gh = torch.empty(K, B, H3, dtype=gi.dtype, device=dev)
-        for t in range(T):
-            bgemm(hseq[:, t], whh, bias=bias, out=gh)
-            _capi.call("flr_gru_fwd_step", gi.data_ptr(), gh.data_ptr(), hseq.data_ptr(), gates.data_ptr(),
-                       K, B, T, H, t, st)
+        # FLR_GRU_FUSED=0: the batched GEMM + gate kernel per step (A/B timing)
+        fused = B <= 32 and os.environ.get("FLR_GRU_FUSED", "1") != "0"
+        if fused:  # one launch per step: the recurrence GEMM with the gate math in its epilogue
+            fill_(hseq)  # h_0 = 0
+            whhP = torch.empty(K, _gru_packed(3, H, H), dtype=whh.dtype, device=dev)
+            _capi.call("flr_gru_pack", whh.data_ptr(), K, 3, H, H, 0, whhP.data_ptr(), st)
+            for t in range(T):
+                _capi.call("flr_gru_fwd_fused", gi.data_ptr(), whhP.data_ptr(), bias.data_ptr(), hseq.data_ptr(),
+                           gates.data_ptr(), K, B, T, H, t, st)
+        else:
+            hseq[:, 0].zero_()
+            gh = torch.empty(K, B, H3, dtype=gi.dtype, device=dev)
+            for t in range(T):
+                bgemm(hseq[:, t], whh, bias=bias, out=gh)
+                _capi.call("flr_gru_fwd_step", gi.data_ptr(), gh.data_ptr(), hseq.data_ptr(), gates.data_ptr(),
+                           K, B, T, H, t, st)
         ctx.save_for_backward(whh, hseq, gates)
+        ctx.fused = fused
         return hseq[:, T].contiguous()
 
     @staticmethod
@@ -231,11 +253,20 @@ class ClientGRU(torch.autograd.Function):
         dh = dhT.contiguous()
         dh_direct = torch.empty(K, B, H, dtype=dhT.dtype, device=dev)
         st = _stream(dh)
-        for t in range(T - 1, -1, -1):
+        if ctx.fused:  # step T-1's gate backward, then one launch per earlier step (GEMM + gate backward)
+            whhT = torch.empty(K, _gru_packed(1, H, 3 * H), dtype=whh.dtype, device=dev)  # W_hh^T, packed
+            _capi.call("flr_gru_pack", whh.data_ptr(), K, 1, H, 3 * H, 1, whhT.data_ptr(), st)
             _capi.call("flr_gru_bwd_step", dh.data_ptr(), gates.data_ptr(), hseq.data_ptr(), dgh.data_ptr(),
-                       dgi.data_ptr(), dh_direct.data_ptr(), K, B, T, H, t, st)
-            if t > 0:  # dL/dh_t = z-path + dgh_t W_hh   (dL/dh_0 is not needed)
-                dh = bgemm(dgh[:, t], whh.transpose(1, 2), add=dh_direct)
+                       dgi.data_ptr(), dh_direct.data_ptr(), K, B, T, H, T - 1, st)
+            for t in range(T - 1, 0, -1):
+                _capi.call("flr_gru_bwd_fused", whhT.data_ptr(), gates.data_ptr(), hseq.data_ptr(), dgh.data_ptr(),
+                           dgi.data_ptr(), dh_direct.data_ptr(), None, K, B, T, H, t, st)
+        else:
+            for t in range(T - 1, -1, -1):
+                _capi.call("flr_gru_bwd_step", dh.data_ptr(), gates.data_ptr(), hseq.data_ptr(), dgh.data_ptr(),
+                           dgi.data_ptr(), dh_direct.data_ptr(), K, B, T, H, t, st)
+                if t > 0:  # dL/dh_t = z-path + dgh_t W_hh   (dL/dh_0 is not needed)
+                    dh = bgemm(dgh[:, t], whh.transpose(1, 2), add=dh_direct)
         dgh2 = dgh.view(K, T * B, 3 * H)
         dwhh = bgemm(dgh2.transpose(1, 2), hseq[:, :T].reshape(K, T * B, H).transpose(1, 2))
         dbhh = sum_rows(dgh2)

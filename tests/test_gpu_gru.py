@@ -13,6 +13,8 @@ SHAPES = [  # (K, B, T, H)
     (3, 4, 5, 8),
     (2, 3, 1, 5),
     (4, 32, 16, 256),  # the model's text branch, 4 clients
+    (2, 32, 4, 300),   # H not a multiple of the fused kernels' 32-unit blocks
+    (2, 33, 3, 40),    # B > 32: the batched-GEMM + gate-kernel path
 ]
 
 
