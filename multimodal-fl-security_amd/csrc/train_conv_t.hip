@@ -547,6 +547,147 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
   __device__ int64_t ldm() const { return RP; }
 };
 
+// The same two GEMMs with the im2col operand gathered on the fly from x
+// ([K][C][B][H][W]; one client's image batch, 393 KB at the C3 stem, stays in
+// L2 across its 49 taps): no column matrix is written or read.  Reduction
+// index r = (ci*KH + kh)*KW + kw (torch weight order), zero past R = Cin*KH*KW.
+struct StemFwd {  // y[co][pix] = sum_r wp[co][r] x(pix; r): M = Cout, N = B*Ho*Wo, R = RP
+  Geom g;
+  int RP, RR;  // RR = Cin*KH*KW
+  conv::FastDiv d_kk, d_kw;
+  const float* x;
+  const float* wp;
+  float* y;
+  static constexpr int LA = RK_VEC, LB = KR_GATHER;
+  __host__ __device__ int M() const { return g.Cout; }
+  __host__ __device__ int N() const { return g.B * g.Ho * g.Wo; }
+  __host__ __device__ int R() const { return RP; }
+  struct State {
+    rsrc_t ra, rb;
+    unsigned a0;
+    bool aok[2], nok;
+    int ih0, iw0, xoff;
+  };
+  __device__ State init(int k, int m0, int n0, int tid) const {
+    State s;
+    s.ra = make_rsrc(wp + (int64_t)k * g.Cout * RP, (int64_t)g.Cout * RP);
+    s.a0 = (unsigned)(((m0 + tid / 8) * RP + 4 * (tid % 8)) * 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) s.aok[i] = m0 + tid / 8 + 32 * i < M();
+    s.rb = make_rsrc(x + k * g.sxk, g.xext);
+    const int n = n0 + tid % 64;
+    s.nok = n < N();
+    const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
+    const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+    s.ih0 = (int)oh * g.stride - g.pad;
+    s.iw0 = (int)ow * g.stride - g.pad;
+    s.xoff = (int)(bb * g.sxb);
+    return s;
+  }
+  __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
+    const bool kok = r0 + 4 * (int)(threadIdx.x % 8) < RP;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 qa = ld4(s.ra, (kok && s.aok[i]) ? s.a0 + (unsigned)((r0 + 32 * i * RP) * 4) : SENT, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[4 * i + e] = qa[e];
+    }
+  }
+  // k-row tid/64 + 4i is the wave's: (ci, kh, kw) are wave-uniform (SGPRs)
+  __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
+    const int KK = g.KH * g.KW;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = uni(r0 + (int)(threadIdx.x / 64) + 4 * i);
+      const int ci = uni((int)udiv((uint32_t)r, d_kk)), rem = r - ci * KK;
+      const int kh = uni((int)udiv((uint32_t)rem, d_kw)), kw = rem - kh * g.KW;
+      const int ih = s.ih0 + kh, iw = s.iw0 + kw;
+      const bool ok = s.nok && r < RR && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const unsigned vb = ok ? (unsigned)((s.xoff + ih * g.W + iw) * 4) : SENT;
+      b[i] = ld1(s.rb, vb, uni(ci * (int)g.sxc * 4));
+    }
+  }
+  __device__ void store(int k, int m, int n, float v) const { y[k * g.syk + m * g.syc + n] = v; }
+  __device__ bool linear() const { return true; }
+  __device__ float* out() const { return y; }
+  __device__ int64_t tile_base(int k, int m0, int n0) const { return k * g.syk + m0 * g.syc + n0; }
+  __device__ int64_t ldm() const { return g.syc; }
+};
+
+struct StemWgt {  // dwp[co][r] = sum_pix dy[co][pix] x(pix; r): M = Cout, N = RP, R = B*Ho*Wo (HoWo % 4 == 0)
+  Geom g;
+  int RP, RR;
+  conv::FastDiv d_kk, d_kw;
+  const float* x;
+  const float* dy;
+  float* dwp;
+  static constexpr int LA = RK_VEC, LB = KR_VEC;
+  __host__ __device__ int M() const { return g.Cout; }
+  __host__ __device__ int N() const { return RP; }
+  __host__ __device__ int R() const { return g.B * g.Ho * g.Wo; }
+  struct State {
+    rsrc_t ra, rb;
+    int arow;
+    bool aok[2];
+    int roff[4];          // this thread's 4 reduction columns r: ci*sxc + kh*W + kw
+    int8_t kh[4], kw[4];  // (kh = -128: r past R)
+  };
+  __device__ State init(int k, int m0, int n0, int tid) const {
+    State s;
+    s.ra = make_rsrc(dy + k * g.syk, g.yext);
+    s.arow = (int)((m0 + tid / 8) * g.syc);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) s.aok[i] = m0 + tid / 8 + 32 * i < M();
+    s.rb = make_rsrc(x + k * g.sxk, g.xext);
+    const int KK = g.KH * g.KW;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = n0 + 4 * (tid % 16) + e;
+      const int ci = (int)udiv((uint32_t)r, d_kk), rem = r - ci * KK;
+      const int kh = (int)udiv((uint32_t)rem, d_kw), kw = rem - kh * g.KW;
+      const bool ok = r < RR;
+      s.kh[e] = ok ? (int8_t)kh : (int8_t)-128;
+      s.kw[e] = (int8_t)kw;
+      s.roff[e] = ok ? ci * (int)g.sxc + kh * g.W + kw : 0;
+    }
+    return s;
+  }
+  __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
+    const int tid = threadIdx.x, R = this->R();
+    const int q = r0 + 4 * (tid % 8);  // dy[co][q]: q = b*Ho*Wo + p contiguous per channel
+    const unsigned va = (unsigned)((s.arow + q) * 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 qa = ld4(s.ra, (q < R && s.aok[i]) ? va + (unsigned)(i * 32 * (int)g.syc * 4) : SENT, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[4 * i + e] = qa[e];
+    }
+  }
+  // KR_VEC image: pixel k-rows tid/16 + 16i, columns r = n0 + 4 (tid % 16) + e
+  __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
+    const int tid = threadIdx.x, R = this->R(), HoWo = g.Ho * g.Wo;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = r0 + tid / 16 + 16 * i;
+      const uint32_t bb = udiv((uint32_t)q, g.d_howo), p = (uint32_t)q - bb * HoWo;
+      const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+      const int ih0 = (int)oh * g.stride - g.pad, iw0 = (int)ow * g.stride - g.pad;
+      const int base = (int)(bb * g.sxb) + ih0 * g.W + iw0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ih = ih0 + s.kh[e], iw = iw0 + s.kw[e];
+        const bool ok = q < R && s.kh[e] >= 0 && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        b[4 * i + e] = ld1(s.rb, ok ? (unsigned)((base + s.roff[e]) * 4) : SENT, 0);
+      }
+    }
+  }
+  __device__ void store(int k, int m, int n, float v) const { dwp[((int64_t)k * g.Cout + m) * RP + n] = v; }
+  __device__ bool linear() const { return true; }
+  __device__ float* out() const { return dwp; }
+  __device__ int64_t tile_base(int k, int m0, int n0) const { return ((int64_t)k * g.Cout + m0) * RP + n0; }
+  __device__ int64_t ldm() const { return RP; }
+};
+
 // col[k][pix][RP] (grid: pixel blocks x K).  A workgroup builds IM_PB whole
 // rows in LDS — one thread per (pix, ci, kh) fills the KW-long run
 // r = (ci*KH + kh)*KW + 0..KW-1 — then streams the IM_PB*RP contiguous floats
@@ -1067,7 +1208,9 @@ size_t im2col_workspace(const Geom& g) {
   const size_t wp = align_up((size_t)g.Kc * g.Cout * padded_r(g) * sizeof(float), 256);
   DenseFwd f; f.g = g; f.RP = padded_r(g);
   DenseWgt w; w.g = g; w.RP = padded_r(g);
-  return col + wp + std::max(splits_bytes(f), splits_bytes(w));
+  StemFwd sf; sf.g = g; sf.RP = padded_r(g);
+  StemWgt sw; sw.g = g; sw.RP = padded_r(g);
+  return col + wp + std::max(std::max(splits_bytes(f), splits_bytes(w)), std::max(splits_bytes(sf), splits_bytes(sw)));
 }
 
 static int run_im2col(const Geom& g, const float* x, float* col, hipStream_t st) {
@@ -1075,6 +1218,19 @@ static int run_im2col(const Geom& g, const float* x, float* col, hipStream_t st)
   hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)cdiv(N, IM_PB), (unsigned)g.Kc), dim3(THREADS),
                      (size_t)IM_PB * RP * sizeof(float), st, g, x, RP, col);
   return launch_status("conv im2col");
+}
+
+// FLR_STEM=col: the explicit im2col column matrix (A/B timing); default: gathered operand
+inline bool stem_col() {
+  const char* e = getenv("FLR_STEM");
+  return e && e[0] == 'c';
+}
+
+template <class Plan>
+inline void stem_divs(Plan& pl, const Geom& g) {
+  pl.RR = g.Cin * g.KH * g.KW;
+  pl.d_kk = conv::make_fastdiv((uint32_t)(g.KH * g.KW));
+  pl.d_kw = conv::make_fastdiv((uint32_t)g.KW);
 }
 
 int fwd_im2col(const Geom& g, const float* x, const float* w, float* y, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -1085,12 +1241,18 @@ int fwd_im2col(const Geom& g, const float* x, const float* w, float* y, void* ws
   const size_t colb = align_up((size_t)g.Kc * g.B * g.Ho * g.Wo * RP * sizeof(float), 256);
   float* wp = reinterpret_cast<float*>(base + colb);
   const size_t wpb = align_up((size_t)g.Kc * g.Cout * RP * sizeof(float), 256);
-  int rc = run_im2col(g, x, col, st);
-  if (rc != FLR_OK) return rc;
   const int64_t wtot = (int64_t)g.Cout * RP;
   hipLaunchKernelGGL(repad_kernel, dim3((unsigned)std::min<int64_t>((wtot + THREADS - 1) / THREADS, 256), (unsigned)g.Kc),
                      dim3(THREADS), 0, st, w, R, wp, RP, g.Cout, R);
-  if ((rc = launch_status("conv pad weights")) != FLR_OK) return rc;
+  int rc = launch_status("conv pad weights");
+  if (rc != FLR_OK) return rc;
+  if (!stem_col()) {
+    StemFwd pl;
+    pl.g = g; pl.RP = RP; pl.x = x; pl.wp = wp; pl.y = y;
+    stem_divs(pl, g);
+    return launch(pl, base + colb + wpb, ws_bytes - colb - wpb, st, "conv fwd (gathered im2col)");
+  }
+  if ((rc = run_im2col(g, x, col, st)) != FLR_OK) return rc;
   DenseFwd pl;
   pl.g = g; pl.RP = RP; pl.col = col; pl.wp = wp; pl.y = y;
   return launch(pl, base + colb + wpb, ws_bytes - colb - wpb, st, "conv fwd (im2col)");
@@ -1105,11 +1267,20 @@ int wgrad_im2col(const Geom& g, const float* x, const float* dy, float* dw, void
   const size_t colb = align_up((size_t)g.Kc * g.B * g.Ho * g.Wo * RP * sizeof(float), 256);
   float* dwp = reinterpret_cast<float*>(base + colb);
   const size_t wpb = align_up((size_t)g.Kc * g.Cout * RP * sizeof(float), 256);
-  int rc = have_col ? FLR_OK : run_im2col(g, x, col, st);  // have_col: the forward's column matrix
+  int rc = FLR_OK;
+  if (!stem_col()) {
+    StemWgt pl;
+    pl.g = g; pl.RP = RP; pl.x = x; pl.dy = dy; pl.dwp = dwp;
+    stem_divs(pl, g);
+    rc = launch(pl, base + colb + wpb, ws_bytes - colb - wpb, st, "conv bwd weight (gathered im2col)");
+  } else {
+    if (!have_col) rc = run_im2col(g, x, col, st);  // have_col: the forward's column matrix
+    if (rc != FLR_OK) return rc;
+    DenseWgt pl;
+    pl.g = g; pl.RP = RP; pl.col = col; pl.dy = dy; pl.dwp = dwp;
+    rc = launch(pl, base + colb + wpb, ws_bytes - colb - wpb, st, "conv bwd weight (im2col)");
+  }
   if (rc != FLR_OK) return rc;
-  DenseWgt pl;
-  pl.g = g; pl.RP = RP; pl.col = col; pl.dy = dy; pl.dwp = dwp;
-  if ((rc = launch(pl, base + colb + wpb, ws_bytes - colb - wpb, st, "conv bwd weight (im2col)")) != FLR_OK) return rc;
   const int64_t wtot = (int64_t)g.Cout * R;
   hipLaunchKernelGGL(repad_kernel, dim3((unsigned)std::min<int64_t>((wtot + THREADS - 1) / THREADS, 256), (unsigned)g.Kc),
                      dim3(THREADS), 0, st, dwp, RP, dw, R, g.Cout, R);

@@ -33,7 +33,11 @@ struct PoolGeom {
 // evaluated from LDS, and the results leave with coalesced stores.
 constexpr int LDS_FLOATS = 4096;
 
-__device__ __forceinline__ void window_range(int i, int P, int K, int S, int n_out, int& lo, int& hi) {
+// SC: the stride as a compile-time constant (1, 2: divisions become shifts) or 0
+// (runtime g.S) — the backward's per-element window ranges are its VALU cost.
+template <int SC>
+__device__ __forceinline__ void window_range(int i, int P, int K, int Sr, int n_out, int& lo, int& hi) {
+  const int S = SC ? SC : Sr;
   // outputs o with o*S - P <= i <= o*S - P + K - 1
   const int a = i + P - K + 1;  // o*S >= a
   lo = a <= 0 ? 0 : (a + S - 1) / S;
@@ -78,16 +82,28 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(const float* __restrict__ 
   }
 }
 
+template <int SC>
 __global__ __launch_bounds__(THREADS) void bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ arg,
                                                       float* __restrict__ dx, int64_t nplanes, int ppb, PoolGeom g) {
-  __shared__ float ds[LDS_FLOATS];
-  __shared__ uint8_t as[LDS_FLOATS];
+  __shared__ __attribute__((aligned(16))) float ds[LDS_FLOATS];
+  __shared__ __attribute__((aligned(16))) uint8_t as[LDS_FLOATS];
   const int64_t p0 = (int64_t)blockIdx.x * ppb;
   const int np = (int)min((int64_t)ppb, nplanes - p0);
   const int HW = g.H * g.W, HoWo = g.Ho * g.Wo;
-  for (int o = threadIdx.x; o < np * HoWo; o += THREADS) {
-    ds[o] = dy[p0 * HoWo + o];
-    as[o] = arg[p0 * HoWo + o];
+  const int nin = np * HoWo;
+  const float* dyb = dy + p0 * HoWo;
+  const uint8_t* ab = arg + p0 * HoWo;
+  if (((p0 * HoWo) & 3) == 0 && (nin & 3) == 0) {  // 16-B dy / 4-B argmax loads
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    for (int o = threadIdx.x; o < nin / 4; o += THREADS) {
+      reinterpret_cast<f32x4*>(ds)[o] = reinterpret_cast<const f32x4*>(dyb)[o];
+      reinterpret_cast<uint32_t*>(as)[o] = reinterpret_cast<const uint32_t*>(ab)[o];
+    }
+  } else {
+    for (int o = threadIdx.x; o < nin; o += THREADS) {
+      ds[o] = dyb[o];
+      as[o] = ab[o];
+    }
   }
   __syncthreads();
   float* xb = dx + p0 * HW;
@@ -95,19 +111,78 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(const float* __restrict__ 
     const int pl = (int)conv::udiv(e, g.d_hw), q = e - pl * HW;
     const int ih = (int)conv::udiv(q, g.d_w), iw = q - ih * g.W;
     int oh_lo, oh_hi, ow_lo, ow_hi;
-    window_range(ih, g.P, g.KH, g.S, g.Ho, oh_lo, oh_hi);
-    window_range(iw, g.P, g.KW, g.S, g.Wo, ow_lo, ow_hi);
+    window_range<SC>(ih, g.P, g.KH, g.S, g.Ho, oh_lo, oh_hi);
+    window_range<SC>(iw, g.P, g.KW, g.S, g.Wo, ow_lo, ow_hi);
     const float* dp = ds + pl * HoWo;
     const uint8_t* ap = as + pl * HoWo;
     float acc = 0.f;
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      const int kh = ih - (oh * g.S - g.P);
+      const int kh = ih - (oh * (SC ? SC : g.S) - g.P);
       for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const int kw = iw - (ow * g.S - g.P);
+        const int kw = iw - (ow * (SC ? SC : g.S) - g.P);
         if (ap[oh * g.Wo + ow] == kh * g.KW + kw) acc = add_rn(acc, dp[oh * g.Wo + ow]);
       }
     }
     xb[e] = acc;
+  }
+}
+
+// 3x3 / stride 2 / pad 1 (the ResNet stem pool): one thread per 2x2 input
+// block (2m .. 2m+1, 2n .. 2n+1).  Window (oh, ow) covers rows 2oh-1 .. 2oh+1,
+// so only windows (m .. m+1, n .. n+1) reach the block; their gradients are
+// added to the block's four accumulators in window-raster order — the order of
+// the generic gather, so the result is bit-identical.
+__global__ __launch_bounds__(THREADS) void bwd_k3s2p1_kernel(const float* __restrict__ dy,
+                                                             const uint8_t* __restrict__ arg, float* __restrict__ dx,
+                                                             int64_t nplanes, int ppb, PoolGeom g) {
+  __shared__ __attribute__((aligned(16))) float ds[LDS_FLOATS];
+  __shared__ __attribute__((aligned(16))) uint8_t as[LDS_FLOATS];
+  const int64_t p0 = (int64_t)blockIdx.x * ppb;
+  const int np = (int)min((int64_t)ppb, nplanes - p0);
+  const int HW = g.H * g.W, HoWo = g.Ho * g.Wo;
+  const int nin = np * HoWo;
+  const float* dyb = dy + p0 * HoWo;
+  const uint8_t* ab = arg + p0 * HoWo;
+  if (((p0 * HoWo) & 3) == 0 && (nin & 3) == 0) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    for (int o = threadIdx.x; o < nin / 4; o += THREADS) {
+      reinterpret_cast<f32x4*>(ds)[o] = reinterpret_cast<const f32x4*>(dyb)[o];
+      reinterpret_cast<uint32_t*>(as)[o] = reinterpret_cast<const uint32_t*>(ab)[o];
+    }
+  } else {
+    for (int o = threadIdx.x; o < nin; o += THREADS) {
+      ds[o] = dyb[o];
+      as[o] = ab[o];
+    }
+  }
+  __syncthreads();
+  const int Hb = (g.H + 1) >> 1, Wb = (g.W + 1) >> 1, nb = Hb * Wb;
+  float* xb = dx + p0 * HW;
+  for (int e = threadIdx.x; e < np * nb; e += THREADS) {
+    const int pl = e / nb, q = e - pl * nb;
+    const int m = q / Wb, n = q - m * Wb;
+    const float* dp = ds + pl * HoWo;
+    const uint8_t* ap = as + pl * HoWo;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};  // (2m, 2n), (2m, 2n+1), (2m+1, 2n), (2m+1, 2n+1)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {  // windows in raster order
+      const int oh = m + (w >> 1), ow = n + (w & 1);
+      if (oh >= g.Ho || ow >= g.Wo) continue;
+      const int a = ap[oh * g.Wo + ow];
+      const int kh = a / 3, kw = a - 3 * kh;
+      const int dh = 2 * oh - 1 + kh - 2 * m, dw = 2 * ow - 1 + kw - 2 * n;  // argmax relative to the block
+      if (dh < 0 || dh > 1 || dw < 0 || dw > 1) continue;
+      acc[2 * dh + dw] = add_rn(acc[2 * dh + dw], dp[oh * g.Wo + ow]);
+    }
+    float* xp = xb + (int64_t)pl * HW;
+    const int ih = 2 * m, iw = 2 * n;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      if (ih + dh >= g.H) continue;
+      float* row = xp + (ih + dh) * g.W + iw;
+      row[0] = acc[2 * dh];
+      if (iw + 1 < g.W) row[1] = acc[2 * dh + 1];
+    }
   }
 }
 
@@ -149,7 +224,9 @@ extern "C" int flr_maxpool2d_bwd(const float* dy, const uint8_t* argmax, float* 
   if (H * W > pool::LDS_FLOATS) return FLR_ERR_UNSUPPORTED;
   if (nplanes == 0) return FLR_OK;
   const int ppb = (int)std::max<int64_t>(1, std::min<int64_t>(pool::LDS_FLOATS / (H * W), 64));
-  hipLaunchKernelGGL(pool::bwd_kernel, dim3((unsigned)((nplanes + ppb - 1) / ppb)), dim3(pool::THREADS), 0,
-                     as_stream(stream), dy, argmax, dx, nplanes, ppb, g);
+  auto kern = stride == 2 ? pool::bwd_kernel<2> : stride == 1 ? pool::bwd_kernel<1> : pool::bwd_kernel<0>;
+  if (KH == 3 && KW == 3 && stride == 2 && pad == 1) kern = pool::bwd_k3s2p1_kernel;
+  hipLaunchKernelGGL(kern, dim3((unsigned)((nplanes + ppb - 1) / ppb)), dim3(pool::THREADS), 0, as_stream(stream), dy,
+                     argmax, dx, nplanes, ppb, g);
   return launch_status("maxpool bwd");
 }

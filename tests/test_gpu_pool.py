@@ -12,7 +12,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("shape,k,s,p", [((4, 6, 16, 16), 3, 2, 1), ((2, 5, 7, 9), 3, 2, 1), ((3, 4, 8, 8), 2, 2, 0),
                                          ((2, 3, 5, 5), 3, 1, 1), ((1, 2, 1, 1), 3, 2, 1),
-                                         ((1, 3, 64, 64), 3, 2, 1), ((2, 3, 33, 17), 3, 2, 1)])
+                                         ((1, 3, 64, 64), 3, 2, 1), ((2, 3, 33, 17), 3, 2, 1),
+                                         ((2, 3, 10, 11), 3, 3, 1)])  # stride 3: the generic-stride kernel
 @pytest.mark.parametrize("relu", [False, True])
 def test_maxpool_matches_torch_cpu(cuda, shape, k, s, p, relu):
     g = torch.Generator().manual_seed(sum(shape) + k)
