@@ -128,5 +128,11 @@ int fwd_im2col(const conv::Geom& g, const float* x, const float* w, float* y, vo
                hipStream_t st);
 int wgrad_im2col(const conv::Geom& g, const float* x, const float* dy, float* dw, void* ws, size_t ws_bytes,
                  hipStream_t st, bool have_col);
+// The direct ResNet-stem kernels (train_stem.hip): images staged in LDS, no im2col.
+bool stem_eligible(const conv::Geom& g);
+size_t stem_workspace(const conv::Geom& g);
+int stem_fwd(const conv::Geom& g, const float* x, const float* w, float* y, hipStream_t st);
+int stem_wgrad(const conv::Geom& g, const float* x, const float* dy, float* dw, void* ws, size_t ws_bytes,
+               hipStream_t st);
 }  // namespace convt
 }  // namespace flr

@@ -1210,7 +1210,8 @@ size_t im2col_workspace(const Geom& g) {
   DenseWgt w; w.g = g; w.RP = padded_r(g);
   StemFwd sf; sf.g = g; sf.RP = padded_r(g);
   StemWgt sw; sw.g = g; sw.RP = padded_r(g);
-  return col + wp + std::max(std::max(splits_bytes(f), splits_bytes(w)), std::max(splits_bytes(sf), splits_bytes(sw)));
+  const size_t gemm = col + wp + std::max(std::max(splits_bytes(f), splits_bytes(w)), std::max(splits_bytes(sf), splits_bytes(sw)));
+  return std::max(gemm, stem_eligible(g) ? stem_workspace(g) : 0);
 }
 
 static int run_im2col(const Geom& g, const float* x, float* col, hipStream_t st) {
@@ -1220,10 +1221,16 @@ static int run_im2col(const Geom& g, const float* x, float* col, hipStream_t st)
   return launch_status("conv im2col");
 }
 
-// FLR_STEM=col: the explicit im2col column matrix (A/B timing); default: gathered operand
+// FLR_STEM=col: the explicit im2col column matrix; =gather: the tiled GEMM with the
+// im2col operand gathered on the fly (A/B timing); default: the direct stem
+// kernels (train_stem.hip) where eligible, else the gathered GEMM.
 inline bool stem_col() {
   const char* e = getenv("FLR_STEM");
   return e && e[0] == 'c';
+}
+inline bool stem_direct(const Geom& g) {
+  const char* e = getenv("FLR_STEM");
+  return !(e && (e[0] == 'c' || e[0] == 'g')) && stem_eligible(g);
 }
 
 template <class Plan>
@@ -1235,6 +1242,7 @@ inline void stem_divs(Plan& pl, const Geom& g) {
 
 int fwd_im2col(const Geom& g, const float* x, const float* w, float* y, void* ws, size_t ws_bytes, hipStream_t st) {
   if (!ws || ws_bytes < im2col_workspace(g)) return FLR_ERR_WORKSPACE;
+  if (stem_direct(g)) return stem_fwd(g, x, w, y, st);
   const int RP = padded_r(g), R = g.Cin * g.KH * g.KW;
   char* base = static_cast<char*>(ws);
   float* col = reinterpret_cast<float*>(base);
@@ -1261,6 +1269,7 @@ int fwd_im2col(const Geom& g, const float* x, const float* w, float* y, void* ws
 int wgrad_im2col(const Geom& g, const float* x, const float* dy, float* dw, void* ws, size_t ws_bytes,
                  hipStream_t st, bool have_col) {
   if (!ws || ws_bytes < im2col_workspace(g)) return FLR_ERR_WORKSPACE;
+  if (stem_direct(g)) return stem_wgrad(g, x, dy, dw, ws, ws_bytes, st);
   const int RP = padded_r(g), R = g.Cin * g.KH * g.KW;
   char* base = static_cast<char*>(ws);
   float* col = reinterpret_cast<float*>(base);

@@ -14,7 +14,10 @@ def cb(t):
     return t.transpose(0, 1).contiguous()
 
 SHAPES = [  # (K, B, Cin, H, W, Cout, KH, stride, pad)
-    (3, 4, 3, 32, 32, 8, 7, 2, 3),     # stem 7x7/2
+    (3, 4, 3, 32, 32, 8, 7, 2, 3),     # stem 7x7/2 (direct stem kernels, Cout < 64)
+    (2, 8, 3, 32, 32, 64, 7, 2, 3),    # the C3 stem: two image groups per client
+    (2, 4, 3, 32, 32, 72, 7, 2, 3),    # stem, Cout past one 64-channel block
+    (2, 5, 3, 32, 32, 16, 7, 2, 3),    # stem, B not a multiple of 4: the gathered GEMM
     (3, 4, 8, 8, 8, 8, 3, 1, 1),       # layer1 3x3
     (2, 4, 8, 8, 8, 16, 3, 2, 1),      # layer2 first conv, stride 2
     (2, 4, 8, 8, 8, 16, 1, 2, 0),      # downsample 1x1/2
