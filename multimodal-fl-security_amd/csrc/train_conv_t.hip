@@ -160,6 +160,7 @@ inline int gemm_form() {
   if (e && e[0] == 'f') return 0;
   if (e && e[0] == 'c') return 1;
   if (e && e[0] == 'A') return 3;  // ablation (timing only, wrong results): one bf16 term, no split
+  if (e && e[0] == 'o') return 4;  // the unpipelined product-major loop (A/B timing)
   return 2;
 }
 
@@ -232,8 +233,10 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
     kw = uni(kw);
     const int HW = (int)g.sxc;  // channel stride
     const int ih = s.ih0 + kh, iw = s.iw0 + kw;
-    const bool ok = s.nok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-    const unsigned vb = ok ? (unsigned)((s.xoff + ih * g.W + iw) * 4) : SENT;
+    // bitwise & (no short-circuit): the gather stays branch-free, one basic block with the MFMAs
+    const bool ok = s.nok & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
+    const unsigned addr = (unsigned)((s.xoff + ih * g.W + iw) * 4);
+    const unsigned vb = ok ? addr : SENT;
     const int cb = ci0 * HW * 4;
 #pragma unroll
     for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, cb + i * 4 * HW * 4);
@@ -309,8 +312,9 @@ struct DgradT {
     // the class guarantees (ih + pad - kh) % stride == 0
     const int nh = s.ih - kh, nw = s.iw - kw;
     const int oh = g.stride == 1 ? nh : nh / g.stride, ow = g.stride == 1 ? nw : nw / g.stride;
-    const bool ok = s.nok && nh >= 0 && nw >= 0 && oh < g.Ho && ow < g.Wo;
-    const unsigned vb = ok ? (unsigned)((s.yoff + oh * g.Wo + ow) * 4) : SENT;
+    const bool ok = s.nok & (nh >= 0) & (nw >= 0) & (oh < g.Ho) & (ow < g.Wo);
+    const unsigned addr = (unsigned)((s.yoff + oh * g.Wo + ow) * 4);
+    const unsigned vb = ok ? addr : SENT;
     const int cs = (int)g.syc;  // channel stride
     const int cb0 = co0 * cs * 4;
 #pragma unroll
@@ -394,8 +398,9 @@ struct WgtT {
       const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
       const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
       const int ih = (int)oh * g.stride - g.pad + s.kh, iw = (int)ow * g.stride - g.pad + s.kw;
-      const bool ok = q < R && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-      const unsigned va = ok ? (unsigned)(((int)(bb * g.sxb) + s.aoff + ih * g.W + iw) * 4) : SENT;
+      const bool ok = (q < R) & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
+      const unsigned addr = (unsigned)(((int)(bb * g.sxb) + s.aoff + ih * g.W + iw) * 4);
+      const unsigned va = ok ? addr : SENT;
 #pragma unroll
       for (int i = 0; i < 8; ++i) a[i] = ld1(s.ra, va, i * 8 * (int)g.sxc * 4);
     }
@@ -602,8 +607,9 @@ struct StemFwd {  // y[co][pix] = sum_r wp[co][r] x(pix; r): M = Cout, N = B*Ho*
       const int ci = uni((int)udiv((uint32_t)r, d_kk)), rem = r - ci * KK;
       const int kh = uni((int)udiv((uint32_t)rem, d_kw)), kw = rem - kh * g.KW;
       const int ih = s.ih0 + kh, iw = s.iw0 + kw;
-      const bool ok = s.nok && r < RR && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-      const unsigned vb = ok ? (unsigned)((s.xoff + ih * g.W + iw) * 4) : SENT;
+      const bool ok = s.nok & (r < RR) & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
+      const unsigned addr = (unsigned)((s.xoff + ih * g.W + iw) * 4);
+      const unsigned vb = ok ? addr : SENT;
       b[i] = ld1(s.rb, vb, uni(ci * (int)g.sxc * 4));
     }
   }
@@ -676,8 +682,9 @@ struct StemWgt {  // dwp[co][r] = sum_pix dy[co][pix] x(pix; r): M = Cout, N = R
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int ih = ih0 + s.kh[e], iw = iw0 + s.kw[e];
-        const bool ok = q < R && s.kh[e] >= 0 && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-        b[4 * i + e] = ld1(s.rb, ok ? (unsigned)((base + s.roff[e]) * 4) : SENT, 0);
+        const bool ok = (q < R) & (s.kh[e] >= 0) & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
+        const unsigned addr = (unsigned)((base + s.roff[e]) * 4);
+        b[4 * i + e] = ld1(s.rb, ok ? addr : SENT, 0);
       }
     }
   }
@@ -767,8 +774,9 @@ struct BGemm : BGemmArgs {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int row = base_row + tid / 8 + 32 * i;
-        const bool ok = row < rows && kk < R;
-        const f32x4 q = ld4(rs, ok ? (unsigned)((row * s_row + kk) * 4) : SENT, 0);
+        const bool ok = (row < rows) & (kk < R);
+        const unsigned addr = (unsigned)((row * s_row + kk) * 4);
+        const f32x4 q = ld4(rs, ok ? addr : SENT, 0);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[4 * i + e] = q[e];
       }
@@ -777,8 +785,9 @@ struct BGemm : BGemmArgs {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int kk = r0 + tid / 16 + 16 * i;
-        const bool ok = row < rows && kk < R;
-        const f32x4 q = ld4(rs, ok ? (unsigned)((kk * s_r + row) * 4) : SENT, 0);
+        const bool ok = (row < rows) & (kk < R);
+        const unsigned addr = (unsigned)((kk * s_r + row) * 4);
+        const f32x4 q = ld4(rs, ok ? addr : SENT, 0);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[4 * i + e] = q[e];
       }
@@ -787,8 +796,9 @@ struct BGemm : BGemmArgs {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int row = base_row + tid / 32 + 8 * i;
-        const bool ok = row < rows && kk < R;
-        v[i] = ld1(rs, ok ? (unsigned)((row * s_row + kk * s_r) * 4) : SENT, 0);
+        const bool ok = (row < rows) & (kk < R);
+        const unsigned addr = (unsigned)((row * s_row + kk * s_r) * 4);
+        v[i] = ld1(rs, ok ? addr : SENT, 0);
       }
     }
   }
@@ -951,6 +961,65 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
 #pragma unroll
     for (int j = 0; j < NS; ++j) stash<Plan::LB>(Bs[buf][j], rb[j], tid);
   };
+  if constexpr (X6 == 2) {
+    // Software-pipelined bf16x6 loop (the default form).  A wave issues in
+    // order, so its fragment reads, bf16 splits, LDS stash and global loads
+    // only overlap its own MFMAs when they sit between them in one basic
+    // block.  Per K-tile t (two 16-deep k-steps, fragments F of step 0 ready):
+    //   phase 0: MFMAs of step 0 || read + split step 1 -> F1, stash tile t+1
+    //   barrier (publishes tile t+1; every read of the buffer it reuses is done)
+    //   phase 1: MFMAs of step 1 || global loads of tile t+2, read + split
+    //            step 0 of tile t+1 -> F0
+    // Tiles past the last are clamped to it (duplicate loads / stashes / splits
+    // that nothing consumes), so both phases are branch-free.
+    static_assert(BK == 32, "two k-steps per K-tile");
+    const int ntile = rend > rbeg ? (rend - rbeg + BK - 1) / BK : 0;
+    if (ntile > 0) {
+      const int rlast = rbeg + (ntile - 1) * BK;
+      bf16x8 ah0[MS], am0[MS], al0[MS], bh0[NS], bm0[NS], bl0[NS];
+      bf16x8 ah1[MS], am1[MS], al1[MS], bh1[NS], bm1[NS], bl1[NS];
+      float va[MS][8], vb[NS][8];
+      auto read_frags = [&](int buf, int s) {
+#pragma unroll
+        for (int i = 0; i < MS; ++i) frag8<Plan::LA>(As[buf][i], 32 * wm + l32, 16 * s + 8 * h, va[i]);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) frag8<Plan::LB>(Bs[buf][j], 32 * wn + l32, 16 * s + 8 * h, vb[j]);
+      };
+#define FLR_SPLIT_ALL(AH, AM, AL, BH, BM, BL)                                       \
+  _Pragma("unroll") for (int i = 0; i < MS; ++i) split3(va[i], AH[i], AM[i], AL[i]); \
+  _Pragma("unroll") for (int j = 0; j < NS; ++j) split3(vb[j], BH[j], BM[j], BL[j]);
+#define FLR_X6P(AV, BV)                                                                           \
+  _Pragma("unroll") for (int i = 0; i < MS; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(AV[i], BV[j], acc[i][j], 0, 0, 0);
+#define FLR_X6P_ALL(AH, AM, AL, BH, BM, BL) \
+  FLR_X6P(AM, BM) FLR_X6P(AH, BL) FLR_X6P(AL, BH) FLR_X6P(AH, BM) FLR_X6P(AM, BH) FLR_X6P(AH, BH)
+      load(rbeg);
+      stash_all(0);
+      __syncthreads();
+      load(std::min(rbeg + BK, rlast));
+      read_frags(0, 0);
+      FLR_SPLIT_ALL(ah0, am0, al0, bh0, bm0, bl0)
+      int cur = 0;
+      for (int t = 0; t < ntile; ++t) {
+        const int r0 = rbeg + t * BK;
+        // phase 0
+        read_frags(cur, 1);
+        FLR_X6P_ALL(ah0, am0, al0, bh0, bm0, bl0)
+        FLR_SPLIT_ALL(ah1, am1, al1, bh1, bm1, bl1)
+        stash_all(cur ^ 1);
+        __syncthreads();
+        // phase 1
+        load(std::min(r0 + 2 * BK, rlast));
+        read_frags(cur ^ 1, 0);
+        FLR_X6P_ALL(ah1, am1, al1, bh1, bm1, bl1)
+        FLR_SPLIT_ALL(ah0, am0, al0, bh0, bm0, bl0)
+        cur ^= 1;
+      }
+#undef FLR_SPLIT_ALL
+#undef FLR_X6P
+#undef FLR_X6P_ALL
+    }
+  } else {
   if (rbeg < rend) {
     load(rbeg);
     stash_all(0);
@@ -987,7 +1056,7 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
           }
         }
         if (prio) __builtin_amdgcn_s_setprio(1);
-        if constexpr (X6 >= 2) {
+        if constexpr (X6 >= 3) {
           // product-major: the MS*NS accumulator chains interleave, so a chain's
           // next MFMA never waits on its own previous one (small terms first)
 #define FLR_X6_STEP(AV, BV)                                                              \
@@ -1041,6 +1110,7 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
     __syncthreads();
     cur ^= 1;
   }
+  }  // old loop (FLR_GEMM=f32 | chain | old | A)
   // C/D map of the 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
 #pragma unroll
   for (int i = 0; i < MS; ++i)
@@ -1156,7 +1226,7 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   int S = choose_splits(M, N, R, K, MS * NS, plan_min_kt<Plan>());
   if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) S = 1;
   const dim3 grid((unsigned)cdiv(N, BN * NS), (unsigned)cdiv(M, BM * MS), (unsigned)(K * S));
-  switch (MS * NS == 1 && gemm_form() == 2 ? 1 : gemm_form()) {  // one tile: the two orders coincide
+  switch (gemm_form()) {  // every form keeps each accumulator's product order: results do not depend on it
     case 0:
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 0>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());
@@ -1167,6 +1237,10 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
       break;
     case 3:
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 3>), grid, dim3(THREADS), 0, st, pl, S,
+                         static_cast<float*>(ws), xcd_remap(), mfma_prio());
+      break;
+    case 4:
+      hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 4>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());
       break;
     default:
