@@ -153,15 +153,17 @@ inline int mfma_prio() {  // measured +0-5 % on the encoder GEMMs and the 3x3 co
 }
 
 // 0: exact f32 MFMA; 1: bf16x6, accumulator-chain order (each output tile's six
-// products back to back); 2: bf16x6, product-major order (the tiles' chains
-// interleave; the default).  FLR_GEMM=f32 | chain | (unset).
+// products back to back); 2: bf16x6, product-major, software-pipelined; 4: the
+// same unpipelined; 5 (default): split at stash time where the plan supports
+// it (fwd / dgrad / batched GEMM), else 2.  FLR_GEMM=f32 | chain | pipe | old | stash.
 inline int gemm_form() {
   const char* e = getenv("FLR_GEMM");
   if (e && e[0] == 'f') return 0;
   if (e && e[0] == 'c') return 1;
   if (e && e[0] == 'A') return 3;  // ablation (timing only, wrong results): one bf16 term, no split
   if (e && e[0] == 'o') return 4;  // the unpipelined product-major loop (A/B timing)
-  return 2;
+  if (e && e[0] == 'p') return 2;  // the pipelined loop for every plan
+  return 5;  // split at stash (bf16 LDS images) where the plan has k8 loads, else pipelined
 }
 
 // ---- load plans ---------------------------------------------------------------
@@ -247,6 +249,53 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
   __device__ float* out() const { return y; }
   __device__ int64_t tile_base(int k, int m0, int n0) const { return k * g.syk + m0 * g.syc + n0; }
   __device__ int64_t ldm() const { return g.syc; }
+  // ---- k-contiguous loads for the split-at-stash kernel: thread (row = tid & 63,
+  // k = 8 (tid >> 6) .. +7) of a 64 x 32 sub-tile
+  struct State8 {
+    rsrc_t ra, rb;
+    unsigned a0;
+    int ih0, iw0, xoff;
+    bool nok;
+  };
+  __device__ State8 init8(int k, int m0, int n0, int tid) const {
+    State8 s;
+    const int KK = g.KH * g.KW;
+    const int row = tid & 63, k0 = 8 * (tid >> 6);
+    s.ra = make_rsrc(w + (int64_t)k * KK * g.Cin * g.Cout, (int64_t)KK * g.Cin * g.Cout);
+    s.rb = make_rsrc(x + k * g.sxk, g.xext);
+    s.a0 = (unsigned)((k0 * g.Cout + m0 + row) * 4);
+    const int n = n0 + row;
+    s.nok = n < N();
+    const uint32_t bb = udiv(n, g.d_howo), p = n - bb * g.Ho * g.Wo;
+    const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+    s.ih0 = (int)oh * g.stride - g.pad;
+    s.iw0 = (int)ow * g.stride - g.pad;
+    s.xoff = (int)(bb * g.sxb + k0 * g.sxc);
+    return s;
+  }
+  __device__ void load_a8(const State8& s, int r0, float (&a)[8]) const {  // A(co, ci): lanes along co
+    const int slot = uni(r0 / g.Cin), ci0 = r0 - slot * g.Cin;
+    int kh, kw;
+    slot_tap(g, slot, kh, kw);
+    const int arow = uni(((kh * g.KW + kw) * g.Cin + ci0) * g.Cout * 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = ld1(s.ra, s.a0, arow + e * g.Cout * 4);
+  }
+  __device__ void load_b8(const State8& s, int r0, float (&b)[8]) const {  // B(pixel, ci): 8 channels
+    const int slot = uni(r0 / g.Cin), ci0 = r0 - slot * g.Cin;
+    int kh, kw;
+    slot_tap(g, slot, kh, kw);
+    kh = uni(kh);
+    kw = uni(kw);
+    const int HW = (int)g.sxc;
+    const int ih = s.ih0 + kh, iw = s.iw0 + kw;
+    const bool ok = s.nok & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
+    const unsigned addr = (unsigned)((s.xoff + ih * g.W + iw) * 4);
+    const unsigned vb = ok ? addr : SENT;
+    const int cb = ci0 * HW * 4;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = ld1(s.rb, vb, cb + e * HW * 4);
+  }
 };
 
 // dx = conv^T(dy, W_t) over ONE stride-parity class of input pixels:
@@ -331,6 +380,56 @@ struct DgradT {
   __device__ float* out() const { return dx; }
   __device__ int64_t tile_base(int k, int m0, int n0) const { return k * g.sxk + m0 * g.sxc + n0; }
   __device__ int64_t ldm() const { return g.sxc; }
+  struct State8 {
+    rsrc_t ra, rb;
+    unsigned a0;
+    int ih, iw, yoff;
+    bool nok;
+  };
+  __device__ State8 init8(int k, int m0, int n0, int tid) const {
+    State8 s;
+    const int KK = g.KH * g.KW;
+    const int row = tid & 63, k0 = 8 * (tid >> 6);
+    s.ra = make_rsrc(w + (int64_t)k * KK * g.Cin * g.Cout, (int64_t)KK * g.Cin * g.Cout);
+    s.rb = make_rsrc(dy + k * g.syk, g.yext);
+    s.a0 = (unsigned)(((m0 + row) * g.Cout + k0) * 4);
+    const int n = n0 + row;
+    s.nok = n < N();
+    const uint32_t bb = udiv(n, d_hcwc), p = n - bb * Hc * Wc;
+    const uint32_t ihc = udiv(p, d_wc), iwc = p - ihc * Wc;
+    s.ih = ca + (int)ihc * g.stride + g.pad;
+    s.iw = cb + (int)iwc * g.stride + g.pad;
+    s.yoff = (int)(bb * g.syb + k0 * g.syc);
+    return s;
+  }
+  __device__ void load_a8(const State8& s, int r0, float (&a)[8]) const {  // A(ci, co): 8 consecutive co
+    const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
+    int kh, kw;
+    conv::rect_tap(crect, slot, kh, kw);
+    const int abase = uni(((kh * g.KW + kw) * g.Cin * g.Cout + co0) * 4);
+    const f32x4 q0 = ld4(s.ra, s.a0, abase), q1 = ld4(s.ra, s.a0, abase + 16);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] = q0[e];
+      a[4 + e] = q1[e];
+    }
+  }
+  __device__ void load_b8(const State8& s, int r0, float (&b)[8]) const {  // B(input pixel, co): 8 channels
+    const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
+    int kh, kw;
+    conv::rect_tap(crect, slot, kh, kw);
+    kh = uni(kh);
+    kw = uni(kw);
+    const int nh = s.ih - kh, nw = s.iw - kw;
+    const int oh = g.stride == 1 ? nh : nh / g.stride, ow = g.stride == 1 ? nw : nw / g.stride;
+    const bool ok = s.nok & (nh >= 0) & (nw >= 0) & (oh < g.Ho) & (ow < g.Wo);
+    const unsigned addr = (unsigned)((s.yoff + oh * g.Wo + ow) * 4);
+    const unsigned vb = ok ? addr : SENT;
+    const int cs = (int)g.syc;
+    const int cb0 = co0 * cs * 4;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = ld1(s.rb, vb, cb0 + e * cs * 4);
+  }
 };
 
 // The parity classes of a dgrad (stride^2 of them, fewer when H or W < stride).
@@ -435,6 +534,58 @@ struct WgtT {
     return (((int64_t)k * g.KH * g.KW + tap_index(g, slot)) * g.Cin + ci0) * g.Cout + n0;
   }
   __device__ int64_t ldm() const { return g.Cout; }
+  struct State8 {
+    rsrc_t ra, rb;
+    int kh, kw, k0;
+    unsigned aoff, boff;
+  };
+  __device__ State8 init8(int k, int m0, int n0, int tid) const {
+    State8 s;
+    s.ra = make_rsrc(x + k * g.sxk, g.xext);
+    s.rb = make_rsrc(dy + k * g.syk, g.yext);
+    const int slot = uni(m0 / g.Cin), ci0 = m0 - slot * g.Cin;
+    int kh, kw;
+    slot_tap(g, slot, kh, kw);
+    s.kh = uni(kh);
+    s.kw = uni(kw);
+    const int row = tid & 63;
+    s.k0 = uni(8 * (tid >> 6));  // the wave's k-group: its 8 pixels are wave-uniform
+    s.aoff = (unsigned)((ci0 + row) * g.sxc * 4);
+    s.boff = (unsigned)((n0 + row) * g.syc * 4);
+    return s;
+  }
+  // A(ci, pixel q): the 8 pixels of the wave's k-group are wave-uniform, so their
+  // decomposition and padding test run on the scalar unit (soffset per pixel)
+  __device__ void load_a8(const State8& s, int r0, float (&a)[8]) const {
+    const int R = this->R(), HoWo = g.Ho * g.Wo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int q = uni(r0 + s.k0 + e);
+      const int bb = uni((int)udiv((uint32_t)q, g.d_howo)), p = q - bb * HoWo;
+      const int oh = uni((int)udiv((uint32_t)p, g.d_wo)), ow = p - oh * g.Wo;
+      const int ih = oh * g.stride - g.pad + s.kh, iw = ow * g.stride - g.pad + s.kw;
+      const bool ok = (q < R) & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
+      const int soff = uni(ok ? (bb * (int)g.sxb + ih * g.W + iw) * 4 : 0);
+      a[e] = ld1(s.ra, ok ? s.aoff : SENT, soff);
+    }
+  }
+  // B(co, q): dy[co][q], q contiguous per channel
+  __device__ void load_b8(const State8& s, int r0, float (&b)[8]) const {
+    const int R = this->R();
+    const int q0 = r0 + s.k0;
+    if constexpr (BVEC) {  // syc % 4 == 0, R % 4 == 0
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = q0 + 4 * i < R;
+        const f32x4 v = ld4(s.rb, ok ? s.boff + (unsigned)((q0 + 4 * i) * 4) : SENT, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b[4 * i + e] = v[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b[e] = ld1(s.rb, (q0 + e < R) ? s.boff + (unsigned)((q0 + e) * 4) : SENT, 0);
+    }
+  }
 };
 
 // ---- explicit im2col (short reductions: the stem) -----------------------------
@@ -829,6 +980,38 @@ struct BGemm : BGemmArgs {
   __device__ float* out() const { return c; }
   __device__ int64_t tile_base(int k, int m0, int n0) const { return k * c_k + m0 * c_m + n0; }
   __device__ int64_t ldm() const { return c_m; }
+  using State8 = State;
+  template <int MODE>
+  __device__ static void load_op8(rsrc_t rs, int base_row, int rows, int r0, int R, int64_t s_row, int64_t s_r,
+                                  float (&v)[8]) {
+    const int tid = threadIdx.x;
+    const int row = base_row + (tid & 63), kk0 = r0 + 8 * (tid >> 6);
+    const bool rok = row < rows;
+    if constexpr (MODE == BM_RK) {  // r contiguous, R % 4 == 0
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = rok & (kk0 + 4 * i < R);
+        const unsigned addr = (unsigned)((row * s_row + kk0 + 4 * i) * 4);
+        const f32x4 q = ld4(rs, ok ? addr : SENT, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * i + e] = q[e];
+      }
+    } else {  // KR (rows contiguous: lanes coalesce) and G
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = rok & (kk0 + e < R);
+        const unsigned addr = (unsigned)((row * s_row + (kk0 + e) * s_r) * 4);
+        v[e] = ld1(rs, ok ? addr : SENT, 0);
+      }
+    }
+  }
+  __device__ State8 init8(int k, int m0, int n0, int tid) const { return init(k, m0, n0, tid); }
+  __device__ void load_a8(const State8& s, int r0, float (&v)[8]) const {
+    load_op8<AM>(s.ra, s.arow, m, r0, r, a_m, a_r, v);
+  }
+  __device__ void load_b8(const State8& s, int r0, float (&v)[8]) const {
+    load_op8<BMD>(s.rb, s.brow, n, r0, r, b_n, b_r, v);
+  }
 };
 
 // out[k][n] = sum_m X[k][m][n] (bias gradients of the batched GEMMs).  Eight
@@ -1140,6 +1323,148 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
     }
 }
 
+// ---- the split-at-stash form (FLR_GEMM=stash) ------------------------------
+// Each value is split into bf16 hi/mid/lo ONCE, by the thread that loaded it,
+// instead of once per wave that reads its fragment: the LDS holds three bf16
+// images per sub-tile, [64 rows][SB] with the row stride 80 B (20 dwords =
+// 4 x odd: conflict-free ds_read_b128 / ds_write_b128), and an MFMA fragment is
+// one ds_read_b128 per term.  The loads are k-contiguous (thread: row tid & 63,
+// k 8 (tid >> 6) .. +7, the plans' init8 / load_a8 / load_b8), so a thread's
+// stash is three 16-B writes per sub-tile.  Single LDS buffer, two barriers
+// per K-tile; the split of tile t+1 sits between tile t's MFMAs.  Every
+// accumulator sees the same bf16 products in the same order as the other
+// bf16x6 forms: the results are bit-identical to them.
+constexpr int SB = 40;            // bf16 per image row (32 + 8 pad)
+constexpr int TERM_B = 64 * SB;   // bf16 per term image
+template <class P> struct has_k8 : std::false_type {};
+template <> struct has_k8<FwdT> : std::true_type {};
+template <> struct has_k8<DgradT> : std::true_type {};
+// WgtT has k8 loads but stays on the pipelined form: its x operand is k-contiguous
+// only along pixels, so the k8 mapping puts the lanes on channels (sxc apart, a
+// cache line per lane): l1 wgrad 202 -> 366 us measured.
+template <int A, int B> struct has_k8<BGemm<A, B>> : std::true_type {};
+
+template <class Plan, int MS, int NS>
+__global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S, float* __restrict__ part,
+                                                            int remap) {
+  __shared__ __attribute__((aligned(16))) __bf16 Ls[MS + NS][3][TERM_B];
+  int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
+  if (remap) xcd_tile(bx, by, bz);
+  const int k = bz / S, split = bz % S;
+  const int M = pl.M(), N = pl.N(), R = pl.R();
+  const int ktiles = cdiv(R, BK);
+  const int rbeg = (int)((int64_t)ktiles * split / S) * BK;
+  const int rend = std::min(R, (int)((int64_t)ktiles * (split + 1) / S) * BK);
+  const int m0 = by * BM * MS, n0 = bx * BN * NS;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int srow = tid & 63, sk = 8 * (tid >> 6);  // this thread's stash row and k offset
+
+  typename Plan::State8 sa[MS], sb[NS];
+#pragma unroll
+  for (int i = 0; i < MS; ++i) sa[i] = pl.init8(k, m0 + BM * i, n0, tid);
+#pragma unroll
+  for (int j = 0; j < NS; ++j) sb[j] = pl.init8(k, m0, n0 + BN * j, tid);
+  float ra[MS][8], rb[NS][8];
+  bf16x8 pa[MS][3], pb[NS][3];
+  f32x16 acc[MS][NS];
+#pragma unroll
+  for (int i = 0; i < MS; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  auto load = [&](int r) {
+#pragma unroll
+    for (int i = 0; i < MS; ++i) pl.load_a8(sa[i], r, ra[i]);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) pl.load_b8(sb[j], r, rb[j]);
+  };
+  auto split_all = [&]() {
+#pragma unroll
+    for (int i = 0; i < MS; ++i) split3(ra[i], pa[i][0], pa[i][1], pa[i][2]);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) split3(rb[j], pb[j][0], pb[j][1], pb[j][2]);
+  };
+  auto write_all = [&]() {
+#pragma unroll
+    for (int i = 0; i < MS; ++i)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[i][t][srow * SB + sk]) = pa[i][t];
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[MS + j][t][srow * SB + sk]) = pb[j][t];
+  };
+  const int ntile = rend > rbeg ? (rend - rbeg + BK - 1) / BK : 0;
+  if (ntile > 0) {
+    const int rlast = rbeg + (ntile - 1) * BK;
+    load(rbeg);
+    split_all();
+    write_all();
+    load(std::min(rbeg + BK, rlast));
+    __syncthreads();
+    for (int t = 0; t < ntile; ++t) {
+      const int r0 = rbeg + t * BK;
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        bf16x8 fa[MS][3], fb[NS][3];
+        const int ko = 16 * s + 8 * h;
+#pragma unroll
+        for (int i = 0; i < MS; ++i)
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            fa[i][q] = *reinterpret_cast<const bf16x8*>(&Ls[i][q][(32 * wm + l32) * SB + ko]);
+#pragma unroll
+        for (int j = 0; j < NS; ++j)
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            fb[j][q] = *reinterpret_cast<const bf16x8*>(&Ls[MS + j][q][(32 * wn + l32) * SB + ko]);
+#define FLR_SX(TA, TB)                                                                              \
+  _Pragma("unroll") for (int i = 0; i < MS; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][TA], fb[j][TB], acc[i][j], 0, 0, 0);
+        // product-major, small terms first (term 0 = hi, 1 = mid, 2 = lo)
+        FLR_SX(1, 1) FLR_SX(0, 2) FLR_SX(2, 0) FLR_SX(0, 1) FLR_SX(1, 0) FLR_SX(0, 0)
+#undef FLR_SX
+      }
+      split_all();      // tile t+1 (clamped: a duplicate that nothing reads after the last tile)
+      __syncthreads();  // every wave's fragment reads of tile t are done
+      write_all();
+      load(std::min(r0 + 2 * BK, rlast));
+      __syncthreads();
+    }
+  }
+  // C/D map of the 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < MS; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int tm0 = m0 + BM * i, tn0 = n0 + BN * j;
+      if (S == 1 && pl.linear()) {
+        float* base = pl.out() + pl.tile_base(k, tm0, tn0);
+        const int64_t ldm = pl.ldm();
+        const int nl = 32 * wn + l32;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int ml = 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (tm0 + ml < M && tn0 + nl < N) base[ml * ldm + nl] = acc[i][j][e];
+        }
+        continue;
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = tm0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int n = tn0 + 32 * wn + l32;
+        if (m < M && n < N) {
+          if (S == 1) pl.store(k, m, n, acc[i][j][e]);
+          else part[(((int64_t)split * pl.g.Kc + k) * M + m) * N + n] = acc[i][j][e];
+        }
+      }
+    }
+}
+
 template <class Plan>
 __global__ void treduce_kernel(const Plan pl, int S, const float* __restrict__ part) {
   // grid (cdiv(M*N, 256), K): one client per grid row, 32-bit index math
@@ -1226,7 +1551,18 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   int S = choose_splits(M, N, R, K, MS * NS, plan_min_kt<Plan>());
   if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) S = 1;
   const dim3 grid((unsigned)cdiv(N, BN * NS), (unsigned)cdiv(M, BM * MS), (unsigned)(K * S));
-  switch (gemm_form()) {  // every form keeps each accumulator's product order: results do not depend on it
+  int form = gemm_form();
+  if constexpr (has_k8<Plan>::value) {
+    if (form == 5) {
+      hipLaunchKernelGGL((sgemm_kernel<Plan, MS, NS>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
+                         xcd_remap());
+      form = -1;
+    }
+  }
+  if (form == 5) form = 2;  // plans without k8 loads
+  switch (form) {  // every form keeps each accumulator's product order: results do not depend on it
+    case -1:
+      break;
     case 0:
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 0>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());

@@ -102,3 +102,48 @@ def test_tap_major_conv_vs_fp64(cuda, shape):
         err = (got.detach().cpu().double() - ref.detach()).abs().max().item()
         scale = ref.detach().abs().max().item()
         assert err <= _tol(shape, which) * max(scale, 1.0), (which, err, scale)
+
+
+def _run_tap_major(cuda, shape, seed):
+    from flr.models.multimodal import to_tap_major
+    from flr.nn import client_conv2d_t
+    K, B, Cin, H, W, Cout, KS, stride, pad = shape
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(B, K * Cin, H, W, generator=g)
+    w = torch.randn(K, Cout, Cin, KS, KS, generator=g) * 0.1
+    xg = cb(x).to(cuda).requires_grad_(True)
+    wt = to_tap_major(w).contiguous().to(cuda).requires_grad_(True)
+    y = client_conv2d_t(xg, wt, stride, pad)
+    dy = torch.randn(y.shape, generator=g).to(cuda)
+    y.backward(dy)
+    torch.cuda.synchronize()
+    return y.detach().clone(), xg.grad.clone(), wt.grad.clone()
+
+
+@pytest.mark.parametrize("form", ["pipe", "old"])
+@pytest.mark.parametrize("shape", TAP_SHAPES, ids=[str(s) for s in TAP_SHAPES])
+def test_gemm_forms_bit_identical(cuda, shape, form, monkeypatch):
+    """Every bf16x6 form (FLR_GEMM: the default split at stash time (bf16 LDS
+    images) where the plan supports it, "pipe", "old") feeds each
+    accumulator the same products in the same order: bit-identical results."""
+    ref = _run_tap_major(cuda, shape, 7)
+    monkeypatch.setenv("FLR_GEMM", form)
+    got = _run_tap_major(cuda, shape, 7)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dims", [(3, 32, 768, 256), (2, 200, 130, 96), (4, 64, 64, 48)])
+def test_bgemm_forms_bit_identical(cuda, dims, monkeypatch):
+    from flr.nn import bgemm
+    K, M, N, R = dims
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    A = torch.randn(K, M, R, generator=g).to(cuda)
+    Bm = torch.randn(K, N, R, generator=g).to(cuda)
+    outs = []
+    for form in (None, "pipe"):
+        if form:
+            monkeypatch.setenv("FLR_GEMM", form)
+        outs += [bgemm(A, Bm).clone(), bgemm(A.transpose(1, 2).contiguous().transpose(1, 2), Bm).clone()]
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
