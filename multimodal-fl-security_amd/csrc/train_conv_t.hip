@@ -1514,9 +1514,22 @@ inline int bgemm_min_kt() {
   return v;
 }
 
+// Fewest K-tiles per conv split-K part.  32 (measured per layer against 8 and 16,
+// tools/conv_bench.py): a workgroup's unhidden prologue (first load, split,
+// barrier) amortises over more K-tiles; the l3b / l4 forward and dgrad gain the
+// most.  FLR_CONV_MINKT overrides (A/B timing).
+inline int conv_min_kt() {
+  static const int v = [] {
+    const char* e = getenv("FLR_CONV_MINKT");
+    const int x = e ? atoi(e) : 0;
+    return x >= 1 && x <= 256 ? x : 32;
+  }();
+  return v;
+}
+
 template <class Plan>
 inline int plan_min_kt() {
-  return std::is_base_of<BGemmArgs, Plan>::value ? bgemm_min_kt() : 8;
+  return std::is_base_of<BGemmArgs, Plan>::value ? bgemm_min_kt() : conv_min_kt();
 }
 
 template <class Plan>
