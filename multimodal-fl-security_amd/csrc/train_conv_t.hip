@@ -1529,7 +1529,11 @@ inline int conv_min_kt() {
 
 template <class Plan>
 inline int plan_min_kt() {
-  return std::is_base_of<BGemmArgs, Plan>::value ? bgemm_min_kt() : conv_min_kt();
+  if (std::is_base_of<BGemmArgs, Plan>::value) return bgemm_min_kt();
+  // a dgrad parity class has few tiles per client (l3a: one 128 x 128 tile):
+  // it keeps the deeper split-K, or the launch runs ~128 workgroups on 256 CUs
+  if (std::is_same<Plan, DgradT>::value) return 8;
+  return conv_min_kt();
 }
 
 template <class Plan>
@@ -1607,7 +1611,12 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
 template <class Plan>
 int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   if (pl.R() == 0 && !std::is_same<Plan, DgradT>::value) return FLR_OK;  // a dgrad class with no tap stores zeros
-  switch (tile_choice(pl.M(), pl.N(), pl.R())) {
+  int tile = tile_choice(pl.M(), pl.N(), pl.R());
+  // dgrad with 64 input channels (layer1): 64 x 128 tiles, the A fragment feeding
+  // two B sub-tiles (measured 178 -> 147 us at l1)
+  if (std::is_same<Plan, DgradT>::value && tile == 11 && pl.M() == 64 && pl.N() % 128 == 0 && !getenv("FLR_CONV_TILE"))
+    tile = 12;
+  switch (tile) {
     case 21: return launch_tiles<Plan, 2, 1>(pl, ws, ws_bytes, st, name);
     case 12: return launch_tiles<Plan, 1, 2>(pl, ws, ws_bytes, st, name);
     case 22: return launch_tiles<Plan, 2, 2>(pl, ws, ws_bytes, st, name);
