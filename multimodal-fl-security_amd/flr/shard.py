@@ -123,6 +123,7 @@ class CoordSlice:
         self.data, self.plan, self.rank, self.comm = data, plan, rank, comm
         self.begin, self.end = plan.coords(rank)
         self.q0, self.q1 = plan.slices(rank)
+        self._gbuf = self._gmine = None
 
     @property
     def K(self) -> int:
@@ -147,8 +148,11 @@ class CoordSlice:
         if world == 1:
             out.copy_(part[: self.n])
             return out
-        buf = torch.zeros(world * plan.ld, dtype=torch.float32, device=part.device)
-        mine = torch.zeros(plan.ld, dtype=torch.float32, device=part.device)
+        if self._gbuf is None or self._gbuf.device != part.device:
+            # allocated once; the tail past n stays zero across rounds
+            self._gbuf = torch.zeros(world * plan.ld, dtype=torch.float32, device=part.device)
+            self._gmine = torch.zeros(plan.ld, dtype=torch.float32, device=part.device)
+        buf, mine = self._gbuf, self._gmine
         mine[: self.n].copy_(part[: self.n])
         self.comm.all_gather(buf, mine)
         for r in range(world):
