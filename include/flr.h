@@ -185,6 +185,20 @@ int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* const* g_bloc
                               float weight_decay, float max_norm, int first_step,
                               float* norms_out, void* workspace,
                               size_t workspace_bytes, void* stream);
+/* The same step; on the LAST step (first_step bit 1) with x_out != NULL the
+ * updated parameters are written to the client matrix instead of back to the
+ * blocks: block j of client k lands at x_out + k*out_ld + out_offsets[j]
+ * (the trainer's "training order" client matrix, run_experiments.py:238),
+ * negated for clients k < nneg (sign-flip attackers, model_poisoning.py:
+ * 274-276).  This folds the round's export pass into the optimizer. */
+int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* const* g_blocks,
+                                float* const* m_blocks, const int64_t* block_numel,
+                                const int64_t* block_client_stride, int64_t nblocks,
+                                int64_t K, float lr, float momentum, float weight_decay,
+                                float max_norm, int first_step, float* x_out,
+                                const int64_t* out_offsets, int64_t out_ld, int64_t nneg,
+                                float* norms_out, void* workspace,
+                                size_t workspace_bytes, void* stream);
 
 /* ---- a2: client-batched 2-D convolution (bias-free, as in the conv blocks)
  * Replaces nn.Conv2d forward/backward for every client of a GPU at once
@@ -283,6 +297,10 @@ int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* dw_t, int64_
  * [Cout][Cin][KK] at dst + k*dst_stride (KK <= 9). */
 int flr_broadcast_rows(const float* src, int64_t n, float* dst, int64_t K,
                        int64_t dst_stride, void* stream);
+/* flr_broadcast_rows with rows k < nneg written as -src (the attackers' copy
+ * of a range the optimizer never updates, e.g. dead conv taps). */
+int flr_broadcast_rows_neg(const float* src, int64_t n, float* dst, int64_t K,
+                           int64_t dst_stride, int64_t nneg, void* stream);
 int flr_copy_rows(const float* src, int64_t src_stride, int64_t n, float* dst,
                   int64_t dst_stride, int64_t K, void* stream);
 int flr_tap_major_to_torch(const float* w_t, int64_t K, int64_t KK, int64_t Cin,

@@ -18,19 +18,21 @@ namespace layout {
 constexpr int THREADS = 256;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// dst[k * dstride + i] = src[i], i < n, k < K  (grid: chunks x K)
+// dst[k * dstride + i] = src[i], i < n, k < K  (grid: chunks x K); rows
+// k < nneg get -src (the sign-flip attackers' copy of an untrained range)
 template <bool VEC>
 __global__ __launch_bounds__(THREADS) void broadcast_kernel(const float* __restrict__ src, int64_t n,
-                                                            float* __restrict__ dst, int64_t dstride) {
+                                                            float* __restrict__ dst, int64_t dstride, int nneg) {
   float* d = dst + (int64_t)blockIdx.y * dstride;
+  const float sg = (int)blockIdx.y < nneg ? -1.f : 1.f;
   if constexpr (VEC) {
     const int64_t nv = n / 4;
     for (int64_t i = (int64_t)blockIdx.x * THREADS + threadIdx.x; i < nv; i += (int64_t)gridDim.x * THREADS)
-      reinterpret_cast<f32x4*>(d)[i] = reinterpret_cast<const f32x4*>(src)[i];
-    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) d[4 * nv + threadIdx.x] = src[4 * nv + threadIdx.x];
+      reinterpret_cast<f32x4*>(d)[i] = reinterpret_cast<const f32x4*>(src)[i] * sg;
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) d[4 * nv + threadIdx.x] = src[4 * nv + threadIdx.x] * sg;
   } else {
     for (int64_t i = (int64_t)blockIdx.x * THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * THREADS)
-      d[i] = src[i];
+      d[i] = src[i] * sg;
   }
 }
 
@@ -118,16 +120,22 @@ using namespace flr;
 
 extern "C" int flr_broadcast_rows(const float* src, int64_t n, float* dst, int64_t K, int64_t dst_stride,
                                   void* stream) {
-  if (!src || !dst || n < 0 || K < 1 || K > 65535 || dst_stride < n) return FLR_ERR_ARG;
+  return flr_broadcast_rows_neg(src, n, dst, K, dst_stride, 0, stream);
+}
+
+extern "C" int flr_broadcast_rows_neg(const float* src, int64_t n, float* dst, int64_t K, int64_t dst_stride,
+                                      int64_t nneg, void* stream) {
+  if (!src || !dst || n < 0 || K < 1 || K > 65535 || dst_stride < n || nneg < 0) return FLR_ERR_ARG;
+  const int ng = (int)std::min<int64_t>(nneg, K);
   if (n == 0) return FLR_OK;
   const bool vec = layout::al16(src) && layout::al16(dst) && dst_stride % 4 == 0;
   const dim3 grid(layout::grid_x(vec ? n / 4 : n), (unsigned)K);
   if (vec)
     hipLaunchKernelGGL(layout::broadcast_kernel<true>, grid, dim3(layout::THREADS), 0, as_stream(stream), src, n, dst,
-                       dst_stride);
+                       dst_stride, ng);
   else
     hipLaunchKernelGGL(layout::broadcast_kernel<false>, grid, dim3(layout::THREADS), 0, as_stream(stream), src, n,
-                       dst, dst_stride);
+                       dst, dst_stride, ng);
   return launch_status("broadcast_rows");
 }
 

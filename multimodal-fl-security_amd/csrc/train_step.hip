@@ -144,14 +144,15 @@ __global__ void scale_rows_kernel(float* __restrict__ d, const float* __restrict
 // client stride cs[j] is n[j] for a whole parameter and larger for a sub-slab
 // (the live kernel taps of a tap-major conv weight; the dead taps' slabs are
 // left out of the step altogether).
-constexpr int MAXB = 96;        // blocks per launch (the table is a kernel argument)
-constexpr int MAX_PARTS = 8;    // launches per step: up to 768 parameter blocks
+constexpr int MAXB = 80;        // blocks per launch (the table is a kernel argument, < 4 KB)
+constexpr int MAX_PARTS = 8;    // launches per step: up to 640 parameter blocks
 struct BlockTable {
   float* x[MAXB];
   const float* g[MAXB];
   float* m[MAXB];
   int64_t pre[MAXB + 1];
   int32_t cs[MAXB];   // client stride of block j (elements)
+  int32_t xo[MAXB];   // last step with an output matrix: block j's offset in an output row
   uint8_t vec[MAXB];  // block j may use 16-B accesses (n % 4 == 0, all three bases 16-B aligned)
   int nb;
 };
@@ -212,14 +213,21 @@ __global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable
 // read); bit 1 = its last step (the new buffer is not written: the optimizer
 // is discarded after the client's local update, run_experiments.py:206-211).
 // The float4 body keeps two groups of (x, g, m) loads in flight per lane.
+// xout (last step only): the updated parameters go to the client matrix row
+// xout + k*xout_ld + xo[j] instead of back to x (the training copy is
+// reloaded from the global model next round anyway), negated for rows
+// k < nneg (the sign-flip attackers' submission, model_poisoning.py:274-276).
 constexpr int NSGD = 256;
 __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable tb, int64_t P,
                                                               const float* __restrict__ coef, float lr, float mom,
-                                                              float wd, int flags) {
+                                                              float wd, int flags, float* __restrict__ xout,
+                                                              int64_t xout_ld, int nneg) {
   const int k = blockIdx.y, b = blockIdx.x;
   const bool first = flags & 1, last = flags & 2;
   const float c = coef ? coef[k] : 1.0f;
   const float nlr = -lr;
+  const bool redirect = last && xout != nullptr;
+  const float sg = (redirect && k < nneg) ? -1.f : 1.f;
   const int64_t p0 = P * b / NSGD, p1 = P * (b + 1) / NSGD;
   auto upd = [&](float xp, float gr, float mp, float& mo, float& xo) {
     float gp = gr * c;
@@ -236,11 +244,12 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
     float* x = tb.x[j] + base;
     const float* g = tb.g[j] + base;
     float* m = tb.m[j] + base;
+    float* xd = redirect ? xout + (int64_t)k * xout_ld + tb.xo[j] - tb.pre[j] : x;
     auto one = [&](int64_t e) {
       float mo, xo;
       upd(x[e], g[e], first ? 0.f : m[e], mo, xo);
       if (!last) m[e] = mo;
-      x[e] = xo;
+      xd[e] = xo * sg;
     };
     auto four = [&](const f32x4& xv, const f32x4& gv, const f32x4& mv, int64_t e) {
       f32x4 mo, xo;
@@ -252,7 +261,7 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
         xo[q] = bq;
       }
       if (!last) *reinterpret_cast<f32x4*>(m + e) = mo;
-      *reinterpret_cast<f32x4*>(x + e) = xo;
+      *reinterpret_cast<f32x4*>(xd + e) = xo * sg;
     };
     if (!tb.vec[j]) {
       for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) one(e);
@@ -352,9 +361,23 @@ extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* co
                                          int64_t nblocks, int64_t K, float lr,
                                          float momentum, float weight_decay, float max_norm, int first_step,
                                          float* norms_out, void* workspace, size_t workspace_bytes, void* stream) {
+  return flr_clip_sgd_step_blocked_x(x_blocks, g_blocks, m_blocks, block_numel, block_client_stride, nblocks, K, lr,
+                                     momentum, weight_decay, max_norm, first_step, nullptr, nullptr, 0, 0, norms_out,
+                                     workspace, workspace_bytes, stream);
+}
+
+extern "C" int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* const* g_blocks,
+                                           float* const* m_blocks, const int64_t* block_numel,
+                                           const int64_t* block_client_stride, int64_t nblocks, int64_t K, float lr,
+                                           float momentum, float weight_decay, float max_norm, int first_step,
+                                           float* x_out, const int64_t* out_offsets, int64_t out_ld, int64_t nneg,
+                                           float* norms_out, void* workspace, size_t workspace_bytes, void* stream) {
   if (K < 1 || nblocks < 1 || nblocks > (int64_t)train::MAXB * train::MAX_PARTS || !x_blocks || !g_blocks ||
       !m_blocks || !block_numel)
     return FLR_ERR_ARG;
+  // the output matrix is written on the last step only
+  float* xout = (first_step & 2) ? x_out : nullptr;
+  if (xout && (!out_offsets || out_ld < 1 || nneg < 0)) return FLR_ERR_ARG;
   if (max_norm > 0 && (!workspace || workspace_bytes < flr_clip_sgd_workspace(K))) return FLR_ERR_WORKSPACE;
   // the blocks in launches of at most MAXB (the table travels as a kernel argument)
   const int nparts = (int)((nblocks + train::MAXB - 1) / train::MAXB);
@@ -378,6 +401,14 @@ extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* co
       const uintptr_t al = reinterpret_cast<uintptr_t>(x_blocks[j]) | reinterpret_cast<uintptr_t>(g_blocks[j]) |
                            reinterpret_cast<uintptr_t>(m_blocks[j]);
       tb.vec[q] = (block_numel[j] % 4 == 0 && cs % 4 == 0 && (al & 15) == 0) ? 1 : 0;
+      tb.xo[q] = 0;
+      if (xout) {
+        const int64_t o = out_offsets[j];
+        if (o < 0 || o + block_numel[j] > out_ld || o >= ((int64_t)1 << 31)) return FLR_ERR_ARG;
+        tb.xo[q] = (int32_t)o;
+        // 16-B output accesses need the row segment 16-B aligned as well
+        if (o % 4 != 0 || out_ld % 4 != 0 || (reinterpret_cast<uintptr_t>(xout) & 15) != 0) tb.vec[q] = 0;
+      }
     }
     P += tb.pre[tb.nb];
   }
@@ -400,7 +431,8 @@ extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* co
   }
   for (int c = 0; c < nparts; ++c) {
     hipLaunchKernelGGL(train::sgd_blocked_kernel, dim3(train::NSGD, (unsigned)K), dim3(train::THREADS), 0, st, tbs[c],
-                       tbs[c].pre[tbs[c].nb], coef, lr, momentum, weight_decay, first_step & 3);
+                       tbs[c].pre[tbs[c].nb], coef, lr, momentum, weight_decay, first_step & 3, xout, out_ld,
+                       (int)std::min<int64_t>(nneg, K));
     if ((rc = launch_status("sgd_blocked_kernel")) != FLR_OK) return rc;
   }
   return FLR_OK;

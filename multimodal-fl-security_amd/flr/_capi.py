@@ -61,6 +61,10 @@ SIGNATURES = {
                                          ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_float, _int, _c_void_p, _c_void_p,
                                          _size_t, _c_void_p]),
+    "flr_clip_sgd_step_blocked_x": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
+                                           ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _int,
+                                           _c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _size_t,
+                                           _c_void_p]),
     "flr_conv2d_workspace": (_size_t, [_i64] * 10),
     "flr_conv2d_tap_major_ok": (_int, [_i64, _i64]),
     "flr_conv2d_t_workspace": (_size_t, [_i64] * 10),
@@ -77,6 +81,7 @@ SIGNATURES = {
     "flr_mean_rows": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p]),
     "flr_scale_client_rows": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p]),
     "flr_broadcast_rows": (_int, [_c_void_p, _i64, _c_void_p, _i64, _i64, _c_void_p]),
+    "flr_broadcast_rows_neg": (_int, [_c_void_p, _i64, _c_void_p, _i64, _i64, _i64, _c_void_p]),
     "flr_copy_rows": (_int, [_c_void_p, _i64, _i64, _c_void_p, _i64, _i64, _c_void_p]),
     "flr_tap_major_to_torch": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p]),
     "flr_copy_rows_neg": (_int, [_c_void_p, _i64, _i64, _c_void_p, _i64, _i64, _i64, _c_void_p]),

@@ -56,6 +56,12 @@ class BaseDefense(ABC):
     # Defenses that need whole rows (norms, dots) do not implement it and run
     # on the all-gathered matrix instead.
     supports_sharded = False
+    # The aggregate's coordinate i depends only on column i and on row-level
+    # quantities invariant under one common permutation of the coordinates
+    # (pairwise distances, row selections): the round engine may then hand
+    # over the client matrix in the trainer's own coordinate order (tap-major
+    # conv weights) and permute only the aggregated vector back.
+    order_free = False
 
     def aggregate_sharded(self, cs, num_examples: List[int]) -> torch.Tensor:
         raise NotImplementedError(f"{self.name} has no coordinate-sharded form")
@@ -80,6 +86,7 @@ class NoDefense(BaseDefense):
         return ops.fedavg(cm.X, list(num_examples))
 
     supports_sharded = True
+    order_free = True
 
     def aggregate_sharded(self, cs, num_examples: List[int]) -> torch.Tensor:
         return ops.fedavg(cs.X, list(num_examples))

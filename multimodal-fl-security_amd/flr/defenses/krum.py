@@ -53,6 +53,7 @@ class KrumDefense(BaseDefense):
         return ops.rows_mean(cm.X, order[: min(self.multi_k, cm.K)], divisor=self.multi_k)
 
     supports_sharded = True
+    order_free = True
 
     def aggregate_sharded(self, cs, num_examples: List[int], publish: bool = True, events=None) -> torch.Tensor:
         """Coordinate-sharded Krum (flr.shard): distances from the per-slice

@@ -26,6 +26,7 @@ class TrimmedMeanDefense(BaseDefense):
         return ops.trimmed_mean(cm.X, self.num_trimmed_per_end)
 
     supports_sharded = True
+    order_free = True
 
     def aggregate_sharded(self, cs, num_examples: List[int]) -> torch.Tensor:
         return self.aggregate_flat(cs, num_examples)  # coordinate-wise: the slice is a client matrix
@@ -51,6 +52,7 @@ class MedianDefense(BaseDefense):
         return ops.median_lower(cm.X)
 
     supports_sharded = True
+    order_free = True
 
     def aggregate_sharded(self, cs, num_examples: List[int]) -> torch.Tensor:
         return ops.median_lower(cs.X)

@@ -101,6 +101,12 @@ class RoundEngine:
         self._graph = None
         self._graph_losses: Optional[torch.Tensor] = None
         self._wants_global = "global_flat" in inspect.signature(self.defense.aggregate_flat).parameters
+        # training-order rounds (BaseDefense.order_free): the client matrix is in
+        # the trainer's coordinate order, written by the last optimizer step;
+        # gtrain is the global model in that order (FLR_ORDER=torch: off)
+        self.train_order = (getattr(self.defense, "order_free", False) and not self._wants_global
+                            and os.environ.get("FLR_ORDER", "train") != "torch")
+        self.gtrain = self.trainer.to_train_order(self.global_flat) if self.train_order else None
         self.round_index = 0
         self.fell_back = False
 
@@ -114,8 +120,24 @@ class RoundEngine:
     def _train_phase(self) -> torch.Tensor:
         """Every local client: global -> local SGD steps -> client-matrix rows
         (run_experiments.py:193-240), the attackers' poisoning in the export."""
+        if self.train_order:
+            self.trainer.load_global_train(self.gtrain)
+            return self.trainer.local_update(self.batches, self.masks, negate_rows=self._num_flipped(),
+                                             gtrain=self.gtrain)
         self.trainer.load_global(self.global_flat)
         return self.trainer.local_update(self.batches, self.masks, negate_rows=self._num_flipped())
+
+    def _publish(self, agg: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The round's aggregate -> global_flat (torch order; and gtrain when
+        training order is on, agg then being in training order)."""
+        if self.train_order:
+            if agg is not None:
+                self.gtrain.copy_(agg)
+            self.trainer.to_torch_order(self.gtrain, self.global_flat)
+        elif agg is not None:
+            self.global_flat.copy_(agg)
+        self.round_index += 1
+        return self.global_flat
 
     def _capture(self) -> None:
         """Capture the training phase (~2.4k kernel launches per round at C3)
@@ -149,9 +171,8 @@ class RoundEngine:
                 part = self.defense.aggregate_sharded(self.slice, self.num_examples, **kw)
             except Exception as e:  # noqa: BLE001 - the reference catches any exception
                 part = self._fallback(e, self.slice.X)
-            self.slice.gather_vector(part, self.global_flat)
-            self.round_index += 1
-            return self.global_flat
+            self.slice.gather_vector(part, self.gtrain if self.train_order else self.global_flat)
+            return self._publish()
         fdist.allgather_rows(self.trainer.X.data, self.full.data)
         if self._wants_global:  # FLTrust: the server update starts from this round's global model
             kw["global_flat"] = self.global_flat.clone()  # global_flat is overwritten below
@@ -159,9 +180,7 @@ class RoundEngine:
             agg = self.defense.aggregate_flat(self.full, self.num_examples, **kw)
         except Exception as e:  # noqa: BLE001
             agg = self._fallback(e, self.full.X)
-        self.global_flat.copy_(agg)
-        self.round_index += 1
-        return self.global_flat
+        return self._publish(agg)
 
     def _fallback(self, err: Exception, X: torch.Tensor) -> torch.Tensor:
         """robust_server.py:120-122: a failing defense falls back to FedAvg
@@ -201,6 +220,8 @@ class RoundEngine:
         sd = ck["model_state_dict"]
         flat = torch.cat([sd[n].reshape(-1).float() for n in names])
         self.global_flat.copy_(flat.to(self.global_flat.device))
+        if self.train_order:
+            self.gtrain.copy_(self.trainer.to_train_order(self.global_flat))
         self.round_index = int(ck["round"])
         return self.round_index
 

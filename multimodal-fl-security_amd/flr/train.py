@@ -29,8 +29,8 @@ import torch
 from . import _capi
 from .matrix import ClientMatrix
 from .models import multimodal as _mm
-from .models.multimodal import (ModelSpec, batched_forward, conv_geometry, live_taps, param_layout, tap_major_names,
-                                to_tap_major)
+from .models.multimodal import (ModelSpec, batched_forward, conv_geometry, from_tap_major, live_taps, param_layout,
+                                tap_major_names, to_tap_major)
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -131,6 +131,7 @@ class ClientBatchTrainer:
         # so its weights and momentum never change and the step skips them.
         self.skip_dead = frozenset()
         blocks = []
+        self.dead_ranges = []  # (row offset, numel): the dead-tap slabs, in training order
         geo = conv_geometry(spec)
         for j, (name, n, shp) in enumerate(zip(self.names, self.numels, self.shapes)):
             live = None
@@ -151,10 +152,18 @@ class ClientBatchTrainer:
                     t0 = b
             for lo, hi in runs:
                 blocks.append((j, lo * slab, (hi - lo) * slab, n))
+            covered = [(lo * slab, hi * slab) for lo, hi in runs]
+            e = 0
+            for a, b in covered + [(n, n)]:
+                if a > e:
+                    self.dead_ranges.append((self.offsets[j] + e, a - e))
+                e = b
         self.blocks = blocks
         nb = len(blocks)
         self._np = (ctypes.c_int64 * nb)(*[c for _, _, c, _ in blocks])
         self._cs = (ctypes.c_int64 * nb)(*[cs for _, _, _, cs in blocks])
+        # the last step's output offsets in a training-order client-matrix row
+        self._xo = (ctypes.c_int64 * nb)(*[self.offsets[j] + o for j, o, _, _ in blocks])
         chunk = cfg.client_chunk if cfg.client_chunk > 0 else self.auto_chunk(spec, self.K)
         self.chunks = [(c0, min(self.K, c0 + chunk)) for c0 in range(0, self.K, chunk)]
         # per chunk: the optimizer's block pointers at the chunk's first client
@@ -184,9 +193,56 @@ class ClientBatchTrainer:
                 src = src.contiguous()
             _capi.call("flr_broadcast_rows", src.data_ptr(), n, w.data_ptr(), self.K, n, st)
 
+    # ---- training order: the coordinate order of the training blocks ---------
+    # Row k of a training-order client matrix holds client k's blocks at the
+    # torch offsets, each block in its training layout (tap-major conv weights
+    # [KH, KW, Cin, Cout] instead of torch's [Cout, Cin, KH, KW]).  The hot-path
+    # aggregators are indifferent to a common coordinate permutation
+    # (BaseDefense.order_free), so the round engine aggregates in this order:
+    # the last optimizer step writes X directly (no export pass) and only the
+    # aggregated P-vector is permuted back.
+    def to_train_order(self, flat: torch.Tensor) -> torch.Tensor:
+        """A torch-order parameter vector -> training order (a new tensor)."""
+        parts = []
+        for name, off, n, shp in zip(self.names, self.offsets, self.numels, self.shapes):
+            src = flat[off:off + n]
+            parts.append(to_tap_major(src.view(shp)).reshape(-1) if name in self.tap_major else src)
+        return torch.cat(parts) if parts else flat.clone()
+
+    def to_torch_order(self, flat: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """A training-order parameter vector -> torch order (into out if given)."""
+        if out is None:
+            out = torch.empty_like(flat)
+        for name, off, n, shp, tshp in zip(self.names, self.offsets, self.numels, self.shapes, self.train_shapes):
+            src = flat[off:off + n]
+            if name in self.tap_major:
+                out[off:off + n].view(shp).copy_(from_tap_major(src.view(tshp)))
+            else:
+                out[off:off + n].copy_(src)
+        return out
+
+    def load_global_train(self, gtrain: torch.Tensor, live_only: bool = True) -> None:
+        """load_global from a training-order global vector: a plain broadcast per
+        block.  live_only skips the dead-tap slabs: no training kernel reads
+        them and the round's client matrix takes them from gtrain directly
+        (local_update's out=), so export() is invalid until the next full load."""
+        st = _stream(self._wbuf)
+        for name, w, off, n in zip(self.names, self.W, self.offsets, self.numels):
+            if live_only and name in self.skip_dead:
+                continue
+            _capi.call("flr_broadcast_rows", gtrain.data_ptr() + 4 * off, n, w.data_ptr(), self.K, n, st)
+        if live_only:
+            for j, o, c, cs in self.blocks:
+                if self.names[j] in self.skip_dead:
+                    _capi.call("flr_broadcast_rows", gtrain.data_ptr() + 4 * (self.offsets[j] + o), c,
+                               self.W[j].data_ptr() + 4 * o, self.K, cs, st)
+        self._dead_stale = live_only and bool(self.skip_dead)
+
     def export(self, negate_rows: int = 0) -> ClientMatrix:
         """Client-major client matrix for the server (row k = client k); rows
         k < negate_rows are written negated (the sign-flip attackers)."""
+        if getattr(self, "_dead_stale", False):
+            raise RuntimeError("export() after load_global_train(live_only=True): the dead-tap slabs are not loaded")
         st = _stream(self._wbuf)
         ld = self.X.data.stride(0)
         base = self.X.data.data_ptr()
@@ -201,8 +257,11 @@ class ClientBatchTrainer:
 
     # ---- one optimizer step for every client -----------------------------
     def step(self, images, tokens, labels, first: bool, dropout_mask=None, last: bool = False,
-             loss_out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """One local step of every client (chunk by chunk); returns the [K] losses."""
+             loss_out: Optional[torch.Tensor] = None, out: Optional[ClientMatrix] = None,
+             negate_rows: int = 0) -> torch.Tensor:
+        """One local step of every client (chunk by chunk); returns the [K] losses.
+        With out (a training-order client matrix) and last, the step writes the
+        updated live parameters into out's rows (rows < negate_rows negated)."""
         if loss_out is None:
             loss_out = torch.empty(self.K, dtype=torch.float32, device=self.device)
         c = self.cfg
@@ -216,9 +275,14 @@ class ClientBatchTrainer:
             loss_k = CrossEntropy.apply(logits, sl(labels))
             grads = [g.contiguous() for g in torch.autograd.grad(loss_k.sum(), leaves)]
             gp = (ctypes.c_void_p * len(self.blocks))(*[grads[j].data_ptr() + 4 * o for j, o, _, _ in self.blocks])
-            _capi.call("flr_clip_sgd_step_blocked", xp, gp, mp, self._np, self._cs, len(self.blocks), c1 - c0,
-                       c.lr, c.momentum, c.weight_decay, c.clip, int(first) | (int(last) << 1),
-                       self.norms.data_ptr() + 4 * c0, self._ws.data_ptr() + self._ws_off, self._ws_bytes,
+            xo, ld, nneg = None, 0, 0
+            if out is not None and last:
+                ld = out.data.stride(0)
+                xo = out.data.data_ptr() + 4 * c0 * ld
+                nneg = max(0, min(negate_rows, c1) - c0)
+            _capi.call("flr_clip_sgd_step_blocked_x", xp, gp, mp, self._np, self._cs, len(self.blocks), c1 - c0,
+                       c.lr, c.momentum, c.weight_decay, c.clip, int(first) | (int(last) << 1), xo, self._xo, ld,
+                       nneg, self.norms.data_ptr() + 4 * c0, self._ws.data_ptr() + self._ws_off, self._ws_bytes,
                        _stream(self._wbuf))
             del grads, leaves, params, logits
             _capi.call("flr_copy_rows", loss_k.data_ptr(), c1 - c0, c1 - c0, loss_out.data_ptr() + 4 * c0, c1 - c0, 1,
@@ -226,17 +290,28 @@ class ClientBatchTrainer:
         return loss_out
 
     def local_update(self, batches: Sequence, dropout_masks: Optional[Sequence] = None,
-                     export: bool = True, negate_rows: int = 0) -> torch.Tensor:
+                     export: bool = True, negate_rows: int = 0, gtrain: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Runs len(batches) steps; returns each client's mean loss [K]
         (fl_client.py:143-149).  The per-step losses land in one [steps, K]
-        buffer and are averaged by one flr_sum_rows pass (sum in step order)."""
+        buffer and are averaged by one flr_sum_rows pass (sum in step order).
+        export: X <- the torch-order client matrix (export()).  gtrain (the
+        round's training-order global vector, loaded by load_global_train):
+        X <- the TRAINING-order client matrix instead, written by the last
+        optimizer step, the untrained dead-tap ranges copied from gtrain."""
         n = max(1, len(batches))
         steps = torch.empty(n, self.K, dtype=torch.float32, device=self.device)
+        direct = gtrain is not None and export and len(batches) > 0
         for s, (images, tokens, labels) in enumerate(batches):
             mask = None if dropout_masks is None else dropout_masks[s]
             self.step(images, tokens, labels, first=(s == 0), dropout_mask=mask, last=(s == len(batches) - 1),
-                      loss_out=steps[s])
-        if export:
+                      loss_out=steps[s], out=self.X if direct else None, negate_rows=negate_rows)
+        if direct:
+            st = _stream(self._wbuf)
+            ld = self.X.data.stride(0)
+            for off, c in self.dead_ranges:
+                _capi.call("flr_broadcast_rows_neg", gtrain.data_ptr() + 4 * off, c, self.X.data.data_ptr() + 4 * off,
+                           self.K, ld, negate_rows, st)
+        elif export:
             self.export(negate_rows)
         total = torch.empty(1, self.K, dtype=torch.float32, device=self.device)
         _capi.call("flr_mean_rows", steps.data_ptr(), len(batches), self.K, total.data_ptr(), _stream(total))

@@ -79,3 +79,43 @@ def test_fltrust_round(cuda):
         assert abs(got_t - want_t) <= 1e-4 * max(1.0, abs(want_t)) + 1e-6
     err = (out.cpu().double() - want[0].double()).abs().max().item()
     assert err <= 1e-5 * max(1.0, want[0].abs().max().item()), err
+
+
+@pytest.mark.parametrize("defense,cfg,attack,f", [
+    ("fedavg", {}, "none", 0),
+    ("median", {}, "sign_flip", 2),
+    ("trimmed_mean", {"trim_ratio": 0.2}, "sign_flip", 2),
+    ("krum", {"multi_k": 4}, "sign_flip", 1),
+])
+def test_training_order_round_equals_torch_order(cuda, monkeypatch, defense, cfg, attack, f):
+    """Training-order rounds (BaseDefense.order_free: the last optimizer step
+    writes the client matrix in the trainer's coordinate order, dead-tap ranges
+    from the global vector, the attackers' rows negated) give the global model
+    of the torch-order export path: bit-identical for coordinate-wise rules
+    (FedAvg, median), the same Krum selection, and the trimmed mean within
+    1e-6 (its torch-restated cascade sum depends on a column's position in
+    torch's vectorised loop).  Full ResNet-18 + GRU model (tap-major convs,
+    dead taps), 2 rounds with HIP-graph replay."""
+    from flr.models.multimodal import ModelSpec
+    spec = ModelSpec()
+    rc = RoundConfig(num_clients=8, batch=4, defense=defense, defense_cfg=dict(cfg), attack=attack, num_attackers=f)
+    outs, sels = [], []
+    for order in ("torch", "train"):
+        monkeypatch.setenv("FLR_ORDER", order)
+        eng = RoundEngine(spec, rc, TrainConfig(local_steps=2), cuda)
+        assert eng.train_order == (order == "train")
+        for _ in range(2):
+            eng.run_round()
+        outs.append(eng.global_flat.clone().cpu())
+        sels.append(list(getattr(eng.defense, "selected_clients", [])))
+    a, b = outs
+    assert torch.isfinite(a).all()
+    if defense == "trimmed_mean":
+        err = ((a - b).abs().max() / a.abs().max()).item()
+        assert err <= 1e-6, err
+    elif defense == "krum":
+        assert sorted(sels[0]) == sorted(sels[1]) and not set(sels[1]) & set(range(f))
+        err = ((a - b).abs().max() / a.abs().max()).item()
+        assert err <= 1e-6, err
+    else:
+        assert torch.equal(a, b)

@@ -297,7 +297,8 @@ def test_c3_round_multikrum_signflip(cuda):
         ref = torch.cat([u.reshape(-1) for u in upd])
         if k < f:
             ref = -ref
-        assert _rel(X[k].cpu(), ref) < 1e-5, (k, _rel(X[k].cpu(), ref))
+        row = eng.trainer.to_torch_order(X[k]) if eng.train_order else X[k]  # X is in training order
+        assert _rel(row.cpu(), ref) < 1e-5, (k, _rel(row.cpu(), ref))
     D = eng.defense.distances.cpu().numpy()
     scores = orc.krum_scores(D, K - f - 2)
     import numpy as np
