@@ -34,15 +34,17 @@ constexpr int MAXTAPS = 49;
 // the critical path).  ok = false: the list is not a rectangle (use the table).
 struct TapRect {
   int kh0, kw0, nkw, step;
+  uint32_t nkw_m;  // ceil(2^16 / nkw): slot / nkw = (slot * nkw_m) >> 16 for slot < MAXTAPS
   bool ok;
 };
 inline TapRect make_rect(const int8_t* kh, const int8_t* kw, int n, int step) {
-  TapRect r{0, 0, 1, step, false};
+  TapRect r{0, 0, 1, step, 65536u, false};
   if (n == 0) { r.ok = true; return r; }
   r.kh0 = kh[0]; r.kw0 = kw[0];
   int nkw = 0;
   while (nkw < n && kh[nkw] == kh[0]) ++nkw;
   r.nkw = nkw;
+  r.nkw_m = (65536u + (uint32_t)nkw - 1) / (uint32_t)nkw;
   if (n % nkw != 0) return r;
   for (int t = 0; t < n; ++t)
     if (kh[t] != r.kh0 + step * (t / nkw) || kw[t] != r.kw0 + step * (t % nkw)) return r;
@@ -50,7 +52,9 @@ inline TapRect make_rect(const int8_t* kh, const int8_t* kw, int n, int step) {
   return r;
 }
 __device__ __forceinline__ void rect_tap(const TapRect& r, int slot, int& kh, int& kw) {
-  const int i = slot / r.nkw;
+  // exact for 0 <= slot < 2^16 / nkw (slot < MAXTAPS = 49, nkw <= 7); a multiply
+  // and a shift on the scalar unit instead of a division sequence per K-tile
+  const int i = (int)(((uint32_t)slot * r.nkw_m) >> 16);
   kh = r.kh0 + r.step * i;
   kw = r.kw0 + r.step * (slot - i * r.nkw);
 }

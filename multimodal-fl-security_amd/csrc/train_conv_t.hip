@@ -126,7 +126,13 @@ __device__ __forceinline__ void frag8(const float* buf, int rb, int k0, float (&
   }
 }
 
+// The residuals r = v - (float)bf16(v) come from v_dot2_f32_bf16 against
+// (-1, 0) / (0, -1): one instruction per value instead of a bf16 -> fp32
+// expansion plus a subtraction.  r is exact either way (|r| <= half a bf16
+// ulp of v, representable in fp32), so the split is bit-identical to the
+// plain form (tools/hip/split_check.hip checks 2^24 random patterns).
 __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#ifdef FLR_AB_SPLIT_PLAIN  // A/B build (tools/ab_build.sh): expansion + subtraction
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const __bf16 a = (__bf16)v[j];
@@ -135,6 +141,31 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& hi, bf16x8& 
     hi[j] = a;
     mid[j] = b;
     lo[j] = (__bf16)(r1 - (float)b);
+  }
+  return;
+#endif
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  // (-1, 0) and (0, -1) as opaque SGPRs: hipcc encodes a (-1, 0) constant as the
+  // inline constant -1.0, which the hardware reads as the fp32 bits, i.e. (0, -1)
+  unsigned klo, khi;
+  asm volatile("s_mov_b32 %0, 0xbf80" : "=s"(klo));
+  asm volatile("s_mov_b32 %0, 0xbf800000" : "=s"(khi));
+  const bf16x2 nl = __builtin_bit_cast(bf16x2, klo), nh = __builtin_bit_cast(bf16x2, khi);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float v0 = v[2 * p], v1 = v[2 * p + 1];
+    const bf16x2 a = {(__bf16)v0, (__bf16)v1};
+    const float r0 = __builtin_amdgcn_fdot2_f32_bf16(a, nl, v0, false);
+    const float r1 = __builtin_amdgcn_fdot2_f32_bf16(a, nh, v1, false);
+    const bf16x2 b = {(__bf16)r0, (__bf16)r1};
+    const float s0 = __builtin_amdgcn_fdot2_f32_bf16(b, nl, r0, false);
+    const float s1 = __builtin_amdgcn_fdot2_f32_bf16(b, nh, r1, false);
+    hi[2 * p] = a[0];
+    hi[2 * p + 1] = a[1];
+    mid[2 * p] = b[0];
+    mid[2 * p + 1] = b[1];
+    lo[2 * p] = (__bf16)s0;
+    lo[2 * p + 1] = (__bf16)s1;
   }
 }
 
@@ -274,7 +305,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
     return s;
   }
   __device__ void load_a8(const State8& s, int r0, float (&a)[8]) const {  // A(co, ci): lanes along co
-    const int slot = uni(r0 / g.Cin), ci0 = r0 - slot * g.Cin;
+    const int slot = uni((int)udiv((uint32_t)r0, g.d_cin)), ci0 = r0 - slot * g.Cin;
     int kh, kw;
     slot_tap(g, slot, kh, kw);
     const int arow = uni(((kh * g.KW + kw) * g.Cin + ci0) * g.Cout * 4);
@@ -282,7 +313,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
     for (int e = 0; e < 8; ++e) a[e] = ld1(s.ra, s.a0, arow + e * g.Cout * 4);
   }
   __device__ void load_b8(const State8& s, int r0, float (&b)[8]) const {  // B(pixel, ci): 8 channels
-    const int slot = uni(r0 / g.Cin), ci0 = r0 - slot * g.Cin;
+    const int slot = uni((int)udiv((uint32_t)r0, g.d_cin)), ci0 = r0 - slot * g.Cin;
     int kh, kw;
     slot_tap(g, slot, kh, kw);
     kh = uni(kh);
@@ -403,7 +434,7 @@ struct DgradT {
     return s;
   }
   __device__ void load_a8(const State8& s, int r0, float (&a)[8]) const {  // A(ci, co): 8 consecutive co
-    const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
+    const int slot = uni((int)udiv((uint32_t)r0, g.d_cout)), co0 = r0 - slot * g.Cout;
     int kh, kw;
     conv::rect_tap(crect, slot, kh, kw);
     const int abase = uni(((kh * g.KW + kw) * g.Cin * g.Cout + co0) * 4);
@@ -415,7 +446,7 @@ struct DgradT {
     }
   }
   __device__ void load_b8(const State8& s, int r0, float (&b)[8]) const {  // B(input pixel, co): 8 channels
-    const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
+    const int slot = uni((int)udiv((uint32_t)r0, g.d_cout)), co0 = r0 - slot * g.Cout;
     int kh, kw;
     conv::rect_tap(crect, slot, kh, kw);
     kh = uni(kh);
