@@ -190,14 +190,19 @@ int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* const* g_bloc
  * blocks: block j of client k lands at x_out + k*out_ld + out_offsets[j]
  * (the trainer's "training order" client matrix, run_experiments.py:238),
  * negated for clients k < nneg (sign-flip attackers, model_poisoning.py:
- * 274-276).  This folds the round's export pass into the optimizer. */
+ * 274-276).  This folds the round's export pass into the optimizer.
+ * Clip norm from producer partials: blocks with block_normed[j] != 0 are left
+ * out of the optimizer's own sum-of-squares pass; their squares come as fp64
+ * partials extra_sq[k*n_extra + i], i < n_extra (e.g. written by
+ * flr_conv2d_bwd_weight_t_sq), summed per client in a fixed order. */
 int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* const* g_blocks,
                                 float* const* m_blocks, const int64_t* block_numel,
                                 const int64_t* block_client_stride, int64_t nblocks,
                                 int64_t K, float lr, float momentum, float weight_decay,
                                 float max_norm, int first_step, float* x_out,
                                 const int64_t* out_offsets, int64_t out_ld, int64_t nneg,
-                                float* norms_out, void* workspace,
+                                const uint8_t* block_normed, const double* extra_sq,
+                                int64_t n_extra, float* norms_out, void* workspace,
                                 size_t workspace_bytes, void* stream);
 
 /* ---- a2: client-batched 2-D convolution (bias-free, as in the conv blocks)
@@ -287,6 +292,20 @@ int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* dw_t, int64_
                             int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                             int64_t pad, int zero_dead_taps, void* workspace,
                             size_t workspace_bytes, void* stream);
+/* The same weight gradient, plus the clip norm's partial sums of squares
+ * (a6, run_experiments.py:234): fp64 sums over fixed parts of client k's
+ * live-tap gradient at sq[k*sq_ld + i], i < the slot count
+ * flr_conv2d_bwd_weight_t_sq_slots returns for the geometry (<= sq_ld).
+ * The parts depend on the per-client shape only, never on K.  Needs the
+ * full flr_conv2d_t_workspace (FLR_ERR_WORKSPACE otherwise). */
+int64_t flr_conv2d_bwd_weight_t_sq_slots(int64_t K, int64_t B, int64_t Cin, int64_t H,
+                                         int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+                                         int64_t stride, int64_t pad);
+int flr_conv2d_bwd_weight_t_sq(const float* x, const float* dy, float* dw_t, int64_t K,
+                               int64_t B, int64_t Cin, int64_t H, int64_t W,
+                               int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                               int64_t pad, int zero_dead_taps, double* sq, int64_t sq_ld,
+                               void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- a1 / a8 / a15: round-boundary layout moves of the training state ----
  * flr_broadcast_rows: dst[k*dst_stride + i] = src[i] (load_global: every

@@ -499,6 +499,11 @@ struct WgtT {
   const float* x;
   const float* dy;
   float* dw;
+  // optional clip-norm partials (flr_conv2d_bwd_weight_t_sq): one fp64 sum of
+  // squares per output tile (split-K 1) or per 256-value treduce block, at
+  // sq[k * sq_ld + slot] — the optimizer's clip norm then never re-reads dw
+  double* sq = nullptr;
+  int sq_ld = 0;
   static constexpr int LA = RK_GATHER, LB = BVEC ? RK_VEC : RK_GATHER;
   __host__ __device__ int M() const { return g.ntaps * g.Cin; }
   __host__ __device__ int N() const { return g.Cout; }
@@ -1132,6 +1137,23 @@ __device__ __forceinline__ void xcd_tile(int& bx, int& by, int& bz) {
   bz = t / (gx * gy);
 }
 
+template <class P> struct has_sq : std::false_type {};
+template <bool V> struct has_sq<WgtT<V>> : std::true_type {};
+
+// Sum over the workgroup in a fixed order (fp64): each thread's own value, a
+// butterfly over the wave, the waves in index order; the result is thread 0's.
+// Every thread of the workgroup must call it (one barrier).
+__device__ __forceinline__ double block_sumsq(double s, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+  return t;
+}
+
 template <class Plan, int MS, int NS, int X6>
 __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S, float* __restrict__ part, int remap,
                                                            int prio) {
@@ -1352,6 +1374,25 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
         }
       }
     }
+  if constexpr (has_sq<Plan>::value) {
+    if (S == 1 && pl.sq) {  // this tile's clip-norm partial (split-K: the treduce pass writes them)
+      double sq = 0.0;
+#pragma unroll
+      for (int i = 0; i < MS; ++i)
+#pragma unroll
+        for (int j = 0; j < NS; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int m = m0 + BM * i + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int n = n0 + BN * j + 32 * wn + l32;
+            const double v = (m < M && n < N) ? (double)acc[i][j][e] : 0.0;
+            sq += v * v;
+          }
+      __shared__ double red[THREADS / 64];
+      const double t = block_sumsq(sq, red);
+      if (tid == 0) pl.sq[(int64_t)k * pl.sq_ld + by * (int)gridDim.x + bx] = t;
+    }
+  }
 }
 
 // ---- the split-at-stash form (FLR_GEMM=stash) ------------------------------
@@ -1503,12 +1544,21 @@ __global__ void treduce_kernel(const Plan pl, int S, const float* __restrict__ p
   const int k = blockIdx.y;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t MN = (int64_t)M * N;
-  if (e >= MN) return;
-  const int m = e / N, n = e - m * N;
-  const int64_t idx = k * MN + e;
-  float v = part[idx];
-  for (int s = 1; s < S; ++s) v += part[(int64_t)s * MN * K + idx];
-  pl.store(k, m, n, v);
+  float v = 0.f;
+  if (e < MN) {
+    const int m = e / N, n = e - m * N;
+    const int64_t idx = k * MN + e;
+    v = part[idx];
+    for (int s = 1; s < S; ++s) v += part[(int64_t)s * MN * K + idx];
+    pl.store(k, m, n, v);
+  }
+  if constexpr (has_sq<Plan>::value) {
+    if (pl.sq) {  // this block's clip-norm partial (slot = blockIdx.x)
+      __shared__ double red[4];
+      const double t = block_sumsq((double)v * (double)v, red);
+      if (threadIdx.x == 0) pl.sq[(int64_t)k * pl.sq_ld + blockIdx.x] = t;
+    }
+  }
 }
 
 // dw_t slabs [k][t] of the taps set in `dead` = 0 (grid: 64 x K).
@@ -1637,6 +1687,19 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   hipLaunchKernelGGL(treduce_kernel<Plan>, dim3((unsigned)((mn + 255) / 256), (unsigned)K), dim3(256), 0, st, pl, S,
                      static_cast<const float*>(ws));
   return launch_status(name);
+}
+
+// Clip-norm partial slots per client a WgtT launch writes (the tile count at
+// split-K 1, else one per 256-value treduce block), under the launch's own
+// tile and split choice — given a workspace of splits_bytes(pl).
+template <class Plan>
+int sq_slots(const Plan& pl) {
+  const int M = pl.M(), N = pl.N(), R = pl.R();
+  const int tile = tile_choice(M, N, R);
+  const int ms = (tile == 21 || tile == 22) ? 2 : 1, ns = (tile == 12 || tile == 22) ? 2 : 1;
+  const int S = choose_splits(M, N, R, pl.g.Kc, ms * ns, plan_min_kt<Plan>());
+  if (S == 1) return cdiv(N, BN * ns) * cdiv(M, BM * ms);
+  return (int)(((int64_t)M * N + 255) / 256);
 }
 
 template <class Plan>
@@ -1834,6 +1897,23 @@ extern "C" int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* d
                                        int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
                                        int64_t stride, int64_t pad, int zero_dead_taps, void* ws, size_t ws_bytes,
                                        void* stream) {
+  return flr_conv2d_bwd_weight_t_sq(x, dy, dw_t, K, B, Cin, H, W, Cout, KH, KW, stride, pad, zero_dead_taps, nullptr,
+                                    0, ws, ws_bytes, stream);
+}
+
+extern "C" int64_t flr_conv2d_bwd_weight_t_sq_slots(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W,
+                                                    int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                                                    int64_t pad) {
+  if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return -1;
+  convt::WgtT<true> pl;  // the slot count does not depend on the B-operand load form
+  pl.g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
+  return pl.R() == 0 ? 0 : convt::sq_slots(pl);
+}
+
+extern "C" int flr_conv2d_bwd_weight_t_sq(const float* x, const float* dy, float* dw_t, int64_t K, int64_t B,
+                                          int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+                                          int64_t stride, int64_t pad, int zero_dead_taps, double* sq,
+                                          int64_t sq_ld, void* ws, size_t ws_bytes, void* stream) {
   if (!x || !dy || !dw_t) return FLR_ERR_ARG;
   if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad))
     return conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) ? FLR_ERR_UNSUPPORTED : FLR_ERR_ARG;
@@ -1847,13 +1927,20 @@ extern "C" int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* d
     const int rc = launch_status("conv bwd weight: zero dead taps");
     if (rc != FLR_OK) return rc;
   }
+  if (sq) {  // the partial slots follow the launch's split choice, which needs the full workspace
+    convt::WgtT<true> probe;
+    probe.g = g;
+    if (sq_ld < convt::sq_slots(probe) || ws_bytes < convt::splits_bytes(probe) ||
+        (convt::splits_bytes(probe) > 0 && !ws))
+      return FLR_ERR_WORKSPACE;
+  }
   if ((g.Ho * g.Wo) % 4 == 0) {
     convt::WgtT<true> pl;
-    pl.g = g; pl.x = x; pl.dy = dy; pl.dw = dw_t;
+    pl.g = g; pl.x = x; pl.dy = dy; pl.dw = dw_t; pl.sq = sq; pl.sq_ld = (int)sq_ld;
     return convt::launch(pl, ws, ws_bytes, st, "conv bwd weight (tap-major)");
   }
   convt::WgtT<false> pl;
-  pl.g = g; pl.x = x; pl.dy = dy; pl.dw = dw_t;
+  pl.g = g; pl.x = x; pl.dy = dy; pl.dw = dw_t; pl.sq = sq; pl.sq_ld = (int)sq_ld;
   return convt::launch(pl, ws, ws_bytes, st, "conv bwd weight (tap-major)");
 }
 

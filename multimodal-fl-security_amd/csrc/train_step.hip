@@ -153,7 +153,8 @@ struct BlockTable {
   int64_t pre[MAXB + 1];
   int32_t cs[MAXB];   // client stride of block j (elements)
   int32_t xo[MAXB];   // last step with an output matrix: block j's offset in an output row
-  uint8_t vec[MAXB];  // block j may use 16-B accesses (n % 4 == 0, all three bases 16-B aligned)
+  uint8_t vec[MAXB];  // bit 0: block j may use 16-B accesses (n % 4 == 0, all three bases 16-B aligned);
+                      // bit 1: its squares arrive as producer partials (extra_sq): sumsq skips it
   int nb;
 };
 
@@ -183,10 +184,10 @@ __global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable
   for (int j = 0; j < tb.nb; ++j) {
     const int64_t lo = p0 > tb.pre[j] ? p0 : tb.pre[j];
     const int64_t hi = p1 < tb.pre[j + 1] ? p1 : tb.pre[j + 1];
-    if (lo >= hi) continue;
+    if (lo >= hi || (tb.vec[j] & 2)) continue;
     const float* g = tb.g[j] + (int64_t)k * tb.cs[j] - tb.pre[j];
     visit_range(
-        lo, hi, tb.pre[j], tb.vec[j] != 0,
+        lo, hi, tb.pre[j], (tb.vec[j] & 1) != 0,
         [&](int64_t e) {
           const double v = (double)g[e];
           acc += v * v;
@@ -205,6 +206,34 @@ __global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable
     double s = 0.0;
     for (int w = 0; w < THREADS / 64; ++w) s += red[w];
     partial[(int64_t)k * NBLK + b] = s;
+  }
+}
+
+// clip_coef_kernel plus producer partials extra[k][0, n_extra) (e.g. the conv
+// weight-gradient epilogues' sums of squares): one workgroup per client sums
+// the nparts*NBLK blocked partials and the extra ones, thread t taking
+// indices t, t+256, ... in order, then a fixed tree over the threads.
+__global__ __launch_bounds__(THREADS) void clip_coef_ex_kernel(const double* __restrict__ partial, int K,
+                                                               float max_norm, float* __restrict__ coef,
+                                                               float* __restrict__ norms_out, int nparts,
+                                                               const double* __restrict__ extra, int64_t n_extra) {
+  __shared__ double red[THREADS];
+  const int k = blockIdx.x, t = threadIdx.x;
+  const int nb = nparts * NBLK;
+  double s = 0.0;
+  for (int64_t i = t; i < nb + n_extra; i += THREADS)
+    s += i < nb ? partial[((int64_t)(i / NBLK) * K + k) * NBLK + i % NBLK] : extra[(int64_t)k * n_extra + (i - nb)];
+  red[t] = s;
+  __syncthreads();
+  for (int o = THREADS / 2; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  if (t == 0) {
+    const float total = (float)sqrt(red[0]);
+    const float c = __fdiv_rn(max_norm, __fadd_rn(total, 1e-6f));
+    coef[k] = c < 1.0f ? c : 1.0f;
+    if (norms_out) norms_out[k] = total;
   }
 }
 
@@ -263,7 +292,7 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
       if (!last) *reinterpret_cast<f32x4*>(m + e) = mo;
       *reinterpret_cast<f32x4*>(xd + e) = xo * sg;
     };
-    if (!tb.vec[j]) {
+    if (!(tb.vec[j] & 1)) {
       for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) one(e);
       continue;
     }
@@ -362,8 +391,8 @@ extern "C" int flr_clip_sgd_step_blocked(float* const* x_blocks, const float* co
                                          float momentum, float weight_decay, float max_norm, int first_step,
                                          float* norms_out, void* workspace, size_t workspace_bytes, void* stream) {
   return flr_clip_sgd_step_blocked_x(x_blocks, g_blocks, m_blocks, block_numel, block_client_stride, nblocks, K, lr,
-                                     momentum, weight_decay, max_norm, first_step, nullptr, nullptr, 0, 0, norms_out,
-                                     workspace, workspace_bytes, stream);
+                                     momentum, weight_decay, max_norm, first_step, nullptr, nullptr, 0, 0, nullptr,
+                                     nullptr, 0, norms_out, workspace, workspace_bytes, stream);
 }
 
 extern "C" int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* const* g_blocks,
@@ -371,7 +400,9 @@ extern "C" int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* 
                                            const int64_t* block_client_stride, int64_t nblocks, int64_t K, float lr,
                                            float momentum, float weight_decay, float max_norm, int first_step,
                                            float* x_out, const int64_t* out_offsets, int64_t out_ld, int64_t nneg,
+                                           const uint8_t* block_normed, const double* extra_sq, int64_t n_extra,
                                            float* norms_out, void* workspace, size_t workspace_bytes, void* stream) {
+  if (n_extra < 0 || (n_extra > 0 && !extra_sq)) return FLR_ERR_ARG;
   if (K < 1 || nblocks < 1 || nblocks > (int64_t)train::MAXB * train::MAX_PARTS || !x_blocks || !g_blocks ||
       !m_blocks || !block_numel)
     return FLR_ERR_ARG;
@@ -401,18 +432,46 @@ extern "C" int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* 
       const uintptr_t al = reinterpret_cast<uintptr_t>(x_blocks[j]) | reinterpret_cast<uintptr_t>(g_blocks[j]) |
                            reinterpret_cast<uintptr_t>(m_blocks[j]);
       tb.vec[q] = (block_numel[j] % 4 == 0 && cs % 4 == 0 && (al & 15) == 0) ? 1 : 0;
+      if (block_normed && block_normed[j]) tb.vec[q] |= 2;
       tb.xo[q] = 0;
       if (xout) {
         const int64_t o = out_offsets[j];
         if (o < 0 || o + block_numel[j] > out_ld || o >= ((int64_t)1 << 31)) return FLR_ERR_ARG;
         tb.xo[q] = (int32_t)o;
         // 16-B output accesses need the row segment 16-B aligned as well
-        if (o % 4 != 0 || out_ld % 4 != 0 || (reinterpret_cast<uintptr_t>(xout) & 15) != 0) tb.vec[q] = 0;
+        if (o % 4 != 0 || out_ld % 4 != 0 || (reinterpret_cast<uintptr_t>(xout) & 15) != 0) tb.vec[q] &= ~1;
       }
     }
     P += tb.pre[tb.nb];
   }
   if (P == 0) return FLR_OK;
+  // the optimizer's own sum-of-squares pass covers the blocks without producer
+  // partials, re-packed into their own tables so its NBLK ranges split only them
+  train::BlockTable sqt[train::MAX_PARTS];
+  int nsq = 0;
+  if (block_normed) {
+    for (int c = 0; c < nparts; ++c)
+      for (int q = 0; q < tbs[c].nb; ++q) {
+        if (tbs[c].vec[q] & 2) continue;
+        if (nsq == 0 || sqt[nsq - 1].nb == train::MAXB) {
+          sqt[nsq].nb = 0;
+          sqt[nsq].pre[0] = 0;
+          ++nsq;
+        }
+        train::BlockTable& t = sqt[nsq - 1];
+        const int r = t.nb++;
+        t.x[r] = tbs[c].x[q];
+        t.g[r] = tbs[c].g[q];
+        t.m[r] = tbs[c].m[q];
+        t.cs[r] = tbs[c].cs[q];
+        t.vec[r] = tbs[c].vec[q];
+        t.xo[r] = 0;
+        t.pre[r + 1] = t.pre[r] + (tbs[c].pre[q + 1] - tbs[c].pre[q]);
+      }
+  } else {
+    for (int c = 0; c < nparts; ++c) sqt[c] = tbs[c];
+    nsq = nparts;
+  }
   hipStream_t st = as_stream(stream);
   float* coef = nullptr;
   int rc;
@@ -420,13 +479,17 @@ extern "C" int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* 
     double* partial = static_cast<double*>(workspace);
     coef = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                     align_up((size_t)train::MAX_PARTS * K * train::NBLK * sizeof(double), 256));
-    for (int c = 0; c < nparts; ++c) {
+    for (int c = 0; c < nsq; ++c) {
       hipLaunchKernelGGL(train::sumsq_blocked_kernel, dim3(train::NBLK, (unsigned)K), dim3(train::THREADS), 0, st,
-                         tbs[c], tbs[c].pre[tbs[c].nb], partial + (int64_t)c * K * train::NBLK);
+                         sqt[c], sqt[c].pre[sqt[c].nb], partial + (int64_t)c * K * train::NBLK);
       if ((rc = launch_status("sumsq_blocked_kernel")) != FLR_OK) return rc;
     }
-    hipLaunchKernelGGL(train::clip_coef_kernel, dim3(cdiv((int)K, 64)), dim3(64), 0, st, partial, (int)K, max_norm,
-                       coef, norms_out, nparts);
+    if (n_extra > 0 || block_normed)
+      hipLaunchKernelGGL(train::clip_coef_ex_kernel, dim3((unsigned)K), dim3(train::THREADS), 0, st, partial, (int)K,
+                         max_norm, coef, norms_out, nsq, extra_sq, n_extra);
+    else
+      hipLaunchKernelGGL(train::clip_coef_kernel, dim3(cdiv((int)K, 64)), dim3(64), 0, st, partial, (int)K, max_norm,
+                         coef, norms_out, nsq);
     if ((rc = launch_status("clip_coef_kernel")) != FLR_OK) return rc;
   }
   for (int c = 0; c < nparts; ++c) {

@@ -63,8 +63,8 @@ SIGNATURES = {
                                          _size_t, _c_void_p]),
     "flr_clip_sgd_step_blocked_x": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
                                            ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _int,
-                                           _c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _size_t,
-                                           _c_void_p]),
+                                           _c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64,
+                                           _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_workspace": (_size_t, [_i64] * 10),
     "flr_conv2d_tap_major_ok": (_int, [_i64, _i64]),
     "flr_conv2d_t_workspace": (_size_t, [_i64] * 10),
@@ -72,6 +72,10 @@ SIGNATURES = {
     "flr_conv2d_bwd_data_t": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_weight_t": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_int, _c_void_p, _size_t,
                                                                                          _c_void_p]),
+    "flr_conv2d_bwd_weight_t_sq_slots": (_i64, [_i64] * 10),
+    "flr_conv2d_bwd_weight_t_sq": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_int, _c_void_p, _i64,
+                                                                                            _c_void_p, _size_t,
+                                                                                            _c_void_p]),
     "flr_conv2d_fwd": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_data": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_weight": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),

@@ -270,15 +270,17 @@ def from_tap_major(w_t: torch.Tensor) -> torch.Tensor:
 
 
 def _gconv(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, need_dx: bool = True,
-           tap_major: bool = False, zero_dead: bool = True) -> torch.Tensor:
+           tap_major: bool = False, zero_dead: bool = True, norm_slot=None) -> torch.Tensor:
     """w [K, Cout, Cin, kh, kw] (or [K, kh, kw, Cin, Cout] when tap_major).
     Native (flr kernels): x [K*Cin, B, H, W] -> [K*Cout, B, H', W'];
-    torch: x [B, K*Cin, H, W] -> [B, K*Cout, H', W'] (grouped conv)."""
+    torch: x [B, K*Cin, H, W] -> [B, K*Cout, H', W'] (grouped conv).
+    norm_slot (tap-major): an nn.NormSlot, where the weight gradient's
+    clip-norm partials go (flr_conv2d_bwd_weight_t_sq)."""
     if tap_major:
         if not x.is_cuda:
             raise RuntimeError("tap-major conv weights need the HIP kernels (no CPU path)")
         from ..nn import client_conv2d_t
-        return client_conv2d_t(x, w, stride, pad, need_dx, zero_dead)
+        return client_conv2d_t(x, w, stride, pad, need_dx, zero_dead, norm_slot)
     if _LAYERS == "native" and x.is_cuda:
         from ..nn import client_conv2d
         return client_conv2d(x, w, stride, pad, need_dx)
@@ -351,7 +353,8 @@ def _eval_stats(bn_stats, name: str, gamma: torch.Tensor):
 
 def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: torch.Tensor, spec: ModelSpec,
                     dropout_mask: Optional[torch.Tensor] = None, tap_major: frozenset = frozenset(),
-                    skip_dead: frozenset = frozenset(), bn_stats: Optional[Dict] = None) -> torch.Tensor:
+                    skip_dead: frozenset = frozenset(), bn_stats: Optional[Dict] = None,
+                    norm_slots: Optional[Dict] = None) -> torch.Tensor:
     """images [K, B, C, H, W], tokens [K, B, T] -> logits [K, B, num_classes].
 
     dropout_mask: optional [K, B, fusion] tensor of {0, 1/(1-p)} (explicit masks
@@ -361,9 +364,11 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
     unwritten (the trainer's optimizer step never reads them).
     bn_stats: None (training: batch statistics) or a dict for eval mode (see
     _eval_stats).
+    norm_slots: tap-major weight name -> nn.NormSlot: the weight
+    gradient's clip-norm partials are written there (the trainer's fused norm).
     """
     if spec.family == "cub":
-        return _cub_forward(p, images, tokens, spec, dropout_mask, tap_major, bn_stats)
+        return _cub_forward(p, images, tokens, spec, dropout_mask, tap_major, bn_stats, norm_slots)
     if spec.family == "vit_bert":
         from .transformer import patchify, vit_bert_forward
         patches = patchify(images, spec.patch) if images.dim() == 5 else images
@@ -373,7 +378,8 @@ def batched_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, tokens: to
         return _eval_stats(bn_stats, bn, p[bn + ".weight"])
 
     def conv(name, x, stride, pad, need_dx=True):
-        return _gconv(x, p[name], stride, pad, need_dx, name in tap_major, name not in skip_dead)
+        return _gconv(x, p[name], stride, pad, need_dx, name in tap_major, name not in skip_dead,
+                      None if norm_slots is None else norm_slots.get(name))
 
     K, B = images.shape[:2]
     native = _LAYERS == "native" and images.is_cuda
@@ -454,7 +460,7 @@ def _linear_op(native: bool):
 
 def _cub_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, attrs: Optional[torch.Tensor], spec: ModelSpec,
                  dropout_mask: Optional[torch.Tensor], tap_major: frozenset,
-                 bn_stats: Optional[Dict] = None) -> torch.Tensor:
+                 bn_stats: Optional[Dict] = None, norm_slots: Optional[Dict] = None) -> torch.Tensor:
     """The C1 model (cub200_cnn.py:95-118) for K clients at once: three
     conv3x3(+bias) -> BN -> ReLU -> MaxPool2 blocks, AdaptiveAvgPool(4, 4),
     image_fc + ReLU, the attribute MLP, concat, the fusion head.
@@ -466,7 +472,8 @@ def _cub_forward(p: Dict[str, torch.Tensor], images: torch.Tensor, attrs: Option
          else images.transpose(0, 1).reshape(B, K * C0, H, W))
     for i, idx in enumerate((0, 4, 8)):
         wn = f"image_conv.{idx}.weight"
-        y = _gconv(x, p[wn], 1, 1, need_dx=i > 0, tap_major=wn in tap_major)
+        y = _gconv(x, p[wn], 1, 1, need_dx=i > 0, tap_major=wn in tap_major,
+                   norm_slot=None if norm_slots is None else norm_slots.get(wn))
         bias = p[f"image_conv.{idx}.bias"].reshape(-1)  # [K * Cout]
         y = y + (bias.view(-1, 1, 1, 1) if native else bias.view(1, -1, 1, 1))
         bn = f"image_conv.{idx + 1}"

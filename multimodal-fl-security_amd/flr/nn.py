@@ -74,10 +74,11 @@ class ClientConv2dT(torch.autograd.Function):
     (flr_conv2d_fwd_t / _bwd_data_t / _bwd_weight_t; Cin, Cout multiples of 64)."""
 
     @staticmethod
-    def forward(ctx, x, w_t, stride: int, pad: int, need_dx: bool = True, zero_dead: bool = True):
+    def forward(ctx, x, w_t, stride: int, pad: int, need_dx: bool = True, zero_dead: bool = True, norm_slot=None):
         x = x.contiguous()
         w_t = w_t.contiguous()
         ctx.zero_dead = zero_dead
+        ctx.norm_slot = norm_slot  # a NormSlot or None
         K, KH, KW, Cin, Cout = w_t.shape
         KC, B, H, W = x.shape
         assert KC == K * Cin, (x.shape, w_t.shape)
@@ -108,9 +109,24 @@ class ClientConv2dT(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w_t)
-            _capi.call("flr_conv2d_bwd_weight_t", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *g,
-                       int(ctx.zero_dead), wsp, n, _stream(dy))
-        return dx, dw, None, None, None, None
+            if ctx.norm_slot is None:
+                _capi.call("flr_conv2d_bwd_weight_t", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *g,
+                           int(ctx.zero_dead), wsp, n, _stream(dy))
+            else:  # + the clip norm's partial sums of squares (flr_clip_sgd_step_blocked_x extra_sq)
+                s = ctx.norm_slot
+                _capi.call("flr_conv2d_bwd_weight_t_sq", x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *g,
+                           int(ctx.zero_dead), s.ptr, s.ld, wsp, n, _stream(dy))
+                s.used = True
+        return dx, dw, None, None, None, None, None
+
+
+class NormSlot:
+    """Where a conv weight gradient's clip-norm partials go (sq pointer, row
+    stride); `used` is set by the backward that wrote them, so the optimizer
+    can refuse a step whose norm would miss a block."""
+
+    def __init__(self, ptr: int, ld: int):
+        self.ptr, self.ld, self.used = ptr, ld, False
 
 
 def _workspace_t(geom, device):
@@ -125,8 +141,8 @@ def tap_major_ok(cin: int, cout: int) -> bool:
 
 
 def client_conv2d_t(x: torch.Tensor, w_t: torch.Tensor, stride: int, pad: int, need_dx: bool = True,
-                    zero_dead: bool = True) -> torch.Tensor:
-    return ClientConv2dT.apply(x, w_t, stride, pad, need_dx, zero_dead)
+                    zero_dead: bool = True, norm_slot=None) -> torch.Tensor:
+    return ClientConv2dT.apply(x, w_t, stride, pad, need_dx, zero_dead, norm_slot)
 
 
 def client_conv2d(x, w, stride: int, pad: int, need_dx: bool = True):

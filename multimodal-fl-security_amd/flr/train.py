@@ -21,6 +21,7 @@ aggregates.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -166,6 +167,15 @@ class ClientBatchTrainer:
         self._xo = (ctypes.c_int64 * nb)(*[self.offsets[j] + o for j, o, _, _ in blocks])
         chunk = cfg.client_chunk if cfg.client_chunk > 0 else self.auto_chunk(spec, self.K)
         self.chunks = [(c0, min(self.K, c0 + chunk)) for c0 in range(0, self.K, chunk)]
+        # fused clip norm: the tap-major conv weights' gradient sums of squares come
+        # from the weight-gradient epilogues (flr_conv2d_bwd_weight_t_sq), so the
+        # optimizer's own norm pass reads only the other blocks (FLR_FUSED_NORM=0: off)
+        self._norm_fused = frozenset(self.tap_major) if (
+            cfg.clip > 0 and os.environ.get("FLR_FUSED_NORM", "1") != "0") else frozenset()
+        self._normed = (ctypes.c_uint8 * nb)(*[int(self.names[j] in self._norm_fused) for j, _, _, _ in blocks])
+        self._sq = None        # [K, sq_ld] fp64 partials, sized at the first step (the slots depend on B)
+        self._sq_B = None
+        self._sq_slots: Dict[str, tuple] = {}
         # per chunk: the optimizer's block pointers at the chunk's first client
         self._xp, self._mp = [], []
         for c0, _ in self.chunks:
@@ -255,6 +265,31 @@ class ClientBatchTrainer:
                 _capi.call("flr_copy_rows_neg", w.data_ptr(), n, n, base + 4 * off, ld, self.K, negate_rows, st)
         return self.X
 
+    def _norm_slots(self, B: int, c0: int, c1: int) -> Optional[Dict[str, tuple]]:
+        """name -> (sq pointer, row stride) of every fused-norm conv weight for
+        the chunk [c0, c1); allocates the partial buffer for batch size B."""
+        if not self._norm_fused:
+            return None
+        if self._sq_B != B:
+            geo = conv_geometry(self.spec)
+            lib = _capi.lib()
+            bases, tot = {}, 0
+            for j, name in enumerate(self.names):
+                if name not in self._norm_fused:
+                    continue
+                cout, cin, kh, kw = self.shapes[j]
+                H, k, st, pd, _ = geo[name]
+                n = int(lib.flr_conv2d_bwd_weight_t_sq_slots(c1 - c0, B, cin, H, H, cout, kh, kw, st, pd))
+                if n < 0:
+                    raise RuntimeError(f"no fused-norm slots for {name}")
+                bases[name] = tot
+                tot += n
+            self._sq = torch.zeros(self.K, max(1, tot), dtype=torch.float64, device=self.device)
+            self._sq_bases, self._sq_B = bases, B
+        from .nn import NormSlot
+        ld = self._sq.shape[1]
+        return {name: NormSlot(self._sq.data_ptr() + 8 * (c0 * ld + b), ld) for name, b in self._sq_bases.items()}
+
     # ---- one optimizer step for every client -----------------------------
     def step(self, images, tokens, labels, first: bool, dropout_mask=None, last: bool = False,
              loss_out: Optional[torch.Tensor] = None, out: Optional[ClientMatrix] = None,
@@ -270,20 +305,26 @@ class ClientBatchTrainer:
             leaves = [(w if whole else w[c0:c1]).detach().requires_grad_(True) for w in self.W]
             params: Dict[str, torch.Tensor] = dict(zip(self.names, leaves))
             sl = (lambda t: t) if whole else (lambda t: None if t is None else t[c0:c1])
+            slots = self._norm_slots(images.shape[1], c0, c1)
             logits = batched_forward(params, sl(images), sl(tokens), self.spec, sl(dropout_mask), self.tap_major,
-                                     self.skip_dead)
+                                     self.skip_dead, norm_slots=slots)
             loss_k = CrossEntropy.apply(logits, sl(labels))
             grads = [g.contiguous() for g in torch.autograd.grad(loss_k.sum(), leaves)]
+            if slots is not None and not all(s.used for s in slots.values()):
+                missed = sorted(n for n, s in slots.items() if not s.used)
+                raise RuntimeError(f"fused clip norm: no partials written for {missed}")
             gp = (ctypes.c_void_p * len(self.blocks))(*[grads[j].data_ptr() + 4 * o for j, o, _, _ in self.blocks])
             xo, ld, nneg = None, 0, 0
             if out is not None and last:
                 ld = out.data.stride(0)
                 xo = out.data.data_ptr() + 4 * c0 * ld
                 nneg = max(0, min(negate_rows, c1) - c0)
+            sq, nsq = (None, 0) if slots is None else (self._sq.data_ptr() + 8 * c0 * self._sq.shape[1],
+                                                       self._sq.shape[1])
             _capi.call("flr_clip_sgd_step_blocked_x", xp, gp, mp, self._np, self._cs, len(self.blocks), c1 - c0,
                        c.lr, c.momentum, c.weight_decay, c.clip, int(first) | (int(last) << 1), xo, self._xo, ld,
-                       nneg, self.norms.data_ptr() + 4 * c0, self._ws.data_ptr() + self._ws_off, self._ws_bytes,
-                       _stream(self._wbuf))
+                       nneg, None if slots is None else self._normed, sq, nsq, self.norms.data_ptr() + 4 * c0,
+                       self._ws.data_ptr() + self._ws_off, self._ws_bytes, _stream(self._wbuf))
             del grads, leaves, params, logits
             _capi.call("flr_copy_rows", loss_k.data_ptr(), c1 - c0, c1 - c0, loss_out.data_ptr() + 4 * c0, c1 - c0, 1,
                        _stream(loss_out))

@@ -147,3 +147,51 @@ def test_bgemm_forms_bit_identical(cuda, dims, monkeypatch):
         outs += [bgemm(A, Bm).clone(), bgemm(A.transpose(1, 2).contiguous().transpose(1, 2), Bm).clone()]
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
+
+
+NORM_SHAPES = [  # ResNet-18 layers at the C3 shapes (B = 32): split-K wgrad (l1), one tile pass, dead taps (l4)
+    (4, 32, 64, 8, 8, 64, 3, 1, 1),
+    (4, 32, 128, 4, 4, 128, 3, 1, 1),
+    (4, 32, 256, 2, 2, 256, 3, 1, 1),
+    (4, 32, 512, 1, 1, 512, 3, 1, 1),
+    (4, 32, 256, 2, 2, 512, 3, 2, 1),
+    (4, 32, 64, 8, 8, 128, 1, 2, 0),
+]
+
+
+@pytest.mark.parametrize("shape", NORM_SHAPES, ids=[str(s) for s in NORM_SHAPES])
+def test_wgrad_norm_partials(cuda, shape):
+    """flr_conv2d_bwd_weight_t_sq: the same dw_t as flr_conv2d_bwd_weight_t
+    (bit-identical), and per-client partials that sum to sum(dw^2) (fp64, the
+    clip norm of run_experiments.py:234) within 1e-12; the partials of a client
+    do not depend on how many clients share the launch (K = 4 vs K = 1)."""
+    from flr import _capi
+    from flr.nn import _stream, _workspace_t
+    K, B, Cin, H, W, Cout, KS, stride, pad = shape
+    g = torch.Generator(device="cpu").manual_seed(sum(shape))
+    x = torch.randn(K * Cin, B, H, W, generator=g).to(cuda)
+    Ho = (H + 2 * pad - KS) // stride + 1
+    dy = torch.randn(K * Cout, B, Ho, Ho, generator=g).to(cuda)
+    outs = []
+    for k_lo, k_n in ((0, K), (2, 1)):
+        geom = (k_n, B, Cin, H, W, Cout, KS, KS, stride, pad)
+        n = int(_capi.lib().flr_conv2d_bwd_weight_t_sq_slots(*geom))
+        assert n > 0
+        ws, nb = _workspace_t(geom, cuda)
+        wsp = None if ws is None else ws.data_ptr()
+        xs, dys = x[k_lo * Cin:(k_lo + k_n) * Cin], dy[k_lo * Cout:(k_lo + k_n) * Cout]
+        dw_ref = torch.zeros(k_n, KS, KS, Cin, Cout, device=cuda)
+        dw = torch.zeros_like(dw_ref)
+        sq = torch.full((k_n, n + 3), float("nan"), dtype=torch.float64, device=cuda)
+        _capi.call("flr_conv2d_bwd_weight_t", xs.data_ptr(), dys.data_ptr(), dw_ref.data_ptr(), *geom, 1, wsp, nb,
+                   _stream(x))
+        _capi.call("flr_conv2d_bwd_weight_t_sq", xs.data_ptr(), dys.data_ptr(), dw.data_ptr(), *geom, 1,
+                   sq.data_ptr(), n + 3, wsp, nb, _stream(x))
+        torch.cuda.synchronize()
+        assert torch.equal(dw, dw_ref)
+        assert torch.isnan(sq[:, n:]).all()  # nothing past the slot count
+        want = dw.double().pow(2).reshape(k_n, -1).sum(1)
+        got = sq[:, :n].sum(1)
+        assert torch.allclose(got, want, rtol=1e-12, atol=0), (got, want)
+        outs.append(sq[:, :n].cpu())
+    assert torch.equal(outs[0][2], outs[1][0])

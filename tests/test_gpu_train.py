@@ -307,3 +307,26 @@ def test_c3_round_multikrum_signflip(cuda):
     assert not set(eng.defense.selected_clients) & set(range(f))
     s = np.sort(np.asarray(scores))
     print(f"\n[C3 round] selection-boundary margin {(s[64] - s[63]) / s[64]:.3e}")
+
+
+def test_fused_clip_norm_matches_optimizer_pass(cuda, monkeypatch):
+    """The clip norm from the conv weight-gradient epilogues' partials
+    (flr_conv2d_bwd_weight_t_sq + flr_clip_sgd_step_blocked_x extra_sq) equals
+    the optimizer's own sum-of-squares pass (FLR_FUSED_NORM=0) up to fp64
+    summation order: per-client norms within 1e-6, trained rows within 1e-6."""
+    spec = ModelSpec()
+    K, B, steps = 3, 8, 2
+    glob = initial_global(spec, 42, cuda)
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("FLR_FUSED_NORM", fused)
+        tr = ClientBatchTrainer(spec, K, cuda, TrainConfig(local_steps=steps))
+        assert bool(tr._norm_fused) == (fused == "1")
+        tr.load_global(glob)
+        tr.local_update(batches)
+        out.append((tr.norms.cpu().clone(), tr.X.data[:, : tr.P].cpu().clone()))
+    (n0, x0), (n1, x1) = out
+    assert torch.all(n0 > 1.0)  # the clip is active (max_norm 1.0)
+    assert ((n0 - n1).abs() / n0).max().item() <= 1e-6
+    assert _rel(x1, x0) <= 1e-6, _rel(x1, x0)
