@@ -560,6 +560,41 @@ int flr_attention_fwd(const float* qkv, int64_t KB, int64_t T, int64_t H, int64_
 int flr_attention_bwd(const float* qkv, const float* ctx, const float* dctx, const float* lse, int64_t KB, int64_t T,
                       int64_t H, int64_t head_dim, float* dqkv, void* stream);
 
+/* ---- a1: the client plugin's local update, one C entry --------------------
+ * Replaces the simulation's per-client loop (run_experiments.py:193-240) and
+ * FLClient.fit / _train (fl_client.py:76-149) for K clients of the C2/C3
+ * model family (ResNet image trunk + embedding / 1-layer GRU text branch +
+ * late-fusion head; the module layout of flr.models.multimodal.MultimodalNet)
+ * without torch: every client starts from `global` (P floats in the
+ * reference's parameters() order), runs `steps` local steps (forward, mean
+ * cross-entropy, backward, clip_grad_norm_(max_norm) when max_norm > 0,
+ * SGD(lr, momentum, weight_decay) re-created per client, so momentum starts at
+ * the first gradient), and writes its parameters() vector to row k of X
+ * (X + k*ld, ld >= P; rows k < nneg negated: the sign-flip attackers,
+ * model_poisoning.py:274-276).  loss_out[k] = the mean of the client's
+ * per-step losses (fl_client.py:143-149); norms_out (optional [K]) receives
+ * the last step's pre-clip gradient norms.  Inputs, device, per step s:
+ * images [steps][K][B][C][H][W] f32, tokens [steps][K][B][T] int64, labels
+ * [steps][K][B] int64, dropout_masks NULL or [steps][K][B][fusion] f32 (the
+ * inverted-dropout multipliers).  The same kernel schedule as the Python
+ * trainer (flr.train.ClientBatchTrainer), so both give the same bits.  All
+ * state lives in the workspace (flr_train_clients_workspace); image_size must
+ * bring the trunk to a 1x1 map (32 for the four stride-2 stages). */
+typedef struct flr_resnet_gru_spec {
+  int64_t num_classes, image_size, in_channels;
+  int64_t widths[4], blocks[4];  /* the four ResNet stages (BasicBlock) */
+  int64_t vocab, seq_len, embed, hidden, fusion;
+} flr_resnet_gru_spec;
+int64_t flr_resnet_gru_num_params(const flr_resnet_gru_spec* spec);
+size_t flr_train_clients_workspace(const flr_resnet_gru_spec* spec, int64_t K, int64_t B,
+                                   int64_t steps);
+int flr_train_clients(const flr_resnet_gru_spec* spec, const float* global, float* X,
+                      int64_t ld, const float* images, const int64_t* tokens,
+                      const int64_t* labels, const float* dropout_masks, int64_t steps,
+                      int64_t K, int64_t B, float lr, float momentum, float weight_decay,
+                      float max_norm, int64_t nneg, float* loss_out, float* norms_out,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

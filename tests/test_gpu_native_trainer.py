@@ -1,0 +1,52 @@
+"""GPU: flr_train_clients (the client plugin as one C entry, SURVEY §8(b);
+FLClient.fit / _train fl_client.py:76-149, run_experiments.py:193-240) gives
+the bits of the Python trainer (ClientBatchTrainer: the same kernels driven
+through torch autograd) — trained rows, per-client mean loss and clip norms —
+and the reference loop (the oracle) at 1e-5."""
+import pytest
+import torch
+
+from oracle import training as otrain
+from flr import native_trainer as nt
+from flr.models.multimodal import TINY, ModelSpec, MultimodalNet
+from flr.round import initial_global
+from flr.train import ClientBatchTrainer, TrainConfig, make_dropout_masks, synthetic_batches
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("spec_name,B,nneg", [("tiny", 4, 1), ("c3", 8, 1), ("c3_b40", 40, 0)])
+def test_native_trainer_bit_identical_to_python_trainer(cuda, spec_name, B, nneg):
+    spec = TINY if spec_name == "tiny" else ModelSpec()
+    K, steps = 3, 2
+    cfg = TrainConfig(local_steps=steps)
+    glob = initial_global(spec, 42, cuda)
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    masks = make_dropout_masks(spec, steps, K, B, cuda, seed=11)
+    tr = ClientBatchTrainer(spec, K, cuda, cfg)
+    tr.load_global(glob)
+    loss_py = tr.local_update(batches, masks, negate_rows=nneg).clone()
+    X_py = tr.X.data[:, : tr.P].clone()
+    norms_py = tr.norms.clone()
+    X, loss, norms = nt.train_clients(spec, glob, batches, cfg, masks, negate_rows=nneg)
+    torch.cuda.synchronize()
+    assert torch.isfinite(X).all()
+    assert torch.equal(loss, loss_py), (loss, loss_py)
+    assert torch.equal(norms, norms_py), (norms, norms_py)
+    assert torch.equal(X, X_py), (X - X_py).abs().max()
+
+
+def test_native_trainer_matches_reference_loop(cuda):
+    spec = ModelSpec()
+    K, B, steps = 2, 8, 2
+    glob = initial_global(spec, 42, cuda)
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    masks = make_dropout_masks(spec, steps, K, B, cuda, seed=3)
+    X, loss, _ = nt.train_clients(spec, glob, batches, TrainConfig(local_steps=steps), masks)
+    for k in range(K):
+        cb = [(im[k].cpu(), tk[k].cpu(), lb[k].cpu()) for im, tk, lb in batches]
+        upd, ref_loss = otrain.local_update(MultimodalNet, spec, glob.cpu(), cb, masks=[m[k].cpu() for m in masks])
+        ref = torch.cat([u.reshape(-1) for u in upd])
+        err = ((X[k].cpu().double() - ref.double()).abs().max() / ref.abs().max()).item()
+        assert err < 1e-5, err
+        assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
