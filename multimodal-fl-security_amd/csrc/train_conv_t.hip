@@ -147,9 +147,9 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& hi, bf16x8& 
   typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
   // (-1, 0) and (0, -1) as opaque SGPRs: hipcc encodes a (-1, 0) constant as the
   // inline constant -1.0, which the hardware reads as the fp32 bits, i.e. (0, -1)
-  unsigned klo, khi;
-  asm volatile("s_mov_b32 %0, 0xbf80" : "=s"(klo));
-  asm volatile("s_mov_b32 %0, 0xbf800000" : "=s"(khi));
+  unsigned klo, khi;  // non-volatile: the compiler may hoist / share them
+  asm("s_mov_b32 %0, 0xbf80" : "=s"(klo));
+  asm("s_mov_b32 %0, 0xbf800000" : "=s"(khi));
   const bf16x2 nl = __builtin_bit_cast(bf16x2, klo), nh = __builtin_bit_cast(bf16x2, khi);
 #pragma unroll
   for (int p = 0; p < 4; ++p) {

@@ -66,6 +66,28 @@ def test_pairwise_gram_vs_direct_and_fp64(cuda, K, P):
         assert np.all(np.diag(D) == 0) and np.array_equal(D, D.T)
 
 
+@pytest.mark.parametrize("K", [129, 300, 512])
+def test_pairwise_two_term_gram_wide(cuda, monkeypatch, K):
+    """The 2-term split that every BASELINE-size call runs (P >= 2^20), forced
+    at a small P for K > 128 (the diagonal 128-row groups and the cross
+    groups).  Against fp64 distances: 1e-4 for every pair, 2e-5 for the benign
+    rows (measured 3.9e-6 / 1.3e-7)."""
+    monkeypatch.setenv("FLR_GRAM_TERMS", "2")
+    P = 65536 + 17
+    f = K // 5
+    X = update_matrix(K, P, f=f, seed=K, device=cuda)[:, :P]
+    D = ops.pairwise_l2(X, "gram").cpu().numpy()
+    Xd = X.double().cpu()
+    exact = torch.cdist(Xd, Xd).numpy()
+    rel = np.abs(D - exact) / np.maximum(exact, 1e-30)
+    np.fill_diagonal(rel, 0)
+    benign = np.arange(K) >= f
+    print(f"\n[2-term Gram K={K}] max rel {rel.max():.2e}, benign rows {rel[benign].max():.2e}")
+    assert rel.max() < 1e-4, rel.max()
+    assert rel[benign].max() < 2e-5
+    assert np.all(np.diag(D) == 0) and np.array_equal(D, D.T)
+
+
 def test_pairwise_large_offset_centering(cuda):
     # a large common component (weights, not deltas) must not cost accuracy
     K, P = 48, 50000
