@@ -280,12 +280,14 @@ def main() -> None:
                 "one all-to-all (client rows -> coordinate ranges), per-GPU aggregation of its range, "
                 "all-gather of the aggregated vector" if sharded else "one all-gather of the client matrix")),
             "exchange": eng.exchange,
-            "training_phase": "one captured HIP graph per round" if eng.use_graph else "eager launches",
+            "training_phase": ("one captured HIP graph per round" if eng.use_graph else "eager launches") + (
+                "; local updates = one flr_train_clients_ex call" if eng.native else
+                "; local updates = the Python autograd composition of the kernels"),
         },
         "aggregate_ms": aggregate_ms,
         "train_ms_per_round": train_ms,
         "attackers_selected": attackers_selected,
-        "round_roofline": round_roofline(K, P, sum(c for _, _, c, _ in eng.trainer.blocks), args.local_steps,
+        "round_roofline": round_roofline(K, P, eng.trainer.live_params, args.local_steps,
                                          elapsed / args.steps * 1e3, world),
         "roofline": {
             "kernel": "gram_partials_kernel (Krum pairwise, centred Gram on MFMA)",

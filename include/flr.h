@@ -284,6 +284,15 @@ int flr_conv2d_bwd_data_t(const float* dy, const float* w_t, float* dx, int64_t 
                           int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
                           int64_t KH, int64_t KW, int64_t stride, int64_t pad,
                           void* workspace, size_t workspace_bytes, void* stream);
+/* dx = dgrad + add (one rounding per element; add in dx's layout, NULL: none):
+ * the residual block's two input-gradient paths summed in the dgrad epilogue,
+ * the value autograd's accumulation of the conv path and the shortcut path
+ * gives (the reference's BasicBlock backward, torchvision resnet18). */
+int flr_conv2d_bwd_data_t_add(const float* dy, const float* w_t, const float* add,
+                              float* dx, int64_t K, int64_t B, int64_t Cin, int64_t H,
+                              int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+                              int64_t stride, int64_t pad, void* workspace,
+                              size_t workspace_bytes, void* stream);
 /* zero_dead_taps: write the dead taps' slabs of dw_t as zeros (1) or leave
  * them untouched (0: the caller never reads them, see
  * flr_clip_sgd_step_blocked). */
@@ -594,6 +603,31 @@ int flr_train_clients(const flr_resnet_gru_spec* spec, const float* global, floa
                       int64_t K, int64_t B, float lr, float momentum, float weight_decay,
                       float max_norm, int64_t nneg, float* loss_out, float* norms_out,
                       void* workspace, size_t workspace_bytes, void* stream);
+/* flags (flr_train_clients_ex):
+ * FLR_TC_TRAIN_ORDER — `global` and X's rows are in TRAINING order: every
+ *   tap-major conv weight (Cin, Cout multiples of 64) as [KH][KW][Cin][Cout]
+ *   at its torch offset (flr_resnet_gru_reorder converts a P-vector either
+ *   way).  The round engine's order (flr.round): Krum distances, row
+ *   selections, coordinate-wise means and order statistics do not depend on a
+ *   common coordinate permutation, so the last optimizer step writes X's rows
+ *   directly (no export pass), the untrained dead-tap ranges are copied from
+ *   `global`, and only the aggregated P-vector is permuted back.
+ * Flag 0 is flr_train_clients. */
+#define FLR_TC_TRAIN_ORDER 1u
+int flr_train_clients_ex(const flr_resnet_gru_spec* spec, const float* global, float* X,
+                         int64_t ld, const float* images, const int64_t* tokens,
+                         const int64_t* labels, const float* dropout_masks, int64_t steps,
+                         int64_t K, int64_t B, float lr, float momentum, float weight_decay,
+                         float max_norm, int64_t nneg, float* loss_out, float* norms_out,
+                         unsigned flags, void* workspace, size_t workspace_bytes, void* stream);
+/* dst <- src (one P-vector) in training order (to_train = 1) or back in the
+ * reference's parameters() order (0); src != dst. */
+int flr_resnet_gru_reorder(const flr_resnet_gru_spec* spec, const float* src, float* dst,
+                           int to_train, void* stream);
+/* Parameters the optimizer updates: P minus the dead conv taps (taps that only
+ * read zero padding at this image size; exact-zero gradients) when
+ * weight_decay == 0, else P. */
+int64_t flr_resnet_gru_live_params(const flr_resnet_gru_spec* spec, float weight_decay);
 
 #ifdef __cplusplus
 }

@@ -58,6 +58,17 @@ __global__ void to_tap_major_kernel(const float* __restrict__ src, float* __rest
   }
 }
 
+// dst[co][ci][t] = src[t][ci][co]: tap-major -> torch order (one vector)
+__global__ void from_tap_major_kernel(const float* __restrict__ src, float* __restrict__ dst, int64_t Cout,
+                                      int64_t Cin, int64_t KK) {
+  const int64_t n = Cout * Cin * KK;
+  for (int64_t i = (int64_t)blockIdx.x * THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * THREADS) {
+    const int64_t t = i % KK, r = i / KK;
+    const int64_t ci = r % Cin, co = r / Cin;
+    dst[i] = src[(t * Cin + ci) * Cout + co];
+  }
+}
+
 inline unsigned grid_for(int64_t n) {
   const int64_t g = (n + THREADS - 1) / THREADS;
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 4096));
@@ -325,6 +336,79 @@ class Net {
     return FLR_OK;
   }
 
+  // Training order (flr.train.ClientBatchTrainer.to_train_order): the P-vector
+  // with every tap-major conv weight in its training layout [KH][KW][Cin][Cout]
+  // at its torch offset.  load_global_train broadcasts only what the kernels
+  // read (the dead-tap slabs stay out of the training state).
+  int load_global_train(const float* gtrain, hipStream_t st) {
+    int rc;
+    for (const auto& b : blocks_opt_) {
+      const Param& p = ps_[b.j];
+      if ((rc = flr_broadcast_rows(gtrain + p.off + b.o, b.n, p.w + b.o, K_, b.cs, st)) != FLR_OK) return rc;
+    }
+    return FLR_OK;
+  }
+
+  // src (one P-vector) -> dst in the other order; to_train: torch -> training
+  int reorder(const float* src, float* dst, bool to_train, hipStream_t st) {
+    int rc;
+    int64_t run0 = 0, run1 = 0;  // a run of consecutive plain parameters: one copy
+    auto flush = [&]() {
+      const int r = run1 > run0 ? flr_copy_rows(src + run0, run1 - run0, run1 - run0, dst + run0, run1 - run0, 1, st)
+                                : (int)FLR_OK;
+      run0 = run1;
+      return r;
+    };
+    for (const auto& p : ps_) {
+      if (!p.tap) {
+        if (run1 != p.off && (rc = flush()) != FLR_OK) return rc;
+        if (run1 == run0) run0 = run1 = p.off;
+        run1 = p.off + p.n;
+        continue;
+      }
+      if ((rc = flush()) != FLR_OK) return rc;
+      run0 = run1 = p.off + p.n;
+      {
+        const int64_t KK = p.shape[2] * p.shape[3];
+        if (to_train)
+          hipLaunchKernelGGL(to_tap_major_kernel, dim3(grid_for(p.n)), dim3(THREADS), 0, st, src + p.off,
+                             dst + p.off, p.shape[0], p.shape[1], KK);
+        else
+          hipLaunchKernelGGL(from_tap_major_kernel, dim3(grid_for(p.n)), dim3(THREADS), 0, st, src + p.off,
+                             dst + p.off, p.shape[0], p.shape[1], KK);
+        if ((rc = launch_status("train_clients: reorder")) != FLR_OK) return rc;
+      }
+    }
+    return flush();
+  }
+
+  // X's dead-tap ranges (training order) <- gtrain, rows k < nneg negated
+  int dead_ranges(const float* gtrain, float* X, int64_t ld, int64_t nneg, hipStream_t st) {
+    int rc;
+    for (size_t j = 0; j < ps_.size(); ++j) {
+      const Param& p = ps_[j];
+      if (!p.dead) continue;
+      int64_t e = 0;
+      auto fill = [&](int64_t a) {
+        if (a > e && (rc = flr_broadcast_rows_neg(gtrain + p.off + e, a - e, X + p.off + e, K_, ld, nneg, st)) !=
+                         FLR_OK)
+          return rc;
+        return (int)FLR_OK;
+      };
+      for (const auto& b : blocks_opt_) {
+        if (b.j != (int)j) continue;
+        if ((rc = fill(b.o)) != FLR_OK) return rc;
+        e = b.o + b.n;
+      }
+      if ((rc = fill(p.n)) != FLR_OK) return rc;
+    }
+    return FLR_OK;
+  }
+
+  // the last step writes X's rows (training order) instead of the weights
+  float* xout_ = nullptr;
+  int64_t xld_ = 0, xneg_ = 0;
+
   int step(const float* images, const int64_t* tokens, const int64_t* labels, const float* mask, bool first,
            bool last, float* loss_row, float lr, float mom, hipStream_t st) {
     int rc;
@@ -432,16 +516,22 @@ class Net {
       FLR_TRY(bn_bwd(bk.b2, d_out, bk.y2, bk.out, true, bk.d_y2, bk.d_res, st));
       FLR_TRY(conv_bwd(bk.c2, bk.a1, bk.d_y2, bk.d_a1, st));
       FLR_TRY(bn_bwd(bk.b1, bk.d_a1, bk.y1, bk.a1, true, bk.d_y1, nullptr, st));
-      FLR_TRY(conv_bwd(bk.c1, bk.x_in, bk.d_y1, bk.d_xm, st));
       const float* other = bk.d_res;  // identity shortcut: the residual gradient itself
       if (bk.has_ds) {
         FLR_TRY(bn_bwd(bk.bds, bk.d_res, bk.yd, nullptr, false, bk.d_yd, nullptr, st));
         FLR_TRY(conv_bwd(bk.ds, bk.x_in, bk.d_yd, bk.d_xd, st));
         other = bk.d_xd;
       }
-      hipLaunchKernelGGL(add_kernel, dim3(grid_for(bk.in_elems)), dim3(THREADS), 0, st, bk.d_xm, other, bk.d_in,
-                         bk.in_elems);
-      FLR_TRY(launch_status("train_clients: gradient sum"));
+      // d_in = dgrad(c1) + other: the two paths' sum (autograd's accumulation),
+      // in the dgrad epilogue when c1 is tap-major, else one extra pass
+      if (ps_[bk.c1.p].tap && fuse_res_) {
+        FLR_TRY(conv_bwd(bk.c1, bk.x_in, bk.d_y1, bk.d_in, st, other));
+      } else {
+        FLR_TRY(conv_bwd(bk.c1, bk.x_in, bk.d_y1, bk.d_xm, st));
+        hipLaunchKernelGGL(add_kernel, dim3(grid_for(bk.in_elems)), dim3(THREADS), 0, st, bk.d_xm, other, bk.d_in,
+                           bk.in_elems);
+        FLR_TRY(launch_status("train_clients: gradient sum"));
+      }
     }
     FLR_TRY(flr_maxpool2d_bwd(d_p0_, arg0_, d_a0_, K_ * s.widths[0] * B_, Hs_, Hs_, 3, 3, 2, 1, st));
     FLR_TRY(bn_bwd(stem_bn_, d_a0_, y0_, a0_, true, d_y0_, nullptr, st));
@@ -451,8 +541,10 @@ class Net {
     std::vector<const float*> gb;
     std::vector<int64_t> nb, cs;
     std::vector<uint8_t> normed;
+    std::vector<int64_t> xoffs;  // the blocks' offsets in a training-order row
     for (const auto& b : blocks_opt_) {
       const Param& p = ps_[b.j];
+      xoffs.push_back(p.off + b.o);
       xb.push_back(p.w + b.o);
       gb.push_back(p.g + b.o);
       mb.push_back(p.m + b.o);
@@ -462,8 +554,9 @@ class Net {
     }
     const bool fuse = clip_ > 0 && nsq_ > 0;
     FLR_TRY(flr_clip_sgd_step_blocked_x(xb.data(), gb.data(), mb.data(), nb.data(), cs.data(), (int64_t)xb.size(), K_,
-                                        lr, mom, wd_, clip_, int(first) | (int(last) << 1), nullptr, nullptr, 0, 0,
-                                        fuse ? normed.data() : nullptr, fuse ? sq_ : nullptr, fuse ? nsq_ : 0,
+                                        lr, mom, wd_, clip_, int(first) | (int(last) << 1),
+                                        last ? xout_ : nullptr, last && xout_ ? xoffs.data() : nullptr, xld_,
+                                        xneg_, fuse ? normed.data() : nullptr, fuse ? sq_ : nullptr, fuse ? nsq_ : 0,
                                         norms_, sgd_ws_, sgd_ws_n_, st));
 #undef FLR_TRY
     return FLR_OK;
@@ -484,6 +577,12 @@ class Net {
   }
 
   float* norms_ = nullptr;  // optional [K] clip norms (the caller's)
+  bool fuse_res_ = true;     // FLR_FUSED_RES=0: the separate gradient-sum pass (A/B)
+  int64_t live_params() const {
+    int64_t n = 0;
+    for (const auto& b : blocks_opt_) n += b.n;
+    return n;
+  }
 
  private:
   struct OptBlock {
@@ -558,12 +657,13 @@ class Net {
     return flr_conv2d_fwd(x, p.w, y, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad, c.fws, c.fws_n, st);
   }
   // dx (when wanted) then dw, as ClientConv2d[T].backward
-  int conv_bwd(const ConvOp& c, const float* x, const float* dy, float* dx, hipStream_t st) {
+  int conv_bwd(const ConvOp& c, const float* x, const float* dy, float* dx, hipStream_t st,
+               const float* add = nullptr) {
     const Param& p = ps_[c.p];
     int rc;
     if (p.tap) {
-      if (dx && (rc = flr_conv2d_bwd_data_t(dy, p.w, dx, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad,
-                                            cws_, cws_n_, st)) != FLR_OK)
+      if (dx && (rc = flr_conv2d_bwd_data_t_add(dy, p.w, add, dx, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride,
+                                                c.pad, cws_, cws_n_, st)) != FLR_OK)
         return rc;
       const int zero_dead = p.dead ? 0 : 1;
       if (p.sq_base >= 0)
@@ -646,8 +746,19 @@ extern "C" int flr_train_clients(const flr_resnet_gru_spec* spec, const float* g
                                  const float* dropout_masks, int64_t steps, int64_t K, int64_t B, float lr,
                                  float momentum, float weight_decay, float max_norm, int64_t nneg, float* loss_out,
                                  float* norms_out, void* workspace, size_t workspace_bytes, void* stream) {
+  return flr_train_clients_ex(spec, global, X, ld, images, tokens, labels, dropout_masks, steps, K, B, lr, momentum,
+                              weight_decay, max_norm, nneg, loss_out, norms_out, 0, workspace, workspace_bytes, stream);
+}
+
+extern "C" int flr_train_clients_ex(const flr_resnet_gru_spec* spec, const float* global, float* X, int64_t ld,
+                                    const float* images, const int64_t* tokens, const int64_t* labels,
+                                    const float* dropout_masks, int64_t steps, int64_t K, int64_t B, float lr,
+                                    float momentum, float weight_decay, float max_norm, int64_t nneg, float* loss_out,
+                                    float* norms_out, unsigned flags, void* workspace, size_t workspace_bytes,
+                                    void* stream) {
   if (!spec || !global || !X || !images || !tokens || !labels || !loss_out || steps < 1 || K < 1 || B < 1 || nneg < 0)
     return FLR_ERR_ARG;
+  if (flags & ~(unsigned)FLR_TC_TRAIN_ORDER) return FLR_ERR_ARG;
   if (!workspace || workspace_bytes < flr_train_clients_workspace(spec, K, B, steps)) return FLR_ERR_WORKSPACE;
   char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
   tc::Net net(*spec, K, B, weight_decay, max_norm, base);
@@ -656,8 +767,22 @@ extern "C" int flr_train_clients(const flr_resnet_gru_spec* spec, const float* g
   if (ld < net.P()) return FLR_ERR_ARG;
   float* step_loss = reinterpret_cast<float*>(base + align_up(net.bytes(), 256));
   net.norms_ = norms_out;
+  static const bool fuse_res = [] {
+    const char* e = getenv("FLR_FUSED_RES");
+    return !(e && e[0] == '0');
+  }();
+  net.fuse_res_ = fuse_res;
+  const bool train_order = (flags & FLR_TC_TRAIN_ORDER) != 0;
   hipStream_t st = as_stream(stream);
-  if ((rc = net.load_global(global, st)) != FLR_OK) return rc;
+  if (train_order) {
+    net.xout_ = X;
+    net.xld_ = ld;
+    net.xneg_ = nneg;
+    rc = net.load_global_train(global, st);
+  } else {
+    rc = net.load_global(global, st);
+  }
+  if (rc != FLR_OK) return rc;
   const int64_t C0 = spec->in_channels, HW0 = spec->image_size * spec->image_size, T = spec->seq_len;
   for (int64_t s = 0; s < steps; ++s) {
     rc = net.step(images + s * K * B * C0 * HW0, tokens + s * K * B * T, labels + s * K * B,
@@ -665,6 +790,23 @@ extern "C" int flr_train_clients(const flr_resnet_gru_spec* spec, const float* g
                   step_loss + s * K, lr, momentum, st);
     if (rc != FLR_OK) return rc;
   }
-  if ((rc = net.export_rows(X, ld, nneg, st)) != FLR_OK) return rc;
+  rc = train_order ? net.dead_ranges(global, X, ld, nneg, st) : net.export_rows(X, ld, nneg, st);
+  if (rc != FLR_OK) return rc;
   return flr_mean_rows(step_loss, steps, K, loss_out, st);
+}
+
+extern "C" int flr_resnet_gru_reorder(const flr_resnet_gru_spec* spec, const float* src, float* dst, int to_train,
+                                      void* stream) {
+  if (!spec || !src || !dst || src == dst) return FLR_ERR_ARG;
+  tc::Net net(*spec, 1, 1, 0.f, 0.f, nullptr);
+  const int rc = net.layout();
+  if (rc != FLR_OK) return rc;
+  return net.reorder(src, dst, to_train != 0, as_stream(stream));
+}
+
+extern "C" int64_t flr_resnet_gru_live_params(const flr_resnet_gru_spec* spec, float weight_decay) {
+  if (!spec) return -1;
+  tc::Net net(*spec, 1, 1, weight_decay, 0.f, nullptr);
+  if (net.layout() != FLR_OK) return -1;
+  return net.live_params();
 }

@@ -340,6 +340,7 @@ struct DgradT {
   const float* dy;
   const float* w;
   float* dx;
+  const float* add;  // optional addend in dx's layout: dx = dgrad + add (one rounding)
   int ca, cb, Hc, Wc, ntc;
   conv::FastDiv d_hcwc, d_wc;
   int8_t ckh[conv::MAXTAPS], ckw[conv::MAXTAPS];
@@ -404,7 +405,14 @@ struct DgradT {
     const uint32_t bb = udiv(n, d_hcwc), p = n - bb * Hc * Wc;
     const uint32_t ihc = udiv(p, d_wc), iwc = p - ihc * Wc;
     const int ih = ca + (int)ihc * g.stride, iw = cb + (int)iwc * g.stride;
-    dx[k * g.sxk + m * g.sxc + bb * g.sxb + ih * g.W + iw] = v;
+    const int64_t i = k * g.sxk + m * g.sxc + bb * g.sxb + ih * g.W + iw;
+    dx[i] = add ? __fadd_rn(v, add[i]) : v;
+  }
+  __device__ int64_t index(int k, int m, int n) const {  // dx offset of output (m, n) of client k
+    const uint32_t bb = udiv(n, d_hcwc), p = n - bb * Hc * Wc;
+    const uint32_t ihc = udiv(p, d_wc), iwc = p - ihc * Wc;
+    const int ih = ca + (int)ihc * g.stride, iw = cb + (int)iwc * g.stride;
+    return k * g.sxk + m * g.sxc + bb * g.sxb + ih * g.W + iw;
   }
   // stride 1 (the one class is every pixel): dx[k][m][n] is linear in n
   __device__ bool linear() const { return g.stride == 1; }
@@ -1154,6 +1162,10 @@ __device__ __forceinline__ double block_sumsq(double s, double* red) {
   return t;
 }
 
+// the epilogue's optional addend (DgradT: the other gradient path of a residual
+// block, summed where autograd would add the two paths)
+template <class P> __device__ inline const float* plan_add(const P&) { return nullptr; }
+__device__ inline const float* plan_add(const DgradT& p) { return p.add; }
 template <class Plan, int MS, int NS, int X6>
 __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S, float* __restrict__ part, int remap,
                                                            int prio) {
@@ -1357,12 +1369,40 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
         float* base = pl.out() + pl.tile_base(k, tm0, tn0);
         const int64_t ldm = pl.ldm();
         const int nl = 32 * wn + l32;
+        if (const float* abase = plan_add(pl)) {  // all 16 addends in flight before the first store
+          abase += pl.tile_base(k, tm0, tn0);
+          float av[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int ml = 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+            av[e] = (tm0 + ml < M && tn0 + nl < N) ? abase[ml * ldm + nl] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] = __fadd_rn(acc[i][j][e], av[e]);
+        }
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int ml = 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
           if (tm0 + ml < M && tn0 + nl < N) base[ml * ldm + nl] = acc[i][j][e];
         }
         continue;
+      }
+      if constexpr (std::is_same<Plan, DgradT>::value) {
+        if (S == 1 && pl.add) {  // parity-class stores: the addends loaded before any store
+          int64_t ix[16];
+          float av[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int m = tm0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int n = tn0 + 32 * wn + l32;
+            ix[e] = (m < M && n < N) ? pl.index(k, m, n) : -1;
+            av[e] = ix[e] >= 0 ? pl.add[ix[e]] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (ix[e] >= 0) pl.dx[ix[e]] = __fadd_rn(acc[i][j][e], av[e]);
+          continue;
+        }
       }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
@@ -1518,12 +1558,40 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
         float* base = pl.out() + pl.tile_base(k, tm0, tn0);
         const int64_t ldm = pl.ldm();
         const int nl = 32 * wn + l32;
+        if (const float* abase = plan_add(pl)) {  // all 16 addends in flight before the first store
+          abase += pl.tile_base(k, tm0, tn0);
+          float av[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int ml = 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+            av[e] = (tm0 + ml < M && tn0 + nl < N) ? abase[ml * ldm + nl] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] = __fadd_rn(acc[i][j][e], av[e]);
+        }
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int ml = 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
           if (tm0 + ml < M && tn0 + nl < N) base[ml * ldm + nl] = acc[i][j][e];
         }
         continue;
+      }
+      if constexpr (std::is_same<Plan, DgradT>::value) {
+        if (S == 1 && pl.add) {  // parity-class stores: the addends loaded before any store
+          int64_t ix[16];
+          float av[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int m = tm0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int n = tn0 + 32 * wn + l32;
+            ix[e] = (m < M && n < N) ? pl.index(k, m, n) : -1;
+            av[e] = ix[e] >= 0 ? pl.add[ix[e]] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (ix[e] >= 0) pl.dx[ix[e]] = __fadd_rn(acc[i][j][e], av[e]);
+          continue;
+        }
       }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
@@ -1878,6 +1946,14 @@ extern "C" int flr_conv2d_fwd_t(const float* x, const float* w_t, float* y, int6
 extern "C" int flr_conv2d_bwd_data_t(const float* dy, const float* w_t, float* dx, int64_t K, int64_t B, int64_t Cin,
                                      int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                                      int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+  return flr_conv2d_bwd_data_t_add(dy, w_t, nullptr, dx, K, B, Cin, H, W, Cout, KH, KW, stride, pad, ws, ws_bytes,
+                                   stream);
+}
+
+extern "C" int flr_conv2d_bwd_data_t_add(const float* dy, const float* w_t, const float* add, float* dx, int64_t K,
+                                         int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH,
+                                         int64_t KW, int64_t stride, int64_t pad, void* ws, size_t ws_bytes,
+                                         void* stream) {
   if (!dy || !w_t || !dx) return FLR_ERR_ARG;
   if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad))
     return conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) ? FLR_ERR_UNSUPPORTED : FLR_ERR_ARG;
@@ -1886,7 +1962,7 @@ extern "C" int flr_conv2d_bwd_data_t(const float* dy, const float* w_t, float* d
   convt::DgradT cls[convt::MAX_CLASSES];
   const int nc = convt::dgrad_classes(g, cls);
   for (int c = 0; c < nc; ++c) {
-    cls[c].dy = dy; cls[c].w = w_t; cls[c].dx = dx;
+    cls[c].dy = dy; cls[c].w = w_t; cls[c].dx = dx; cls[c].add = add;
     const int rc = convt::launch(cls[c], ws, ws_bytes, as_stream(stream), "conv bwd data (tap-major)");
     if (rc != FLR_OK) return rc;
   }

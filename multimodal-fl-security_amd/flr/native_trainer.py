@@ -67,3 +67,101 @@ def train_clients(spec: ModelSpec, global_flat: torch.Tensor, batches: Sequence,
                cfg.lr, cfg.momentum, cfg.weight_decay, cfg.clip, negate_rows, loss.data_ptr(), norms.data_ptr(),
                ws.data_ptr(), n, torch.cuda.current_stream(dev).cuda_stream)
     return X, loss, norms
+
+
+class NativeRoundTrainer:
+    """The round engine's trainer for the ResNet + GRU family on
+    flr_train_clients_ex: the whole local update of this GPU's clients is one
+    C call (captured into the round's HIP graph by flr.round), so no torch
+    kernel runs in the training phase.  The same surface RoundEngine uses of
+    flr.train.ClientBatchTrainer (X, P, to_train_order / to_torch_order,
+    load_global[_train], local_update), with the same bits: the kernel
+    schedule is the Python trainer's, plus the residual blocks' two gradient
+    paths summed in the dgrad epilogue (one rounding, as autograd's add)."""
+
+    def __init__(self, spec: ModelSpec, num_clients: int, device, cfg: TrainConfig = TrainConfig(), batch: int = 32):
+        from .matrix import ClientMatrix
+        from .models.multimodal import param_layout
+        self.spec, self.cfg = spec, cfg
+        self.device = torch.device(device)
+        self.K = int(num_clients)
+        self.B = int(batch)
+        self._sp = ResNetGruSpec.of(spec)
+        shapes = [s for _, s in param_layout(spec)]
+        self.X = ClientMatrix.empty(self.K, shapes, self.device)
+        self.P = self.X.P
+        if num_params(spec) != self.P:
+            raise RuntimeError(f"flr_train_clients lays out {num_params(spec)} parameters, the model {self.P}")
+        self.live_params = int(_capi.lib().flr_resnet_gru_live_params(ctypes.byref(self._sp), cfg.weight_decay))
+        self.chunks = [(0, self.K)]
+        steps = max(1, cfg.local_steps)
+        self._ws_bytes = workspace_bytes(spec, self.K, self.B, steps)
+        if self._ws_bytes == 0:
+            raise ValueError("flr_train_clients: unsupported model or shape")
+        self._ws = torch.empty(self._ws_bytes, dtype=torch.uint8, device=self.device)
+        self._ws_steps = steps
+        self.loss = torch.empty(self.K, dtype=torch.float32, device=self.device)
+        self.norms = torch.empty(self.K, dtype=torch.float32, device=self.device)
+        self._global = None   # the vector the next local_update starts from, and its order
+        self._order = 0
+        self._bound = None    # (batches, masks) -> contiguous [steps][K]... inputs
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _reorder(self, src: torch.Tensor, dst: torch.Tensor, to_train: bool) -> torch.Tensor:
+        src = src.to(self.device, torch.float32).contiguous()
+        _capi.call("flr_resnet_gru_reorder", ctypes.byref(self._sp), src.data_ptr(), dst.data_ptr(), int(to_train),
+                   self._stream())
+        return dst
+
+    def to_train_order(self, flat: torch.Tensor) -> torch.Tensor:
+        return self._reorder(flat, torch.empty(self.P, dtype=torch.float32, device=self.device), True)
+
+    def to_torch_order(self, flat: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty(self.P, dtype=torch.float32, device=self.device)
+        return self._reorder(flat, out, False)
+
+    def load_global(self, global_flat: torch.Tensor) -> None:
+        """Every client starts from global_flat (torch order) at the next local_update."""
+        self._global, self._order = global_flat, 0
+
+    def load_global_train(self, gtrain: torch.Tensor, live_only: bool = True) -> None:
+        """The same from a training-order vector; the next local_update then
+        writes X in training order (FLR_TC_TRAIN_ORDER)."""
+        self._global, self._order = gtrain, 1
+
+    def _inputs(self, batches: Sequence, masks: Optional[Sequence]):
+        if self._bound is not None and self._bound[0] is batches and self._bound[1] is masks:
+            return self._bound[2]
+        imgs = torch.stack([b[0] for b in batches]).float().contiguous()
+        toks = torch.stack([b[1] for b in batches]).long().contiguous()
+        labs = torch.stack([b[2] for b in batches]).long().contiguous()
+        m = None if masks is None else torch.stack(list(masks)).float().contiguous()
+        if labs.shape[1:] != (self.K, self.B):
+            raise ValueError(f"labels {tuple(labs.shape)}: expected [steps, {self.K}, {self.B}]")
+        self._bound = (batches, masks, (imgs, toks, labs, m))
+        return self._bound[2]
+
+    def local_update(self, batches: Sequence, dropout_masks: Optional[Sequence] = None, export: bool = True,
+                     negate_rows: int = 0, gtrain: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """len(batches) local steps of every client from the loaded global
+        vector; X <- the client rows (training order after load_global_train,
+        else torch order), rows < negate_rows negated; returns the [K] mean losses."""
+        if self._global is None:
+            raise RuntimeError("local_update before load_global / load_global_train")
+        if gtrain is not None and (self._order != 1 or gtrain.data_ptr() != self._global.data_ptr()):
+            raise ValueError("local_update(gtrain=) must follow load_global_train(gtrain)")
+        steps = len(batches)
+        if steps > self._ws_steps:
+            raise ValueError(f"{steps} local steps, workspace sized for {self._ws_steps}")
+        imgs, toks, labs, m = self._inputs(batches, dropout_masks)
+        c = self.cfg
+        g = self._global
+        _capi.call("flr_train_clients_ex", ctypes.byref(self._sp), g.data_ptr(), self.X.data.data_ptr(),
+                   self.X.data.stride(0), imgs.data_ptr(), toks.data_ptr(), labs.data_ptr(),
+                   None if m is None else m.data_ptr(), steps, self.K, self.B, c.lr, c.momentum, c.weight_decay,
+                   c.clip, int(negate_rows), self.loss.data_ptr(), self.norms.data_ptr(), self._order,
+                   self._ws.data_ptr(), self._ws_bytes, self._stream())
+        return self.loss

@@ -66,7 +66,16 @@ class RoundEngine:
         K = rcfg.num_clients
         self.lo, self.hi = fdist.shard(K, world, rank)
         shapes = [s for _, s in param_layout(spec)]
-        self.trainer = ClientBatchTrainer(spec, self.hi - self.lo, self.device, tcfg)
+        # the ResNet + GRU family trains through the one C entry flr_train_clients_ex
+        # (no torch kernel in the training phase); FLR_TRAINER=python: the
+        # autograd composition of the same kernels (A/B; the other families)
+        self.native = (spec.family == "resnet_gru" and self.device.type == "cuda"
+                       and os.environ.get("FLR_TRAINER", "native") != "python")
+        if self.native:
+            from .native_trainer import NativeRoundTrainer
+            self.trainer = NativeRoundTrainer(spec, self.hi - self.lo, self.device, tcfg, batch=rcfg.batch)
+        else:
+            self.trainer = ClientBatchTrainer(spec, self.hi - self.lo, self.device, tcfg)
         cfg = dict(rcfg.defense_cfg)
         if rcfg.defense in ("krum", "multi_krum", "krum_trimmed_mean"):  # run_experiments.py:155-162
             cfg.setdefault("num_malicious", rcfg.num_attackers)

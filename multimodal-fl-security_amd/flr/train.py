@@ -160,6 +160,7 @@ class ClientBatchTrainer:
                     self.dead_ranges.append((self.offsets[j] + e, a - e))
                 e = b
         self.blocks = blocks
+        self.live_params = sum(c for _, _, c, _ in blocks)
         nb = len(blocks)
         self._np = (ctypes.c_int64 * nb)(*[c for _, _, c, _ in blocks])
         self._cs = (ctypes.c_int64 * nb)(*[cs for _, _, _, cs in blocks])

@@ -195,3 +195,33 @@ def test_wgrad_norm_partials(cuda, shape):
         assert torch.allclose(got, want, rtol=1e-12, atol=0), (got, want)
         outs.append(sq[:, :n].cpu())
     assert torch.equal(outs[0][2], outs[1][0])
+
+
+@pytest.mark.parametrize("form", [None, "pipe"])
+@pytest.mark.parametrize("shape", TAP_SHAPES, ids=[str(s) for s in TAP_SHAPES])
+def test_dgrad_addend_bit_identical(cuda, shape, form, monkeypatch):
+    """flr_conv2d_bwd_data_t_add: dx = dgrad + add in the epilogue (linear
+    stride-1 stores, the parity-class stores, the split-K reduce, classes with
+    no tap) equals flr_conv2d_bwd_data_t followed by one fp32 add — the sum
+    autograd forms of a residual block's two input-gradient paths."""
+    from flr import _capi
+    from flr.nn import _stream, _workspace_t
+    if form:
+        monkeypatch.setenv("FLR_GEMM", form)
+    K, B, Cin, H, W, Cout, KS, stride, pad = shape
+    g = torch.Generator(device="cpu").manual_seed(sum(shape) + 3)
+    Ho, Wo = (H + 2 * pad - KS) // stride + 1, (W + 2 * pad - KS) // stride + 1
+    dy = torch.randn(K * Cout, B, Ho, Wo, generator=g).to(cuda)
+    wt = (torch.randn(K, KS, KS, Cin, Cout, generator=g) * 0.1).to(cuda)
+    add = torch.randn(K * Cin, B, H, W, generator=g).to(cuda)
+    geom = (K, B, Cin, H, W, Cout, KS, KS, stride, pad)
+    ws, nb = _workspace_t(geom, cuda)
+    wsp = None if ws is None else ws.data_ptr()
+    dx = torch.full_like(add, float("nan"))
+    _capi.call("flr_conv2d_bwd_data_t", dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), *geom, wsp, nb, _stream(dy))
+    want = dx + add
+    got = torch.full_like(add, float("nan"))
+    _capi.call("flr_conv2d_bwd_data_t_add", dy.data_ptr(), wt.data_ptr(), add.data_ptr(), got.data_ptr(), *geom,
+               wsp, nb, _stream(dy))
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)

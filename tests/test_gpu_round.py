@@ -119,3 +119,32 @@ def test_training_order_round_equals_torch_order(cuda, monkeypatch, defense, cfg
         assert err <= 1e-6, err
     else:
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("order", ["train", "torch"])
+def test_native_trainer_round_equals_python_trainer(cuda, monkeypatch, order):
+    """The round engine's ResNet + GRU trainer is the one C entry
+    flr_train_clients_ex (training order: live-only load, the last step
+    writing X, dead-tap ranges from the global vector; torch order: the
+    export pass), with the residual blocks' two gradient paths summed in the
+    dgrad epilogue.  Against the Python autograd composition of the same
+    kernels (FLR_TRAINER=python): the same global model bit for bit, the
+    same per-client losses, over 2 rounds of HIP-graph replay with sign-flip
+    attackers, on the full ResNet-18 + GRU model (tap-major convs, dead taps)."""
+    from flr.models.multimodal import ModelSpec
+    spec = ModelSpec()
+    rc = RoundConfig(num_clients=6, batch=4, defense="median", attack="sign_flip", num_attackers=2)
+    monkeypatch.setenv("FLR_ORDER", order)
+    res = []
+    for trainer in ("python", "native"):
+        monkeypatch.setenv("FLR_TRAINER", trainer)
+        eng = RoundEngine(spec, rc, TrainConfig(local_steps=2), cuda)
+        assert eng.native == (trainer == "native") and eng.train_order == (order == "train")
+        for _ in range(2):
+            eng.run_round()
+        res.append((eng.global_flat.clone().cpu(), eng.losses.clone().cpu(), eng.trainer.X.X.clone().cpu()))
+    (ga, la, xa), (gb, lb, xb) = res
+    assert torch.isfinite(ga).all()
+    assert torch.equal(la, lb)
+    assert torch.equal(xa, xb)
+    assert torch.equal(ga, gb)
