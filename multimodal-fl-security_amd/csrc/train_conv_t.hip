@@ -1676,19 +1676,30 @@ inline int conv_min_kt() {
   return v;
 }
 
+// Stride-1 dgrad (one class: the forward's GEMM shape, transposed) takes the
+// forward's split rule unless FLR_DGRAD_MINKT1 overrides it (A/B timing).
+inline int dgrad_min_kt1() {
+  static const int v = [] {
+    const char* e = getenv("FLR_DGRAD_MINKT1");
+    const int x = e ? atoi(e) : 0;
+    return x >= 1 && x <= 256 ? x : 0;
+  }();
+  return v ? v : conv_min_kt();
+}
+
 template <class Plan>
-inline int plan_min_kt() {
+inline int plan_min_kt(const Plan& pl) {
   if (std::is_base_of<BGemmArgs, Plan>::value) return bgemm_min_kt();
-  // a dgrad parity class has few tiles per client (l3a: one 128 x 128 tile):
-  // it keeps the deeper split-K, or the launch runs ~128 workgroups on 256 CUs
-  if (std::is_same<Plan, DgradT>::value) return 8;
+  // a strided dgrad's parity class has few tiles per client (l3a: one 128 x 128
+  // tile): it keeps the deeper split-K, or the launch runs ~128 workgroups on 256 CUs
+  if constexpr (std::is_same<Plan, DgradT>::value) return pl.g.stride == 1 ? dgrad_min_kt1() : 8;
   return conv_min_kt();
 }
 
 template <class Plan>
 size_t splits_bytes(const Plan& pl) {  // enough for any sub-tile shape
-  const int S = std::max(choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 1, plan_min_kt<Plan>()),
-                         choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 2, plan_min_kt<Plan>()));
+  const int S = std::max(choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 1, plan_min_kt(pl)),
+                         choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 2, plan_min_kt(pl)));
   return S > 1 ? (size_t)S * pl.g.Kc * pl.M() * pl.N() * sizeof(float) : 0;
 }
 
@@ -1714,7 +1725,7 @@ inline int tile_choice(int M, int N, int R) {
 template <class Plan, int MS, int NS>
 int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   const int M = pl.M(), N = pl.N(), R = pl.R(), K = pl.g.Kc;
-  int S = choose_splits(M, N, R, K, MS * NS, plan_min_kt<Plan>());
+  int S = choose_splits(M, N, R, K, MS * NS, plan_min_kt(pl));
   if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) S = 1;
   const dim3 grid((unsigned)cdiv(N, BN * NS), (unsigned)cdiv(M, BM * MS), (unsigned)(K * S));
   int form = gemm_form();
@@ -1765,7 +1776,7 @@ int sq_slots(const Plan& pl) {
   const int M = pl.M(), N = pl.N(), R = pl.R();
   const int tile = tile_choice(M, N, R);
   const int ms = (tile == 21 || tile == 22) ? 2 : 1, ns = (tile == 12 || tile == 22) ? 2 : 1;
-  const int S = choose_splits(M, N, R, pl.g.Kc, ms * ns, plan_min_kt<Plan>());
+  const int S = choose_splits(M, N, R, pl.g.Kc, ms * ns, plan_min_kt(pl));
   if (S == 1) return cdiv(N, BN * ns) * cdiv(M, BM * ms);
   return (int)(((int64_t)M * N + 255) / 256);
 }

@@ -97,7 +97,7 @@ class Comm:
     def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> None:
         """out [world * n] <- concat over ranks of t [n] (rank order)."""
         if self.world == 1:
-            out.copy_(t.reshape(out.shape))
+            _copy(t, out, t.numel())
             return
         ho, ht = self._host(out), self._host(t.contiguous())
         dist.all_gather_into_tensor(ho, ht, group=self.group)
@@ -146,7 +146,7 @@ class CoordSlice:
         """out [P] <- concatenation of every rank's aggregated range (all-gather)."""
         plan, world = self.plan, self.plan.world
         if world == 1:
-            out.copy_(part[: self.n])
+            _copy(part, out, self.n)
             return out
         if self._gbuf is None or self._gbuf.device != part.device:
             # allocated once; the tail past n stays zero across rounds
@@ -159,6 +159,17 @@ class CoordSlice:
             b, e = plan.coords(r)
             out[b:e].copy_(buf[r * plan.ld: r * plan.ld + (e - b)])
         return out
+
+
+def _copy(src: torch.Tensor, dst: torch.Tensor, n: int) -> None:
+    """dst[:n] <- src[:n] (contiguous, same dtype): flr_copy_rows on the
+    device (bytes as float32 words), torch's copy on the host."""
+    if src.is_cuda and dst.is_cuda and src.is_contiguous() and dst.is_contiguous() and src.dtype == dst.dtype \
+            and (n * src.element_size()) % 4 == 0:
+        w = n * src.element_size() // 4
+        _capi.call("flr_copy_rows", src.data_ptr(), w, w, dst.data_ptr(), w, 1, _stream(src))
+    else:
+        dst.reshape(-1)[:n].copy_(src.reshape(-1)[:n])
 
 
 def _stream(t: torch.Tensor) -> int:

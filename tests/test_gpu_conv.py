@@ -225,3 +225,4 @@ def test_dgrad_addend_bit_identical(cuda, shape, form, monkeypatch):
                wsp, nb, _stream(dy))
     torch.cuda.synchronize()
     assert torch.equal(got, want)
+
