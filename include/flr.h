@@ -204,6 +204,21 @@ int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* const* g_bl
                                 const uint8_t* block_normed, const double* extra_sq,
                                 int64_t n_extra, float* norms_out, void* workspace,
                                 size_t workspace_bytes, void* stream);
+/* flr_clip_sgd_step_blocked_x whose FIRST step reads every client's parameters
+ * of block j from one shared vector, x_src + src_offsets[j] (the global model
+ * all clients start from, so no per-client copy of it is loaded; offset < 0:
+ * the block reads x_blocks[j]); the update still goes to x_blocks (or x_out on
+ * a last step, where src_offsets[j] must equal out_offsets[j]).  x_src NULL:
+ * flr_clip_sgd_step_blocked_x. */
+int flr_clip_sgd_step_blocked_src(float* const* x_blocks, const float* const* g_blocks,
+                                  float* const* m_blocks, const int64_t* block_numel,
+                                  const int64_t* block_client_stride, int64_t nblocks, int64_t K,
+                                  float lr, float momentum, float weight_decay, float max_norm,
+                                  int first_step, float* x_out, const int64_t* out_offsets,
+                                  int64_t out_ld, int64_t nneg, const uint8_t* block_normed,
+                                  const double* extra_sq, int64_t n_extra, const float* x_src,
+                                  const int64_t* src_offsets, float* norms_out, void* workspace,
+                                  size_t workspace_bytes, void* stream);
 
 /* ---- a2: client-batched 2-D convolution (bias-free, as in the conv blocks)
  * Replaces nn.Conv2d forward/backward for every client of a GPU at once
@@ -293,6 +308,19 @@ int flr_conv2d_bwd_data_t_add(const float* dy, const float* w_t, const float* ad
                               int64_t W, int64_t Cout, int64_t KH, int64_t KW,
                               int64_t stride, int64_t pad, void* workspace,
                               size_t workspace_bytes, void* stream);
+/* The forward and the input gradient with w_stride floats between clients'
+ * weights (KH*KW*Cin*Cout: the per-client layout above; 0: every client reads
+ * the one copy at w_t — the first local step, when every client still holds
+ * the global model, needs no per-client copy of it). */
+int flr_conv2d_fwd_t_ex(const float* x, const float* w_t, int64_t w_stride, float* y,
+                        int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
+                        int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* workspace,
+                        size_t workspace_bytes, void* stream);
+int flr_conv2d_bwd_data_t_ex(const float* dy, const float* w_t, int64_t w_stride,
+                             const float* add, float* dx, int64_t K, int64_t B, int64_t Cin,
+                             int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+                             int64_t stride, int64_t pad, void* workspace,
+                             size_t workspace_bytes, void* stream);
 /* zero_dead_taps: write the dead taps' slabs of dw_t as zeros (1) or leave
  * them untouched (0: the caller never reads them, see
  * flr_clip_sgd_step_blocked). */

@@ -342,8 +342,10 @@ class Net {
   // read (the dead-tap slabs stay out of the training state).
   int load_global_train(const float* gtrain, hipStream_t st) {
     int rc;
+    gshared_ = shared_first_ ? gtrain : nullptr;
     for (const auto& b : blocks_opt_) {
       const Param& p = ps_[b.j];
+      if (gshared_ && p.tap) continue;  // the first step reads the one copy in gtrain
       if ((rc = flr_broadcast_rows(gtrain + p.off + b.o, b.n, p.w + b.o, K_, b.cs, st)) != FLR_OK) return rc;
     }
     return FLR_OK;
@@ -405,6 +407,11 @@ class Net {
     return FLR_OK;
   }
 
+  // training order: the first step's tap-major conv weights are gshared_ (the
+  // global vector, one copy for every client; FLR_SHARED_FIRST=0: broadcast)
+  bool shared_first_ = true;
+  const float* gshared_ = nullptr;
+  bool first_ = false;
   // the last step writes X's rows (training order) instead of the weights
   float* xout_ = nullptr;
   int64_t xld_ = 0, xneg_ = 0;
@@ -416,6 +423,7 @@ class Net {
   if ((rc = (x)) != FLR_OK) return rc
     const auto& s = s_;
     const int64_t C0 = s.in_channels, HW0 = s.image_size * s.image_size, N = B_ * T_;
+    first_ = first;
     // ---------------- forward ----------------
     hipLaunchKernelGGL(permute_images_kernel, dim3(grid_for(K_ * B_ * C0 * HW0)), dim3(THREADS), 0, st, images,
                        ximg_, K_, B_, C0, HW0);
@@ -553,11 +561,17 @@ class Net {
       normed.push_back(p.sq_base >= 0 ? 1 : 0);
     }
     const bool fuse = clip_ > 0 && nsq_ > 0;
-    FLR_TRY(flr_clip_sgd_step_blocked_x(xb.data(), gb.data(), mb.data(), nb.data(), cs.data(), (int64_t)xb.size(), K_,
-                                        lr, mom, wd_, clip_, int(first) | (int(last) << 1),
-                                        last ? xout_ : nullptr, last && xout_ ? xoffs.data() : nullptr, xld_,
-                                        xneg_, fuse ? normed.data() : nullptr, fuse ? sq_ : nullptr, fuse ? nsq_ : 0,
-                                        norms_, sgd_ws_, sgd_ws_n_, st));
+    // first step in training order: the tap-major blocks read the shared global copy
+    std::vector<int64_t> soffs;
+    const bool src = first && gshared_;
+    if (src)
+      for (const auto& b : blocks_opt_) soffs.push_back(ps_[b.j].tap ? ps_[b.j].off + b.o : -1);
+    FLR_TRY(flr_clip_sgd_step_blocked_src(xb.data(), gb.data(), mb.data(), nb.data(), cs.data(), (int64_t)xb.size(),
+                                          K_, lr, mom, wd_, clip_, int(first) | (int(last) << 1),
+                                          last ? xout_ : nullptr, last && xout_ ? xoffs.data() : nullptr, xld_,
+                                          xneg_, fuse ? normed.data() : nullptr, fuse ? sq_ : nullptr,
+                                          fuse ? nsq_ : 0, src ? gshared_ : nullptr, src ? soffs.data() : nullptr,
+                                          norms_, sgd_ws_, sgd_ws_n_, st));
 #undef FLR_TRY
     return FLR_OK;
   }
@@ -650,10 +664,21 @@ class Net {
     cws_n_ = std::max(cws_n_, n);
   }
 
+  // a tap-major conv weight: per client, or (first step, training order) the
+  // one global copy every client reads with client stride 0
+  const float* tap_w(const Param& p, int64_t& stride) const {
+    const bool shared = first_ && gshared_;
+    stride = shared ? 0 : p.n;
+    return shared ? gshared_ + p.off : p.w;
+  }
   int conv_fwd(const ConvOp& c, const float* x, float* y, hipStream_t st) {
     const Param& p = ps_[c.p];
-    if (p.tap) return flr_conv2d_fwd_t(x, p.w, y, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad, cws_,
-                                       cws_n_, st);
+    if (p.tap) {
+      int64_t wst;
+      const float* w = tap_w(p, wst);
+      return flr_conv2d_fwd_t_ex(x, w, wst, y, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad, cws_,
+                                 cws_n_, st);
+    }
     return flr_conv2d_fwd(x, p.w, y, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad, c.fws, c.fws_n, st);
   }
   // dx (when wanted) then dw, as ClientConv2d[T].backward
@@ -662,8 +687,10 @@ class Net {
     const Param& p = ps_[c.p];
     int rc;
     if (p.tap) {
-      if (dx && (rc = flr_conv2d_bwd_data_t_add(dy, p.w, add, dx, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride,
-                                                c.pad, cws_, cws_n_, st)) != FLR_OK)
+      int64_t wst;
+      const float* w = tap_w(p, wst);
+      if (dx && (rc = flr_conv2d_bwd_data_t_ex(dy, w, wst, add, dx, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k,
+                                               c.stride, c.pad, cws_, cws_n_, st)) != FLR_OK)
         return rc;
       const int zero_dead = p.dead ? 0 : 1;
       if (p.sq_base >= 0)
@@ -772,6 +799,11 @@ extern "C" int flr_train_clients_ex(const flr_resnet_gru_spec* spec, const float
     return !(e && e[0] == '0');
   }();
   net.fuse_res_ = fuse_res;
+  static const bool shared_first = [] {
+    const char* e = getenv("FLR_SHARED_FIRST");
+    return !(e && e[0] == '0');
+  }();
+  net.shared_first_ = shared_first;
   const bool train_order = (flags & FLR_TC_TRAIN_ORDER) != 0;
   hipStream_t st = as_stream(stream);
   if (train_order) {

@@ -219,6 +219,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
   const float* x;
   const float* w;
   float* y;
+  int64_t wsk;  // weight floats between clients (KK*Cin*Cout; 0: every client reads one shared copy)
   static constexpr int LA = KR_VEC, LB = KR_GATHER;
   __host__ __device__ int M() const { return g.Cout; }
   __host__ __device__ int N() const { return g.B * g.Ho * g.Wo; }
@@ -232,7 +233,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
   __device__ State init(int k, int m0, int n0, int tid) const {
     State s;
     const int KK = g.KH * g.KW;
-    s.ra = make_rsrc(w + (int64_t)k * KK * g.Cin * g.Cout, (int64_t)KK * g.Cin * g.Cout);
+    s.ra = make_rsrc(w + (int64_t)k * wsk, (int64_t)KK * g.Cin * g.Cout);
     s.rb = make_rsrc(x + k * g.sxk, g.xext);
     s.a0 = (unsigned)(((tid / 16) * g.Cout + m0 + 4 * (tid % 16)) * 4);
     const int n = n0 + tid % 64;
@@ -292,7 +293,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
     State8 s;
     const int KK = g.KH * g.KW;
     const int row = tid & 63, k0 = 8 * (tid >> 6);
-    s.ra = make_rsrc(w + (int64_t)k * KK * g.Cin * g.Cout, (int64_t)KK * g.Cin * g.Cout);
+    s.ra = make_rsrc(w + (int64_t)k * wsk, (int64_t)KK * g.Cin * g.Cout);
     s.rb = make_rsrc(x + k * g.sxk, g.xext);
     s.a0 = (unsigned)((k0 * g.Cout + m0 + row) * 4);
     const int n = n0 + row;
@@ -341,6 +342,7 @@ struct DgradT {
   const float* w;
   float* dx;
   const float* add;  // optional addend in dx's layout: dx = dgrad + add (one rounding)
+  int64_t wsk;       // weight floats between clients (KK*Cin*Cout; 0: one shared copy)
   int ca, cb, Hc, Wc, ntc;
   conv::FastDiv d_hcwc, d_wc;
   int8_t ckh[conv::MAXTAPS], ckw[conv::MAXTAPS];
@@ -358,7 +360,7 @@ struct DgradT {
   __device__ State init(int k, int m0, int n0, int tid) const {
     State s;
     const int KK = g.KH * g.KW;
-    s.ra = make_rsrc(w + (int64_t)k * KK * g.Cin * g.Cout, (int64_t)KK * g.Cin * g.Cout);
+    s.ra = make_rsrc(w + (int64_t)k * wsk, (int64_t)KK * g.Cin * g.Cout);
     s.rb = make_rsrc(dy + k * g.syk, g.yext);
     s.a0 = (unsigned)(((m0 + tid / 8) * g.Cout + 4 * (tid % 8)) * 4);
     const int n = n0 + tid % 64;
@@ -429,7 +431,7 @@ struct DgradT {
     State8 s;
     const int KK = g.KH * g.KW;
     const int row = tid & 63, k0 = 8 * (tid >> 6);
-    s.ra = make_rsrc(w + (int64_t)k * KK * g.Cin * g.Cout, (int64_t)KK * g.Cin * g.Cout);
+    s.ra = make_rsrc(w + (int64_t)k * wsk, (int64_t)KK * g.Cin * g.Cout);
     s.rb = make_rsrc(dy + k * g.syk, g.yext);
     s.a0 = (unsigned)(((m0 + row) * g.Cout + k0) * 4);
     const int n = n0 + row;
@@ -1945,12 +1947,19 @@ extern "C" size_t flr_conv2d_t_workspace(int64_t K, int64_t B, int64_t Cin, int6
 extern "C" int flr_conv2d_fwd_t(const float* x, const float* w_t, float* y, int64_t K, int64_t B, int64_t Cin,
                                 int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                                 int64_t pad, void* ws, size_t ws_bytes, void* stream) {
-  if (!x || !w_t || !y) return FLR_ERR_ARG;
+  return flr_conv2d_fwd_t_ex(x, w_t, KH * KW * Cin * Cout, y, K, B, Cin, H, W, Cout, KH, KW, stride, pad, ws,
+                             ws_bytes, stream);
+}
+
+extern "C" int flr_conv2d_fwd_t_ex(const float* x, const float* w_t, int64_t w_stride, float* y, int64_t K, int64_t B,
+                                   int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+                                   int64_t stride, int64_t pad, void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !w_t || !y || w_stride < 0) return FLR_ERR_ARG;
   if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad))
     return conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) ? FLR_ERR_UNSUPPORTED : FLR_ERR_ARG;
   convt::FwdT pl;
   pl.g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
-  pl.x = x; pl.w = w_t; pl.y = y;
+  pl.x = x; pl.w = w_t; pl.y = y; pl.wsk = w_stride;
   return convt::launch(pl, ws, ws_bytes, as_stream(stream), "conv fwd (tap-major)");
 }
 
@@ -1965,7 +1974,15 @@ extern "C" int flr_conv2d_bwd_data_t_add(const float* dy, const float* w_t, cons
                                          int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH,
                                          int64_t KW, int64_t stride, int64_t pad, void* ws, size_t ws_bytes,
                                          void* stream) {
-  if (!dy || !w_t || !dx) return FLR_ERR_ARG;
+  return flr_conv2d_bwd_data_t_ex(dy, w_t, KH * KW * Cin * Cout, add, dx, K, B, Cin, H, W, Cout, KH, KW, stride, pad,
+                                  ws, ws_bytes, stream);
+}
+
+extern "C" int flr_conv2d_bwd_data_t_ex(const float* dy, const float* w_t, int64_t w_stride, const float* add,
+                                        float* dx, int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W,
+                                        int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* ws,
+                                        size_t ws_bytes, void* stream) {
+  if (!dy || !w_t || !dx || w_stride < 0) return FLR_ERR_ARG;
   if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad))
     return conv::geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad) ? FLR_ERR_UNSUPPORTED : FLR_ERR_ARG;
   if (stride > 4) return FLR_ERR_UNSUPPORTED;  // <= MAX_CLASSES parity classes
@@ -1973,7 +1990,7 @@ extern "C" int flr_conv2d_bwd_data_t_add(const float* dy, const float* w_t, cons
   convt::DgradT cls[convt::MAX_CLASSES];
   const int nc = convt::dgrad_classes(g, cls);
   for (int c = 0; c < nc; ++c) {
-    cls[c].dy = dy; cls[c].w = w_t; cls[c].dx = dx; cls[c].add = add;
+    cls[c].dy = dy; cls[c].w = w_t; cls[c].dx = dx; cls[c].add = add; cls[c].wsk = w_stride;
     const int rc = convt::launch(cls[c], ws, ws_bytes, as_stream(stream), "conv bwd data (tap-major)");
     if (rc != FLR_OK) return rc;
   }

@@ -154,7 +154,8 @@ struct BlockTable {
   int32_t cs[MAXB];   // client stride of block j (elements)
   int32_t xo[MAXB];   // last step with an output matrix: block j's offset in an output row
   uint8_t vec[MAXB];  // bit 0: block j may use 16-B accesses (n % 4 == 0, all three bases 16-B aligned);
-                      // bit 1: its squares arrive as producer partials (extra_sq): sumsq skips it
+                      // bit 1: its squares arrive as producer partials (extra_sq): sumsq skips it;
+                      // bit 2: the first step reads its parameters from the shared x_src + xo[j]
   int nb;
 };
 
@@ -250,7 +251,8 @@ constexpr int NSGD = 256;
 __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable tb, int64_t P,
                                                               const float* __restrict__ coef, float lr, float mom,
                                                               float wd, int flags, float* __restrict__ xout,
-                                                              int64_t xout_ld, int nneg) {
+                                                              int64_t xout_ld, int nneg,
+                                                              const float* __restrict__ xsrc) {
   const int k = blockIdx.y, b = blockIdx.x;
   const bool first = flags & 1, last = flags & 2;
   const float c = coef ? coef[k] : 1.0f;
@@ -274,9 +276,12 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
     const float* g = tb.g[j] + base;
     float* m = tb.m[j] + base;
     float* xd = redirect ? xout + (int64_t)k * xout_ld + tb.xo[j] - tb.pre[j] : x;
+    // the first step of a round may read every client's parameters from one
+    // shared copy (the global model they all start from)
+    const float* xr = (first && xsrc && (tb.vec[j] & 4)) ? xsrc + tb.xo[j] - tb.pre[j] : x;
     auto one = [&](int64_t e) {
       float mo, xo;
-      upd(x[e], g[e], first ? 0.f : m[e], mo, xo);
+      upd(xr[e], g[e], first ? 0.f : m[e], mo, xo);
       if (!last) m[e] = mo;
       xd[e] = xo * sg;
     };
@@ -305,7 +310,7 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
     int64_t e = vlo + 4 * (int64_t)threadIdx.x;
     for (; e + 4 * THREADS < vhi; e += 8 * THREADS) {  // two float4 groups per lane in flight
       const int64_t e2 = e + 4 * THREADS;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(x + e), x1 = *reinterpret_cast<const f32x4*>(x + e2);
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr + e), x1 = *reinterpret_cast<const f32x4*>(xr + e2);
       const f32x4 g0 = *reinterpret_cast<const f32x4*>(g + e), g1 = *reinterpret_cast<const f32x4*>(g + e2);
       const f32x4 m0 = first ? z : *reinterpret_cast<const f32x4*>(m + e);
       const f32x4 m1 = first ? z : *reinterpret_cast<const f32x4*>(m + e2);
@@ -313,7 +318,7 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
       four(x1, g1, m1, e2);
     }
     if (e < vhi) {
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(x + e), g0 = *reinterpret_cast<const f32x4*>(g + e);
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr + e), g0 = *reinterpret_cast<const f32x4*>(g + e);
       four(x0, g0, first ? z : *reinterpret_cast<const f32x4*>(m + e), e);
     }
     for (int64_t t = (vhi > vlo ? vhi : vlo) + threadIdx.x; t < hi; t += THREADS) one(t);
@@ -402,7 +407,24 @@ extern "C" int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* 
                                            float* x_out, const int64_t* out_offsets, int64_t out_ld, int64_t nneg,
                                            const uint8_t* block_normed, const double* extra_sq, int64_t n_extra,
                                            float* norms_out, void* workspace, size_t workspace_bytes, void* stream) {
+  return flr_clip_sgd_step_blocked_src(x_blocks, g_blocks, m_blocks, block_numel, block_client_stride, nblocks, K, lr,
+                                       momentum, weight_decay, max_norm, first_step, x_out, out_offsets, out_ld, nneg,
+                                       block_normed, extra_sq, n_extra, nullptr, nullptr, norms_out, workspace,
+                                       workspace_bytes, stream);
+}
+
+extern "C" int flr_clip_sgd_step_blocked_src(float* const* x_blocks, const float* const* g_blocks,
+                                             float* const* m_blocks, const int64_t* block_numel,
+                                             const int64_t* block_client_stride, int64_t nblocks, int64_t K, float lr,
+                                             float momentum, float weight_decay, float max_norm, int first_step,
+                                             float* x_out, const int64_t* out_offsets, int64_t out_ld, int64_t nneg,
+                                             const uint8_t* block_normed, const double* extra_sq, int64_t n_extra,
+                                             const float* x_src, const int64_t* src_offsets, float* norms_out,
+                                             void* workspace, size_t workspace_bytes, void* stream) {
   if (n_extra < 0 || (n_extra > 0 && !extra_sq)) return FLR_ERR_ARG;
+  // the first step's shared parameter source: block j at x_src + src_offsets[j] (< 0: none)
+  const float* xsrc = (first_step & 1) ? x_src : nullptr;
+  if (xsrc && !src_offsets) return FLR_ERR_ARG;
   if (K < 1 || nblocks < 1 || nblocks > (int64_t)train::MAXB * train::MAX_PARTS || !x_blocks || !g_blocks ||
       !m_blocks || !block_numel)
     return FLR_ERR_ARG;
@@ -440,6 +462,13 @@ extern "C" int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* 
         tb.xo[q] = (int32_t)o;
         // 16-B output accesses need the row segment 16-B aligned as well
         if (o % 4 != 0 || out_ld % 4 != 0 || (reinterpret_cast<uintptr_t>(xout) & 15) != 0) tb.vec[q] &= ~1;
+      }
+      if (xsrc && src_offsets[j] >= 0) {  // xo holds the source offset (one step both: they must agree)
+        const int64_t o = src_offsets[j];
+        if (o >= ((int64_t)1 << 31) || (xout && o != tb.xo[q])) return FLR_ERR_ARG;
+        tb.xo[q] = (int32_t)o;
+        tb.vec[q] |= 4;
+        if (o % 4 != 0 || (reinterpret_cast<uintptr_t>(xsrc) & 15) != 0) tb.vec[q] &= ~1;
       }
     }
     P += tb.pre[tb.nb];
@@ -495,7 +524,7 @@ extern "C" int flr_clip_sgd_step_blocked_x(float* const* x_blocks, const float* 
   for (int c = 0; c < nparts; ++c) {
     hipLaunchKernelGGL(train::sgd_blocked_kernel, dim3(train::NSGD, (unsigned)K), dim3(train::THREADS), 0, st, tbs[c],
                        tbs[c].pre[tbs[c].nb], coef, lr, momentum, weight_decay, first_step & 3, xout, out_ld,
-                       (int)std::min<int64_t>(nneg, K));
+                       (int)std::min<int64_t>(nneg, K), xsrc);
     if ((rc = launch_status("sgd_blocked_kernel")) != FLR_OK) return rc;
   }
   return FLR_OK;

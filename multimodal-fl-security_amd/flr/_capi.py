@@ -65,6 +65,10 @@ SIGNATURES = {
                                            ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _int,
                                            _c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64,
                                            _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "flr_clip_sgd_step_blocked_src": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
+                                             ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _int,
+                                             _c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64,
+                                             _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_workspace": (_size_t, [_i64] * 10),
     "flr_resnet_gru_num_params": (_i64, [_c_void_p]),
     "flr_train_clients_workspace": (_size_t, [_c_void_p, _i64, _i64, _i64]),
@@ -82,6 +86,10 @@ SIGNATURES = {
     "flr_conv2d_fwd_t": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_data_t": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_data_t_add": (_int, [_c_void_p] * 4 + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),
+    "flr_conv2d_fwd_t_ex": (_int, [_c_void_p, _c_void_p, _i64, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t,
+                                                                                          _c_void_p]),
+    "flr_conv2d_bwd_data_t_ex": (_int, [_c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p] + [_i64] * 10 +
+                                 [_c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_bwd_weight_t": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_int, _c_void_p, _size_t,
                                                                                          _c_void_p]),
     "flr_conv2d_bwd_weight_t_sq_slots": (_i64, [_i64] * 10),
