@@ -214,7 +214,21 @@ __device__ __forceinline__ int tap_index(const Geom& g, int slot) {
 // loads that take them as soffset need no waterfall loop.
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Split-at-stash forms (sgemm_body): the thread that loads 8 consecutive k of
+// one operand row stashes them as bf16x8.  Row-contiguous operands put the 64
+// lanes of a wave on 64 consecutive rows (coalesced along the row); a
+// k-contiguous operand instead puts 4 lanes on each row (QUAD: row tid / 4,
+// k 8 (tid % 4)), so a wave's load covers 16 rows x 128 B instead of 64 rows x
+// 32 B (64 cache lines per instruction).  FLR_QUAD=0 at build time: the plain
+// mapping everywhere (A/B).
+#ifndef FLR_QUAD
+#define FLR_QUAD 1
+#endif
+template <bool QUAD> __device__ __forceinline__ int stash_row(int tid) { return QUAD ? tid >> 2 : tid & 63; }
+template <bool QUAD> __device__ __forceinline__ int stash_k(int tid) { return QUAD ? 8 * (tid & 3) : 8 * (tid >> 6); }
+
 struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
+  static constexpr bool QUAD_A = false, QUAD_B = false;
   Geom g;
   const float* x;
   const float* w;
@@ -337,6 +351,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
 // dgrad runs the four classes and does the fwd's MFMA work, not four times
 // it.  Stride 1 is the single class (0, 0) with every live tap.
 struct DgradT {
+  static constexpr bool QUAD_A = FLR_QUAD != 0, QUAD_B = false;
   Geom g;
   const float* dy;
   const float* w;
@@ -433,7 +448,8 @@ struct DgradT {
     const int row = tid & 63, k0 = 8 * (tid >> 6);
     s.ra = make_rsrc(w + (int64_t)k * wsk, (int64_t)KK * g.Cin * g.Cout);
     s.rb = make_rsrc(dy + k * g.syk, g.yext);
-    s.a0 = (unsigned)(((m0 + row) * g.Cout + k0) * 4);
+    // A = W(ci, co) is k-contiguous: quad lanes (stash_row / stash_k, QUAD_A)
+    s.a0 = (unsigned)(((m0 + stash_row<QUAD_A>(tid)) * g.Cout + stash_k<QUAD_A>(tid)) * 4);
     const int n = n0 + row;
     s.nok = n < N();
     const uint32_t bb = udiv(n, d_hcwc), p = n - bb * Hc * Wc;
@@ -952,6 +968,7 @@ __device__ __forceinline__ float apply_act(int act, float v, const float* aux, i
 
 template <int AM, int BMD>
 struct BGemm : BGemmArgs {
+  static constexpr bool QUAD_A = FLR_QUAD != 0 && AM == BM_RK, QUAD_B = FLR_QUAD != 0 && BMD == BM_RK;
   static constexpr int LA = AM == BM_RK ? RK_VEC : (AM == BM_KR ? KR_VEC : RK_GATHER);
   static constexpr int LB = BMD == BM_RK ? RK_VEC : (BMD == BM_KR ? KR_VEC : RK_GATHER);
   __host__ __device__ int M() const { return m; }
@@ -1031,7 +1048,8 @@ struct BGemm : BGemmArgs {
   __device__ static void load_op8(rsrc_t rs, int base_row, int rows, int r0, int R, int64_t s_row, int64_t s_r,
                                   float (&v)[8]) {
     const int tid = threadIdx.x;
-    const int row = base_row + (tid & 63), kk0 = r0 + 8 * (tid >> 6);
+    constexpr bool Q = FLR_QUAD != 0 && MODE == BM_RK;
+    const int row = base_row + stash_row<Q>(tid), kk0 = r0 + stash_k<Q>(tid);
     const bool rok = row < rows;
     if constexpr (MODE == BM_RK) {  // r contiguous, R % 4 == 0
 #pragma unroll
@@ -1474,7 +1492,9 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, l32 = lane & 31;
-  const int srow = tid & 63, sk = 8 * (tid >> 6);  // this thread's stash row and k offset
+  // this thread's stash row and k offset per operand (Plan::QUAD_A / QUAD_B)
+  const int srowA = stash_row<Plan::QUAD_A>(tid), skA = stash_k<Plan::QUAD_A>(tid);
+  const int srowB = stash_row<Plan::QUAD_B>(tid), skB = stash_k<Plan::QUAD_B>(tid);
 
   typename Plan::State8 sa[MS], sb[NS];
 #pragma unroll
@@ -1506,11 +1526,11 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
 #pragma unroll
     for (int i = 0; i < MS; ++i)
 #pragma unroll
-      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[i][t][srow * SB + sk]) = pa[i][t];
+      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[i][t][srowA * SB + skA]) = pa[i][t];
 #pragma unroll
     for (int j = 0; j < NS; ++j)
 #pragma unroll
-      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[MS + j][t][srow * SB + sk]) = pb[j][t];
+      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[MS + j][t][srowB * SB + skB]) = pb[j][t];
   };
   const int ntile = rend > rbeg ? (rend - rbeg + BK - 1) / BK : 0;
   if (ntile > 0) {
