@@ -1667,7 +1667,7 @@ __global__ void zero_taps_kernel(float* __restrict__ dw, int KK, int64_t slab, u
 // on how many clients share its GPU (bit-identical results at 1/2/4/8 GPUs).
 // 16 tiles per client = the 2048-workgroup target at the nominal 128 clients.
 // min_kt: fewest K-tiles a split may keep (8 for the convolutions; the batched
-// GEMMs read FLR_BGEMM_MINKT, default 8, for A/B runs of the GRU recurrence).
+// GEMMs read FLR_BGEMM_MINKT, default 32: 8 cost 1.7 ms per C3 round in split-K partials and reduce passes).
 inline int choose_splits(int M, int N, int R, int /*K*/, int sub = 1, int min_kt = 8) {
   const int tiles = cdiv(M, BM) * cdiv(N, BN) / sub;
   const int ktiles = cdiv(R, BK);
@@ -1680,7 +1680,7 @@ inline int bgemm_min_kt() {
   static const int v = [] {
     const char* e = getenv("FLR_BGEMM_MINKT");
     const int x = e ? atoi(e) : 0;
-    return x >= 1 && x <= 64 ? x : 8;
+    return x >= 1 && x <= 64 ? x : 32;
   }();
   return v;
 }
@@ -1709,12 +1709,22 @@ inline int dgrad_min_kt1() {
   return v ? v : conv_min_kt();
 }
 
+// Strided dgrad classes (FLR_DGRAD_MINKT2 overrides 8 for A/B timing).
+inline int dgrad_min_kt2() {
+  static const int v = [] {
+    const char* e = getenv("FLR_DGRAD_MINKT2");
+    const int x = e ? atoi(e) : 0;
+    return x >= 1 && x <= 256 ? x : 8;
+  }();
+  return v;
+}
+
 template <class Plan>
 inline int plan_min_kt(const Plan& pl) {
   if (std::is_base_of<BGemmArgs, Plan>::value) return bgemm_min_kt();
   // a strided dgrad's parity class has few tiles per client (l3a: one 128 x 128
   // tile): it keeps the deeper split-K, or the launch runs ~128 workgroups on 256 CUs
-  if constexpr (std::is_same<Plan, DgradT>::value) return pl.g.stride == 1 ? dgrad_min_kt1() : 8;
+  if constexpr (std::is_same<Plan, DgradT>::value) return pl.g.stride == 1 ? dgrad_min_kt1() : dgrad_min_kt2();
   return conv_min_kt();
 }
 
