@@ -47,6 +47,48 @@ def gram_traffic(K: int, P: int):
     return (2.0 * t["fetch_kib"] + t["write_kib"]) * 1024.0
 
 
+def conv_utilisation(spec, K: int, batch: int, steps: int, rounds_in_profile_key: str = "sgd_blocked_kernel"):
+    """Convolution MFMA utilisation of the headline config from the committed
+    rocprofv3 summary of the bench (profiles/r2_c3_kernel_stats_final.txt):
+    the round's useful conv FLOPs (fwd + dgrad + wgrad over the live taps;
+    the stem has no dgrad) over the conv kernels' summed time per round, against
+    the bf16x6 form's ceiling (2.5 PF/s dense bf16 / 6 products).  None when the
+    profile is absent or the spec has no convolutions."""
+    import re
+    from flr.models.multimodal import conv_geometry, live_taps, param_layout
+    path = os.path.join(ROOT, "profiles", "r2_c3_kernel_stats_final.txt")
+    geo = conv_geometry(spec)
+    if not geo or not os.path.exists(path):
+        return None
+    shapes = dict(param_layout(spec))
+    flops = 0.0
+    for name, (H, k, st, pd, Ho) in geo.items():
+        cout, cin = shapes[name][0], shapes[name][1]
+        f = 2.0 * batch * Ho * Ho * cout * cin * len(live_taps(H, k, st, pd))
+        flops += f * (2 if name == "conv1.weight" else 3)
+    flops *= K * steps
+    conv_ms = sgd_calls = 0.0
+    for line in open(path).read().splitlines()[2:]:
+        m = re.match(r"(.{90})\s+(\d+)\s+([\d.]+)", line)
+        if not m:
+            continue
+        name, calls, ms = m.group(1), int(m.group(2)), float(m.group(3))
+        if rounds_in_profile_key in name:
+            sgd_calls += calls
+        if "convt::" in name and any(t in name for t in ("FwdT", "DgradT", "WgtT")) or "stem::" in name \
+                or "zero_taps" in name:
+            conv_ms += ms
+    if not sgd_calls or not conv_ms:
+        return None
+    rounds = sgd_calls / steps
+    per_round = conv_ms / rounds
+    achieved = flops / (per_round * 1e-3) / 1e12
+    peak = 2500.0 / 6.0
+    return {"source": os.path.relpath(path, ROOT), "flops_per_round": flops, "kernel_ms_per_round": per_round,
+            "achieved_tflops": achieved, "peak_tflops": peak, "frac": achieved / peak,
+            "peak_note": "bf16x6 form: 6 v_mfma_f32_32x32x16_bf16 products per fp32 product, 2.5 PF/s dense bf16"}
+
+
 def cpu_model() -> str:
     """`lscpu` model name (from /proc/cpuinfo)."""
     try:
@@ -289,6 +331,8 @@ def main() -> None:
         "attackers_selected": attackers_selected,
         "round_roofline": round_roofline(K, P, eng.trainer.live_params, args.local_steps,
                                          elapsed / args.steps * 1e3, world),
+        "conv_mfma": conv_utilisation(spec, K, rcfg.batch, args.local_steps) if args.config == "C3" and not custom
+        else None,
         "roofline": {
             "kernel": "gram_partials_kernel (Krum pairwise, centred Gram on MFMA)",
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
