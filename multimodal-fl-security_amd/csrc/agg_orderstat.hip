@@ -210,20 +210,34 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
   }
   oem_sort<0, 128>(v);
   const float inf = __builtin_huge_valf();
+  // Rank pruning for the median: after the last merge's cross-lane stages every
+  // lane holds exactly its 128 ranks (unsorted).  When the median is the top
+  // rank of a lane (med % 128 == 127: K = 255/256 over 2 lanes, 511/512 over
+  // 4) it is that lane's maximum, so the final in-lane half-cleaner (7 stages
+  // of 64 compare-exchanges) becomes one 127-step max.  Wave-uniform (K).
+  const int medk = (K - 1) / 2;
+  const bool top = MODE == 1 && (medk & 127) == 127;
   // pairs (0,1), (2,3): quad permutation [1,0,3,2]
   merge_flip<0xB1>(v, (g & 1) ? inf : -inf);
-  half_clean_lane(v);
   if constexpr (L == 4) {
+    half_clean_lane(v);
     // (0,1) against (2,3): flip partners g^3 = quad permutation [3,2,1,0]
     merge_flip<0x1B>(v, g < 2 ? -inf : inf);
     merge_cross<0xB1>(v, (g & 1) ? inf : -inf);
-    half_clean_lane(v);
   }
+  if (!top) half_clean_lane(v);
   __builtin_amdgcn_sched_barrier(0);
   float r = 0.f;
   if constexpr (MODE == 1) {
-    const int med = (K - 1) / 2;
+    const int med = medk;
     const int loc = med - 128 * g;
+    if (top) {
+      float mx = v[0];
+#pragma unroll
+      for (int i = 1; i < 128; ++i) mx = fmaxf(mx, v[i]);
+      if (active && g == med / 128) out[p] = nnan > 0 ? __builtin_nanf("") : mx;
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 128; ++i) r = (i == loc) ? v[i] : r;
     if (active && g == med / 128) out[p] = nnan > 0 ? __builtin_nanf("") : r;  // the lane that owns rank med

@@ -172,7 +172,7 @@ def test_stat_defenses_vs_golden(cuda, path):
     np.testing.assert_array_equal(fa, fx["fedavg"])
 
 
-@pytest.mark.parametrize("K", [2, 3, 5, 8, 9, 16, 31, 64, 100, 128, 129, 200, 256, 300, 512])
+@pytest.mark.parametrize("K", [2, 3, 5, 8, 9, 16, 31, 64, 100, 128, 129, 200, 255, 256, 300, 511, 512])
 def test_order_stats_vs_torch(cuda, K):
     P = 5003
     X = torch.randn(K, P, device=cuda)
@@ -196,7 +196,7 @@ def test_order_stats_vs_torch(cuda, K):
     del ref_sorted
 
 
-@pytest.mark.parametrize("K", [5, 16, 100, 128, 200, 512])
+@pytest.mark.parametrize("K", [5, 16, 100, 128, 200, 256, 512])
 def test_order_stats_nan_like_torch(cuda, K):
     """A Byzantine client sending NaN: torch.sort orders NaN last, torch.median
     returns NaN for a column with any NaN, and the trimmed mean is NaN only

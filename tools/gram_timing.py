@@ -28,7 +28,7 @@ for K, P in shapes:
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 3
     gbs = 4.0 * K * P / (ms * 1e-3) / 1e9
-    print(json.dumps({"K": K, "P": P, "ms": round(ms, 3), "GB/s": round(gbs, 1), "frac_8TBs": round(gbs / 8000, 3),
-                      "pipe": os.environ.get("FLR_GRAM_PIPE", "1")}), flush=True)
+    print(json.dumps({"K": K, "P": P, "ms": round(ms, 3), "GB/s": round(gbs, 1), "frac_8TBs": round(gbs / 8000, 3)}),
+          flush=True)
     del X
     torch.cuda.empty_cache()
