@@ -8,16 +8,18 @@ import torch
 from flr import nn as fnn
 
 K = int(os.environ.get("K", 32))
+ONLY = os.environ.get("ONLY")
 SHAPES = [  # name, M, N, R, mode (fwd: x W^T | dx: dy W | dw: dy^T x)
     ("vit.qkv", 2080, 1152, 384, "fwd"), ("vit.fc1", 2080, 1536, 384, "fwd"), ("vit.fc2", 2080, 384, 1536, "fwd"),
     ("vit.fc1.dx", 2080, 384, 1536, "dx"), ("vit.fc1.dw", 1536, 384, 2080, "dw"), ("vit.qkv.dw", 1152, 384, 2080, "dw"),
     ("bert.fc1", 512, 1024, 256, "fwd"), ("bert.fc1.dw", 1024, 256, 512, "dw"),
     ("gru.hh", 32, 768, 256, "fwd"), ("gru.hh.dx", 32, 256, 768, "dx"), ("gru.ih", 512, 768, 128, "fwd"),
+    ("gru.ih+b", 512, 768, 128, "fwdb"), ("gru.ih+add", 512, 768, 128, "fwda"),
 ]
 
 
 def operands(M, N, R, mode):
-    if mode == "fwd":   # A = x [M, R], B = W [N, R]
+    if mode in ("fwd", "fwdb", "fwda"):   # A = x [M, R], B = W [N, R] (fwdb: + bias [K, N]; fwda: + addend)
         return torch.randn(K, M, R, device="cuda"), torch.randn(K, N, R, device="cuda")
     if mode == "dx":    # A = dy [M, R], B = W^T view [N, R] of W [R, N]
         return torch.randn(K, M, R, device="cuda"), torch.randn(K, R, N, device="cuda").transpose(1, 2)
@@ -32,19 +34,23 @@ def main():
             variants.append(dict(kv.split("=") for kv in v.split(",") if kv))
     print("K =", K, "variants:", variants, flush=True)
     for name, M, N, R, mode in SHAPES:
+        if ONLY and not name.startswith(ONLY):
+            continue
         A, B = operands(M, N, R, mode)
         out = torch.empty(K, M, N, device="cuda")
+        bias = torch.randn(K, N, device="cuda") if mode == "fwdb" else None
+        addt = torch.randn(K, M, N, device="cuda") if mode == "fwda" else None
         cells = []
         for var in variants:
             old = {k: os.environ.get(k) for k in var}
             os.environ.update(var)
-            fnn.bgemm(A, B, out=out)
+            fnn.bgemm(A, B, bias=bias, add=addt, out=out)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             reps = 10
             e0.record()
             for _ in range(reps):
-                fnn.bgemm(A, B, out=out)
+                fnn.bgemm(A, B, bias=bias, add=addt, out=out)
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / reps * 1e3
