@@ -421,6 +421,15 @@ int flr_gru_fwd_fused(const float* gi, const float* whhP, const float* bhh, floa
 int flr_gru_bwd_fused(const float* whhTP, const float* gates, const float* hseq, float* dgh, float* dgi,
                       float* dh_direct, float* dh0, int64_t K, int64_t B, int64_t T, int64_t H, int64_t t,
                       void* stream);
+/* The fused steps with shared_w = 1: every client reads the ONE packed copy at
+ * whh / whhT (flr_gru_pack with K = 1): the first local step, when all clients
+ * still hold the global W_hh.  shared_w = 0: the calls above. */
+int flr_gru_fwd_fused_ex(const float* gi, const float* whh, int shared_w, const float* bhh,
+                         float* hseq, float* gates, int64_t K, int64_t B, int64_t T, int64_t H,
+                         int64_t t, void* stream);
+int flr_gru_bwd_fused_ex(const float* whhT, int shared_w, const float* gates, const float* hseq,
+                         float* dgh, float* dgi, float* dh_direct, float* dh0, int64_t K,
+                         int64_t B, int64_t T, int64_t H, int64_t t, void* stream);
 /* Pack a per-client weight into the fused kernels' MFMA-fragment order: the
  * [NG*H][C] operand (trans = 0: w is [NG*H][C]; trans = 1, NG = 1: w is [C][H]
  * and the operand is its transpose) in 32-row blocks x 16-deep k-steps, each

@@ -451,10 +451,13 @@ class Net {
     const int64_t H3 = 3 * H_;
     FLR_TRY(gemm(emb_, N * E_, E_, 1, wih.w, H3 * E_, E_, 1, gi_, N * H3, H3, 1, bih.w, H3, nullptr, N, H3, E_, st));
     const bool fused = B_ <= 32;
+    // first step in training order: one packed copy of the global W_hh for every client
+    const bool wsh = first_ && gshared_ != nullptr;
     if (fused) {
       FLR_TRY(flr_fill(hseq_, K_ * (T_ + 1) * B_ * H_, 0.f, st));
-      FLR_TRY(flr_gru_pack(whh.w, K_, 3, H_, H_, 0, whhP_, st));
-      for (int64_t t = 0; t < T_; ++t) FLR_TRY(flr_gru_fwd_fused(gi_, whhP_, bhh.w, hseq_, gates_, K_, B_, T_, H_, t, st));
+      FLR_TRY(flr_gru_pack(wsh ? gshared_ + whh.off : whh.w, wsh ? 1 : K_, 3, H_, H_, 0, whhP_, st));
+      for (int64_t t = 0; t < T_; ++t)
+        FLR_TRY(flr_gru_fwd_fused_ex(gi_, whhP_, wsh ? 1 : 0, bhh.w, hseq_, gates_, K_, B_, T_, H_, t, st));
     } else {
       FLR_TRY(flr_fill(hseq_, K_ * (T_ + 1) * B_ * H_, 0.f, st));
       for (int64_t t = 0; t < T_; ++t) {
@@ -493,10 +496,11 @@ class Net {
     FLR_TRY(rowsum(dpre_, B_ * F_, F_, B_, F_, b1.g, st));
     // GRU (ClientGRU.backward)
     if (fused) {
-      FLR_TRY(flr_gru_pack(whh.w, K_, 1, H_, H3, 1, whhT_, st));
+      FLR_TRY(flr_gru_pack(wsh ? gshared_ + whh.off : whh.w, wsh ? 1 : K_, 1, H_, H3, 1, whhT_, st));
       FLR_TRY(flr_gru_bwd_step(dh_, gates_, hseq_, dgh_, dgi_, dh_direct_, K_, B_, T_, H_, T_ - 1, st));
       for (int64_t t = T_ - 1; t > 0; --t)
-        FLR_TRY(flr_gru_bwd_fused(whhT_, gates_, hseq_, dgh_, dgi_, dh_direct_, nullptr, K_, B_, T_, H_, t, st));
+        FLR_TRY(flr_gru_bwd_fused_ex(whhT_, wsh ? 1 : 0, gates_, hseq_, dgh_, dgi_, dh_direct_, nullptr, K_, B_, T_,
+                                     H_, t, st));
     } else {
       const float* dh = dh_;
       for (int64_t t = T_ - 1; t >= 0; --t) {

@@ -33,6 +33,7 @@ __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x))
 
 struct Dims {
   int K, B, T, H, t;
+  int wshared;  // 1: every client reads the one packed W_hh copy (the first local step)
 };
 
 __device__ __forceinline__ void decompose(const Dims& d, int64_t idx, int& k, int& b, int& j) {
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(64 * NW) void fwd_fused_kernel(const float* __restr
   const int B = d.B, H = d.H;
   const rsrc_t rh = make_rsrc(hseq + ((int64_t)k * (d.T + 1) + d.t) * B * H, (int64_t)B * H);
   const int S = (H + 15) / 16, per = (S + NW - 1) / NW;
-  const rsrc_t rw = make_rsrc(whhP + (int64_t)k * 3 * nub * S * 512, (int64_t)3 * nub * S * 512);
+  const rsrc_t rw = make_rsrc(whhP + (d.wshared ? 0 : (int64_t)k * 3 * nub * S * 512), (int64_t)3 * nub * S * 512);
   const rsrc_t rg = make_rsrc(gi + (int64_t)k * B * d.T * 3 * H, (int64_t)B * d.T * 3 * H);
   const rsrc_t rbias = make_rsrc(bhh + (int64_t)k * 3 * H, (int64_t)3 * H);
   // epilogue operands: element p = tid + 64 NW i -> (e, ln) of the MFMA tile
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(64 * NW) void bwd_fused_kernel(const float* __restr
   const int t = d.t + 1;  // this launch's GEMM step
   const rsrc_t ra = make_rsrc(dgh + ((int64_t)k * d.T + t) * B * R, (int64_t)B * R);
   const int S = (R + 15) / 16, per = (S + NW - 1) / NW;
-  const rsrc_t rb = make_rsrc(whhTP + (int64_t)k * nub * S * 512, (int64_t)nub * S * 512);
+  const rsrc_t rb = make_rsrc(whhTP + (d.wshared ? 0 : (int64_t)k * nub * S * 512), (int64_t)nub * S * 512);
   const rsrc_t rdd = make_rsrc(dh_direct + (int64_t)k * B * H, (int64_t)B * H);
   // epilogue operands: dh_direct, and step t-1's gates and h_{t-1} when d.t >= 0
   const bool elem = d.t >= 0;
@@ -490,9 +491,15 @@ inline void launch_bwd(int cfg, dim3 grid, hipStream_t st, const float* whhT, co
 
 extern "C" int flr_gru_fwd_fused(const float* gi, const float* whh, const float* bhh, float* hseq, float* gates,
                                  int64_t K, int64_t B, int64_t T, int64_t H, int64_t t, void* stream) {
+  return flr_gru_fwd_fused_ex(gi, whh, 0, bhh, hseq, gates, K, B, T, H, t, stream);
+}
+
+extern "C" int flr_gru_fwd_fused_ex(const float* gi, const float* whh, int shared_w, const float* bhh, float* hseq,
+                                    float* gates, int64_t K, int64_t B, int64_t T, int64_t H, int64_t t,
+                                    void* stream) {
   if (!gi || !whh || !bhh || !hseq || !gates || !gru::dims_ok(K, B, T, H, t) || B > 32 || K > 65535)
     return FLR_ERR_ARG;
-  const gru::Dims d{(int)K, (int)B, (int)T, (int)H, (int)t};
+  const gru::Dims d{(int)K, (int)B, (int)T, (int)H, (int)t, shared_w ? 1 : 0};
   const int nub = (int)((H + 31) / 32);
   const int cfg = gru::cfg_index("FLR_GRU_FW", 1);  // read per call: captured launches keep theirs
   if (H % 8 == 0)
@@ -505,10 +512,16 @@ extern "C" int flr_gru_fwd_fused(const float* gi, const float* whh, const float*
 extern "C" int flr_gru_bwd_fused(const float* whhT, const float* gates, const float* hseq, float* dgh, float* dgi,
                                  float* dh_direct, float* dh0, int64_t K, int64_t B, int64_t T, int64_t H, int64_t t,
                                  void* stream) {
+  return flr_gru_bwd_fused_ex(whhT, 0, gates, hseq, dgh, dgi, dh_direct, dh0, K, B, T, H, t, stream);
+}
+
+extern "C" int flr_gru_bwd_fused_ex(const float* whhT, int shared_w, const float* gates, const float* hseq,
+                                    float* dgh, float* dgi, float* dh_direct, float* dh0, int64_t K, int64_t B,
+                                    int64_t T, int64_t H, int64_t t, void* stream) {
   if (!whhT || !gates || !hseq || !dgh || !dgi || !dh_direct || !gru::dims_ok(K, B, T, H, t) || t < 1 || B > 32 ||
       K > 65535)
     return FLR_ERR_ARG;
-  const gru::Dims d{(int)K, (int)B, (int)T, (int)H, (int)(t - 1)};
+  const gru::Dims d{(int)K, (int)B, (int)T, (int)H, (int)(t - 1), shared_w ? 1 : 0};
   const int nub = (int)((H + 31) / 32);
   const int cfg = gru::cfg_index("FLR_GRU_BW", 1);
   if (H % 8 == 0)

@@ -152,6 +152,8 @@ SIGNATURES = {
     "flr_gru_fwd_fused": (_int, [_c_void_p] * 5 + [_i64] * 5 + [_c_void_p]),
     "flr_gru_bwd_fused": (_int, [_c_void_p] * 7 + [_i64] * 5 + [_c_void_p]),
     "flr_gru_pack": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _int, _c_void_p, _c_void_p]),
+    "flr_gru_fwd_fused_ex": (_int, [_c_void_p, _c_void_p, _int] + [_c_void_p] * 3 + [_i64] * 5 + [_c_void_p]),
+    "flr_gru_bwd_fused_ex": (_int, [_c_void_p, _int] + [_c_void_p] * 6 + [_i64] * 5 + [_c_void_p]),
     "flr_batchnorm_infer": (_int, [_c_void_p] * 7 + [_i64, _i64, ctypes.c_float, _int, _c_void_p]),
     "flr_classify_rows": (_int, [_c_void_p, _c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p,
                                  _c_void_p]),
