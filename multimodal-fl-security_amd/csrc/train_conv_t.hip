@@ -1090,7 +1090,8 @@ struct BGemm : BGemmArgs {
       cb[(int64_t)r * c_m] = v;
     }
   }
-  __device__ bool linear() const { return c_n == 1 && !bias && !add && !act && !mul && !pre; }
+  // the plain epilogue (row-major output, at most a bias: added there as bias + v)
+  __device__ bool linear() const { return c_n == 1 && !add && !act && !mul && !pre; }
   __device__ float* out() const { return c; }
   __device__ int64_t tile_base(int k, int m0, int n0) const { return k * c_k + m0 * c_m + n0; }
   __device__ int64_t ldm() const { return c_m; }
@@ -1440,6 +1441,13 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
         float* base = pl.out() + pl.tile_base(k, tm0, tn0);
         const int64_t ldm = pl.ldm();
         const int nl = 32 * wn + l32;
+        if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
+          if (pl.bias) {  // the batched GEMM's bias: one value per lane column, bias + v
+            const float bv = tn0 + nl < N ? pl.bias[k * pl.bias_k + tn0 + nl] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = bv + acc[i][j][e];
+          }
+        }
         if (const float* abase = plan_add(pl)) {  // all 16 addends in flight before the first store
           abase += pl.tile_base(k, tm0, tn0);
           float av[16];
@@ -1637,6 +1645,13 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
         float* base = pl.out() + pl.tile_base(k, tm0, tn0);
         const int64_t ldm = pl.ldm();
         const int nl = 32 * wn + l32;
+        if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
+          if (pl.bias) {  // the batched GEMM's bias: one value per lane column, bias + v
+            const float bv = tn0 + nl < N ? pl.bias[k * pl.bias_k + tn0 + nl] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = bv + acc[i][j][e];
+          }
+        }
         if (const float* abase = plan_add(pl)) {  // all 16 addends in flight before the first store
           abase += pl.tile_base(k, tm0, tn0);
           float av[16];
