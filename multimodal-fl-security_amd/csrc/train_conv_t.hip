@@ -1057,37 +1057,37 @@ struct BGemm : BGemmArgs {
   // first store.  Per value, store()'s load -> store chain serialised on memory
   // latency (the stores may alias the operands): the bias epilogue cost 141 us
   // of 252 on the GRU input projection.  Same operations in the same order.
-  __device__ void store_tile(int k, int m0, int n, const f32x16& acc, int M, int N) const {
-    if (n >= N) return;
-    // one 64-bit tile offset per lane; the 16 rows add uniform 32-bit offsets
-    // (r c_m, r = (e & 3) + 8 (e >> 2): scalar products of a kernel argument)
-    const int64_t o0 = k * c_k + (int64_t)m0 * c_m + (int64_t)n * c_n;
-    float* cb = c + o0;
-    const float* ab = add ? add + o0 : nullptr;
-    const float* xb = (act >= FLR_ACT_DRELU && aux) ? aux + o0 : nullptr;
-    const float* mb = mul ? mul + o0 : nullptr;
-    float* pb = pre ? pre + o0 : nullptr;
-    const float bv = bias ? bias[k * bias_k + n] : 0.f;
+  __device__ void store_tile(int k, int tm0, int tn0, int ml0, int nl, const f32x16& acc, int M, int N) const {
+    // the plain epilogue's addressing: one uniform tile base, per value the
+    // offset ml c_m + nl c_n (ml = ml0 + r, r = (e & 3) + 8 (e >> 2)), bounds as
+    // predicates (no early exit)
+    const int64_t tb = k * c_k + (int64_t)tm0 * c_m + (int64_t)tn0 * c_n;
+    const bool nok = tn0 + nl < N;
+    const float bv = (bias && nok) ? bias[k * bias_k + tn0 + nl] : 0.f;
+    const bool use_aux = act >= FLR_ACT_DRELU && aux;
     float av[16], xv[16], mv[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int r = (e & 3) + 8 * (e >> 2);
-      const bool ok = m0 + r < M;
-      av[e] = (ab && ok) ? ab[(int64_t)r * c_m] : 0.f;
-      xv[e] = (xb && ok) ? xb[(int64_t)r * c_m] : 0.f;
-      mv[e] = (mb && ok) ? mb[(int64_t)r * c_m] : 0.f;
+      const int ml = ml0 + (e & 3) + 8 * (e >> 2);
+      const bool ok = nok && tm0 + ml < M;
+      const int64_t o = tb + ml * c_m + nl * c_n;
+      av[e] = (add && ok) ? add[o] : 0.f;
+      xv[e] = (use_aux && ok) ? aux[o] : 0.f;
+      mv[e] = (mul && ok) ? mul[o] : 0.f;
     }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int r = (e & 3) + 8 * (e >> 2);
-      if (m0 + r >= M) continue;
-      float v = acc[e];
-      if (bias) v = bv + v;
-      if (ab) v = av[e] + v;
-      if (pb) pb[(int64_t)r * c_m] = v;
-      if (act) v = apply_act_v(act, v, xv[e]);
-      if (mb) v = v * mv[e];
-      cb[(int64_t)r * c_m] = v;
+      const int ml = ml0 + (e & 3) + 8 * (e >> 2);
+      if (nok && tm0 + ml < M) {
+        const int64_t o = tb + ml * c_m + nl * c_n;
+        float v = acc[e];
+        if (bias) v = bv + v;
+        if (add) v = av[e] + v;
+        if (pre) pre[o] = v;
+        if (act) v = apply_act_v(act, v, xv[e]);
+        if (mul) v = v * mv[e];
+        c[o] = v;
+      }
     }
   }
   // the plain epilogue (row-major output, at most a bias: added there as bias + v)
@@ -1485,7 +1485,7 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
       }
       if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
         if (S == 1) {
-          pl.store_tile(k, tm0 + 32 * wm + 4 * h, tn0 + 32 * wn + l32, acc[i][j], M, N);
+          pl.store_tile(k, tm0, tn0, 32 * wm + 4 * h, 32 * wn + l32, acc[i][j], M, N);
           continue;
         }
       }
@@ -1689,7 +1689,7 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
       }
       if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
         if (S == 1) {
-          pl.store_tile(k, tm0 + 32 * wm + 4 * h, tn0 + 32 * wn + l32, acc[i][j], M, N);
+          pl.store_tile(k, tm0, tn0, 32 * wm + 4 * h, 32 * wn + l32, acc[i][j], M, N);
           continue;
         }
       }
