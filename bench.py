@@ -47,16 +47,39 @@ def gram_traffic(K: int, P: int):
     return (2.0 * t["fetch_kib"] + t["write_kib"]) * 1024.0
 
 
-def conv_utilisation(spec, K: int, batch: int, steps: int, rounds_in_profile_key: str = "sgd_blocked_kernel"):
-    """Convolution MFMA utilisation of the headline config from the committed
-    rocprofv3 summary of the bench (profiles/r2_c3_kernel_stats_final.txt):
-    the round's useful conv FLOPs (fwd + dgrad + wgrad over the live taps;
-    the stem has no dgrad) over the conv kernels' summed time per round, against
-    the bf16x6 form's ceiling (2.5 PF/s dense bf16 / 6 products).  None when the
-    profile is absent or the spec has no convolutions."""
+COMMITTED_C3_STATS = "profiles/r3_c3_kernel_stats.txt"
+
+
+def _kernel_rows(path: str):
+    """(name, calls, total ms) per kernel from a rocprofv3 --stats summary: the
+    kernel_stats.csv it writes, or the fixed-width text summary committed under
+    profiles/ (name in the first 90 columns)."""
+    import csv
     import re
+    if path.endswith(".csv"):
+        with open(path) as fh:
+            for r in csv.DictReader(fh):
+                yield r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]) * 1e-6
+        return
+    for line in open(path).read().splitlines()[2:]:
+        m = re.match(r"(.{90})\s+(\d+)\s+([\d.]+)", line)
+        if m:
+            yield m.group(1), int(m.group(2)), float(m.group(3))
+
+
+def conv_utilisation(spec, K: int, batch: int, steps: int, stats_path=None,
+                     rounds_in_profile_key: str = "sgd_blocked_kernel"):
+    """Convolution MFMA utilisation of the headline config from a rocprofv3
+    summary of the C3 bench (NOT this run's kernels: the profiler wraps a
+    separate bench run; --kernel-stats names it, else the newest committed
+    summary): the round's useful conv FLOPs (fwd + dgrad + wgrad over the live
+    taps; the stem has no dgrad) over the conv kernels' summed time per round,
+    against the bf16x6 form's ceiling (2.5 PF/s dense bf16 / 6 products).
+    None when the profile is absent or the spec has no convolutions."""
     from flr.models.multimodal import conv_geometry, live_taps, param_layout
-    path = os.path.join(ROOT, "profiles", "r2_c3_kernel_stats_final.txt")
+    path = stats_path or os.path.join(ROOT, COMMITTED_C3_STATS)
+    if not os.path.exists(path):
+        path = os.path.join(ROOT, "profiles", "r2_c3_kernel_stats_final.txt")
     geo = conv_geometry(spec)
     if not geo or not os.path.exists(path):
         return None
@@ -68,11 +91,7 @@ def conv_utilisation(spec, K: int, batch: int, steps: int, rounds_in_profile_key
         flops += f * (2 if name == "conv1.weight" else 3)
     flops *= K * steps
     conv_ms = sgd_calls = 0.0
-    for line in open(path).read().splitlines()[2:]:
-        m = re.match(r"(.{90})\s+(\d+)\s+([\d.]+)", line)
-        if not m:
-            continue
-        name, calls, ms = m.group(1), int(m.group(2)), float(m.group(3))
+    for name, calls, ms in _kernel_rows(path):
         if rounds_in_profile_key in name:
             sgd_calls += calls
         if "convt::" in name and any(t in name for t in ("FwdT", "DgradT", "WgtT")) or "stem::" in name \
@@ -84,7 +103,8 @@ def conv_utilisation(spec, K: int, batch: int, steps: int, rounds_in_profile_key
     per_round = conv_ms / rounds
     achieved = flops / (per_round * 1e-3) / 1e12
     peak = 2500.0 / 6.0
-    return {"source": os.path.relpath(path, ROOT), "flops_per_round": flops, "kernel_ms_per_round": per_round,
+    return {"source": os.path.relpath(path, ROOT), "measured_in_this_run": False,
+            "flops_per_round": flops, "kernel_ms_per_round": per_round,
             "achieved_tflops": achieved, "peak_tflops": peak, "frac": achieved / peak,
             "peak_note": "bf16x6 form: 6 v_mfma_f32_32x32x16_bf16 products per fp32 product, 2.5 PF/s dense bf16"}
 
@@ -114,11 +134,15 @@ def round_roofline(K: int, P: int, P_live: int, steps: int, ms_per_round: float,
     live = K * (steps * 36.0 * P_live + 8.0 * P)
     sec = ms_per_round * 1e-3
     peak = HBM_PEAK_GBS * world
+    # primary: the live parameters (the dead-tap slabs are never trained, so the
+    # full-P figure would credit bytes no kernel moves)
     return {
         "bound": "hbm", "unit": "GB/s", "peak": peak,
-        "bytes_per_round": full, "achieved": full / sec / 1e9, "frac": full / sec / 1e9 / peak,
-        "bytes_per_round_live": live, "achieved_live": live / sec / 1e9, "frac_live": live / sec / 1e9 / peak,
-        "P": P, "P_live": P_live, "formula": "K*(steps*36*P + 8*P) (SURVEY 8d)",
+        "bytes_per_round": live, "achieved": live / sec / 1e9, "frac": live / sec / 1e9 / peak,
+        "bytes_per_round_full_P": full, "achieved_full_P": full / sec / 1e9, "frac_full_P": full / sec / 1e9 / peak,
+        "P": P, "P_live": P_live, "formula": "K*(steps*36*P_live + 8*P) (SURVEY 8d, live parameters)",
+        "note": "SURVEY 8d's HBM model omits the convolution / GEMM FLOPs; the conv_mfma / gemm_mfma fields "
+                "give the compute side",
     }
 
 
@@ -171,12 +195,43 @@ def cpu_baseline(spec, P, K, f, multi_k, steps, batch, budget_s: float = 20.0):
     return {
         "value": 1.0 / round_s, "unit": "rounds/s", "cores": threads, "kind": "port",
         "cpu_model": cpu_model(), "host_cpus": host_cpus,
-        "sample": (f"oracle (reference loop restated, torch CPU fp32, {threads} threads): {n_clients} client "
+        "sample": (f"oracle (reference loop restated, torch CPU fp32, {threads} threads = this job's CPU share "
+                   f"(OMP_NUM_THREADS) of the host's {host_cpus} CPUs): {n_clients} client "
                    f"local update(s) x {steps} steps timed ({t_client:.3f} s/client), {n_pairs} Krum pair "
                    f"norms at P={P} ({t_pair * 1e3:.1f} ms/pair), 4-row mean ({t_mean / multi_k * 1e3:.1f} "
                    f"ms/row); round = {K}*client + {K * (K - 1) // 2}*pair + {multi_k}*row = {round_s:.1f} s"),
         "round_s": round_s, "t_client_s": t_client, "t_pair_ms": t_pair * 1e3,
     }
+
+
+def round_collectives(eng, defense: str, K: int, P: int, world: int):
+    """The per-round collectives of this configuration and the bytes each GPU
+    sends (flr.shard / flr.ops.pairwise_l2_sharded / flr.dist), fp32 unless
+    noted.  World 1: none."""
+    if world == 1:
+        return []
+    from flr import _capi
+    from flr.shard import PW_SLICES
+    kl = K // world
+    out = []
+    if eng.exchange == "alltoall":
+        ld = eng.xchg.plan.ld
+        out.append({"op": "all_to_all", "what": "client rows -> coordinate ranges",
+                    "bytes_sent_per_gpu": 4 * (world - 1) * kl * ld})
+        if defense in ("krum", "multi_krum", "krum_trimmed_mean"):
+            S = int(_capi.lib().flr_pairwise_sample_len(P))
+            glen = int(_capi.lib().flr_pairwise_gsum_len(K))
+            out += [{"op": "all_reduce", "what": "pivot sample [K, S]",
+                     "bytes_per_gpu": 4 * K * S},
+                    {"op": "all_reduce", "what": "tail term [K, K] fp64", "bytes_per_gpu": 8 * K * K},
+                    {"op": "all_gather", "what": "per-slice Gram records fp64",
+                     "bytes_sent_per_gpu": 8 * glen * PW_SLICES // world}]
+        out.append({"op": "all_gather", "what": "aggregated P-vector slices",
+                    "bytes_sent_per_gpu": 4 * eng.xchg.plan.ld})
+    else:
+        out.append({"op": "all_gather", "what": "client matrix rows (replicated aggregation)",
+                    "bytes_sent_per_gpu": 4 * kl * eng.full.data.stride(0)})
+    return out
 
 
 # BASELINE.json configs as presets: (model, clients, defense, defense_cfg, attack, attacker fraction)
@@ -211,6 +266,9 @@ def main() -> None:
     ap.add_argument("--defense", default=None, help="override the preset's defense (fedavg, krum, trimmed_mean, median)")
     ap.add_argument("--model", default=None, choices=["resnet_gru", "cub", "vit_bert"])
     ap.add_argument("--client-chunk", type=int, default=0, help="clients per forward/backward pass (0: automatic)")
+    ap.add_argument("--kernel-stats", default=None,
+                    help="rocprofv3 kernel_stats.csv (or the committed text summary) of THIS code's C3 bench, "
+                         "for conv_mfma_from_profile (default: the newest committed profiles/*c3_kernel_stats*)")
     args = ap.parse_args()
 
     import torch
@@ -331,8 +389,9 @@ def main() -> None:
         "attackers_selected": attackers_selected,
         "round_roofline": round_roofline(K, P, eng.trainer.live_params, args.local_steps,
                                          elapsed / args.steps * 1e3, world),
-        "conv_mfma": conv_utilisation(spec, K, rcfg.batch, args.local_steps) if args.config == "C3" and not custom
-        else None,
+        "conv_mfma_from_profile": conv_utilisation(spec, K, rcfg.batch, args.local_steps, args.kernel_stats)
+        if args.config == "C3" and not custom else None,
+        "collectives": round_collectives(eng, defense, K, P, world),
         "roofline": {
             "kernel": "gram_partials_kernel (Krum pairwise, centred Gram on MFMA)",
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -43,6 +43,10 @@ const char* flr_last_error(void);
  *   D[i][j] = float32(||X_i - X_j||_2) stored as float64, D[i][i] = 0.
  * Engine: centred Gram matrix on MFMA (bf16 hi/lo split, fp32 accumulate),
  * fixed-order fp64 reduction of per-segment partials.  Any K >= 1.
+ * Pairs the centring cannot condition (two rows close to each other but far
+ * from the medoid pivot, e.g. a cluster of sign-flipped updates) are flagged
+ * from the pivot sample and recomputed from exact fp32 differences (at most 64
+ * such rows per call).
  */
 size_t flr_pairwise_l2_workspace(int64_t K, int64_t P);
 int flr_pairwise_l2(const float* X, int64_t K, int64_t P, int64_t ldx,
@@ -63,7 +67,8 @@ int flr_pairwise_l2_ex(const float* X, int64_t K, int64_t P, int64_t ldx,
  * D bit-identical to flr_pairwise_l2 on the whole matrix:
  *   1. flr_pairwise_sample on every holder, then an exact SUM of the [K][S]
  *      samples (the positions a holder does not own are written as 0);
- *   2. flr_pairwise_pivot on the combined sample (replicated);
+ *   2. flr_pairwise_pivot on the combined sample (replicated) -> the pivot
+ *      record, flr_pairwise_pivot_len() int32 (pivot, refined-row count, rows);
  *   3. flr_pairwise_gram_slices for the holder's slices [q0, q1): X's column
  *      0 is the first coordinate of slice q0 (chunk flr_pw_slice_chunks(q0));
  *      gsum [q1-q0][flr_pairwise_gsum_len(K)] fp64;
@@ -76,6 +81,7 @@ int flr_pairwise_l2_ex(const float* X, int64_t K, int64_t P, int64_t ldx,
 int flr_pw_slice_chunks(int64_t P, int64_t q, int64_t* chunk_begin, int64_t* chunk_end);
 int64_t flr_pairwise_sample_len(int64_t P);
 size_t flr_pairwise_gsum_len(int64_t K);
+int64_t flr_pairwise_pivot_len(void);
 size_t flr_pairwise_sliced_workspace(int64_t K, int64_t P, int64_t nslices);
 int flr_pairwise_sample(const float* X, int64_t K, int64_t ldx, int64_t P, int64_t chunk0,
                         int64_t chunk1, float* Xs, void* stream);
@@ -113,6 +119,9 @@ int flr_krum_select(const double* D, int64_t K, int64_t f, double* scores,
  *   out = (((0 + X[rows[0]]) + X[rows[1]]) + ...) / divisor   (fp32, in order)
  * rows: device int32 [m] (e.g. the first m entries of `order`); divisor is
  * the reference's multi_k (== m unless multi_k > K).
+ * Precondition: every rows[i] in [0, K).  The indices are device-resident, so
+ * this is not checked on the host; an out-of-range index is clamped into range
+ * on the device (no out-of-bounds read) and the result is then unspecified.
  */
 int flr_rows_mean(const float* X, int64_t K, int64_t P, int64_t ldx,
                   const int32_t* rows, int64_t m, int64_t divisor, float* out,
@@ -146,7 +155,9 @@ int flr_median_lower(const float* X, int64_t K, int64_t P, int64_t ldx,
 
 /* The same two order statistics over the row subset rows[0..m) of X (device
  * int32 indices, m <= K <= 512): the coordinate-wise trimmed mean of the
- * Multi-Krum selection ("Krum + trimmed-mean", BASELINE.json configs[4]). */
+ * Multi-Krum selection ("Krum + trimmed-mean", BASELINE.json configs[4]).
+ * Precondition as flr_rows_mean: rows[i] in [0, K) (out-of-range indices are
+ * clamped on the device, never read out of bounds; the result is unspecified). */
 int flr_trimmed_mean_rows(const float* X, int64_t K, int64_t P, int64_t ldx, const int32_t* rows, int64_t m,
                           int64_t t, float* out, void* stream);
 int flr_median_lower_rows(const float* X, int64_t K, int64_t P, int64_t ldx, const int32_t* rows, int64_t m,

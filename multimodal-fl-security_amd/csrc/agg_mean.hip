@@ -22,9 +22,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <bool VEC>
 __global__ __launch_bounds__(THREADS) void rows_mean_kernel(const float* __restrict__ X, int64_t P,
                                                             int64_t ldx, const int32_t* __restrict__ rows,
-                                                            int m, float fm, float* __restrict__ out) {
+                                                            int m, float fm, float* __restrict__ out,
+                                                            uint32_t rmax) {
   __shared__ int32_t rs[MAXROWS];
-  for (int t = threadIdx.x; t < m; t += THREADS) rs[t] = rows[t];
+  // an index outside [0, K) is clamped into range: no out-of-bounds read (flr.h)
+  for (int t = threadIdx.x; t < m; t += THREADS) rs[t] = (int32_t)min((uint32_t)rows[t], rmax);
   __syncthreads();
   if constexpr (VEC) {
     const int64_t nv = P / 4;
@@ -123,10 +125,10 @@ extern "C" int flr_rows_mean(const float* X, int64_t K, int64_t P, int64_t ldx, 
   hipStream_t st = as_stream(stream);
   if (mean::vec_ok(X, ldx, P, out)) {
     hipLaunchKernelGGL(mean::rows_mean_kernel<true>, dim3(mean::grid_for(P / 4)), dim3(mean::THREADS), 0, st,
-                       X, P, ldx, rows, (int)m, fdiv, out);
+                       X, P, ldx, rows, (int)m, fdiv, out, (uint32_t)(K - 1));
   } else {
     hipLaunchKernelGGL(mean::rows_mean_kernel<false>, dim3(mean::grid_for(P)), dim3(mean::THREADS), 0, st, X,
-                       P, ldx, rows, (int)m, fdiv, out);
+                       P, ldx, rows, (int)m, fdiv, out, (uint32_t)(K - 1));
   }
   return launch_status("rows_mean_kernel");
 }

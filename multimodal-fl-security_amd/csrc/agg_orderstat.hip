@@ -85,13 +85,13 @@ template <int NP, int MODE>
 // trimmed sum from pushing the kernel over the 168-VGPR occupancy step.
 __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __restrict__ X, int K, int64_t P,
                                                             int64_t ldx, int t, float* __restrict__ out,
-                                                            const int32_t* __restrict__ rows) {
+                                                            const int32_t* __restrict__ rows, uint32_t rmax) {
   const int64_t p = (int64_t)blockIdx.x * THREADS + threadIdx.x;
   if (p >= P) return;
   float v[NP];
   if (rows) {  // a row subset (e.g. the Multi-Krum selection); the index loads are wave-uniform
 #pragma unroll
-    for (int k = 0; k < NP; ++k) v[k] = k < K ? X[(int64_t)rows[k] * ldx + p] : __builtin_huge_valf();
+    for (int k = 0; k < NP; ++k) v[k] = k < K ? X[(int64_t)min((uint32_t)rows[k], rmax) * ldx + p] : __builtin_huge_valf();
   } else {
 #pragma unroll
     for (int k = 0; k < NP; ++k) v[k] = k < K ? X[(int64_t)k * ldx + p] : __builtin_huge_valf();
@@ -182,7 +182,8 @@ template <int L, int MODE>
 __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const float* __restrict__ X, int K,
                                                                          int64_t P, int64_t ldx, int t,
                                                                          float* __restrict__ out,
-                                                                         const int32_t* __restrict__ rows) {
+                                                                         const int32_t* __restrict__ rows,
+                                                                         uint32_t rmax) {
   const int64_t gidx = (int64_t)blockIdx.x * THREADS + threadIdx.x;
   const int64_t p = gidx / L;
   const int g = (int)(gidx % L);
@@ -192,7 +193,8 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
   if (rows) {  // a row subset (e.g. the Multi-Krum selection)
     const int32_t* rg = rows + 128 * g;
 #pragma unroll
-    for (int i = 0; i < 128; ++i) v[i] = 128 * g + i < K ? X[(int64_t)rg[i] * ldx + pc] : __builtin_huge_valf();
+    for (int i = 0; i < 128; ++i)
+      v[i] = 128 * g + i < K ? X[(int64_t)min((uint32_t)rg[i], rmax) * ldx + pc] : __builtin_huge_valf();
   } else {
     const float* __restrict__ base = X + (int64_t)(128 * g) * ldx + pc;
     if (K >= 128 * L) {  // wave-uniform: every register holds a client (K = 256, 512)
@@ -265,24 +267,27 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
 
 template <int MODE>
 int launch(const float* X, int K, int64_t P, int64_t ldx, int t, float* out, hipStream_t st,
-           const int32_t* rows = nullptr) {
+           const int32_t* rows = nullptr, int64_t nrows = 0) {
+  // a row index outside [0, nrows) is clamped into range: no out-of-bounds read
+  // (the result is then unspecified; flr.h states the precondition)
+  const uint32_t rmax = (uint32_t)(nrows > 0 ? nrows - 1 : 0);
   const dim3 grid((unsigned)((P + THREADS - 1) / THREADS));
   if (K <= 8)
-    hipLaunchKernelGGL((orderstat_kernel<8, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
+    hipLaunchKernelGGL((orderstat_kernel<8, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows, rmax);
   else if (K <= 16)
-    hipLaunchKernelGGL((orderstat_kernel<16, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
+    hipLaunchKernelGGL((orderstat_kernel<16, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows, rmax);
   else if (K <= 32)
-    hipLaunchKernelGGL((orderstat_kernel<32, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
+    hipLaunchKernelGGL((orderstat_kernel<32, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows, rmax);
   else if (K <= 64)
-    hipLaunchKernelGGL((orderstat_kernel<64, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
+    hipLaunchKernelGGL((orderstat_kernel<64, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows, rmax);
   else if (K <= 128)
-    hipLaunchKernelGGL((orderstat_kernel<128, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
+    hipLaunchKernelGGL((orderstat_kernel<128, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows, rmax);
   else if (K <= 256)
     hipLaunchKernelGGL((orderstat_multilane_kernel<2, MODE>), dim3((unsigned)((2 * P + THREADS - 1) / THREADS)),
-                       dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
+                       dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows, rmax);
   else if (K <= 512)
     hipLaunchKernelGGL((orderstat_multilane_kernel<4, MODE>), dim3((unsigned)((4 * P + THREADS - 1) / THREADS)),
-                       dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows);
+                       dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows, rmax);
   else
     return FLR_ERR_UNSUPPORTED;
   return launch_status("orderstat_kernel");
@@ -311,12 +316,12 @@ extern "C" int flr_trimmed_mean_rows(const float* X, int64_t K, int64_t P, int64
   if (K < 1 || m < 1 || m > K || P < 0 || ldx < P || t < 0 || m - 2 * t < 1 || !X || !out || !rows)
     return FLR_ERR_ARG;
   if (P == 0) return FLR_OK;
-  return ostat::launch<0>(X, (int)m, P, ldx, (int)t, out, as_stream(stream), rows);
+  return ostat::launch<0>(X, (int)m, P, ldx, (int)t, out, as_stream(stream), rows, K);
 }
 
 extern "C" int flr_median_lower_rows(const float* X, int64_t K, int64_t P, int64_t ldx, const int32_t* rows,
                                      int64_t m, float* out, void* stream) {
   if (K < 1 || m < 1 || m > K || P < 0 || ldx < P || !X || !out || !rows) return FLR_ERR_ARG;
   if (P == 0) return FLR_OK;
-  return ostat::launch<1>(X, (int)m, P, ldx, 0, out, as_stream(stream), rows);
+  return ostat::launch<1>(X, (int)m, P, ldx, 0, out, as_stream(stream), rows, K);
 }

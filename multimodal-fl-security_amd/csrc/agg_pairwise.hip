@@ -47,6 +47,24 @@ constexpr int MAX_SEG = 512;
 // record write + reduction); 1/G of them per GPU when sharded.
 constexpr int TARGET_BLOCKS = 512;
 
+// Far clusters.  The centred Gram's error on a pair is about 1e-7 of
+// |y_i|^2 + |y_j|^2 (y = x - x_pivot), so a pair whose distance is tiny next to
+// its distance from the pivot — two members of a cluster far from the medoid,
+// e.g. the sign-flipped attackers of a trained round (|x| ~ 1e3 |x_i - x_j|)
+// — cancels catastrophically.  The pivot prepass estimates each pair's
+// cancellation factor (|y_i|^2 + |y_j|^2) / |y_i - y_j|^2 from the exact sample
+// distances; rows in any pair above COND_FLAG (at most RMAX of them, lowest
+// index first) get their mutual distances from exact fp32 differences over the
+// whole vector instead ("refine" records, kept per canonical slice next to the
+// Gram records so the sharded composition stays bit-identical).
+constexpr int RMAX = 64;                    // refined rows per call
+constexpr int RHDR = 1 + RMAX;              // refine header: count, row list (as doubles)
+constexpr int RBLK = RHDR + RMAX * RMAX;    // fp64 per slice: header + [RMAX][RMAX] sums
+constexpr int PREC = 2 + RMAX;              // pivot record (int32): pivot, count, rows
+constexpr double COND_FLAG = 16.0;
+constexpr int RSEG_MAX = 64;                // refine segments per slice
+constexpr int MAXK_PIVOT = 1024;
+
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < N) {
@@ -389,13 +407,124 @@ __global__ __launch_bounds__(256) void reduce_records_kernel(const float* __rest
         ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
 }
 
-__global__ void reduce_splits_kernel(const double* __restrict__ stage1, int ngroups, double* __restrict__ gsum) {
+// nrec = slices x groups records (slice-major); gsum rows are glen doubles per
+// slice (the groups' records, then the slice's refine block).
+__global__ void reduce_splits_kernel(const double* __restrict__ stage1, int nrec, int ngroups, int64_t glen,
+                                     double* __restrict__ gsum) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)ngroups * REC) return;
+  if (idx >= (int64_t)nrec * REC) return;
   const int g = (int)(idx / REC), e = (int)(idx % REC);
   double s = 0.0;
   for (int z = 0; z < RSPLIT; ++z) s += stage1[((int64_t)g * RSPLIT + z) * REC + e];
-  gsum[idx] = s;
+  gsum[(int64_t)(g / ngroups) * glen + (int64_t)(g % ngroups) * REC + e] = s;
+}
+
+// ---- refine: exact differences for the flagged rows (see COND_FLAG) ----
+// grid (nseg, 3 block pairs (0,0) (0,1) (1,1) of the row list, slices).  Each
+// workgroup sums (x_i - x_j)^2 over its segment of the slice's chunks: fp32
+// within a 64-coordinate chunk, fp64 across chunks.
+__global__ __launch_bounds__(256) void refine_partials_kernel(const float* __restrict__ X, int64_t ldx,
+                                                              int64_t nch_total, int q_base, int64_t chunk0,
+                                                              const int* __restrict__ prec, int nseg,
+                                                              double* __restrict__ rpart) {
+  __shared__ float A[32][CW + 1];
+  __shared__ float B[32][CW + 1];
+  const int c = prec[1];
+  const int pr = blockIdx.y;
+  const int a = pr == 2 ? 1 : 0, b = pr == 0 ? 0 : 1;
+  if (32 * b >= c) return;  // an empty block of the row list (uniform: the whole workgroup leaves)
+  const int seg = blockIdx.x;
+  const int q = q_base + (int)blockIdx.z;
+  const int64_t s0 = slice_chunk(nch_total, q) - chunk0, s1 = slice_chunk(nch_total, q + 1) - chunk0;
+  const int64_t c_begin = s0 + (s1 - s0) * seg / nseg, c_end = s0 + (s1 - s0) * (seg + 1) / nseg;
+  const int tid = threadIdx.x;
+  const int ia = 2 * (tid >> 4), jb = 2 * (tid & 15);
+  // the 32 rows of each block this workgroup stages (positions past the count repeat row 0)
+  const int rr = tid >> 3, cc0 = 8 * (tid & 7);
+  const int pa = 32 * a + rr, pb = 32 * b + rr;
+  const float* ra = X + (int64_t)prec[2 + (pa < c ? pa : 0)] * ldx;
+  const float* rb = X + (int64_t)prec[2 + (pb < c ? pb : 0)] * ldx;
+  double d00 = 0.0, d01 = 0.0, d10 = 0.0, d11 = 0.0;
+  for (int64_t ch = c_begin; ch < c_end; ++ch) {
+    const int64_t p0 = ch * CW + cc0;
+    const f32x4 va0 = *reinterpret_cast<const f32x4*>(ra + p0), va1 = *reinterpret_cast<const f32x4*>(ra + p0 + 4);
+    const f32x4 vb0 = *reinterpret_cast<const f32x4*>(rb + p0), vb1 = *reinterpret_cast<const f32x4*>(rb + p0 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      A[rr][cc0 + e] = va0[e];
+      A[rr][cc0 + 4 + e] = va1[e];
+      B[rr][cc0 + e] = vb0[e];
+      B[rr][cc0 + 4 + e] = vb1[e];
+    }
+    __syncthreads();
+    float s00 = 0.f, s01 = 0.f, s10 = 0.f, s11 = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < CW; ++k) {
+      const float a0 = A[ia][k], a1 = A[ia + 1][k], b0 = B[jb][k], b1 = B[jb + 1][k];
+      float d;
+      d = a0 - b0; s00 = __builtin_fmaf(d, d, s00);
+      d = a0 - b1; s01 = __builtin_fmaf(d, d, s01);
+      d = a1 - b0; s10 = __builtin_fmaf(d, d, s10);
+      d = a1 - b1; s11 = __builtin_fmaf(d, d, s11);
+    }
+    d00 += (double)s00;
+    d01 += (double)s01;
+    d10 += (double)s10;
+    d11 += (double)s11;
+    __syncthreads();
+  }
+  double* rec = rpart + (((int64_t)blockIdx.z * 3 + pr) * nseg + seg) * 1024;
+  rec[ia * 32 + jb] = d00;
+  rec[ia * 32 + jb + 1] = d01;
+  rec[(ia + 1) * 32 + jb] = d10;
+  rec[(ia + 1) * 32 + jb + 1] = d11;
+}
+
+// Per slice: the segments summed in order into the slice's refine block
+// (gsum + z * glen + ngroups * REC): header (count, rows) then [RMAX][RMAX].
+__global__ __launch_bounds__(256) void refine_reduce_kernel(const double* __restrict__ rpart, int nseg,
+                                                            const int* __restrict__ prec, int ngroups,
+                                                            int64_t glen, double* __restrict__ gsum) {
+  const int z = blockIdx.y, pr = blockIdx.x;
+  double* blk = gsum + (int64_t)z * glen + (int64_t)ngroups * REC;
+  const int c = prec[1];
+  if (pr == 0)
+    for (int t = threadIdx.x; t < RHDR; t += 256) blk[t] = t == 0 ? (double)c : (double)prec[1 + t];
+  const int a = pr == 2 ? 1 : 0, b = pr == 0 ? 0 : 1;
+  if (32 * b >= c) return;
+  for (int e = threadIdx.x; e < 1024; e += 256) {
+    const double* p = rpart + ((int64_t)z * 3 + pr) * nseg * 1024 + e;
+    double s = 0.0;
+    for (int k = 0; k < nseg; ++k) s += p[(int64_t)k * 1024];
+    blk[RHDR + (32 * a + (e >> 5)) * RMAX + 32 * b + (e & 31)] = s;
+  }
+}
+
+// Rows to refine, from the exact sample distances Ds and the pivot (one
+// workgroup): row i is flagged when some j has
+//   Ds[i][j]^2 * COND_FLAG < Ds[i][p]^2 + Ds[j][p]^2.
+// The first RMAX flagged rows in index order go to prec[2..], their count to prec[1].
+__global__ __launch_bounds__(256) void flag_rows_kernel(const double* __restrict__ Ds, int K, int* __restrict__ prec) {
+  __shared__ unsigned char flag[MAXK_PIVOT];
+  const int p = prec[0];
+  for (int i = threadIdx.x; i < K; i += 256) {
+    const double dip = Ds[(int64_t)i * K + p];
+    int f = 0;
+    for (int j = 0; j < K && !f; ++j) {
+      if (j == i) continue;
+      const double dij = Ds[(int64_t)i * K + j], djp = Ds[(int64_t)j * K + p];
+      f = dij * dij * COND_FLAG < dip * dip + djp * djp;
+    }
+    flag[i] = (unsigned char)f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int c = 0;
+    for (int i = 0; i < K && c < RMAX; ++i)
+      if (flag[i]) prec[2 + c++] = i;
+    prec[1] = c;
+    for (int t = c; t < RMAX; ++t) prec[2 + t] = 0;
+  }
 }
 
 // Exact-difference contribution of the coordinates that do not fill a chunk.
@@ -424,8 +553,8 @@ __device__ __forceinline__ int tile_entry(int row, int col) {
 }
 
 // D from the per-slice group sums, adding the slices in slice order.
-__global__ void assemble_kernel(const double* __restrict__ gsum, int ngroups, const double* __restrict__ tail,
-                                int K, double* __restrict__ D) {
+__global__ void assemble_kernel(const double* __restrict__ gsum, int ngroups, int64_t glen,
+                                const double* __restrict__ tail, int K, double* __restrict__ D) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)K * K) return;
   int i = (int)(idx / K), j = (int)(idx % K);
@@ -463,14 +592,31 @@ __global__ void assemble_kernel(const double* __restrict__ gsum, int ngroups, co
       t = lb_i * CROSS_NJ + bj % CROSS_NJ;
     }
   }
-  double gij = 0.0, gii = 0.0, gjj = 0.0;
-  for (int q = 0; q < FLR_PW_SLICES; ++q) {
-    const double* rec = gsum + ((int64_t)q * ngroups + g) * REC;
-    gij += rec[t * 1024 + tile_entry(ri, rj)];
-    gii += rec[REC_TILES * 1024 + 32 * lb_i + ri];
-    gjj += rec[REC_TILES * 1024 + 32 * lb_j + rj];
+  // a refined pair (both rows in the refine list): the exact-difference sums
+  const double* hdr = gsum + (int64_t)ngroups * REC;  // slice 0's header (every slice holds the same)
+  const int c = (int)hdr[0];
+  int pi = -1, pj = -1;
+  for (int u = 0; u < c; ++u) {
+    const int row = (int)hdr[1 + u];
+    pi = row == i ? u : pi;
+    pj = row == j ? u : pj;
   }
-  double d2 = gii + gjj - 2.0 * gij + tail[idx];
+  double d2;
+  if (pi >= 0 && pj >= 0) {
+    const int lo = pi < pj ? pi : pj, hi = pi < pj ? pj : pi;
+    d2 = 0.0;
+    for (int q = 0; q < FLR_PW_SLICES; ++q) d2 += gsum[(int64_t)q * glen + (int64_t)ngroups * REC + RHDR + lo * RMAX + hi];
+    d2 += tail[idx];
+  } else {
+    double gij = 0.0, gii = 0.0, gjj = 0.0;
+    for (int q = 0; q < FLR_PW_SLICES; ++q) {
+      const double* rec = gsum + (int64_t)q * glen + (int64_t)g * REC;
+      gij += rec[t * 1024 + tile_entry(ri, rj)];
+      gii += rec[REC_TILES * 1024 + 32 * lb_i + ri];
+      gjj += rec[REC_TILES * 1024 + 32 * lb_j + rj];
+    }
+    d2 = gii + gjj - 2.0 * gij + tail[idx];
+  }
   if (d2 < 0.0) d2 = 0.0;
   D[idx] = (double)(float)sqrt(d2);
 }
@@ -479,7 +625,6 @@ __global__ void assemble_kernel(const double* __restrict__ gsum, int ngroups, co
 // Xs[i][s] = X[i][s*stride] (row-major, ld = SAMPLE); the sample's exact
 // distances come from the direct kernel below; pivot = argmin_i sum_j Ds[i][j].
 constexpr int SAMPLE = 2048;
-constexpr int MAXK_PIVOT = 1024;
 constexpr int SAMPLE_NSEG = 8;
 
 // Xs[i][s] = X[i][s*stride - 64*chunk0] for the sample positions s*stride that
@@ -583,12 +728,20 @@ inline int direct_npairs(int64_t K) {
 
 inline int64_t sample_len(int64_t P) { return std::min<int64_t>(SAMPLE, (P / CW) * CW); }
 
-inline size_t gsum_doubles(int64_t K) { return (size_t)make_plan(K, (int64_t)CW * FLR_PW_SLICES).ngroups() * REC; }
+// fp64 per slice of gsum: the groups' Gram records, then the slice's refine block
+inline size_t gsum_doubles(int64_t K) {
+  return (size_t)make_plan(K, (int64_t)CW * FLR_PW_SLICES).ngroups() * REC + RBLK;
+}
+// refine segments per slice: depends on P only (the same records at every GPU count)
+inline int refine_nseg(int64_t P) {
+  const int64_t min_slice = (P / CW) / FLR_PW_SLICES;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(min_slice, RSEG_MAX));
+}
 
 // Workspace carve-up (every piece 256-B aligned).  `nsl` = slices computed by
 // this call (FLR_PW_SLICES for the whole-vector call).
 struct Layout {
-  size_t partials, stage1, gsum, tail, xs, spart, ds, pivot, total;
+  size_t partials, stage1, gsum, tail, xs, spart, ds, pivot, rpart, total;
 };
 inline Layout layout(int64_t K, int64_t P, int nsl = FLR_PW_SLICES) {
   const Plan p = make_plan(K, P);
@@ -597,22 +750,30 @@ inline Layout layout(int64_t K, int64_t P, int nsl = FLR_PW_SLICES) {
   auto take = [&](size_t bytes) { const size_t o = off; off += align_up(bytes, 256); return o; };
   l.partials = take((size_t)nsl * p.ngroups() * p.nseg * REC * sizeof(float));
   l.stage1 = take((size_t)nsl * p.ngroups() * RSPLIT * REC * sizeof(double));
-  l.gsum = take((size_t)FLR_PW_SLICES * p.ngroups() * REC * sizeof(double));
+  l.gsum = take((size_t)FLR_PW_SLICES * gsum_doubles(K) * sizeof(double));
   l.tail = take((size_t)K * K * sizeof(double));
   l.xs = take((size_t)K * SAMPLE * sizeof(float));
   l.spart = take((size_t)direct_npairs(K) * SAMPLE_NSEG * 1024 * sizeof(float));
   l.ds = take((size_t)K * K * sizeof(double));
-  l.pivot = take(sizeof(int));
+  l.pivot = take(PREC * sizeof(int));
+  l.rpart = take((size_t)nsl * 3 * refine_nseg(P) * 1024 * sizeof(double));
   l.total = off;
   return l;
 }
 
+// Wrong-result ablations (timing only: FLR_GRAM_ABLATE=1 skips the MFMAs, =2
+// the loads) exist only in a tools build (make ABLATION=1 -> -DFLR_ABLATION);
+// the shipped library has no switch that changes results.
 inline int gram_ablate() {
+#ifdef FLR_ABLATION
   static const int a = [] {
     const char* e = getenv("FLR_GRAM_ABLATE");
     return e ? atoi(e) : 0;
   }();
   return a;
+#else
+  return 0;
+#endif
 }
 
 // bf16 terms per value: 3 (hi+mid+lo, 6 MFMA products) removes the split's
@@ -647,6 +808,7 @@ int launch_gram(const GramArgs& a, const Plan& p, int group_base, int ngroups, h
     FLR_GRAM_LAUNCH(3, 0);
     return launch_status("gram_partials_kernel");
   }
+#ifdef FLR_ABLATION
   if constexpr (NL == 4 && !CROSS) {
     if (gram_ablate() == 1) {
       FLR_GRAM_LAUNCH(2, 1);
@@ -657,6 +819,7 @@ int launch_gram(const GramArgs& a, const Plan& p, int group_base, int ngroups, h
       return launch_status("gram_partials_kernel");
     }
   }
+#endif
   FLR_GRAM_LAUNCH(2, 0);
 #undef FLR_GRAM_LAUNCH
   return launch_status("gram_partials_kernel");
@@ -760,12 +923,15 @@ int pivot_phase(const float* Xs, int K, int S, float* spart, double* Ds, int* pi
   hipLaunchKernelGGL(direct_assemble_kernel, dim3(nblk), dim3(256), 0, st, spart, K, snseg, Ds);
   if ((rc = launch_status("direct_assemble_kernel(sample)")) != FLR_OK) return rc;
   hipLaunchKernelGGL(pivot_kernel, dim3(1), dim3(256), 0, st, Ds, K, pivot);
-  return launch_status("pivot_kernel");
+  if ((rc = launch_status("pivot_kernel")) != FLR_OK) return rc;
+  hipLaunchKernelGGL(flag_rows_kernel, dim3(1), dim3(256), 0, st, Ds, K, pivot);
+  return launch_status("flag_rows_kernel");
 }
 
 // Centred-Gram records of slices [q0, q0 + nsl), reduced per (slice, group)
 // in fixed order into gsum [nsl][ngroups][REC] (fp64).
-int gram_phase(const GramArgs& a, double* stage1, double* gsum, hipStream_t st, void* ev_begin, void* ev_end) {
+int gram_phase(const GramArgs& a, double* stage1, double* gsum, double* rpart, hipStream_t st, void* ev_begin,
+               void* ev_end) {
   const Plan p = make_plan(a.K, a.P);
   int rc;
   if (ev_begin && hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), st) != hipSuccess) return FLR_ERR_HIP;
@@ -786,8 +952,19 @@ int gram_phase(const GramArgs& a, double* stage1, double* gsum, hipStream_t st, 
   hipLaunchKernelGGL(reduce_records_kernel, dim3(cdiv(REC, 64), nrec, RSPLIT), dim3(256), 0, st, a.partials,
                      p.nseg, p.ngroups(), p.ngroups_diag, p.nseg_diag, p.nseg_cross, stage1);
   if ((rc = launch_status("reduce_records_kernel")) != FLR_OK) return rc;
-  hipLaunchKernelGGL(reduce_splits_kernel, dim3(cdiv(nrec * REC, 256)), dim3(256), 0, st, stage1, nrec, gsum);
-  return launch_status("reduce_splits_kernel");
+  const int64_t glen = (int64_t)gsum_doubles(a.K);
+  hipLaunchKernelGGL(reduce_splits_kernel, dim3(cdiv(nrec * REC, 256)), dim3(256), 0, st, stage1, nrec,
+                     p.ngroups(), glen, gsum);
+  if ((rc = launch_status("reduce_splits_kernel")) != FLR_OK) return rc;
+  // the flagged rows' exact-difference records of these slices (workgroups of an
+  // empty row-list block leave at once)
+  const int rseg = refine_nseg(a.P);
+  hipLaunchKernelGGL(refine_partials_kernel, dim3(rseg, 3, a.nsl), dim3(256), 0, st, a.X, a.ldx, p.nchunks, a.q0,
+                     a.chunk0, a.pivot, rseg, rpart);
+  if ((rc = launch_status("refine_partials_kernel")) != FLR_OK) return rc;
+  hipLaunchKernelGGL(refine_reduce_kernel, dim3(3, a.nsl), dim3(256), 0, st, rpart, rseg, a.pivot, p.ngroups(),
+                     glen, gsum);
+  return launch_status("refine_reduce_kernel");
 }
 
 bool aligned16(const void* p, int64_t ld) { return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (ld % 4 == 0); }
@@ -837,16 +1014,18 @@ extern "C" int flr_pairwise_l2_ex(const float* X, int64_t K, int64_t P, int64_t 
     if (rc != FLR_OK) return rc;
     // 2.-3. centred Gram records of every canonical slice, fixed-order fp64 sums
     const GramArgs a{X, K32, ldx, P, 0, 0, FLR_PW_SLICES, pivot, reinterpret_cast<float*>(w + L.partials)};
-    rc = gram_phase(a, reinterpret_cast<double*>(w + L.stage1), gsum, st, ev_begin, ev_end);
+    rc = gram_phase(a, reinterpret_cast<double*>(w + L.stage1), gsum, reinterpret_cast<double*>(w + L.rpart), st,
+                    ev_begin, ev_end);
     if (rc != FLR_OK) return rc;
-  } else {
-    if (hipMemsetAsync(gsum, 0, (size_t)FLR_PW_SLICES * p.ngroups() * REC * sizeof(double), st) != hipSuccess)
+  } else {  // no full chunk: the tail is everything (and the refine list empty)
+    if (hipMemsetAsync(gsum, 0, (size_t)FLR_PW_SLICES * gsum_doubles(K) * sizeof(double), st) != hipSuccess)
       return FLR_ERR_HIP;
   }
   // 4. exact contribution of the trailing partial chunk, then D (slices in order)
   hipLaunchKernelGGL(tail_d2_kernel, dim3(nblk), dim3(256), 0, st, X, K32, ldx, p_main, P, tail);
   if ((rc = launch_status("tail_d2_kernel")) != FLR_OK) return rc;
-  hipLaunchKernelGGL(assemble_kernel, dim3(nblk), dim3(256), 0, st, gsum, p.ngroups(), tail, K32, D);
+  hipLaunchKernelGGL(assemble_kernel, dim3(nblk), dim3(256), 0, st, gsum, p.ngroups(), (int64_t)gsum_doubles(K),
+                     tail, K32, D);
   return launch_status("assemble_kernel");
 }
 
@@ -862,6 +1041,8 @@ extern "C" int flr_pw_slice_chunks(int64_t P, int64_t q, int64_t* chunk_begin, i
 extern "C" int64_t flr_pairwise_sample_len(int64_t P) { return P < 0 ? 0 : sample_len(P); }
 
 extern "C" size_t flr_pairwise_gsum_len(int64_t K) { return K < 1 ? 0 : gsum_doubles(K); }
+
+extern "C" int64_t flr_pairwise_pivot_len(void) { return PREC; }
 
 extern "C" size_t flr_pairwise_sliced_workspace(int64_t K, int64_t P, int64_t nslices) {
   if (K < 1 || P < 0 || nslices < 1 || nslices > FLR_PW_SLICES) return 0;
@@ -903,7 +1084,8 @@ extern "C" int flr_pairwise_gram_slices(const float* X, int64_t K, int64_t ldx, 
     return FLR_ERR_WORKSPACE;
   char* w = static_cast<char*>(workspace);
   const GramArgs a{X, (int)K, ldx, P, c0, (int)q0, (int)(q1 - q0), pivot, reinterpret_cast<float*>(w + L.partials)};
-  return gram_phase(a, reinterpret_cast<double*>(w + L.stage1), gsum, as_stream(stream), ev_begin, ev_end);
+  return gram_phase(a, reinterpret_cast<double*>(w + L.stage1), gsum, reinterpret_cast<double*>(w + L.rpart),
+                    as_stream(stream), ev_begin, ev_end);
 }
 
 extern "C" int flr_pairwise_tail(const float* X, int64_t K, int64_t ldx, int64_t p0, int64_t p1, double* tail,
@@ -917,7 +1099,7 @@ extern "C" int flr_pairwise_tail(const float* X, int64_t K, int64_t ldx, int64_t
 extern "C" int flr_pairwise_finish(const double* gsum, const double* tail, int64_t K, double* D, void* stream) {
   if (K < 1 || K > MAXK_PIVOT || !gsum || !tail || !D) return FLR_ERR_ARG;
   hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((K * K + 255) / 256)), dim3(256), 0, as_stream(stream), gsum,
-                     make_plan(K, (int64_t)CW * FLR_PW_SLICES).ngroups(), tail, (int)K, D);
+                     make_plan(K, (int64_t)CW * FLR_PW_SLICES).ngroups(), (int64_t)gsum_doubles(K), tail, (int)K, D);
   return launch_status("assemble_kernel");
 }
 

@@ -30,6 +30,25 @@
 #include <cstdlib>
 #include <type_traits>
 
+// The file compiles as one translation unit, or (Makefile) as five parts that
+// build in parallel, -DFLR_CT_PART=0..4: 0 the im2col / stem path and the
+// workspace query, 1 the forward, 2 the data gradient, 3 the weight gradient,
+// 4 the batched GEMM and row sums.  Device templates are shared; each part
+// instantiates only the kernels its entry points launch.
+#ifdef FLR_CT_PART
+#define FLR_CT_P0 (FLR_CT_PART == 0)
+#define FLR_CT_P1 (FLR_CT_PART == 1)
+#define FLR_CT_P2 (FLR_CT_PART == 2)
+#define FLR_CT_P3 (FLR_CT_PART == 3)
+#define FLR_CT_P4 (FLR_CT_PART == 4)
+#else
+#define FLR_CT_P0 1
+#define FLR_CT_P1 1
+#define FLR_CT_P2 1
+#define FLR_CT_P3 1
+#define FLR_CT_P4 1
+#endif
+
 namespace flr {
 namespace convt {
 
@@ -191,7 +210,9 @@ inline int gemm_form() {
   const char* e = getenv("FLR_GEMM");
   if (e && e[0] == 'f') return 0;
   if (e && e[0] == 'c') return 1;
-  if (e && e[0] == 'A') return 3;  // ablation (timing only, wrong results): one bf16 term, no split
+#ifdef FLR_ABLATION
+  if (e && e[0] == 'A') return 3;  // ablation (timing only, wrong results): one bf16 term, no split; tools build only
+#endif
   if (e && e[0] == 'o') return 4;  // the unpipelined product-major loop (A/B timing)
   if (e && e[0] == 'p') return 2;  // the pipelined loop for every plan
   return 5;  // split at stash (bf16 LDS images) where the plan has k8 loads, else pipelined
@@ -1130,6 +1151,7 @@ struct BGemm : BGemmArgs {
   }
 };
 
+#if FLR_CT_P4
 // out[k][n] = sum_m X[k][m][n] (bias gradients of the batched GEMMs).  Eight
 // interleaved accumulators (rows m = 8i + j go to accumulator j), combined in a
 // fixed tree: deterministic, and eight independent load/add chains per lane
@@ -1149,8 +1171,10 @@ __global__ void sum_rows_kernel(const float* __restrict__ x, int64_t x_k, int64_
   for (int j = 0; mm < M; ++mm, ++j) a[j] += p[(int64_t)mm * x_m];
   out[k * out_k + nn] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
+#endif
 
-constexpr int IM_PB = 32, IM_MAXRP = 512;
+[[maybe_unused]] constexpr int IM_PB = 32, IM_MAXRP = 512;
+#if FLR_CT_P0
 __global__ __launch_bounds__(THREADS) void im2col_kernel(const Geom g, const float* __restrict__ x, int RP,
                                                          float* __restrict__ col) {
   extern __shared__ __attribute__((aligned(16))) float rows[];  // [IM_PB][RP]
@@ -1180,7 +1204,9 @@ __global__ __launch_bounds__(THREADS) void im2col_kernel(const Geom g, const flo
   const f32x4* in = reinterpret_cast<const f32x4*>(rows);
   for (int e = threadIdx.x; e < np * RP / 4; e += THREADS) out[e] = in[e];
 }
+#endif
 
+#if FLR_CT_P0
 // dst[k][co][RP] <- src[k][co][R] (zero pad) or the reverse (unpad) (grid: chunks x K)
 __global__ __launch_bounds__(THREADS) void repad_kernel(const float* __restrict__ src, int sld, float* __restrict__ dst,
                                                         int dld, int rows, int R) {
@@ -1191,6 +1217,7 @@ __global__ __launch_bounds__(THREADS) void repad_kernel(const float* __restrict_
     dst[(int64_t)k * total + e] = r < R ? src[((int64_t)k * rows + row) * sld + r] : 0.f;
   }
 }
+#endif
 
 // ---- the kernel ---------------------------------------------------------------
 // Workgroup tile (64*MS) x (64*NS): MS A sub-tiles and NS B sub-tiles of 64
@@ -1729,6 +1756,7 @@ __global__ void treduce_kernel(const Plan pl, int S, const float* __restrict__ p
   }
 }
 
+#if FLR_CT_P3
 // dw_t slabs [k][t] of the taps set in `dead` = 0 (grid: 64 x K).
 __global__ void zero_taps_kernel(float* __restrict__ dw, int KK, int64_t slab, uint64_t dead) {
   const int k = blockIdx.y;
@@ -1739,6 +1767,7 @@ __global__ void zero_taps_kernel(float* __restrict__ dw, int KK, int64_t slab, u
       p[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 }
+#endif
 
 // Split-K count from the PER-CLIENT problem only (never the client count K):
 // a client's reduction order — and so its trained weights — must not depend
@@ -1807,9 +1836,9 @@ inline int plan_min_kt(const Plan& pl) {
 }
 
 template <class Plan>
-size_t splits_bytes(const Plan& pl) {  // enough for any sub-tile shape
-  const int S = std::max(choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 1, plan_min_kt(pl)),
-                         choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 2, plan_min_kt(pl)));
+size_t splits_bytes(const Plan& pl) {  // enough for any sub-tile count (1, 2, 3, 4)
+  int S = 1;
+  for (int sub : {1, 2, 3, 4}) S = std::max(S, choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, sub, plan_min_kt(pl)));
   return S > 1 ? (size_t)S * pl.g.Kc * pl.M() * pl.N() * sizeof(float) : 0;
 }
 
@@ -1836,7 +1865,13 @@ template <class Plan, int MS, int NS>
 int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   const int M = pl.M(), N = pl.N(), R = pl.R(), K = pl.g.Kc;
   int S = choose_splits(M, N, R, K, MS * NS, plan_min_kt(pl));
-  if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) S = 1;
+  if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) {
+    // a clip-norm launch must write the slots sq_slots() promised: no silent fallback
+    if constexpr (has_sq<Plan>::value) {
+      if (pl.sq) return FLR_ERR_WORKSPACE;
+    }
+    S = 1;
+  }
   const dim3 grid((unsigned)cdiv(N, BN * NS), (unsigned)cdiv(M, BM * MS), (unsigned)(K * S));
   int form = gemm_form();
   if constexpr (has_k8<Plan>::value) {
@@ -1858,10 +1893,12 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 1>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());
       break;
+#ifdef FLR_ABLATION
     case 3:
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 3>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());
       break;
+#endif
     case 4:
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 4>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());
@@ -1878,14 +1915,43 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   return launch_status(name);
 }
 
+// Tile code 10 * MS + NS.  Besides the square shapes above, the tap-major
+// convolutions take 64 x 192 / 192 x 64 (13 / 31) and 64 x 256 / 256 x 64
+// (14 / 41): a 64-row operand (layer1's 64 channels) then feeds three or four
+// MFMA sub-tiles per fragment read instead of one or two (LDS: five sub-tiles
+// of bf16 images, still two workgroups per CU).
+template <class Plan>
+constexpr bool wide_tiles() {
+  return std::is_same<Plan, FwdT>::value || std::is_same<Plan, DgradT>::value ||
+         std::is_same<Plan, WgtT<true>>::value || std::is_same<Plan, WgtT<false>>::value;
+}
+
+template <class Plan>
+inline int plan_tile(const Plan& pl) {
+  const int M = pl.M(), N = pl.N(), R = pl.R();
+  const char* e = getenv("FLR_CONV_TILE");
+  const int forced = e ? atoi(e) : 0;
+  if (forced) {  // A/B timing: any shape that leaves no sub-tile empty
+    const int ms = forced / 10, ns = forced % 10;
+    const bool ok = ms >= 1 && ns >= 1 && ms * ns <= 4 && (wide_tiles<Plan>() || (ms <= 2 && ns <= 2)) &&
+                    M > 64 * (ms - 1) && N > 64 * (ns - 1);
+    if (ok) return forced;
+  }
+  int tile = tile_choice(M, N, R);
+  // dgrad with 64 input channels (layer1): 64 x 128 tiles, the A fragment feeding
+  // two B sub-tiles (measured 178 -> 147 us at l1)
+  if (std::is_same<Plan, DgradT>::value && tile == 11 && M == 64 && N % 128 == 0) tile = 12;
+  return tile;
+}
+
 // Clip-norm partial slots per client a WgtT launch writes (the tile count at
 // split-K 1, else one per 256-value treduce block), under the launch's own
 // tile and split choice — given a workspace of splits_bytes(pl).
 template <class Plan>
 int sq_slots(const Plan& pl) {
   const int M = pl.M(), N = pl.N(), R = pl.R();
-  const int tile = tile_choice(M, N, R);
-  const int ms = (tile == 21 || tile == 22) ? 2 : 1, ns = (tile == 12 || tile == 22) ? 2 : 1;
+  const int tile = plan_tile(pl);
+  const int ms = tile / 10, ns = tile % 10;
   const int S = choose_splits(M, N, R, pl.g.Kc, ms * ns, plan_min_kt(pl));
   if (S == 1) return cdiv(N, BN * ns) * cdiv(M, BM * ms);
   return (int)(((int64_t)M * N + 255) / 256);
@@ -1894,11 +1960,16 @@ int sq_slots(const Plan& pl) {
 template <class Plan>
 int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   if (pl.R() == 0 && !std::is_same<Plan, DgradT>::value) return FLR_OK;  // a dgrad class with no tap stores zeros
-  int tile = tile_choice(pl.M(), pl.N(), pl.R());
-  // dgrad with 64 input channels (layer1): 64 x 128 tiles, the A fragment feeding
-  // two B sub-tiles (measured 178 -> 147 us at l1)
-  if (std::is_same<Plan, DgradT>::value && tile == 11 && pl.M() == 64 && pl.N() % 128 == 0 && !getenv("FLR_CONV_TILE"))
-    tile = 12;
+  const int tile = plan_tile(pl);
+  if constexpr (wide_tiles<Plan>()) {
+    switch (tile) {
+      case 13: return launch_tiles<Plan, 1, 3>(pl, ws, ws_bytes, st, name);
+      case 31: return launch_tiles<Plan, 3, 1>(pl, ws, ws_bytes, st, name);
+      case 14: return launch_tiles<Plan, 1, 4>(pl, ws, ws_bytes, st, name);
+      case 41: return launch_tiles<Plan, 4, 1>(pl, ws, ws_bytes, st, name);
+      default: break;
+    }
+  }
   switch (tile) {
     case 21: return launch_tiles<Plan, 2, 1>(pl, ws, ws_bytes, st, name);
     case 12: return launch_tiles<Plan, 1, 2>(pl, ws, ws_bytes, st, name);
@@ -1912,12 +1983,15 @@ inline bool shape_ok(int64_t Cin, int64_t Cout) { return Cin % 64 == 0 && Cout %
 // ---- im2col path (declared in conv_common.h) ----------------------------------
 inline int padded_r(const Geom& g) { return (g.Cin * g.KH * g.KW + 3) / 4 * 4; }
 
+#if FLR_CT_P0
 bool im2col_eligible(const Geom& g) {
   const int64_t N = (int64_t)g.B * g.Ho * g.Wo;
   return padded_r(g) <= IM_MAXRP && !shape_ok(g.Cin, g.Cout) && (g.Ho * g.Wo) % 4 == 0 &&
          N * padded_r(g) * 4 < (int64_t(1) << 31) && (int64_t)g.Cout * padded_r(g) * 4 < (int64_t(1) << 31);
 }
+#endif
 
+#if FLR_CT_P0
 size_t im2col_workspace(const Geom& g) {
   const size_t col = align_up((size_t)g.Kc * g.B * g.Ho * g.Wo * padded_r(g) * sizeof(float), 256);
   const size_t wp = align_up((size_t)g.Kc * g.Cout * padded_r(g) * sizeof(float), 256);
@@ -1928,14 +2002,18 @@ size_t im2col_workspace(const Geom& g) {
   const size_t gemm = col + wp + std::max(std::max(splits_bytes(f), splits_bytes(w)), std::max(splits_bytes(sf), splits_bytes(sw)));
   return std::max(gemm, stem_eligible(g) ? stem_workspace(g) : 0);
 }
+#endif
 
+#if FLR_CT_P0
 static int run_im2col(const Geom& g, const float* x, float* col, hipStream_t st) {
   const int N = g.B * g.Ho * g.Wo, RP = padded_r(g);
   hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)cdiv(N, IM_PB), (unsigned)g.Kc), dim3(THREADS),
                      (size_t)IM_PB * RP * sizeof(float), st, g, x, RP, col);
   return launch_status("conv im2col");
 }
+#endif
 
+#if FLR_CT_P0
 // FLR_STEM=col: the explicit im2col column matrix; =gather: the tiled GEMM with the
 // im2col operand gathered on the fly (A/B timing); default: the direct stem
 // kernels (train_stem.hip) where eligible, else the gathered GEMM.
@@ -1943,18 +2021,24 @@ inline bool stem_col() {
   const char* e = getenv("FLR_STEM");
   return e && e[0] == 'c';
 }
+#endif
+#if FLR_CT_P0
 inline bool stem_direct(const Geom& g) {
   const char* e = getenv("FLR_STEM");
   return !(e && (e[0] == 'c' || e[0] == 'g')) && stem_eligible(g);
 }
+#endif
 
+#if FLR_CT_P0
 template <class Plan>
 inline void stem_divs(Plan& pl, const Geom& g) {
   pl.RR = g.Cin * g.KH * g.KW;
   pl.d_kk = conv::make_fastdiv((uint32_t)(g.KH * g.KW));
   pl.d_kw = conv::make_fastdiv((uint32_t)g.KW);
 }
+#endif
 
+#if FLR_CT_P0
 int fwd_im2col(const Geom& g, const float* x, const float* w, float* y, void* ws, size_t ws_bytes, hipStream_t st) {
   if (!ws || ws_bytes < im2col_workspace(g)) return FLR_ERR_WORKSPACE;
   if (stem_direct(g)) return stem_fwd(g, x, w, y, st);
@@ -1980,7 +2064,9 @@ int fwd_im2col(const Geom& g, const float* x, const float* w, float* y, void* ws
   pl.g = g; pl.RP = RP; pl.col = col; pl.wp = wp; pl.y = y;
   return launch(pl, base + colb + wpb, ws_bytes - colb - wpb, st, "conv fwd (im2col)");
 }
+#endif
 
+#if FLR_CT_P0
 int wgrad_im2col(const Geom& g, const float* x, const float* dy, float* dw, void* ws, size_t ws_bytes,
                  hipStream_t st, bool have_col) {
   if (!ws || ws_bytes < im2col_workspace(g)) return FLR_ERR_WORKSPACE;
@@ -2010,6 +2096,7 @@ int wgrad_im2col(const Geom& g, const float* x, const float* dy, float* dw, void
                      dim3(THREADS), 0, st, dwp, RP, dw, R, g.Cout, R);
   return launch_status("conv unpad dw");
 }
+#endif
 
 inline bool args_ok(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
                     int64_t stride, int64_t pad) {
@@ -2035,8 +2122,11 @@ inline bool args_ok(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int
 
 using namespace flr;
 
+#if FLR_CT_P0
 extern "C" int flr_conv2d_tap_major_ok(int64_t Cin, int64_t Cout) { return convt::shape_ok(Cin, Cout) ? 1 : 0; }
+#endif
 
+#if FLR_CT_P0
 extern "C" size_t flr_conv2d_t_workspace(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
                                          int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
   if (!convt::args_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return 0;
@@ -2051,14 +2141,18 @@ extern "C" size_t flr_conv2d_t_workspace(int64_t K, int64_t B, int64_t Cin, int6
   }
   return m;
 }
+#endif
 
+#if FLR_CT_P1
 extern "C" int flr_conv2d_fwd_t(const float* x, const float* w_t, float* y, int64_t K, int64_t B, int64_t Cin,
                                 int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                                 int64_t pad, void* ws, size_t ws_bytes, void* stream) {
   return flr_conv2d_fwd_t_ex(x, w_t, KH * KW * Cin * Cout, y, K, B, Cin, H, W, Cout, KH, KW, stride, pad, ws,
                              ws_bytes, stream);
 }
+#endif
 
+#if FLR_CT_P1
 extern "C" int flr_conv2d_fwd_t_ex(const float* x, const float* w_t, int64_t w_stride, float* y, int64_t K, int64_t B,
                                    int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
                                    int64_t stride, int64_t pad, void* ws, size_t ws_bytes, void* stream) {
@@ -2070,14 +2164,18 @@ extern "C" int flr_conv2d_fwd_t_ex(const float* x, const float* w_t, int64_t w_s
   pl.x = x; pl.w = w_t; pl.y = y; pl.wsk = w_stride;
   return convt::launch(pl, ws, ws_bytes, as_stream(stream), "conv fwd (tap-major)");
 }
+#endif
 
+#if FLR_CT_P2
 extern "C" int flr_conv2d_bwd_data_t(const float* dy, const float* w_t, float* dx, int64_t K, int64_t B, int64_t Cin,
                                      int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                                      int64_t pad, void* ws, size_t ws_bytes, void* stream) {
   return flr_conv2d_bwd_data_t_add(dy, w_t, nullptr, dx, K, B, Cin, H, W, Cout, KH, KW, stride, pad, ws, ws_bytes,
                                    stream);
 }
+#endif
 
+#if FLR_CT_P2
 extern "C" int flr_conv2d_bwd_data_t_add(const float* dy, const float* w_t, const float* add, float* dx, int64_t K,
                                          int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH,
                                          int64_t KW, int64_t stride, int64_t pad, void* ws, size_t ws_bytes,
@@ -2085,7 +2183,9 @@ extern "C" int flr_conv2d_bwd_data_t_add(const float* dy, const float* w_t, cons
   return flr_conv2d_bwd_data_t_ex(dy, w_t, KH * KW * Cin * Cout, add, dx, K, B, Cin, H, W, Cout, KH, KW, stride, pad,
                                   ws, ws_bytes, stream);
 }
+#endif
 
+#if FLR_CT_P2
 extern "C" int flr_conv2d_bwd_data_t_ex(const float* dy, const float* w_t, int64_t w_stride, const float* add,
                                         float* dx, int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W,
                                         int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* ws,
@@ -2104,7 +2204,9 @@ extern "C" int flr_conv2d_bwd_data_t_ex(const float* dy, const float* w_t, int64
   }
   return FLR_OK;
 }
+#endif
 
+#if FLR_CT_P3
 extern "C" int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* dw_t, int64_t K, int64_t B,
                                        int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
                                        int64_t stride, int64_t pad, int zero_dead_taps, void* ws, size_t ws_bytes,
@@ -2112,7 +2214,9 @@ extern "C" int flr_conv2d_bwd_weight_t(const float* x, const float* dy, float* d
   return flr_conv2d_bwd_weight_t_sq(x, dy, dw_t, K, B, Cin, H, W, Cout, KH, KW, stride, pad, zero_dead_taps, nullptr,
                                     0, ws, ws_bytes, stream);
 }
+#endif
 
+#if FLR_CT_P3
 extern "C" int64_t flr_conv2d_bwd_weight_t_sq_slots(int64_t K, int64_t B, int64_t Cin, int64_t H, int64_t W,
                                                     int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                                                     int64_t pad) {
@@ -2121,7 +2225,9 @@ extern "C" int64_t flr_conv2d_bwd_weight_t_sq_slots(int64_t K, int64_t B, int64_
   pl.g = conv::make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
   return pl.R() == 0 ? 0 : convt::sq_slots(pl);
 }
+#endif
 
+#if FLR_CT_P3
 extern "C" int flr_conv2d_bwd_weight_t_sq(const float* x, const float* dy, float* dw_t, int64_t K, int64_t B,
                                           int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
                                           int64_t stride, int64_t pad, int zero_dead_taps, double* sq,
@@ -2155,7 +2261,9 @@ extern "C" int flr_conv2d_bwd_weight_t_sq(const float* x, const float* dy, float
   pl.g = g; pl.x = x; pl.dy = dy; pl.dw = dw_t; pl.sq = sq; pl.sq_ld = (int)sq_ld;
   return convt::launch(pl, ws, ws_bytes, st, "conv bwd weight (tap-major)");
 }
+#endif
 
+#if FLR_CT_P4
 namespace {
 // operand mode from strides: RK (r contiguous) / KR (rows contiguous) / G
 int bgemm_mode(const float* p, int64_t s_k, int64_t s_row, int64_t s_r, int64_t rows, int64_t R) {
@@ -2313,3 +2421,5 @@ extern "C" int flr_sum_rows_ex(const float* X, int64_t x_k, int64_t x_m, int64_t
                      st, part, nch, (int)N, out, out_k);
   return launch_status("sum_rows_finish");
 }
+
+#endif

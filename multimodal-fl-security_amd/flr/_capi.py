@@ -38,6 +38,7 @@ SIGNATURES = {
     "flr_pw_slice_chunks": (_int, [_i64, _i64, _c_void_p, _c_void_p]),
     "flr_pairwise_sample_len": (_i64, [_i64]),
     "flr_pairwise_gsum_len": (_size_t, [_i64]),
+    "flr_pairwise_pivot_len": (_i64, []),
     "flr_pairwise_sliced_workspace": (_size_t, [_i64, _i64, _i64]),
     "flr_pairwise_sample": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p]),
     "flr_pairwise_pivot": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),

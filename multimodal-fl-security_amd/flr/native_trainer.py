@@ -104,7 +104,7 @@ class NativeRoundTrainer:
         self.norms = torch.empty(self.K, dtype=torch.float32, device=self.device)
         self._global = None   # the vector the next local_update starts from, and its order
         self._order = 0
-        self._bound = None    # (batches, masks) -> contiguous [steps][K]... inputs
+        self._bound = None    # (key, stacked copies) when the inputs are not views of one buffer
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -132,17 +132,46 @@ class NativeRoundTrainer:
         writes X in training order (FLR_TC_TRAIN_ORDER)."""
         self._global, self._order = gtrain, 1
 
+    @staticmethod
+    def _adjacent(ts: Sequence[torch.Tensor], dtype) -> Optional[torch.Tensor]:
+        """The [steps, ...] tensor the per-step tensors ts are consecutive
+        slices of (synthetic_batches / make_dropout_masks return such views),
+        as a view: no copy, so the trainer (and a captured graph) reads the
+        caller's tensors live.  None if they are not laid out that way."""
+        t0 = ts[0]
+        if t0.dtype != dtype or not t0.is_contiguous() or t0.device.type != "cuda":
+            return None
+        step = t0.numel() * t0.element_size()
+        for i, t in enumerate(ts):
+            if (t.shape != t0.shape or t.dtype != dtype or not t.is_contiguous()
+                    or t.data_ptr() != t0.data_ptr() + i * step):
+                return None
+        return t0.as_strided((len(ts),) + tuple(t0.shape), (t0.numel(),) + tuple(t0.stride()))
+
     def _inputs(self, batches: Sequence, masks: Optional[Sequence]):
-        if self._bound is not None and self._bound[0] is batches and self._bound[1] is masks:
-            return self._bound[2]
-        imgs = torch.stack([b[0] for b in batches]).float().contiguous()
-        toks = torch.stack([b[1] for b in batches]).long().contiguous()
-        labs = torch.stack([b[2] for b in batches]).long().contiguous()
-        m = None if masks is None else torch.stack(list(masks)).float().contiguous()
+        """[steps][K][B]... inputs.  Step tensors that are consecutive slices
+        of one buffer are bound as views (live data, no copy); otherwise they
+        are stacked into a copy, re-made whenever an element tensor changes
+        (data pointer or in-place version) — but a HIP graph captured on a copy
+        keeps reading that copy, so the round engine's inputs are always views."""
+        cols = [[b[i] for b in batches] for i in range(3)]
+        dts = (torch.float32, torch.int64, torch.int64)
+        views = [self._adjacent(c, dt) for c, dt in zip(cols, dts)]
+        mview = None if masks is None else self._adjacent(list(masks), torch.float32)
+        if all(v is not None for v in views) and (masks is None or mview is not None):
+            imgs, toks, labs = views
+            m = mview
+        else:
+            key = tuple((t.data_ptr(), t._version) for c in cols for t in c) + (
+                () if masks is None else tuple((t.data_ptr(), t._version) for t in masks))
+            if self._bound is None or self._bound[0] != key:
+                stacked = [torch.stack(c).to(dt).contiguous() for c, dt in zip(cols, dts)]
+                mm = None if masks is None else torch.stack(list(masks)).float().contiguous()
+                self._bound = (key, (*stacked, mm))
+            imgs, toks, labs, m = self._bound[1]
         if labs.shape[1:] != (self.K, self.B):
             raise ValueError(f"labels {tuple(labs.shape)}: expected [steps, {self.K}, {self.B}]")
-        self._bound = (batches, masks, (imgs, toks, labs, m))
-        return self._bound[2]
+        return imgs, toks, labs, m
 
     def local_update(self, batches: Sequence, dropout_masks: Optional[Sequence] = None, export: bool = True,
                      negate_rows: int = 0, gtrain: Optional[torch.Tensor] = None) -> torch.Tensor:

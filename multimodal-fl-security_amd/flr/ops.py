@@ -226,7 +226,7 @@ def pairwise_l2_sharded(cs, events=None) -> torch.Tensor:
     nsl = cs.q1 - cs.q0
     nbytes = int(lib.flr_pairwise_sliced_workspace(K, P, nsl))
     ws, wp = _ws(nbytes, dev)
-    pivot = torch.empty(1, dtype=torch.int32, device=dev)
+    pivot = torch.empty(int(lib.flr_pairwise_pivot_len()), dtype=torch.int32, device=dev)  # the pivot record
     _capi.call("flr_pairwise_pivot", Xs.data_ptr(), K, P, pivot.data_ptr(), wp, nbytes, st)
     glen = int(lib.flr_pairwise_gsum_len(K))
     mine = torch.empty(nsl * glen, dtype=torch.float64, device=dev)

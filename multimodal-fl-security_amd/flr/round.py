@@ -118,6 +118,7 @@ class RoundEngine:
         self.gtrain = self.trainer.to_train_order(self.global_flat) if self.train_order else None
         self.round_index = 0
         self.fell_back = False
+        self.fallback_error: Optional[str] = None   # exception type of the last FedAvg fallback
 
     def _num_flipped(self) -> int:
         """Local rows of sign-flip attackers (clients 0..f-1): they submit
@@ -174,6 +175,7 @@ class RoundEngine:
             self.losses = self._train_phase()
         kw = {"publish": False} if hasattr(self.defense, "publish") else {}
         self.fell_back = False
+        self.fallback_error = None
         if self.exchange == "alltoall":
             self.slice = self.xchg.exchange(self.trainer.X.data)
             try:
@@ -194,10 +196,14 @@ class RoundEngine:
     def _fallback(self, err: Exception, X: torch.Tensor) -> torch.Tensor:
         """robust_server.py:120-122: a failing defense falls back to FedAvg
         (only with RoundConfig.fallback_fedavg; otherwise the error propagates)."""
-        if not self.rcfg.fallback_fedavg:
+        from ._capi import FlrError
+        # device / library failures (kernel launch, workspace, HIP or RCCL errors)
+        # are real faults, not defense-logic errors: never hidden behind FedAvg
+        if not self.rcfg.fallback_fedavg or isinstance(err, (FlrError, torch.cuda.OutOfMemoryError)):
             raise err
         logging.getLogger(__name__).error("Defense aggregation failed: %s, falling back to FedAvg", err)
         self.fell_back = True
+        self.fallback_error = type(err).__name__
         return ops.fedavg(X, self.num_examples)
 
     # ---- checkpoint / resume (run_experiments.py:268-279) ----------------------

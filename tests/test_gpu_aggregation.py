@@ -88,6 +88,48 @@ def test_pairwise_two_term_gram_wide(cuda, monkeypatch, K):
     assert np.all(np.diag(D) == 0) and np.array_equal(D, D.T)
 
 
+def _far_cluster_matrix(K, P, f, seed, device):
+    """A trained round's geometry (SURVEY §8 a16 sign flip on full weights):
+    every client close to a large common vector g, the f attackers at -x, so
+    |x_i - x_j| ~ 1e-4 |x| inside both clusters."""
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    X = torch.zeros((K, padded_ld(P)), dtype=torch.float32, device=device)
+    g = torch.randn(P, generator=gen, device=device)
+    for i in range(K):
+        row = X[i, :P]
+        row.normal_(0.0, 1e-4 * (1.0 + 0.5 * i / K), generator=gen)
+        row.add_(g)
+        if i < f:
+            row.neg_()
+    return X
+
+
+def _fp64_dist(X):
+    Xd = X.double()
+    G = (Xd - Xd[0:1]) @ (Xd - Xd[0:1]).T
+    d = G.diagonal()
+    return (d[:, None] + d[None, :] - 2 * G).clamp_min(0).sqrt().fill_diagonal_(0)
+
+
+@pytest.mark.parametrize("K,P,f", [(40, 64 * 1000 + 7, 8), (128, 200_000, 25), (128, 70_000, 40),
+                                   (130, 64 * 900, 30), (300, 64 * 700, 60)])
+def test_pairwise_far_cluster_refined(cuda, K, P, f):
+    """Pairs inside a cluster far from the medoid pivot (cancellation factor ~1e8
+    here) come from the exact-difference refine, every pair within 2e-5 of
+    fp64 — including the 33..64-row lists (two row-list blocks) and K > 128."""
+    X = _far_cluster_matrix(K, P, f, seed=K + f, device=cuda)
+    D = ops.pairwise_l2(X[:, :P], "gram")
+    ref = _fp64_dist(X[:, :P])
+    off = ~torch.eye(K, dtype=torch.bool, device=cuda)
+    err = ((D - ref).abs()[off] / ref[off]).max().item()
+    assert err < 2e-5, err
+    # the sharded composition (the phases over any split of the slices) stays bit-identical
+    from test_gpu_shard import _phases
+    for world in (2, 8):
+        assert torch.equal(_phases(X, K, P, world), D)
+
+
 def test_pairwise_large_offset_centering(cuda):
     # a large common component (weights, not deltas) must not cost accuracy
     K, P = 48, 50000
@@ -278,7 +320,7 @@ def test_order_stats_row_subset(cuda, K, m):
         torch.testing.assert_close(ops.trimmed_mean(X, t, rows=rows).cpu(), ref, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("K,P", [(40, 4099), (128, 20_011)])
+@pytest.mark.parametrize("K,P", [(40, 4099), (128, 20_011), (512, 4099)])
 def test_krum_trimmed_mean_vs_oracle(cuda, K, P):
     """Multi-Krum selection (krum.py:149-176) then the trimmed mean of the
     selected updates (trimmed_mean.py:63-90), both halves on the oracle."""

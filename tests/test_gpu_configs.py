@@ -1,0 +1,277 @@
+"""GPU: BASELINE.json configs C3 / C4 / C5 at round level, against the oracle.
+
+* C3 — the Krum indices of a TRAINED round (K = 128, batch 32, 5 local steps,
+  P = 11,800,394, 25 sign-flip attackers) against the reference's own
+  distances: fp32 ``torch.norm(fi - fj).item()`` per pair (krum.py:73-99,
+  restated by oracle.aggregation.distance_matrix's op), its scores and
+  ``np.argsort`` (krum.py:101-131, 174).  The selection boundary margin and the
+  reference's own fp32 error against fp64 are asserted and written to a record
+  (profiles/ keeps the committed copy).
+* C4 — a K = 256 trimmed-mean round of the ViT-S/4 + BERT-mini model
+  (trimmed_mean.py:48-90, run_experiments.py:188-259): sampled clients' rows
+  against the oracle loop, the aggregate against oracle.trimmed_mean on a
+  strided sample of > 1M coordinates.
+* C5 — a K = 512 backdoor round (backdoor.py:253-290 on clients 0..101) with
+  Multi-Krum then the trimmed mean of the selection (krum.py:133-192 +
+  trimmed_mean.py:48-90): the GPU's distance matrix against fp64, the
+  selection against the oracle's scores and argsort, the aggregate against
+  the oracle's trimmed mean of the selected rows.
+"""
+import json
+import os
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import aggregation as orc
+from oracle import training as otrain
+from flr.models.multimodal import VIT_BERT, ModelSpec, model_class
+from flr.round import RoundConfig, RoundEngine
+from flr.train import TrainConfig, make_dropout_masks, synthetic_batches
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _record(name: str, payload: dict) -> None:
+    d = os.environ.get("FLR_RECORD_DIR", os.path.join(ROOT, "gpurun_out", "records"))
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, name), "w") as fh:
+        json.dump(payload, fh, indent=1)
+    print(f"\n[record {name}] " + json.dumps({k: v for k, v in payload.items() if not isinstance(v, list)}))
+
+
+def _rel(a, b):
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def fp64_distances(X: torch.Tensor, P: int, chunk: int = 1 << 20) -> torch.Tensor:
+    """K×K ℓ2 distances in fp64 on the device: the Gram matrix of the rows
+    centred on row 0, accumulated over coordinate chunks in fp64 (cancellation
+    costs at most ~1e-9 relative here)."""
+    K = X.shape[0]
+    G = torch.zeros(K, K, dtype=torch.float64, device=X.device)
+    for c0 in range(0, P, chunk):
+        c1 = min(P, c0 + chunk)
+        y = X[:, c0:c1].double() - X[0:1, c0:c1].double()
+        G += y @ y.T
+        del y
+    d = G.diagonal()
+    return (d[:, None] + d[None, :] - 2.0 * G).clamp_min(0.0).sqrt().fill_diagonal_(0.0)
+
+
+def reference_distances(rows, threads: int = 16) -> np.ndarray:
+    """krum.py:89-97 on host rows: fp64 matrix of fp32 torch.norm(fi - fj).item().
+    The pairs run on a thread pool with torch's intra-op pool at one thread; a
+    single-output fp32 norm is one sequential reduction and the
+    subtraction is elementwise, so the values are the reference's."""
+    n = len(rows)
+    out = np.zeros((n, n))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        def row(a):
+            return a, [torch.norm(rows[a] - rows[b]).item() for b in range(a + 1, n)]
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            for a, vals in ex.map(row, range(n)):
+                for j, v in enumerate(vals):
+                    out[a, a + 1 + j] = v
+                    out[a + 1 + j, a] = v
+                if a % 16 == 15:  # progress (a long host loop must not look hung)
+                    print(f"[reference norms] rows 0..{a} done, {time.perf_counter() - t0:.1f} s", flush=True)
+    finally:
+        torch.set_num_threads(prev)
+    return out
+
+
+def _order_report(scores_a, scores_b, scores64, multi_k):
+    """Compare two Krum orders (np.argsort of the two score vectors) given the
+    fp64 scores: positions that differ must be swaps within the combined score
+    error (ill-conditioned, both orders equally right)."""
+    sa, sb, s64 = (np.asarray(s, dtype=np.float64) for s in (scores_a, scores_b, scores64))
+    oa, ob = np.argsort(sa), np.argsort(sb)
+    err = float(np.max(np.abs(sa - s64)) + np.max(np.abs(sb - s64)))
+    diff = [int(r) for r in np.nonzero(oa != ob)[0]]
+    ill = all(abs(s64[oa[r]] - s64[ob[r]]) <= err for r in diff)
+    s_sorted = np.sort(s64)
+    margin = float((s_sorted[multi_k] - s_sorted[multi_k - 1]) / s_sorted[multi_k]) if multi_k < len(s64) else None
+    gaps = np.diff(s_sorted) / s_sorted[1:]
+    return {"order_a": oa, "order_b": ob, "score_err_abs": err, "positions_differing": diff,
+            "differences_within_error": ill, "boundary_margin_rel": margin,
+            "boundary_margin_abs": float(s_sorted[multi_k] - s_sorted[multi_k - 1]) if margin is not None else None,
+            "min_adjacent_gap_rel": float(gaps.min()), "median_adjacent_gap_rel": float(np.median(gaps))}
+
+
+@pytest.mark.timeout(900)
+def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
+    """C3 exactly as bench.py runs it (K = 128, B = 32, 5 local steps, full
+    P): the engine's Multi-Krum selection equals the reference's — fp32
+    torch.norm distances of the trained (sign-flipped) rows in torch order,
+    numpy scores, np.argsort (krum.py:89-97, 126-129, 174)."""
+    spec = ModelSpec()
+    K, f, B, steps, mk = 128, 25, 32, 5, 64
+    rc = RoundConfig(num_clients=K, batch=B, defense="krum", attack="sign_flip", num_attackers=f)
+    eng = RoundEngine(spec, rc, TrainConfig(local_steps=steps), cuda)
+    eng.run_round()
+    eng.defense.publish()
+    torch.cuda.synchronize()
+    P = eng.trainer.P
+    X = eng.trainer.X.data[:, :P]
+    D_gpu = eng.defense.distances.double()
+    D64 = fp64_distances(X, P)
+    t0 = time.perf_counter()
+    rows = []
+    for k in range(K):  # the reference's flattened updates: torch (parameters()) order
+        r = eng.trainer.to_torch_order(X[k]) if eng.train_order else X[k]
+        rows.append(r.cpu())
+    t_copy = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    D_ref = reference_distances(rows)
+    t_ref = time.perf_counter() - t0
+    del rows
+    D64h = D64.cpu().numpy()
+    off = ~np.eye(K, dtype=bool)
+    err_ref = float(np.max(np.abs(D_ref - D64h)[off] / D64h[off]))
+    err_gpu = float(np.max(np.abs(D_gpu.cpu().numpy() - D64h)[off] / D64h[off]))
+    m = K - f - 2
+    s_ref = orc.krum_scores(D_ref, m)
+    s_gpu = orc.krum_scores(D_gpu.cpu().numpy(), m)
+    s64 = orc.krum_scores(D64h, m)
+    rep = _order_report(s_ref, s_gpu, s64, mk)
+    order_ref = rep.pop("order_a").tolist()
+    rep.pop("order_b")
+    sel_ref, rej_ref = order_ref[:mk], order_ref[mk:]
+    # the engine's published selection is its device order (krum.py:171-176)
+    assert eng.defense.client_scores == pytest.approx(s_gpu, rel=1e-12)
+    payload = {
+        "config": "C3: K=128, f=25 sign-flip, multi_k=64, B=32, 5 local steps, P=11800394, one trained round",
+        "torch": torch.__version__, "numpy": np.__version__,
+        "distance_rel_err_reference_fp32_vs_fp64": err_ref, "distance_rel_err_gpu_vs_fp64": err_gpu,
+        "selected_identical": eng.defense.selected_clients == sel_ref,
+        "rejected_identical": eng.defense.rejected_clients == rej_ref,
+        "selected_set_identical": set(eng.defense.selected_clients) == set(sel_ref),
+        "attackers_selected": sorted(set(eng.defense.selected_clients) & set(range(f))),
+        "host_copy_s": t_copy, "reference_norms_s": t_ref, **rep,
+        "selected_reference": sel_ref, "selected_gpu": eng.defense.selected_clients,
+    }
+    conditioned = rep["boundary_margin_abs"] > rep["score_err_abs"]
+    payload["boundary_well_conditioned"] = bool(conditioned)
+    _record("c3_krum_trained_round.json", payload)
+    assert not set(eng.defense.selected_clients) & set(range(f))
+    assert rep["differences_within_error"], rep["positions_differing"]
+    if conditioned:
+        assert set(eng.defense.selected_clients) == set(sel_ref)
+    if not rep["positions_differing"]:
+        assert eng.defense.selected_clients == sel_ref and eng.defense.rejected_clients == rej_ref
+
+
+def _strided(P: int, n: int = 1_100_000) -> torch.Tensor:
+    step = max(1, P // n)
+    return torch.arange(0, P, step, dtype=torch.int64)
+
+
+def _sample_rows(eng, clients, idx: torch.Tensor) -> torch.Tensor:
+    """[len(clients), len(idx)] host copy of the client rows' torch-order
+    coordinates idx (one row converted at a time)."""
+    X = eng.trainer.X.data[:, : eng.trainer.P]
+    di = idx.to(X.device)
+    out = []
+    for k in clients:
+        r = eng.trainer.to_torch_order(X[k]) if eng.train_order else X[k]
+        out.append(r[di].cpu())
+    return torch.stack(out)
+
+
+def _check_clients(eng, spec, glob, clients, batches_dev, masks_dev, negate=()):
+    for k in clients:
+        j = k - eng.lo
+        cb = [(im[j].cpu(), tk[j].cpu(), lb[j].cpu()) for im, tk, lb in batches_dev]
+        cm = None if masks_dev is None else [m[j].cpu() for m in masks_dev]
+        upd, _ = otrain.local_update(model_class(spec), spec, glob, cb, masks=cm)
+        ref = torch.cat([u.reshape(-1) for u in upd])
+        if k in negate:
+            ref = -ref
+        row = eng.trainer.X.data[j, : eng.trainer.P]
+        row = eng.trainer.to_torch_order(row) if eng.train_order else row
+        assert _rel(row.cpu(), ref) < 1e-5, (k, _rel(row.cpu(), ref))
+
+
+@pytest.mark.timeout(600)
+def test_c4_round_trimmed_mean_vit_bert(cuda):
+    """C4: trimmed mean (trim 0.1 -> t = 25 of 256) over K = 256 clients of
+    ViT-S/4 + BERT-mini, 1 local step at batch 8."""
+    spec = VIT_BERT
+    K, B, steps = 256, 8, 1
+    rc = RoundConfig(num_clients=K, batch=B, defense="trimmed_mean", defense_cfg={"trim_ratio": 0.1},
+                     attack="none", num_attackers=0)
+    eng = RoundEngine(spec, rc, TrainConfig(local_steps=steps), cuda)
+    glob = eng.global_flat.clone().cpu()
+    new = eng.run_round().clone()
+    torch.cuda.synchronize()
+    assert eng.defense.num_trimmed_per_end == 25
+    _check_clients(eng, spec, glob, [0, 77, 200, 255], eng.batches, eng.masks)
+    P = eng.trainer.P
+    idx = _strided(P)
+    sub = _sample_rows(eng, range(K), idx)
+    want, t = orc.trimmed_mean([[sub[k]] for k in range(K)], 0.1)
+    assert t == 25
+    got = new[idx.to(cuda)].cpu()
+    err = _rel(got, want[0])
+    _record("c4_trimmed_round.json", {"config": "C4: K=256 trimmed mean (t=25), ViT-S/4 + BERT-mini, B=8, 1 step",
+                                      "P": P, "coords_checked": int(idx.numel()), "aggregate_rel_err": err})
+    assert err < 1e-5, err
+
+
+@pytest.mark.timeout(900)
+def test_c5_round_backdoor_krum_trimmed_mean(cuda):
+    """C5: K = 512, backdoor on clients 0..101 (f = int(0.2 K)), Multi-Krum
+    (multi_k = 256) then the trimmed mean (t = 25) of the selected rows."""
+    spec = VIT_BERT
+    K, B, steps = 512, 32, 1
+    f = int(0.2 * K)
+    rc = RoundConfig(num_clients=K, batch=B, defense="krum_trimmed_mean", defense_cfg={"trim_ratio": 0.1},
+                     attack="backdoor", num_attackers=f)
+    eng = RoundEngine(spec, rc, TrainConfig(local_steps=steps), cuda)
+    # the attackers' data is poisoned (backdoor.py:253-290), the benign clients' is not
+    clean = synthetic_batches(spec, steps, [0, 101, 102, 511], B, cuda)
+    for j, k in enumerate([0, 101, 102, 511]):
+        same = all(torch.equal(c[0][j], e[0][k]) and torch.equal(c[2][j], e[2][k])
+                   for c, e in zip(clean, eng.batches))
+        assert same == (k >= f), k
+    glob = eng.global_flat.clone().cpu()
+    new = eng.run_round().clone()
+    eng.defense.publish()
+    torch.cuda.synchronize()
+    _check_clients(eng, spec, glob, [0, 101, 102, 511], eng.batches, eng.masks)
+    P = eng.trainer.P
+    X = eng.trainer.X.data[:, :P]
+    D_gpu = eng.defense.distances.double()
+    D64 = fp64_distances(X, P)
+    off = ~torch.eye(K, dtype=torch.bool, device=cuda)
+    dist_err = ((D_gpu - D64).abs()[off] / D64[off]).max().item()
+    assert dist_err < 5e-5, dist_err
+    m, mk = K - f - 2, K // 2
+    s_gpu = orc.krum_scores(D_gpu.cpu().numpy(), m)
+    s64 = orc.krum_scores(D64.cpu().numpy(), m)
+    order = np.argsort(s_gpu, kind="stable")
+    assert eng.defense.selected_clients == order[:mk].tolist()
+    rep = _order_report(s_gpu, s64, s64, mk)
+    rep.pop("order_a"), rep.pop("order_b")
+    sel = eng.defense.selected_clients
+    idx = _strided(P)
+    sub = _sample_rows(eng, sel, idx)  # in selection (score) order, as the reference stacks them
+    want, t = orc.trimmed_mean([[sub[i]] for i in range(len(sel))], 0.1)
+    assert t == eng.defense.num_trimmed_per_end == 25
+    got = new[idx.to(cuda)].cpu()
+    err = _rel(got, want[0])
+    _record("c5_backdoor_round.json", {
+        "config": "C5: K=512, backdoor clients 0..101, Multi-Krum (multi_k=256) + trimmed mean (t=25), "
+                  "ViT-S/4 + BERT-mini, B=32, 1 step",
+        "P": P, "distance_rel_err_gpu_vs_fp64": dist_err, "coords_checked": int(idx.numel()),
+        "aggregate_rel_err": err, "backdoor_clients_selected": sorted(set(sel) & set(range(f))), **rep})
+    assert err < 1e-5, err

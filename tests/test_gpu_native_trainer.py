@@ -15,7 +15,10 @@ from flr.train import ClientBatchTrainer, TrainConfig, make_dropout_masks, synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("spec_name,B,nneg", [("tiny", 4, 1), ("c3", 8, 1), ("c3_b40", 40, 0)])
+# c3_b128: batch 128 gives the 128 x 128 weight-gradient tiles a deeper split-K
+# than the smaller tiles (the workspace and the fused clip-norm slots
+# must follow the tile the launch takes)
+@pytest.mark.parametrize("spec_name,B,nneg", [("tiny", 4, 1), ("c3", 8, 1), ("c3_b40", 40, 0), ("c3_b128", 128, 0)])
 def test_native_trainer_bit_identical_to_python_trainer(cuda, spec_name, B, nneg):
     spec = TINY if spec_name == "tiny" else ModelSpec()
     K, steps = 3, 2

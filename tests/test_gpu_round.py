@@ -41,12 +41,23 @@ def test_fedavg_fallback_when_defense_raises(cuda):
     kw = dict(num_clients=4, batch=4, attack="sign_flip", num_attackers=1, graph=False)
     eng = RoundEngine(TINY, RoundConfig(defense="krum", fallback_fedavg=True, **kw), TrainConfig(local_steps=1), cuda)
     out = eng.run_round().clone()
-    assert eng.fell_back
+    assert eng.fell_back and eng.fallback_error == "ValueError"
     ref = RoundEngine(TINY, RoundConfig(defense="fedavg", **kw), TrainConfig(local_steps=1), cuda).run_round()
     assert torch.equal(out, ref)
     strict = RoundEngine(TINY, RoundConfig(defense="krum", **kw), TrainConfig(local_steps=1), cuda)
     with pytest.raises(ValueError):
         strict.run_round()
+    # a device / library failure is never hidden behind the fallback
+    from flr._capi import FlrError
+    boom = RoundEngine(TINY, RoundConfig(defense="fedavg", fallback_fedavg=True, **kw), TrainConfig(local_steps=1),
+                       cuda)
+
+    def _fail(*a, **k):
+        raise FlrError("flr_fedavg", -3, "injected")
+    boom.defense.aggregate_flat = _fail
+    boom.defense.aggregate_sharded = _fail
+    with pytest.raises(FlrError):
+        boom.run_round()
 
 
 def test_fltrust_round(cuda):

@@ -44,7 +44,7 @@ def _phases(X_full, K, P, world):
     nsl = PW_SLICES // world
     nbytes = int(lib.flr_pairwise_sliced_workspace(K, P, nsl))
     ws, wp = ops._ws(nbytes, dev)
-    pivot = torch.empty(1, dtype=torch.int32, device=dev)
+    pivot = torch.empty(int(lib.flr_pairwise_pivot_len()), dtype=torch.int32, device=dev)
     _capi.call("flr_pairwise_pivot", Xs.data_ptr(), K, P, pivot.data_ptr(), wp, nbytes, st)
     glen = int(lib.flr_pairwise_gsum_len(K))
     gsum = torch.empty((PW_SLICES, glen), dtype=torch.float64, device=dev)
@@ -162,3 +162,16 @@ def test_sharded_round_two_ranks_equals_one(cuda, defense, exchange):
     two = _run(2, defense, exchange)
     assert np.array_equal(one[0][1], two[0][1]) and np.array_equal(two[0][1], two[1][1])
     assert one[0][2] == two[0][2] == two[1][2]
+
+
+@pytest.mark.parametrize("defense,exchange", [("krum", "alltoall"), ("krum", "allgather"),
+                                              ("median", "alltoall")])
+def test_sharded_round_four_ranks_equals_one(cuda, defense, exchange):
+    """World 4 (the K/G = 2 clients per rank of the C4/C5 partition at this
+    size): every rank's global model and Krum selection equal the one-rank
+    round bit for bit, for both exchanges."""
+    one = _run(1, defense, exchange)
+    four = _run(4, defense, exchange)
+    for r in range(4):
+        assert np.array_equal(one[0][1], four[r][1]), r
+        assert one[0][2] == four[r][2]
