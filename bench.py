@@ -68,7 +68,7 @@ def _kernel_rows(path: str):
 
 
 def conv_utilisation(spec, K: int, batch: int, steps: int, stats_path=None,
-                     rounds_in_profile_key: str = "sgd_blocked_kernel"):
+                     rounds_in_profile_key: str = "ce_kernel"):
     """Convolution MFMA utilisation of the headline config from a rocprofv3
     summary of the C3 bench (NOT this run's kernels: the profiler wraps a
     separate bench run; --kernel-stats names it, else the newest committed
@@ -202,6 +202,57 @@ def cpu_baseline(spec, P, K, f, multi_k, steps, batch, budget_s: float = 20.0):
                    f"ms/row); round = {K}*client + {K * (K - 1) // 2}*pair + {multi_k}*row = {round_s:.1f} s"),
         "round_s": round_s, "t_client_s": t_client, "t_pair_ms": t_pair * 1e3,
     }
+
+
+def gemm_flops_per_sample(spec) -> float:
+    """Useful batched-GEMM FLOPs of one training sample (forward + input and
+    weight gradients) of the model's nn.Linear layers, counted with forward
+    hooks on one sample; the first layer on the raw input (the ViT patch
+    embedding) has no input gradient."""
+    import torch
+    from flr.models.multimodal import model_class
+    torch.manual_seed(0)
+    m = model_class(spec)(spec)
+    macs = []
+
+    def hook(mod, inp, out):
+        macs.append(inp[0].numel() // inp[0].shape[-1] * mod.in_features * mod.out_features)
+    hs = [mod.register_forward_hook(hook) for mod in m.modules() if isinstance(mod, torch.nn.Linear)]
+    with torch.no_grad():
+        img = torch.randn(1, spec.in_channels, spec.image_size, spec.image_size)
+        tok = torch.randint(0, spec.vocab, (1, spec.seq_len))
+        m.eval()(img, tok)
+    for h in hs:
+        h.remove()
+    return 2.0 * (3 * sum(macs) - (macs[0] if macs else 0))
+
+
+def gemm_utilisation(spec, K: int, batch: int, steps: int, stats_path=None):
+    """Batched-GEMM MFMA utilisation for the encoder family (C4/C5): useful GEMM
+    FLOPs per round (gemm_flops_per_sample) over the BGemm kernels' summed time
+    per round in a rocprofv3 summary of that config's bench (--kernel-stats; the
+    optimizer kernel's call count / local steps gives the rounds profiled),
+    against the bf16x6 ceiling.  None without a summary."""
+    if not stats_path or not os.path.exists(stats_path):
+        return None
+    flops = gemm_flops_per_sample(spec) * K * steps * batch
+    ms = calls_ce = 0.0
+    for name, calls, t in _kernel_rows(stats_path):
+        if "BGemm" in name:
+            ms += t
+        if "ce_kernel" in name:
+            calls_ce += calls
+    if not calls_ce or not ms:
+        return None
+    # the cross-entropy kernel runs once per client chunk (32 clients) and local step
+    rounds = calls_ce / (steps * max(1, -(-K // 32)))
+    per_round = ms / rounds
+    achieved = flops / (per_round * 1e-3) / 1e12
+    peak = 2500.0 / 6.0
+    return {"source": os.path.relpath(stats_path, ROOT), "measured_in_this_run": False,
+            "flops_per_round": flops, "kernel_ms_per_round": per_round, "achieved_tflops": achieved,
+            "peak_tflops": peak, "frac": achieved / peak,
+            "peak_note": "bf16x6 form: 6 v_mfma_f32_32x32x16_bf16 products per fp32 product, 2.5 PF/s dense bf16"}
 
 
 def round_collectives(eng, defense: str, K: int, P: int, world: int):
@@ -391,6 +442,8 @@ def main() -> None:
                                          elapsed / args.steps * 1e3, world),
         "conv_mfma_from_profile": conv_utilisation(spec, K, rcfg.batch, args.local_steps, args.kernel_stats)
         if args.config == "C3" and not custom else None,
+        "gemm_mfma_from_profile": gemm_utilisation(spec, K, rcfg.batch, args.local_steps, args.kernel_stats)
+        if model == "vit_bert" else None,
         "collectives": round_collectives(eng, defense, K, P, world),
         "roofline": {
             "kernel": "gram_partials_kernel (Krum pairwise, centred Gram on MFMA)",

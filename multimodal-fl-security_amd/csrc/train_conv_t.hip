@@ -218,6 +218,14 @@ inline int gemm_form() {
   return 5;  // split at stash (bf16 LDS images) where the plan has k8 loads, else pipelined
 }
 
+// Register-prefetch depth of the split-at-stash kernels: 2 (one tile of global
+// loads in flight behind the tile being computed) or 3 (two).  FLR_PREFETCH=2|3,
+// read per launch (A/B timing).
+inline int prefetch_depth() {
+  const char* e = getenv("FLR_PREFETCH");
+  return (e && e[0] == '3') ? 3 : 2;
+}
+
 // ---- load plans ---------------------------------------------------------------
 // Tap of a reduction slot: W_t offset of (tap, 0, 0) = tap_index * Cin * Cout.
 // (kh, kw) of a tile-uniform reduction slot, by rectangle arithmetic (the host
@@ -668,6 +676,45 @@ struct WgtT {
 #pragma unroll
       for (int e = 0; e < 8; ++e) b[e] = ld1(s.rb, (q0 + e < R) ? s.boff + (unsigned)((q0 + e) * 4) : SENT, 0);
     }
+  }
+  // ---- transposed-image loads (wsgemm_kernel): thread t holds rows 8 (t >> 5) .. +7 of
+  // the 64-row sub-tile at reduction index k = t & 31 — the 32 lanes of a half-wave
+  // read 32 consecutive pixels of one row (128 B), and the thread's 8 values are
+  // the 8 consecutive rows of one k, one 16-B chunk of a [k][row] LDS image
+  struct StateT {
+    rsrc_t ra, rb;
+    int kh, kw;
+    unsigned arow, brow;
+  };
+  __device__ StateT initT(int k, int m0, int n0, int tid) const {
+    StateT s;
+    s.ra = make_rsrc(x + k * g.sxk, g.xext);
+    s.rb = make_rsrc(dy + k * g.syk, g.yext);
+    const int slot = uni(m0 / g.Cin), ci0 = m0 - slot * g.Cin;
+    int kh, kw;
+    slot_tap(g, slot, kh, kw);
+    s.kh = uni(kh);
+    s.kw = uni(kw);
+    const int rg = tid >> 5;
+    s.arow = (unsigned)((ci0 + 8 * rg) * g.sxc * 4);
+    s.brow = (unsigned)((n0 + 8 * rg) * g.syc * 4);
+    return s;
+  }
+  __device__ void load_at8(const StateT& s, int r0, float (&a)[8]) const {  // x(ci, pixel q of tap (kh, kw))
+    const int q = r0 + (int)(threadIdx.x & 31), HoWo = g.Ho * g.Wo;
+    const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
+    const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
+    const int ih = (int)oh * g.stride - g.pad + s.kh, iw = (int)ow * g.stride - g.pad + s.kw;
+    const bool ok = (q < R()) & (ih >= 0) & (ih < g.H) & (iw >= 0) & (iw < g.W);
+    const unsigned va = ok ? s.arow + (unsigned)(((int)(bb * g.sxb) + ih * g.W + iw) * 4) : SENT;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = ld1(s.ra, va, i * (int)g.sxc * 4);
+  }
+  __device__ void load_bt8(const StateT& s, int r0, float (&b)[8]) const {  // dy(co, q), q contiguous
+    const int q = r0 + (int)(threadIdx.x & 31);
+    const unsigned vb = q < R() ? s.brow + (unsigned)(q * 4) : SENT;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, i * (int)g.syc * 4);
   }
 };
 
@@ -1568,7 +1615,7 @@ template <> struct has_k8<DgradT> : std::true_type {};
 // cache line per lane): l1 wgrad 202 -> 366 us measured.
 template <int A, int B> struct has_k8<BGemm<A, B>> : std::true_type {};
 
-template <class Plan, int MS, int NS>
+template <class Plan, int MS, int NS, int D>
 __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S, float* __restrict__ part,
                                                             int remap) {
   __shared__ __attribute__((aligned(16))) __bf16 Ls[MS + NS][3][TERM_B];
@@ -1593,7 +1640,7 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
   for (int i = 0; i < MS; ++i) sa[i] = pl.init8(k, m0 + BM * i, n0, tid);
 #pragma unroll
   for (int j = 0; j < NS; ++j) sb[j] = pl.init8(k, m0, n0 + BN * j, tid);
-  float ra[MS][8], rb[NS][8];
+  float ra[2][MS][8], rb[2][NS][8];  // register sets; D == 3 keeps two tiles of loads in flight
   bf16x8 pa[MS][3], pb[NS][3];
   f32x16 acc[MS][NS];
 #pragma unroll
@@ -1602,17 +1649,19 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
     for (int j = 0; j < NS; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  auto load = [&](int r) {
+  auto load = [&](int r, auto qc) {
+    constexpr int Q = decltype(qc)::value;
 #pragma unroll
-    for (int i = 0; i < MS; ++i) pl.load_a8(sa[i], r, ra[i]);
+    for (int i = 0; i < MS; ++i) pl.load_a8(sa[i], r, ra[Q][i]);
 #pragma unroll
-    for (int j = 0; j < NS; ++j) pl.load_b8(sb[j], r, rb[j]);
+    for (int j = 0; j < NS; ++j) pl.load_b8(sb[j], r, rb[Q][j]);
   };
-  auto split_all = [&]() {
+  auto split_all = [&](auto qc) {
+    constexpr int Q = decltype(qc)::value;
 #pragma unroll
-    for (int i = 0; i < MS; ++i) split3(ra[i], pa[i][0], pa[i][1], pa[i][2]);
+    for (int i = 0; i < MS; ++i) split3(ra[Q][i], pa[i][0], pa[i][1], pa[i][2]);
 #pragma unroll
-    for (int j = 0; j < NS; ++j) split3(rb[j], pb[j][0], pb[j][1], pb[j][2]);
+    for (int j = 0; j < NS; ++j) split3(rb[Q][j], pb[j][0], pb[j][1], pb[j][2]);
   };
   auto write_all = [&]() {
 #pragma unroll
@@ -1624,16 +1673,7 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
 #pragma unroll
       for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[MS + j][t][srowB * SB + skB]) = pb[j][t];
   };
-  const int ntile = rend > rbeg ? (rend - rbeg + BK - 1) / BK : 0;
-  if (ntile > 0) {
-    const int rlast = rbeg + (ntile - 1) * BK;
-    load(rbeg);
-    split_all();
-    write_all();
-    load(std::min(rbeg + BK, rlast));
-    __syncthreads();
-    for (int t = 0; t < ntile; ++t) {
-      const int r0 = rbeg + t * BK;
+  auto compute_tile = [&]() {
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
         bf16x8 fa[MS][3], fb[NS][3];
@@ -1655,11 +1695,37 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
         FLR_SX(1, 1) FLR_SX(0, 2) FLR_SX(2, 0) FLR_SX(0, 1) FLR_SX(1, 0) FLR_SX(0, 0)
 #undef FLR_SX
       }
-      split_all();      // tile t+1 (clamped: a duplicate that nothing reads after the last tile)
+  };
+  const int ntile = rend > rbeg ? (rend - rbeg + BK - 1) / BK : 0;
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
+  if (ntile > 0) {
+    const int rlast = rbeg + (ntile - 1) * BK;
+    load(rbeg, Q0{});
+    split_all(Q0{});
+    write_all();
+    load(std::min(rbeg + BK, rlast), Q0{});
+    if constexpr (D == 3) load(std::min(rbeg + 2 * BK, rlast), Q1{});
+    __syncthreads();
+    // one K-tile: the MFMAs of tile t from the LDS images, the split of tile t+1
+    // (register set Q) between them, its stash, then the global loads of tile
+    // t+D-1 into the set just freed (clamped past the last tile: duplicates)
+    auto tile_body = [&](int t, auto qc) {
+      const int r0 = rbeg + t * BK;
+      compute_tile();
+      split_all(qc);
       __syncthreads();  // every wave's fragment reads of tile t are done
       write_all();
-      load(std::min(r0 + 2 * BK, rlast));
+      load(std::min(r0 + D * BK, rlast), qc);
       __syncthreads();
+    };
+    if constexpr (D == 3) {
+      for (int t = 0; t < ntile; t += 2) {
+        tile_body(t, Q0{});
+        if (t + 1 < ntile) tile_body(t + 1, Q1{});
+      }
+    } else {
+      for (int t = 0; t < ntile; ++t) tile_body(t, Q0{});
     }
   }
   // C/D map of the 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
@@ -1730,6 +1796,238 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
         }
       }
     }
+}
+
+// ---- the weight gradient on split-at-stash images, transposed ----------------
+// Both operands of dW are contiguous along the reduction (pixels), so the loads
+// put a half-wave on 32 consecutive pixels of one channel (coalesced) and each
+// thread holds 8 consecutive channels at one pixel (StateT).  The split images
+// are [k = 32][row = 64] bf16 per term (128-B k-rows, 16-B chunks of 8 rows
+// XOR-swizzled by tswz(k): conflict-free ds_write_b128 stashes and transposed
+// reads), and an MFMA fragment (8 consecutive k of one row) is two
+// ds_read_b64_tr_b16: each 16-lane group reads a 4 k x 16 row block and gets it
+// column-major.  Products and their order per accumulator are the other bf16x6
+// forms': bit-identical dw and clip-norm partials.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__host__ __device__ constexpr int tswz(int k) { return (k & 3) | ((((k >> 1) ^ (k >> 2)) & 1) << 2); }
+constexpr int TIMG = 32 * 64;  // bf16 per transposed term image
+
+template <class Plan, int MS, int NS, int D>
+__global__ __launch_bounds__(THREADS, 2) void wsgemm_kernel(const Plan pl, int S, float* __restrict__ part,
+                                                            int remap) {
+  __shared__ __attribute__((aligned(16))) __bf16 Lt[MS + NS][3][TIMG];
+  int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
+  if (remap) xcd_tile(bx, by, bz);
+  const int k = bz / S, split = bz % S;
+  const int M = pl.M(), N = pl.N(), R = pl.R();
+  const int ktiles = cdiv(R, BK);
+  const int rbeg = (int)((int64_t)ktiles * split / S) * BK;
+  const int rend = std::min(R, (int)((int64_t)ktiles * (split + 1) / S) * BK);
+  const int m0 = by * BM * MS, n0 = bx * BN * NS;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, l32 = lane & 31;
+  // stash slot: k = tid & 31, chunk (tid >> 5) ^ tswz(k)
+  const int skq = tid & 31;
+  const int sidx = skq * 64 + 8 * ((tid >> 5) ^ tswz(skq));
+  // transposed-read lane addresses (bf16 index in a term image) for the two 4-k halves
+  // of this lane's 8-k fragment; k-step s adds 16 * 64
+  const int gq = (lane & 15) >> 2, gp = lane & 3, g1 = (lane >> 4) & 1;
+  int ra_off[2], rb_off[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int kk = 8 * h + 4 * j + gq;
+    const int ca = 4 * wm + 2 * g1 + (gp >> 1), cb = 4 * wn + 2 * g1 + (gp >> 1);
+    ra_off[j] = kk * 64 + 8 * (ca ^ tswz(kk)) + 4 * (gp & 1);
+    rb_off[j] = kk * 64 + 8 * (cb ^ tswz(kk)) + 4 * (gp & 1);
+  }
+
+  typename Plan::StateT sa[MS], sb[NS];
+#pragma unroll
+  for (int i = 0; i < MS; ++i) sa[i] = pl.initT(k, m0 + BM * i, n0, tid);
+#pragma unroll
+  for (int j = 0; j < NS; ++j) sb[j] = pl.initT(k, m0, n0 + BN * j, tid);
+  float ra[2][MS][8], rb[2][NS][8];  // register sets; D == 3 keeps two tiles of loads in flight
+  bf16x8 pa[MS][3], pb[NS][3];
+  f32x16 acc[MS][NS];
+#pragma unroll
+  for (int i = 0; i < MS; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  auto load = [&](int r, auto qc) {
+    constexpr int Q = decltype(qc)::value;
+#pragma unroll
+    for (int i = 0; i < MS; ++i) pl.load_at8(sa[i], r, ra[Q][i]);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) pl.load_bt8(sb[j], r, rb[Q][j]);
+  };
+  auto split_all = [&](auto qc) {
+    constexpr int Q = decltype(qc)::value;
+#pragma unroll
+    for (int i = 0; i < MS; ++i) split3(ra[Q][i], pa[i][0], pa[i][1], pa[i][2]);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) split3(rb[Q][j], pb[j][0], pb[j][1], pb[j][2]);
+  };
+  auto write_all = [&]() {
+#pragma unroll
+    for (int i = 0; i < MS; ++i)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Lt[i][t][sidx]) = pa[i][t];
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Lt[MS + j][t][sidx]) = pb[j][t];
+  };
+  auto tread = [&](const __bf16* img, const int (&off)[2], int s) -> bf16x8 {
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off[0] + 1024 * s));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off[1] + 1024 * s));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  auto compute_tile = [&]() {
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        bf16x8 fa[MS][3], fb[NS][3];
+#pragma unroll
+        for (int i = 0; i < MS; ++i)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) fa[i][q] = tread(Lt[i][q], ra_off, s);
+#pragma unroll
+        for (int j = 0; j < NS; ++j)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) fb[j][q] = tread(Lt[MS + j][q], rb_off, s);
+#define FLR_SX(TA, TB)                                                                              \
+  _Pragma("unroll") for (int i = 0; i < MS; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][TA], fb[j][TB], acc[i][j], 0, 0, 0);
+        // product-major, small terms first (term 0 = hi, 1 = mid, 2 = lo)
+        FLR_SX(1, 1) FLR_SX(0, 2) FLR_SX(2, 0) FLR_SX(0, 1) FLR_SX(1, 0) FLR_SX(0, 0)
+#undef FLR_SX
+      }
+  };
+  const int ntile = rend > rbeg ? (rend - rbeg + BK - 1) / BK : 0;
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
+  if (ntile > 0) {
+    const int rlast = rbeg + (ntile - 1) * BK;
+    load(rbeg, Q0{});
+    split_all(Q0{});
+    write_all();
+    load(std::min(rbeg + BK, rlast), Q0{});
+    if constexpr (D == 3) load(std::min(rbeg + 2 * BK, rlast), Q1{});
+    __syncthreads();
+    // one K-tile: the MFMAs of tile t from the LDS images, the split of tile t+1
+    // (register set Q) between them, its stash, then the global loads of tile
+    // t+D-1 into the set just freed (clamped past the last tile: duplicates)
+    auto tile_body = [&](int t, auto qc) {
+      const int r0 = rbeg + t * BK;
+      compute_tile();
+      split_all(qc);
+      __syncthreads();  // every wave's fragment reads of tile t are done
+      write_all();
+      load(std::min(r0 + D * BK, rlast), qc);
+      __syncthreads();
+    };
+    if constexpr (D == 3) {
+      for (int t = 0; t < ntile; t += 2) {
+        tile_body(t, Q0{});
+        if (t + 1 < ntile) tile_body(t + 1, Q1{});
+      }
+    } else {
+      for (int t = 0; t < ntile; ++t) tile_body(t, Q0{});
+    }
+  }
+  // C/D map of the 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < MS; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int tm0 = m0 + BM * i, tn0 = n0 + BN * j;
+      if (S == 1 && pl.linear()) {  // one tile base, then row * ldm + col per element
+        float* base = pl.out() + pl.tile_base(k, tm0, tn0);
+        const int64_t ldm = pl.ldm();
+        const int nl = 32 * wn + l32;
+        if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
+          if (pl.bias) {  // the batched GEMM's bias: one value per lane column, bias + v
+            const float bv = tn0 + nl < N ? pl.bias[k * pl.bias_k + tn0 + nl] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = bv + acc[i][j][e];
+          }
+        }
+        if (const float* abase = plan_add(pl)) {  // all 16 addends in flight before the first store
+          abase += pl.tile_base(k, tm0, tn0);
+          float av[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int ml = 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+            av[e] = (tm0 + ml < M && tn0 + nl < N) ? abase[ml * ldm + nl] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] = __fadd_rn(acc[i][j][e], av[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int ml = 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (tm0 + ml < M && tn0 + nl < N) base[ml * ldm + nl] = acc[i][j][e];
+        }
+        continue;
+      }
+      if constexpr (std::is_same<Plan, DgradT>::value) {
+        if (S == 1 && pl.add) {  // parity-class stores: the addends loaded before any store
+          int64_t ix[16];
+          float av[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int m = tm0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int n = tn0 + 32 * wn + l32;
+            ix[e] = (m < M && n < N) ? pl.index(k, m, n) : -1;
+            av[e] = ix[e] >= 0 ? pl.add[ix[e]] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (ix[e] >= 0) pl.dx[ix[e]] = __fadd_rn(acc[i][j][e], av[e]);
+          continue;
+        }
+      }
+      if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
+        if (S == 1) {
+          pl.store_tile(k, tm0, tn0, 32 * wm + 4 * h, 32 * wn + l32, acc[i][j], M, N);
+          continue;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = tm0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int n = tn0 + 32 * wn + l32;
+        if (m < M && n < N) {
+          if (S == 1) pl.store(k, m, n, acc[i][j][e]);
+          else part[(((int64_t)split * pl.g.Kc + k) * M + m) * N + n] = acc[i][j][e];
+        }
+      }
+    }
+  if constexpr (has_sq<Plan>::value) {
+    if (S == 1 && pl.sq) {  // this tile's clip-norm partial (split-K: the treduce pass writes them)
+      double sq = 0.0;
+#pragma unroll
+      for (int i = 0; i < MS; ++i)
+#pragma unroll
+        for (int j = 0; j < NS; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int m = m0 + BM * i + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int n = n0 + BN * j + 32 * wn + l32;
+            const double v = (m < M && n < N) ? (double)acc[i][j][e] : 0.0;
+            sq += v * v;
+          }
+      __shared__ double red[THREADS / 64];
+      const double t = block_sumsq(sq, red);
+      if (tid == 0) pl.sq[(int64_t)k * pl.sq_ld + by * (int)gridDim.x + bx] = t;
+    }
+  }
 }
 
 template <class Plan>
@@ -1876,8 +2174,23 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   int form = gemm_form();
   if constexpr (has_k8<Plan>::value) {
     if (form == 5) {
-      hipLaunchKernelGGL((sgemm_kernel<Plan, MS, NS>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
-                         xcd_remap());
+      if (prefetch_depth() == 3)
+        hipLaunchKernelGGL((sgemm_kernel<Plan, MS, NS, 3>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
+                           xcd_remap());
+      else
+        hipLaunchKernelGGL((sgemm_kernel<Plan, MS, NS, 2>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
+                           xcd_remap());
+      form = -1;
+    }
+  }
+  if constexpr (std::is_same<Plan, WgtT<true>>::value || std::is_same<Plan, WgtT<false>>::value) {
+    if (form == 5) {
+      if (prefetch_depth() == 3)
+        hipLaunchKernelGGL((wsgemm_kernel<Plan, MS, NS, 3>), grid, dim3(THREADS), 0, st, pl, S,
+                           static_cast<float*>(ws), xcd_remap());
+      else
+        hipLaunchKernelGGL((wsgemm_kernel<Plan, MS, NS, 2>), grid, dim3(THREADS), 0, st, pl, S,
+                           static_cast<float*>(ws), xcd_remap());
       form = -1;
     }
   }
