@@ -68,7 +68,7 @@ def _kernel_rows(path: str):
 
 
 def conv_utilisation(spec, K: int, batch: int, steps: int, stats_path=None,
-                     rounds_in_profile_key: str = "ce_kernel"):
+                     rounds_in_profile_key: str = "::ce_kernel("):
     """Convolution MFMA utilisation of the headline config from a rocprofv3
     summary of the C3 bench (NOT this run's kernels: the profiler wraps a
     separate bench run; --kernel-stats names it, else the newest committed
@@ -240,7 +240,7 @@ def gemm_utilisation(spec, K: int, batch: int, steps: int, stats_path=None):
     for name, calls, t in _kernel_rows(stats_path):
         if "BGemm" in name:
             ms += t
-        if "ce_kernel" in name:
+        if "::ce_kernel(" in name:
             calls_ce += calls
     if not calls_ce or not ms:
         return None

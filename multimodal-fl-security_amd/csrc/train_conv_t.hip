@@ -218,14 +218,6 @@ inline int gemm_form() {
   return 5;  // split at stash (bf16 LDS images) where the plan has k8 loads, else pipelined
 }
 
-// Register-prefetch depth of the split-at-stash kernels: 2 (one tile of global
-// loads in flight behind the tile being computed) or 3 (two).  FLR_PREFETCH=2|3,
-// read per launch (A/B timing).
-inline int prefetch_depth() {
-  const char* e = getenv("FLR_PREFETCH");
-  return (e && e[0] == '3') ? 3 : 2;
-}
-
 // ---- load plans ---------------------------------------------------------------
 // Tap of a reduction slot: W_t offset of (tap, 0, 0) = tap_index * Cin * Cout.
 // (kh, kw) of a tile-uniform reduction slot, by rectangle arithmetic (the host
@@ -550,6 +542,7 @@ constexpr int MAX_CLASSES = 16;
 // N = Cout, R = B*Ho*Wo.  A 64-row m-tile lies inside one tap (Cin % 64 == 0).
 template <bool BVEC>
 struct WgtT {
+  static constexpr bool QUAD_A = false, QUAD_B = false;
   Geom g;
   const float* x;
   const float* dy;
@@ -1196,6 +1189,26 @@ struct BGemm : BGemmArgs {
   __device__ void load_b8(const State8& s, int r0, float (&v)[8]) const {
     load_op8<BMD>(s.rb, s.brow, n, r0, r, b_n, b_r, v);
   }
+  // transposed-image loads of a k-contiguous (RK) operand (wsgemm_kernel): thread t
+  // reads k = r0 + (t & 31) of rows 8 (t >> 5) .. +7 — a half-wave covers 128 B of a row
+  using StateT = State;
+  __device__ StateT initT(int k, int m0, int n0, int tid) const { return init(k, m0, n0, tid); }
+  __device__ static void load_opT(rsrc_t rs, int base_row, int rows, int r0, int R, int64_t s_row, float (&v)[8]) {
+    const int kk = r0 + (int)(threadIdx.x & 31);
+    const int row0 = base_row + 8 * (int)(threadIdx.x >> 5);
+    const unsigned base = (unsigned)((row0 * s_row + kk) * 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bool ok = (row0 + i < rows) & (kk < R);
+      v[i] = ld1(rs, ok ? base + (unsigned)(i * s_row * 4) : SENT, 0);
+    }
+  }
+  __device__ void load_at8(const StateT& s, int r0, float (&v)[8]) const {
+    load_opT(s.ra, s.arow, m, r0, r, a_m, v);
+  }
+  __device__ void load_bt8(const StateT& s, int r0, float (&v)[8]) const {
+    load_opT(s.rb, s.brow, n, r0, r, b_n, v);
+  }
 };
 
 #if FLR_CT_P4
@@ -1640,7 +1653,9 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
   for (int i = 0; i < MS; ++i) sa[i] = pl.init8(k, m0 + BM * i, n0, tid);
 #pragma unroll
   for (int j = 0; j < NS; ++j) sb[j] = pl.init8(k, m0, n0 + BN * j, tid);
-  float ra[2][MS][8], rb[2][NS][8];  // register sets; D == 3 keeps two tiles of loads in flight
+  // register sets; D == 3 keeps two tiles of global loads in flight (measured: no gain over D == 2 at the
+  // C3 conv and C4 GEMM shapes — the loop is not load-latency-bound; D == 2 is the one instantiated)
+  float ra[2][MS][8], rb[2][NS][8];
   bf16x8 pa[MS][3], pb[NS][3];
   f32x16 acc[MS][NS];
 #pragma unroll
@@ -1812,10 +1827,12 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 __host__ __device__ constexpr int tswz(int k) { return (k & 3) | ((((k >> 1) ^ (k >> 2)) & 1) << 2); }
 constexpr int TIMG = 32 * 64;  // bf16 per transposed term image
 
-template <class Plan, int MS, int NS, int D>
+template <class Plan, int MS, int NS, int D, bool TA, bool TB>
 __global__ __launch_bounds__(THREADS, 2) void wsgemm_kernel(const Plan pl, int S, float* __restrict__ part,
                                                             int remap) {
-  __shared__ __attribute__((aligned(16))) __bf16 Lt[MS + NS][3][TIMG];
+  // a term image: transposed [32 k][64 rows] (TIMG) or row-major [64 rows][SB] (TERM_B)
+  constexpr int IMG = (TA || TB) && !(TA && TB) ? TERM_B : (TA ? TIMG : TERM_B);
+  __shared__ __attribute__((aligned(16))) __bf16 Lt[MS + NS][3][IMG];
   int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
   if (remap) xcd_tile(bx, by, bz);
   const int k = bz / S, split = bz % S;
@@ -1843,12 +1860,26 @@ __global__ __launch_bounds__(THREADS, 2) void wsgemm_kernel(const Plan pl, int S
     rb_off[j] = kk * 64 + 8 * (cb ^ tswz(kk)) + 4 * (gp & 1);
   }
 
-  typename Plan::StateT sa[MS], sb[NS];
+  // row-major images: the split-at-stash kernel's stash slot and fragment rows
+  const int srowA = stash_row<Plan::QUAD_A>(tid), skA = stash_k<Plan::QUAD_A>(tid);
+  const int srowB = stash_row<Plan::QUAD_B>(tid), skB = stash_k<Plan::QUAD_B>(tid);
+  using SA = std::conditional_t<TA, typename Plan::StateT, typename Plan::State8>;
+  using SBt = std::conditional_t<TB, typename Plan::StateT, typename Plan::State8>;
+  SA sa[MS];
+  SBt sb[NS];
 #pragma unroll
-  for (int i = 0; i < MS; ++i) sa[i] = pl.initT(k, m0 + BM * i, n0, tid);
+  for (int i = 0; i < MS; ++i) {
+    if constexpr (TA) sa[i] = pl.initT(k, m0 + BM * i, n0, tid);
+    else sa[i] = pl.init8(k, m0 + BM * i, n0, tid);
+  }
 #pragma unroll
-  for (int j = 0; j < NS; ++j) sb[j] = pl.initT(k, m0, n0 + BN * j, tid);
-  float ra[2][MS][8], rb[2][NS][8];  // register sets; D == 3 keeps two tiles of loads in flight
+  for (int j = 0; j < NS; ++j) {
+    if constexpr (TB) sb[j] = pl.initT(k, m0, n0 + BN * j, tid);
+    else sb[j] = pl.init8(k, m0, n0 + BN * j, tid);
+  }
+  // register sets; D == 3 keeps two tiles of global loads in flight (measured: no gain over D == 2 at the
+  // C3 conv and C4 GEMM shapes — the loop is not load-latency-bound; D == 2 is the one instantiated)
+  float ra[2][MS][8], rb[2][NS][8];
   bf16x8 pa[MS][3], pb[NS][3];
   f32x16 acc[MS][NS];
 #pragma unroll
@@ -1860,9 +1891,15 @@ __global__ __launch_bounds__(THREADS, 2) void wsgemm_kernel(const Plan pl, int S
   auto load = [&](int r, auto qc) {
     constexpr int Q = decltype(qc)::value;
 #pragma unroll
-    for (int i = 0; i < MS; ++i) pl.load_at8(sa[i], r, ra[Q][i]);
+    for (int i = 0; i < MS; ++i) {
+      if constexpr (TA) pl.load_at8(sa[i], r, ra[Q][i]);
+      else pl.load_a8(sa[i], r, ra[Q][i]);
+    }
 #pragma unroll
-    for (int j = 0; j < NS; ++j) pl.load_bt8(sb[j], r, rb[Q][j]);
+    for (int j = 0; j < NS; ++j) {
+      if constexpr (TB) pl.load_bt8(sb[j], r, rb[Q][j]);
+      else pl.load_b8(sb[j], r, rb[Q][j]);
+    }
   };
   auto split_all = [&](auto qc) {
     constexpr int Q = decltype(qc)::value;
@@ -1875,11 +1912,13 @@ __global__ __launch_bounds__(THREADS, 2) void wsgemm_kernel(const Plan pl, int S
 #pragma unroll
     for (int i = 0; i < MS; ++i)
 #pragma unroll
-      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Lt[i][t][sidx]) = pa[i][t];
+      for (int t = 0; t < 3; ++t)
+        *reinterpret_cast<bf16x8*>(&Lt[i][t][TA ? sidx : srowA * SB + skA]) = pa[i][t];
 #pragma unroll
     for (int j = 0; j < NS; ++j)
 #pragma unroll
-      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Lt[MS + j][t][sidx]) = pb[j][t];
+      for (int t = 0; t < 3; ++t)
+        *reinterpret_cast<bf16x8*>(&Lt[MS + j][t][TB ? sidx : srowB * SB + skB]) = pb[j][t];
   };
   auto tread = [&](const __bf16* img, const int (&off)[2], int s) -> bf16x8 {
     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -1896,11 +1935,17 @@ __global__ __launch_bounds__(THREADS, 2) void wsgemm_kernel(const Plan pl, int S
 #pragma unroll
         for (int i = 0; i < MS; ++i)
 #pragma unroll
-          for (int q = 0; q < 3; ++q) fa[i][q] = tread(Lt[i][q], ra_off, s);
+          for (int q = 0; q < 3; ++q) {
+            if constexpr (TA) fa[i][q] = tread(Lt[i][q], ra_off, s);
+            else fa[i][q] = *reinterpret_cast<const bf16x8*>(&Lt[i][q][(32 * wm + l32) * SB + 16 * s + 8 * h]);
+          }
 #pragma unroll
         for (int j = 0; j < NS; ++j)
 #pragma unroll
-          for (int q = 0; q < 3; ++q) fb[j][q] = tread(Lt[MS + j][q], rb_off, s);
+          for (int q = 0; q < 3; ++q) {
+            if constexpr (TB) fb[j][q] = tread(Lt[MS + j][q], rb_off, s);
+            else fb[j][q] = *reinterpret_cast<const bf16x8*>(&Lt[MS + j][q][(32 * wn + l32) * SB + 16 * s + 8 * h]);
+          }
 #define FLR_SX(TA, TB)                                                                              \
   _Pragma("unroll") for (int i = 0; i < MS; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
       acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][TA], fb[j][TB], acc[i][j], 0, 0, 0);
@@ -2159,6 +2204,21 @@ inline int tile_choice(int M, int N, int R) {
   return 11;
 }
 
+template <class P> struct is_bgemm_t : std::false_type {
+  static constexpr bool ta = false, tb = false;
+};
+template <int A, int B> struct is_bgemm_t<BGemm<A, B>> : std::true_type {
+  static constexpr bool ta = A == BM_RK, tb = B == BM_RK;
+};
+// FLR_BGEMM_TIMG=1: k-contiguous batched-GEMM operands on transposed images
+// (A/B; off by default: the eight 4-B loads per thread cost more than the
+// quad-lane stash's 2-way bank conflicts save — vit.qkv 493 vs 426 us at K=32,
+// profiles/r3_bgemm_timg.txt)
+inline bool bgemm_timg() {
+  const char* e = getenv("FLR_BGEMM_TIMG");
+  return e && e[0] == '1';
+}
+
 template <class Plan, int MS, int NS>
 int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   const int M = pl.M(), N = pl.N(), R = pl.R(), K = pl.g.Kc;
@@ -2172,25 +2232,27 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   }
   const dim3 grid((unsigned)cdiv(N, BN * NS), (unsigned)cdiv(M, BM * MS), (unsigned)(K * S));
   int form = gemm_form();
+  if constexpr (is_bgemm_t<Plan>::ta || is_bgemm_t<Plan>::tb) {
+    // batched GEMMs with a k-contiguous operand: that operand on a transposed
+    // image (coalesced 128-B row reads, conflict-free stashes; the row-major
+    // image of a quad-lane load stashes 2-way bank-conflicted)
+    if (form == 5 && bgemm_timg()) {
+      hipLaunchKernelGGL((wsgemm_kernel<Plan, MS, NS, 2, is_bgemm_t<Plan>::ta, is_bgemm_t<Plan>::tb>), grid,
+                         dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws), xcd_remap());
+      form = -1;
+    }
+  }
   if constexpr (has_k8<Plan>::value) {
     if (form == 5) {
-      if (prefetch_depth() == 3)
-        hipLaunchKernelGGL((sgemm_kernel<Plan, MS, NS, 3>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
-                           xcd_remap());
-      else
-        hipLaunchKernelGGL((sgemm_kernel<Plan, MS, NS, 2>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
-                           xcd_remap());
+      hipLaunchKernelGGL((sgemm_kernel<Plan, MS, NS, 2>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
+                         xcd_remap());
       form = -1;
     }
   }
   if constexpr (std::is_same<Plan, WgtT<true>>::value || std::is_same<Plan, WgtT<false>>::value) {
     if (form == 5) {
-      if (prefetch_depth() == 3)
-        hipLaunchKernelGGL((wsgemm_kernel<Plan, MS, NS, 3>), grid, dim3(THREADS), 0, st, pl, S,
-                           static_cast<float*>(ws), xcd_remap());
-      else
-        hipLaunchKernelGGL((wsgemm_kernel<Plan, MS, NS, 2>), grid, dim3(THREADS), 0, st, pl, S,
-                           static_cast<float*>(ws), xcd_remap());
+      hipLaunchKernelGGL((wsgemm_kernel<Plan, MS, NS, 2, true, true>), grid, dim3(THREADS), 0, st, pl, S,
+                         static_cast<float*>(ws), xcd_remap());
       form = -1;
     }
   }

@@ -120,7 +120,7 @@ def _run_tap_major(cuda, shape, seed):
     return y.detach().clone(), xg.grad.clone(), wt.grad.clone()
 
 
-@pytest.mark.parametrize("form", ["pipe", "old", "FLR_PREFETCH=3"])
+@pytest.mark.parametrize("form", ["pipe", "old"])
 @pytest.mark.parametrize("shape", TAP_SHAPES, ids=[str(s) for s in TAP_SHAPES])
 def test_gemm_forms_bit_identical(cuda, shape, form, monkeypatch):
     """Every bf16x6 form (FLR_GEMM: the default split at stash time (bf16 LDS
@@ -145,16 +145,17 @@ def test_bgemm_forms_bit_identical(cuda, dims, monkeypatch):
     A = torch.randn(K, M, R, generator=g).to(cuda)
     Bm = torch.randn(K, N, R, generator=g).to(cuda)
     outs = []
-    for form in (None, "pipe", "FLR_PREFETCH=3"):
+    # default (row-major images), k-contiguous operands on transposed images, the per-wave split
+    for form in (None, "FLR_BGEMM_TIMG=1", "pipe"):
         if form and "=" in form:
-            monkeypatch.delenv("FLR_GEMM", raising=False)
             monkeypatch.setenv(*form.split("="))
         elif form:
             monkeypatch.setenv("FLR_GEMM", form)
-        outs += [bgemm(A, Bm).clone(), bgemm(A.transpose(1, 2).contiguous().transpose(1, 2), Bm).clone()]
+        outs += [bgemm(A, Bm).clone(), bgemm(A.transpose(1, 2).contiguous().transpose(1, 2), Bm).clone(),
+                 bgemm(A, Bm.transpose(1, 2).contiguous().transpose(1, 2)).clone()]
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
-    assert torch.equal(outs[0], outs[4]) and torch.equal(outs[1], outs[5])
+    for i in range(3):
+        assert torch.equal(outs[i], outs[3 + i]) and torch.equal(outs[i], outs[6 + i]), i
 
 
 NORM_SHAPES = [  # ResNet-18 layers at the C3 shapes (B = 32): split-K wgrad (l1), one tile pass, dead taps (l4)
