@@ -48,6 +48,8 @@ def gram_traffic(K: int, P: int):
 
 
 COMMITTED_C3_STATS = "profiles/r3_c3_kernel_stats.txt"
+# the C4 bench's rocprofv3 summary (gemm_mfma_from_profile of an unmodified C4 line)
+COMMITTED_C4_STATS = "profiles/r3_c4_kernel_stats.txt"
 
 
 def _kernel_rows(path: str):
@@ -432,7 +434,8 @@ def main() -> None:
                 "all-gather of the aggregated vector" if sharded else "one all-gather of the client matrix")),
             "exchange": eng.exchange,
             "training_phase": ("one captured HIP graph per round" if eng.use_graph else "eager launches") + (
-                "; local updates = one flr_train_clients_ex call" if eng.native else
+                ("; local updates = one flr_train_vit_bert call" if spec.family == "vit_bert" else
+                 "; local updates = one flr_train_clients_ex call") if eng.native else
                 "; local updates = the Python autograd composition of the kernels"),
         },
         "aggregate_ms": aggregate_ms,
@@ -442,7 +445,10 @@ def main() -> None:
                                          elapsed / args.steps * 1e3, world),
         "conv_mfma_from_profile": conv_utilisation(spec, K, rcfg.batch, args.local_steps, args.kernel_stats)
         if args.config == "C3" and not custom else None,
-        "gemm_mfma_from_profile": gemm_utilisation(spec, K, rcfg.batch, args.local_steps, args.kernel_stats)
+        "gemm_mfma_from_profile": gemm_utilisation(
+            spec, K, rcfg.batch, args.local_steps,
+            args.kernel_stats or (os.path.join(ROOT, COMMITTED_C4_STATS) if args.config == "C4" and not custom
+                                  else None))
         if model == "vit_bert" else None,
         "collectives": round_collectives(eng, defense, K, P, world),
         "roofline": {

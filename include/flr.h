@@ -677,6 +677,38 @@ int flr_resnet_gru_reorder(const flr_resnet_gru_spec* spec, const float* src, fl
  * weight_decay == 0, else P. */
 int64_t flr_resnet_gru_live_params(const flr_resnet_gru_spec* spec, float weight_decay);
 
+/* ---- a1 for the C4/C5 family: flr_train_vit_bert ---------------------------
+ * The same client-plugin local update (run_experiments.py:193-240,
+ * fl_client.py:76-149) for the ViT-S + BERT-mini late-fusion model
+ * (flr.models.transformer.ViTBertNet: ViT patch embedding, class token,
+ * position embedding, vit_depth pre-LN blocks, final LayerNorm; BERT word /
+ * position / token-type embeddings, embedding LayerNorm, bert_depth post-LN
+ * layers, tanh pooler; fc1 over [img | txt], ReLU, dropout mask, fc2), with no
+ * torch: the kernel schedule of the Python trainer (flr.train.
+ * ClientBatchTrainer), so both give the same bits.  Clients run in passes of
+ * `chunk` clients (0: min(K, 32)); activations scale with the chunk, weights
+ * (and momentum when steps > 1) with K.  Heads of width 64, <= 96 tokens per
+ * sequence, widths <= 1024, B*seq_len <= 4096.  Inputs as flr_train_clients
+ * (images [steps][K][B][C][S][S], tokens [steps][K][B][seq_len] int64 ids,
+ * labels [steps][K][B], dropout_masks NULL or [steps][K][B][fusion]).  The
+ * family has no training-layout change: X's rows are in parameters() order
+ * with or without FLR_TC_TRAIN_ORDER, written by the last optimizer step. */
+typedef struct flr_vit_bert_spec {
+  int64_t num_classes, image_size, in_channels, patch;
+  int64_t vit_dim, vit_depth, vit_heads, vit_mlp;
+  int64_t vocab, seq_len, bert_dim, bert_depth, bert_heads, bert_ffn, bert_max_pos;
+  int64_t fusion;
+} flr_vit_bert_spec;
+int64_t flr_vit_bert_num_params(const flr_vit_bert_spec* spec);
+size_t flr_train_vit_bert_workspace(const flr_vit_bert_spec* spec, int64_t K, int64_t B, int64_t steps,
+                                    int64_t chunk);
+int flr_train_vit_bert(const flr_vit_bert_spec* spec, const float* global, float* X, int64_t ld,
+                       const float* images, const int64_t* tokens, const int64_t* labels,
+                       const float* dropout_masks, int64_t steps, int64_t K, int64_t B, float lr,
+                       float momentum, float weight_decay, float max_norm, int64_t nneg, float* loss_out,
+                       float* norms_out, unsigned flags, int64_t chunk, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,6 +82,12 @@ SIGNATURES = {
                                     _c_void_p]),
     "flr_resnet_gru_reorder": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p]),
     "flr_resnet_gru_live_params": (_i64, [_c_void_p, ctypes.c_float]),
+    "flr_vit_bert_num_params": (_i64, [_c_void_p]),
+    "flr_train_vit_bert_workspace": (_size_t, [_c_void_p, _i64, _i64, _i64, _i64]),
+    "flr_train_vit_bert": (_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p,
+                                  _c_void_p, _i64, _i64, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                  ctypes.c_float, _i64, _c_void_p, _c_void_p, ctypes.c_uint, _i64, _c_void_p,
+                                  _size_t, _c_void_p]),
     "flr_conv2d_tap_major_ok": (_int, [_i64, _i64]),
     "flr_conv2d_t_workspace": (_size_t, [_i64] * 10),
     "flr_conv2d_fwd_t": (_int, [_c_void_p, _c_void_p, _c_void_p] + [_i64] * 10 + [_c_void_p, _size_t, _c_void_p]),

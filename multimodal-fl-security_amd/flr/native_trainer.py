@@ -1,5 +1,6 @@
-"""flr_train_clients from Python: the C entry that trains a batch of clients
-of the C2/C3 model family with no torch in the loop (include/flr.h; the
+"""flr_train_clients / flr_train_vit_bert from Python: the C entries that
+train a batch of clients of the C2/C3 (ResNet + GRU) and C4/C5 (ViT + BERT)
+model families with no torch in the loop (include/flr.h; the
 client plugin of SURVEY §8(b), FLClient.fit / _train fl_client.py:76-149 and
 the simulation body run_experiments.py:193-240).  This wrapper only marshals
 device buffers (torch is the allocator here); a non-torch caller binds the
@@ -29,6 +30,19 @@ class ResNetGruSpec(ctypes.Structure):
         return cls(spec.num_classes, spec.image_size, spec.in_channels, (ctypes.c_int64 * 4)(*spec.widths),
                    (ctypes.c_int64 * 4)(*spec.blocks), spec.vocab, spec.seq_len, spec.embed, spec.hidden,
                    spec.fusion)
+
+
+class VitBertSpec(ctypes.Structure):
+    """flr_vit_bert_spec (include/flr.h): the C4/C5 family's geometry."""
+    _fields_ = [(n, ctypes.c_int64) for n in (
+        "num_classes", "image_size", "in_channels", "patch", "vit_dim", "vit_depth", "vit_heads", "vit_mlp", "vocab",
+        "seq_len", "bert_dim", "bert_depth", "bert_heads", "bert_ffn", "bert_max_pos", "fusion")]
+
+    @classmethod
+    def of(cls, spec: ModelSpec) -> "VitBertSpec":
+        if spec.family != "vit_bert":
+            raise ValueError(f"flr_train_vit_bert serves the ViT + BERT family, not {spec.family!r}")
+        return cls(*[int(getattr(spec, n)) for n, _ in cls._fields_])
 
 
 def num_params(spec: ModelSpec) -> int:
@@ -69,15 +83,25 @@ def train_clients(spec: ModelSpec, global_flat: torch.Tensor, batches: Sequence,
     return X, loss, norms
 
 
+def vit_bert_num_params(spec: ModelSpec) -> int:
+    return int(_capi.lib().flr_vit_bert_num_params(ctypes.byref(VitBertSpec.of(spec))))
+
+
+def vit_bert_workspace_bytes(spec: ModelSpec, K: int, B: int, steps: int, chunk: int = 0) -> int:
+    return int(_capi.lib().flr_train_vit_bert_workspace(ctypes.byref(VitBertSpec.of(spec)), K, B, steps, chunk))
+
+
 class NativeRoundTrainer:
-    """The round engine's trainer for the ResNet + GRU family on
-    flr_train_clients_ex: the whole local update of this GPU's clients is one
-    C call (captured into the round's HIP graph by flr.round), so no torch
-    kernel runs in the training phase.  The same surface RoundEngine uses of
+    """The round engine's trainer on the one-call C entries: flr_train_clients_ex
+    (the ResNet + GRU family) and flr_train_vit_bert (the ViT + BERT family).
+    The whole local update of this GPU's clients is one C call (captured into
+    the round's HIP graph by flr.round), so no torch kernel runs in the
+    training phase.  The same surface RoundEngine uses of
     flr.train.ClientBatchTrainer (X, P, to_train_order / to_torch_order,
     load_global[_train], local_update), with the same bits: the kernel
-    schedule is the Python trainer's, plus the residual blocks' two gradient
-    paths summed in the dgrad epilogue (one rounding, as autograd's add)."""
+    schedule is the Python trainer's (ResNet + GRU: plus the residual blocks'
+    two gradient paths summed in the dgrad epilogue, one rounding, as
+    autograd's add)."""
 
     def __init__(self, spec: ModelSpec, num_clients: int, device, cfg: TrainConfig = TrainConfig(), batch: int = 32):
         from .matrix import ClientMatrix
@@ -86,18 +110,27 @@ class NativeRoundTrainer:
         self.device = torch.device(device)
         self.K = int(num_clients)
         self.B = int(batch)
-        self._sp = ResNetGruSpec.of(spec)
+        self.vit = spec.family == "vit_bert"
+        self._sp = VitBertSpec.of(spec) if self.vit else ResNetGruSpec.of(spec)
         shapes = [s for _, s in param_layout(spec)]
         self.X = ClientMatrix.empty(self.K, shapes, self.device)
         self.P = self.X.P
-        if num_params(spec) != self.P:
-            raise RuntimeError(f"flr_train_clients lays out {num_params(spec)} parameters, the model {self.P}")
-        self.live_params = int(_capi.lib().flr_resnet_gru_live_params(ctypes.byref(self._sp), cfg.weight_decay))
-        self.chunks = [(0, self.K)]
+        n = vit_bert_num_params(spec) if self.vit else num_params(spec)
+        if n != self.P:
+            raise RuntimeError(f"the C trainer lays out {n} parameters, the model {self.P}")
         steps = max(1, cfg.local_steps)
-        self._ws_bytes = workspace_bytes(spec, self.K, self.B, steps)
+        if self.vit:  # no dead taps, no layout change; passes of `chunk` clients as ClientBatchTrainer
+            self.live_params = self.P
+            from .train import ClientBatchTrainer
+            self._chunk = cfg.client_chunk if cfg.client_chunk > 0 else ClientBatchTrainer.auto_chunk(spec, self.K)
+            self.chunks = [(c0, min(self.K, c0 + self._chunk)) for c0 in range(0, self.K, self._chunk)]
+            self._ws_bytes = vit_bert_workspace_bytes(spec, self.K, self.B, steps, self._chunk)
+        else:
+            self.live_params = int(_capi.lib().flr_resnet_gru_live_params(ctypes.byref(self._sp), cfg.weight_decay))
+            self.chunks = [(0, self.K)]
+            self._ws_bytes = workspace_bytes(spec, self.K, self.B, steps)
         if self._ws_bytes == 0:
-            raise ValueError("flr_train_clients: unsupported model or shape")
+            raise ValueError("native trainer: unsupported model or shape")
         self._ws = torch.empty(self._ws_bytes, dtype=torch.uint8, device=self.device)
         self._ws_steps = steps
         self.loss = torch.empty(self.K, dtype=torch.float32, device=self.device)
@@ -111,6 +144,9 @@ class NativeRoundTrainer:
 
     def _reorder(self, src: torch.Tensor, dst: torch.Tensor, to_train: bool) -> torch.Tensor:
         src = src.to(self.device, torch.float32).contiguous()
+        if self.vit:  # training order is the parameters() order
+            _capi.call("flr_copy_rows", src.data_ptr(), self.P, self.P, dst.data_ptr(), self.P, 1, self._stream())
+            return dst
         _capi.call("flr_resnet_gru_reorder", ctypes.byref(self._sp), src.data_ptr(), dst.data_ptr(), int(to_train),
                    self._stream())
         return dst
@@ -188,6 +224,13 @@ class NativeRoundTrainer:
         imgs, toks, labs, m = self._inputs(batches, dropout_masks)
         c = self.cfg
         g = self._global
+        if self.vit:
+            _capi.call("flr_train_vit_bert", ctypes.byref(self._sp), g.data_ptr(), self.X.data.data_ptr(),
+                       self.X.data.stride(0), imgs.data_ptr(), toks.data_ptr(), labs.data_ptr(),
+                       None if m is None else m.data_ptr(), steps, self.K, self.B, c.lr, c.momentum,
+                       c.weight_decay, c.clip, int(negate_rows), self.loss.data_ptr(), self.norms.data_ptr(),
+                       self._order, self._chunk, self._ws.data_ptr(), self._ws_bytes, self._stream())
+            return self.loss
         _capi.call("flr_train_clients_ex", ctypes.byref(self._sp), g.data_ptr(), self.X.data.data_ptr(),
                    self.X.data.stride(0), imgs.data_ptr(), toks.data_ptr(), labs.data_ptr(),
                    None if m is None else m.data_ptr(), steps, self.K, self.B, c.lr, c.momentum, c.weight_decay,

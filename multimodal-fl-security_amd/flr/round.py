@@ -66,10 +66,11 @@ class RoundEngine:
         K = rcfg.num_clients
         self.lo, self.hi = fdist.shard(K, world, rank)
         shapes = [s for _, s in param_layout(spec)]
-        # the ResNet + GRU family trains through the one C entry flr_train_clients_ex
-        # (no torch kernel in the training phase); FLR_TRAINER=python: the
-        # autograd composition of the same kernels (A/B; the other families)
-        self.native = (spec.family == "resnet_gru" and self.device.type == "cuda"
+        # the ResNet + GRU and ViT + BERT families train through one C entry
+        # (flr_train_clients_ex / flr_train_vit_bert: no torch kernel in the
+        # training phase); FLR_TRAINER=python: the autograd composition of the
+        # same kernels (A/B; the CUB family)
+        self.native = (spec.family in ("resnet_gru", "vit_bert") and self.device.type == "cuda"
                        and os.environ.get("FLR_TRAINER", "native") != "python")
         if self.native:
             from .native_trainer import NativeRoundTrainer

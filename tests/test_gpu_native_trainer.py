@@ -53,3 +53,57 @@ def test_native_trainer_matches_reference_loop(cuda):
         err = ((X[k].cpu().double() - ref.double()).abs().max() / ref.abs().max()).item()
         assert err < 1e-5, err
         assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+
+
+def _vit_python(spec, glob, batches, masks, K, steps, chunk, nneg, cuda):
+    tr = ClientBatchTrainer(spec, K, cuda, TrainConfig(local_steps=steps, client_chunk=chunk))
+    tr.load_global(glob)
+    loss = tr.local_update(batches, masks, negate_rows=nneg).clone()
+    return loss, tr.X.data[:, : tr.P].clone(), tr.norms.clone()
+
+
+# flr_train_vit_bert (the C4/C5 family's one-call trainer) vs the Python
+# trainer: the same kernels driven through torch autograd, the same bits.
+# tiny: ragged client passes (chunk 2 of K 3); full: the ViT-S/4 + BERT-mini
+# model itself with dropout masks, attackers negated
+@pytest.mark.parametrize("spec_name,K,B,steps,chunk,nneg", [("vit_tiny", 3, 4, 2, 2, 1), ("vit_tiny_b32", 2, 32, 1, 0, 0),
+                                                            ("vit_full", 2, 4, 2, 0, 1)])
+def test_native_vit_bert_bit_identical_to_python_trainer(cuda, spec_name, K, B, steps, chunk, nneg):
+    from flr.models.multimodal import VIT_BERT, VIT_BERT_TINY
+    spec = VIT_BERT if spec_name == "vit_full" else VIT_BERT_TINY.__class__(**{**VIT_BERT_TINY.__dict__,
+                                                                              "dropout": 0.5})
+    glob = initial_global(spec, 42, cuda)
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    masks = make_dropout_masks(spec, steps, K, B, cuda, seed=5)
+    loss_py, X_py, norms_py = _vit_python(spec, glob, batches, masks, K, steps, chunk, nneg, cuda)
+    tr = nt.NativeRoundTrainer(spec, K, cuda, TrainConfig(local_steps=steps, client_chunk=chunk), batch=B)
+    assert tr.chunks == ClientBatchTrainer(spec, K, cuda, TrainConfig(local_steps=steps, client_chunk=chunk)).chunks
+    tr.load_global(glob)
+    loss = tr.local_update(batches, masks, negate_rows=nneg)
+    torch.cuda.synchronize()
+    X = tr.X.data[:, : tr.P]
+    assert torch.isfinite(X).all()
+    assert torch.equal(loss, loss_py), (loss, loss_py)
+    assert torch.equal(tr.norms, norms_py), (tr.norms, norms_py)
+    assert torch.equal(X, X_py), (X - X_py).abs().max()
+
+
+def test_native_vit_bert_matches_reference_loop(cuda):
+    """flr_train_vit_bert vs the oracle loop on one ViTBertNet per client (1e-5)."""
+    from flr.models.multimodal import VIT_BERT_TINY, model_class
+    spec = VIT_BERT_TINY.__class__(**{**VIT_BERT_TINY.__dict__, "dropout": 0.5})
+    K, B, steps = 3, 8, 3
+    glob = initial_global(spec, 42, cuda)
+    batches = synthetic_batches(spec, steps, range(K), B, cuda)
+    masks = make_dropout_masks(spec, steps, K, B, cuda, seed=4)
+    tr = nt.NativeRoundTrainer(spec, K, cuda, TrainConfig(local_steps=steps), batch=B)
+    tr.load_global(glob)
+    loss = tr.local_update(batches, masks).cpu()
+    for k in range(K):
+        cb = [(im[k].cpu(), tk[k].cpu(), lb[k].cpu()) for im, tk, lb in batches]
+        upd, ref_loss = otrain.local_update(model_class(spec), spec, glob.cpu(), cb, masks=[m[k].cpu() for m in masks])
+        ref = torch.cat([u.reshape(-1) for u in upd])
+        got = tr.X.data[k, : tr.P].cpu()
+        err = ((got.double() - ref.double()).abs().max() / ref.abs().max()).item()
+        assert err < 1e-5, err
+        assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
