@@ -230,6 +230,27 @@ int flr_clip_sgd_step_blocked_src(float* const* x_blocks, const float* const* g_
                                   const double* extra_sq, int64_t n_extra, const float* x_src,
                                   const int64_t* src_offsets, float* norms_out, void* workspace,
                                   size_t workspace_bytes, void* stream);
+/* flr_clip_sgd_step_blocked_src in two phases, so the update can overlap
+ * other work (the native trainers run it on a side stream, parameter group by
+ * parameter group, under the next local step's forward):
+ *   FLR_SGD_PHASE_NORM   the clip norms and coefficients of ALL the blocks
+ *                        passed (per-client, into the workspace; norms_out);
+ *   FLR_SGD_PHASE_UPDATE the clip + momentum + parameter update of the blocks
+ *                        passed (any subset, any order), reading the
+ *                        coefficients a NORM phase left in the same workspace;
+ *   FLR_SGD_PHASE_ALL    both (= flr_clip_sgd_step_blocked_src).
+ * The update is elementwise: splitting it over calls changes no bit. */
+#define FLR_SGD_PHASE_NORM 1
+#define FLR_SGD_PHASE_UPDATE 2
+#define FLR_SGD_PHASE_ALL 3
+int flr_clip_sgd_step_phase(float* const* x_blocks, const float* const* g_blocks, float* const* m_blocks,
+                            const int64_t* block_numel, const int64_t* block_client_stride,
+                            int64_t nblocks, int64_t K, float lr, float momentum, float weight_decay,
+                            float max_norm, int first_step, float* x_out, const int64_t* out_offsets,
+                            int64_t out_ld, int64_t nneg, const uint8_t* block_normed,
+                            const double* extra_sq, int64_t n_extra, const float* x_src,
+                            const int64_t* src_offsets, float* norms_out, int phase, void* workspace,
+                            size_t workspace_bytes, void* stream);
 
 /* ---- a2: client-batched 2-D convolution (bias-free, as in the conv blocks)
  * Replaces nn.Conv2d forward/backward for every client of a GPU at once

@@ -1,0 +1,61 @@
+// A per-device side stream and its events, for the native trainers' overlap of
+// one local step's optimizer update (HBM-bound) with the next step's forward
+// (MFMA / latency-bound): the update runs on the side stream parameter group
+// by parameter group, each group's event recorded after it, and the forward
+// waits on a group's event before its first use of those parameters.  Every
+// side-stream branch is joined back into the caller's stream within the same
+// call, so the entry points stay stream-ordered and capturable in a HIP graph
+// (fork / join through events is how a capture spans two streams).
+//
+// The stream and events are created once per device, outside any capture
+// (flr_*_workspace queries create them; a call that finds none while its
+// stream is capturing runs the update on the caller's stream instead — same
+// results, no overlap).  FLR_SGD_OVERLAP=0 turns the overlap off (A/B timing).
+#pragma once
+
+#include <cstdlib>
+#include <mutex>
+
+#include "flr_common.h"
+
+namespace flr {
+
+struct SideStream {
+  static constexpr int NEV = 48;
+  hipStream_t s = nullptr;
+  hipEvent_t ev[NEV] = {};
+};
+
+inline bool side_overlap_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FLR_SGD_OVERLAP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// The current device's side stream; created on first use when create is set
+// (never during a capture of `st`).  nullptr: none (or overlap disabled).
+inline SideStream* side_stream(bool create, hipStream_t st = nullptr) {
+  if (!side_overlap_enabled()) return nullptr;
+  static SideStream pool[64];
+  static bool made[64] = {};
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (made[dev]) return &pool[dev];
+  if (!create) return nullptr;
+  if (st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  }
+  SideStream& ss = pool[dev];
+  if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  for (int i = 0; i < SideStream::NEV; ++i)
+    if (hipEventCreateWithFlags(&ss.ev[i], hipEventDisableTiming) != hipSuccess) return nullptr;
+  made[dev] = true;
+  return &ss;
+}
+
+}  // namespace flr

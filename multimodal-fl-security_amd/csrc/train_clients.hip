@@ -17,6 +17,7 @@
 // every activation of a step, and the kernels' scratch.  The schedule is laid
 // out once by a dry run (Net with base == nullptr) that only sums sizes.
 #include "flr_common.h"
+#include "side_stream.h"
 
 #include <algorithm>
 #include <cstring>
@@ -176,6 +177,23 @@ class Net {
       p.off = P_;
       P_ += p.n;
     }
+    // forward segments and the parameters each needs first (side-stream optimizer
+    // groups, side_stream.h): the stem, every residual block, the text branch, the head
+    gthr_.clear();
+    gthr_.push_back(std::max({pc1, pbw, pbb}) + 1);
+    for (const auto& bk : blocks_) {
+      int m = std::max({bk.c1.p, bk.b1.pg, bk.b1.pb, bk.c2.p, bk.b2.pg, bk.b2.pb});
+      if (bk.has_ds) m = std::max({m, bk.ds.p, bk.bds.pg, bk.bds.pb});
+      gthr_.push_back(std::max(m + 1, gthr_.back()));
+    }
+    gthr_.push_back(std::max({p_emb_, p_wih_, p_whh_, p_bih_, p_bhh_}) + 1);
+    gthr_.push_back((int)ps_.size());
+    gtext_ = (int)gthr_.size() - 2;
+    ghead_ = (int)gthr_.size() - 1;
+    gorder_.assign(1, gtext_);
+    for (int g = 0; g < gtext_; ++g) gorder_.push_back(g);
+    gorder_.push_back(ghead_);
+    if ((int)gthr_.size() + 1 > SideStream::NEV) return FLR_ERR_UNSUPPORTED;
     // tap-major convs and their dead taps (flr.train.ClientBatchTrainer)
     mark_conv(stem_);
     for (auto& bk : blocks_) {
@@ -428,24 +446,11 @@ class Net {
     hipLaunchKernelGGL(permute_images_kernel, dim3(grid_for(K_ * B_ * C0 * HW0)), dim3(THREADS), 0, st, images,
                        ximg_, K_, B_, C0, HW0);
     FLR_TRY(launch_status("train_clients: images"));
-    FLR_TRY(conv_fwd(stem_, ximg_, y0_, st));
-    FLR_TRY(bn_fwd(stem_bn_, y0_, nullptr, a0_, true, st));
-    FLR_TRY(flr_maxpool2d_fwd(a0_, p0_, arg0_, K_ * s.widths[0] * B_, Hs_, Hs_, 3, 3, 2, 1, st));
-    for (auto& bk : blocks_) {
-      const float* idt = bk.x_in;
-      if (bk.has_ds) {
-        FLR_TRY(conv_fwd(bk.ds, bk.x_in, bk.yd, st));
-        FLR_TRY(bn_fwd(bk.bds, bk.yd, nullptr, bk.ad, false, st));
-        idt = bk.ad;
-      }
-      FLR_TRY(conv_fwd(bk.c1, bk.x_in, bk.y1, st));
-      FLR_TRY(bn_fwd(bk.b1, bk.y1, nullptr, bk.a1, true, st));
-      FLR_TRY(conv_fwd(bk.c2, bk.a1, bk.y2, st));
-      FLR_TRY(bn_fwd(bk.b2, bk.y2, idt, bk.out, true, st));
-    }
-    const float* x4 = blocks_.back().out;  // [K][Dimg][B]: img[k][b][c] = x4[k][c][b]
+    // the text branch first: its recurrence is latency-bound, so the previous step's
+    // side-stream update of the trunk (HBM-bound) runs under it (side_stream.h)
     const Param &emb = ps_[p_emb_], &wih = ps_[p_wih_], &whh = ps_[p_whh_], &bih = ps_[p_bih_],
                 &bhh = ps_[p_bhh_], &w1 = ps_[p_w1_], &b1 = ps_[p_b1_], &w2 = ps_[p_w2_], &b2 = ps_[p_b2_];
+    FLR_TRY(wait_group(gtext_, st));
     FLR_TRY(flr_embedding_fwd(emb.w, s.vocab * E_, s.vocab, tokens, N, nullptr, 0, 0, nullptr, 0, nullptr, 0, 0,
                               nullptr, 0, K_, N, E_, emb_, st));
     const int64_t H3 = 3 * H_;
@@ -466,9 +471,30 @@ class Net {
         FLR_TRY(flr_gru_fwd_step(gi_, gh_, hseq_, gates_, K_, B_, T_, H_, t, st));
       }
     }
+    int seg = 0;  // the previous step's update of each trunk segment's parameters (side stream)
+    FLR_TRY(wait_group(seg++, st));
+    FLR_TRY(conv_fwd(stem_, ximg_, y0_, st));
+    FLR_TRY(bn_fwd(stem_bn_, y0_, nullptr, a0_, true, st));
+    FLR_TRY(flr_maxpool2d_fwd(a0_, p0_, arg0_, K_ * s.widths[0] * B_, Hs_, Hs_, 3, 3, 2, 1, st));
+    for (auto& bk : blocks_) {
+      const float* idt = bk.x_in;
+      FLR_TRY(wait_group(seg++, st));
+      if (bk.has_ds) {
+        FLR_TRY(conv_fwd(bk.ds, bk.x_in, bk.yd, st));
+        FLR_TRY(bn_fwd(bk.bds, bk.yd, nullptr, bk.ad, false, st));
+        idt = bk.ad;
+      }
+      FLR_TRY(conv_fwd(bk.c1, bk.x_in, bk.y1, st));
+      FLR_TRY(bn_fwd(bk.b1, bk.y1, nullptr, bk.a1, true, st));
+      FLR_TRY(conv_fwd(bk.c2, bk.a1, bk.y2, st));
+      FLR_TRY(bn_fwd(bk.b2, bk.y2, idt, bk.out, true, st));
+    }
+    const float* x4 = blocks_.back().out;  // [K][Dimg][B]: img[k][b][c] = x4[k][c][b]
     const float* hT = hseq_ + T_ * B_ * H_;  // [K][B][H] at client stride (T+1)*B*H
     const int64_t hk = (T_ + 1) * B_ * H_, DI = Dimg_ + H_;
     // fc1 over the column blocks [img | h] (never concatenated), ReLU + dropout mask in the epilogue
+    FLR_TRY(wait_group(ghead_, st));
+    pending_ = false;  // every side-stream update of the previous step is joined
     FLR_TRY(flr_bgemm_ex(x4, Dimg_ * B_, 1, B_, w1.w, F_ * DI, DI, 1, h1_, B_ * F_, F_, 1, b1.w, F_, nullptr,
                          FLR_ACT_NONE, nullptr, nullptr, nullptr, K_, B_, F_, Dimg_, gws_, gws_n_, st));
     FLR_TRY(flr_bgemm_ex(hT, hk, H_, 1, w1.w + Dimg_, F_ * DI, DI, 1, h1_, B_ * F_, F_, 1, nullptr, 0, h1_,
@@ -570,13 +596,55 @@ class Net {
     const bool src = first && gshared_;
     if (src)
       for (const auto& b : blocks_opt_) soffs.push_back(ps_[b.j].tap ? ps_[b.j].off + b.o : -1);
-    FLR_TRY(flr_clip_sgd_step_blocked_src(xb.data(), gb.data(), mb.data(), nb.data(), cs.data(), (int64_t)xb.size(),
-                                          K_, lr, mom, wd_, clip_, int(first) | (int(last) << 1),
-                                          last ? xout_ : nullptr, last && xout_ ? xoffs.data() : nullptr, xld_,
-                                          xneg_, fuse ? normed.data() : nullptr, fuse ? sq_ : nullptr,
-                                          fuse ? nsq_ : 0, src ? gshared_ : nullptr, src ? soffs.data() : nullptr,
-                                          norms_, sgd_ws_, sgd_ws_n_, st));
+    const int flags = int(first) | (int(last) << 1);
+    if (last || !side_) {  // the last step writes X: nothing after it in the call to overlap
+      FLR_TRY(flr_clip_sgd_step_blocked_src(xb.data(), gb.data(), mb.data(), nb.data(), cs.data(),
+                                            (int64_t)xb.size(), K_, lr, mom, wd_, clip_, flags, last ? xout_ : nullptr,
+                                            last && xout_ ? xoffs.data() : nullptr, xld_, xneg_,
+                                            fuse ? normed.data() : nullptr, fuse ? sq_ : nullptr, fuse ? nsq_ : 0,
+                                            src ? gshared_ : nullptr, src ? soffs.data() : nullptr, norms_, sgd_ws_,
+                                            sgd_ws_n_, st));
+      return FLR_OK;
+    }
+    // the clip norms on this stream; the update on the side stream, one launch per
+    // forward segment's parameter group, each followed by its event (wait_group)
+    FLR_TRY(flr_clip_sgd_step_phase(xb.data(), gb.data(), mb.data(), nb.data(), cs.data(), (int64_t)xb.size(), K_, lr,
+                                    mom, wd_, clip_, flags, nullptr, nullptr, 0, 0, fuse ? normed.data() : nullptr,
+                                    fuse ? sq_ : nullptr, fuse ? nsq_ : 0, nullptr, nullptr, norms_,
+                                    FLR_SGD_PHASE_NORM, sgd_ws_, sgd_ws_n_, st));
+    const int ng = (int)gthr_.size();
+    hipEvent_t fork = side_->ev[ng];
+    if (hipEventRecord(fork, st) != hipSuccess || hipStreamWaitEvent(side_->s, fork, 0) != hipSuccess)
+      return launch_status("train_clients: side-stream fork");
+    // group g = the blocks of parameters [gthr_[g-1], gthr_[g]); launched in forward order
+    // (text branch, stem, residual blocks, head), each followed by its event
+    size_t nlaunched = 0;
+    for (int g : gorder_) {
+      const int jlo = g ? gthr_[g - 1] : 0;
+      size_t i0 = 0;
+      while (i0 < blocks_opt_.size() && blocks_opt_[i0].j < jlo) ++i0;
+      size_t i1 = i0;
+      while (i1 < blocks_opt_.size() && blocks_opt_[i1].j < gthr_[g]) ++i1;
+      nlaunched += i1 - i0;
+      if (i1 > i0) {
+        auto sub = [&](auto& v) { return v.data() + i0; };
+        FLR_TRY(flr_clip_sgd_step_phase(sub(xb), sub(gb), sub(mb), sub(nb), sub(cs), (int64_t)(i1 - i0), K_, lr, mom,
+                                        wd_, clip_, flags, nullptr, nullptr, 0, 0, nullptr, nullptr, 0,
+                                        src ? gshared_ : nullptr, src ? sub(soffs) : nullptr, nullptr,
+                                        FLR_SGD_PHASE_UPDATE, sgd_ws_, sgd_ws_n_, side_->s));
+      }
+      if (hipEventRecord(side_->ev[g], side_->s) != hipSuccess) return launch_status("train_clients: side-stream event");
+    }
+    if (nlaunched != blocks_opt_.size()) return FLR_ERR_ARG;  // a block outside every group: parameters out of order
+    pending_ = true;
 #undef FLR_TRY
+    return FLR_OK;
+  }
+
+  // the forward's wait for the previous step's side-stream update of group g
+  int wait_group(int g, hipStream_t st) {
+    if (!pending_) return FLR_OK;
+    if (hipStreamWaitEvent(st, side_->ev[g], 0) != hipSuccess) return launch_status("train_clients: side-stream join");
     return FLR_OK;
   }
 
@@ -741,6 +809,13 @@ class Net {
   int64_t T_ = 0, H_ = 0, E_ = 0, F_ = 0, C_ = 0, Dimg_ = 0, P_ = 0, Hs_ = 0, Hp_ = 0, nsq_ = 0;
   int p_emb_ = 0, p_wih_ = 0, p_whh_ = 0, p_bih_ = 0, p_bhh_ = 0, p_w1_ = 0, p_b1_ = 0, p_w2_ = 0, p_b2_ = 0;
   double* sq_ = nullptr;
+  std::vector<int> gthr_;  // optimizer group g: parameters [gthr_[g-1], gthr_[g]) (forward segments)
+  std::vector<int> gorder_;  // the groups in forward order: text branch, stem, residual blocks, head
+  int gtext_ = 0, ghead_ = 0;
+ public:
+  SideStream* side_ = nullptr;  // the optimizer's side stream (nullptr: the update runs on the caller's stream)
+ private:
+  bool pending_ = false;        // a side-stream update the next forward must wait for
   char *sgd_ws_ = nullptr, *gws_ = nullptr, *rws_ = nullptr, *ews_ = nullptr, *cws_ = nullptr;
   size_t sgd_ws_n_ = 0, gws_n_ = 0, rws_n_ = 0, ews_n_ = 0, cws_n_ = 0;
   float *ximg_ = nullptr, *y0_ = nullptr, *a0_ = nullptr, *d_a0_ = nullptr, *d_y0_ = nullptr, *p0_ = nullptr,
@@ -767,6 +842,7 @@ extern "C" int64_t flr_resnet_gru_num_params(const flr_resnet_gru_spec* spec) {
 extern "C" size_t flr_train_clients_workspace(const flr_resnet_gru_spec* spec, int64_t K, int64_t B,
                                               int64_t steps) {
   if (!spec || K < 1 || B < 1 || steps < 1) return 0;
+  side_stream(true);  // created here, before any capture of the training call
   tc::Net net(*spec, K, B, 0.f, 1.f, nullptr);
   if (net.layout() != FLR_OK) return 0;
   return align_up(net.bytes(), 256) + align_up((size_t)steps * K * sizeof(float), 256) + 256;
@@ -810,6 +886,7 @@ extern "C" int flr_train_clients_ex(const flr_resnet_gru_spec* spec, const float
   net.shared_first_ = shared_first;
   const bool train_order = (flags & FLR_TC_TRAIN_ORDER) != 0;
   hipStream_t st = as_stream(stream);
+  net.side_ = side_stream(true, st);
   if (train_order) {
     net.xout_ = X;
     net.xld_ = ld;

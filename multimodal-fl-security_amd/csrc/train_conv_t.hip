@@ -1610,16 +1610,40 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
 // ---- the split-at-stash form (FLR_GEMM=stash) ------------------------------
 // Each value is split into bf16 hi/mid/lo ONCE, by the thread that loaded it,
 // instead of once per wave that reads its fragment: the LDS holds three bf16
-// images per sub-tile, [64 rows][SB] with the row stride 80 B (20 dwords =
-// 4 x odd: conflict-free ds_read_b128 / ds_write_b128), and an MFMA fragment is
-// one ds_read_b128 per term.  The loads are k-contiguous (thread: row tid & 63,
+// images per sub-tile, [64 rows][32 k] with the four 16-B k-chunks of a row
+// XOR-swizzled by zswz(row) (no padding: conflict-free ds_read_b128 fragment
+// reads and ds_write_b128 stashes under both stash mappings, checked
+// exhaustively over the lane groups), and an MFMA fragment is one
+// ds_read_b128 per term.  48 KB per 128 x 128 tile, so three workgroups fit a
+// CU's LDS (the padded 80-B rows took 61 KB: two).  The loads are k-contiguous (thread: row tid & 63,
 // k 8 (tid >> 6) .. +7, the plans' init8 / load_a8 / load_b8), so a thread's
 // stash is three 16-B writes per sub-tile.  Single LDS buffer, two barriers
 // per K-tile; the split of tile t+1 sits between tile t's MFMAs.  Every
 // accumulator sees the same bf16 products in the same order as the other
 // bf16x6 forms: the results are bit-identical to them.
-constexpr int SB = 40;            // bf16 per image row (32 + 8 pad)
+#ifndef FLR_LDS_SWZ
+#define FLR_LDS_SWZ 1
+#endif
+#if FLR_LDS_SWZ
+constexpr int SB = 32;            // bf16 per image row (chunks swizzled, no pad)
+#else
+constexpr int SB = 40;            // bf16 per image row (32 + 8 pad; A/B build)
+#endif
 constexpr int TERM_B = 64 * SB;   // bf16 per term image
+// bf16 offset of (row, k-chunk c = k / 8) in a row-major term image
+__device__ __forceinline__ int zimg(int row, int c) {
+#if FLR_LDS_SWZ
+  const int f = ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 1);
+  return row * SB + 8 * (c ^ f);
+#else
+  return row * SB + 8 * c;
+#endif
+}
+// waves per SIMD the split-at-stash kernels are compiled for (FLR_SG_OCC=3: at
+// most 168 VGPRs, three 128 x 128 workgroups per CU)
+#ifndef FLR_SG_OCC
+#define FLR_SG_OCC 2
+#endif
 template <class P> struct has_k8 : std::false_type {};
 template <> struct has_k8<FwdT> : std::true_type {};
 template <> struct has_k8<DgradT> : std::true_type {};
@@ -1628,10 +1652,14 @@ template <> struct has_k8<DgradT> : std::true_type {};
 // cache line per lane): l1 wgrad 202 -> 366 us measured.
 template <int A, int B> struct has_k8<BGemm<A, B>> : std::true_type {};
 
+// Two LDS stages (one barrier per K-tile, tile t+1 stashed into the other stage
+// during tile t's MFMAs, one workgroup per CU by LDS) were measured 20-35 %
+// slower than this one-stage form at two workgroups per CU (C3 conv and C4
+// GEMM shapes, profiles/r3_sgemm_db.txt).
 template <class Plan, int MS, int NS, int D>
-__global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S, float* __restrict__ part,
-                                                            int remap) {
-  __shared__ __attribute__((aligned(16))) __bf16 Ls[MS + NS][3][TERM_B];
+__device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restrict__ part, int remap) {
+  constexpr int NST = 1;
+  __shared__ __attribute__((aligned(16))) __bf16 Ls[NST][MS + NS][3][TERM_B];
   int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
   if (remap) xcd_tile(bx, by, bz);
   const int k = bz / S, split = bz % S;
@@ -1678,17 +1706,19 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
 #pragma unroll
     for (int j = 0; j < NS; ++j) split3(rb[Q][j], pb[j][0], pb[j][1], pb[j][2]);
   };
-  auto write_all = [&]() {
+  auto write_all = [&](auto stc) {
+    constexpr int ST = decltype(stc)::value;
 #pragma unroll
     for (int i = 0; i < MS; ++i)
 #pragma unroll
-      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[i][t][srowA * SB + skA]) = pa[i][t];
+      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[ST][i][t][zimg(srowA, skA >> 3)]) = pa[i][t];
 #pragma unroll
     for (int j = 0; j < NS; ++j)
 #pragma unroll
-      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[MS + j][t][srowB * SB + skB]) = pb[j][t];
+      for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[ST][MS + j][t][zimg(srowB, skB >> 3)]) = pb[j][t];
   };
-  auto compute_tile = [&]() {
+  auto compute_tile = [&](auto stc) {
+      constexpr int ST = decltype(stc)::value;
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
         bf16x8 fa[MS][3], fb[NS][3];
@@ -1697,12 +1727,12 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
         for (int i = 0; i < MS; ++i)
 #pragma unroll
           for (int q = 0; q < 3; ++q)
-            fa[i][q] = *reinterpret_cast<const bf16x8*>(&Ls[i][q][(32 * wm + l32) * SB + ko]);
+            fa[i][q] = *reinterpret_cast<const bf16x8*>(&Ls[ST][i][q][zimg(32 * wm + l32, ko >> 3)]);
 #pragma unroll
         for (int j = 0; j < NS; ++j)
 #pragma unroll
           for (int q = 0; q < 3; ++q)
-            fb[j][q] = *reinterpret_cast<const bf16x8*>(&Ls[MS + j][q][(32 * wn + l32) * SB + ko]);
+            fb[j][q] = *reinterpret_cast<const bf16x8*>(&Ls[ST][MS + j][q][zimg(32 * wn + l32, ko >> 3)]);
 #define FLR_SX(TA, TB)                                                                              \
   _Pragma("unroll") for (int i = 0; i < MS; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
       acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][TA], fb[j][TB], acc[i][j], 0, 0, 0);
@@ -1718,29 +1748,31 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
     const int rlast = rbeg + (ntile - 1) * BK;
     load(rbeg, Q0{});
     split_all(Q0{});
-    write_all();
+    write_all(Q0{});
     load(std::min(rbeg + BK, rlast), Q0{});
     if constexpr (D == 3) load(std::min(rbeg + 2 * BK, rlast), Q1{});
     __syncthreads();
-    // one K-tile: the MFMAs of tile t from the LDS images, the split of tile t+1
-    // (register set Q) between them, its stash, then the global loads of tile
-    // t+D-1 into the set just freed (clamped past the last tile: duplicates)
-    auto tile_body = [&](int t, auto qc) {
-      const int r0 = rbeg + t * BK;
-      compute_tile();
-      split_all(qc);
-      __syncthreads();  // every wave's fragment reads of tile t are done
-      write_all();
-      load(std::min(r0 + D * BK, rlast), qc);
-      __syncthreads();
-    };
-    if constexpr (D == 3) {
-      for (int t = 0; t < ntile; t += 2) {
-        tile_body(t, Q0{});
-        if (t + 1 < ntile) tile_body(t + 1, Q1{});
+    {
+      // one K-tile: the MFMAs of tile t from the LDS images, the split of tile t+1
+      // (register set Q) between them, its stash, then the global loads of tile
+      // t+D-1 into the set just freed (clamped past the last tile: duplicates)
+      auto tile_body = [&](int t, auto qc) {
+        const int r0 = rbeg + t * BK;
+        compute_tile(Q0{});
+        split_all(qc);
+        __syncthreads();  // every wave's fragment reads of tile t are done
+        write_all(Q0{});
+        load(std::min(r0 + D * BK, rlast), qc);
+        __syncthreads();
+      };
+      if constexpr (D == 3) {
+        for (int t = 0; t < ntile; t += 2) {
+          tile_body(t, Q0{});
+          if (t + 1 < ntile) tile_body(t + 1, Q1{});
+        }
+      } else {
+        for (int t = 0; t < ntile; ++t) tile_body(t, Q0{});
       }
-    } else {
-      for (int t = 0; t < ntile; ++t) tile_body(t, Q0{});
     }
   }
   // C/D map of the 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
@@ -1813,6 +1845,12 @@ __global__ __launch_bounds__(THREADS, 2) void sgemm_kernel(const Plan pl, int S,
     }
 }
 
+template <class Plan, int MS, int NS, int D>
+__global__ __launch_bounds__(THREADS, FLR_SG_OCC) void sgemm_kernel(const Plan pl, int S, float* __restrict__ part,
+                                                                     int remap) {
+  sgemm_body<Plan, MS, NS, D>(pl, S, part, remap);
+}
+
 // ---- the weight gradient on split-at-stash images, transposed ----------------
 // Both operands of dW are contiguous along the reduction (pixels), so the loads
 // put a half-wave on 32 consecutive pixels of one channel (coalesced) and each
@@ -1828,7 +1866,7 @@ __host__ __device__ constexpr int tswz(int k) { return (k & 3) | ((((k >> 1) ^ (
 constexpr int TIMG = 32 * 64;  // bf16 per transposed term image
 
 template <class Plan, int MS, int NS, int D, bool TA, bool TB>
-__global__ __launch_bounds__(THREADS, 2) void wsgemm_kernel(const Plan pl, int S, float* __restrict__ part,
+__global__ __launch_bounds__(THREADS, FLR_SG_OCC) void wsgemm_kernel(const Plan pl, int S, float* __restrict__ part,
                                                             int remap) {
   // a term image: transposed [32 k][64 rows] (TIMG) or row-major [64 rows][SB] (TERM_B)
   constexpr int IMG = (TA || TB) && !(TA && TB) ? TERM_B : (TA ? TIMG : TERM_B);
@@ -1913,12 +1951,12 @@ __global__ __launch_bounds__(THREADS, 2) void wsgemm_kernel(const Plan pl, int S
     for (int i = 0; i < MS; ++i)
 #pragma unroll
       for (int t = 0; t < 3; ++t)
-        *reinterpret_cast<bf16x8*>(&Lt[i][t][TA ? sidx : srowA * SB + skA]) = pa[i][t];
+        *reinterpret_cast<bf16x8*>(&Lt[i][t][TA ? sidx : zimg(srowA, skA >> 3)]) = pa[i][t];
 #pragma unroll
     for (int j = 0; j < NS; ++j)
 #pragma unroll
       for (int t = 0; t < 3; ++t)
-        *reinterpret_cast<bf16x8*>(&Lt[MS + j][t][TB ? sidx : srowB * SB + skB]) = pb[j][t];
+        *reinterpret_cast<bf16x8*>(&Lt[MS + j][t][TB ? sidx : zimg(srowB, skB >> 3)]) = pb[j][t];
   };
   auto tread = [&](const __bf16* img, const int (&off)[2], int s) -> bf16x8 {
     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -1937,14 +1975,14 @@ __global__ __launch_bounds__(THREADS, 2) void wsgemm_kernel(const Plan pl, int S
 #pragma unroll
           for (int q = 0; q < 3; ++q) {
             if constexpr (TA) fa[i][q] = tread(Lt[i][q], ra_off, s);
-            else fa[i][q] = *reinterpret_cast<const bf16x8*>(&Lt[i][q][(32 * wm + l32) * SB + 16 * s + 8 * h]);
+            else fa[i][q] = *reinterpret_cast<const bf16x8*>(&Lt[i][q][zimg(32 * wm + l32, 2 * s + h)]);
           }
 #pragma unroll
         for (int j = 0; j < NS; ++j)
 #pragma unroll
           for (int q = 0; q < 3; ++q) {
             if constexpr (TB) fb[j][q] = tread(Lt[MS + j][q], rb_off, s);
-            else fb[j][q] = *reinterpret_cast<const bf16x8*>(&Lt[MS + j][q][(32 * wn + l32) * SB + 16 * s + 8 * h]);
+            else fb[j][q] = *reinterpret_cast<const bf16x8*>(&Lt[MS + j][q][zimg(32 * wn + l32, 2 * s + h)]);
           }
 #define FLR_SX(TA, TB)                                                                              \
   _Pragma("unroll") for (int i = 0; i < MS; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \

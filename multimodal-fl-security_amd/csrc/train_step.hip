@@ -262,7 +262,8 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
   const float nlr = -lr;
   const bool redirect = last && xout != nullptr;
   const float sg = (redirect && k < nneg) ? -1.f : 1.f;
-  const int64_t p0 = P * b / NSGD, p1 = P * (b + 1) / NSGD;
+  const int64_t nsgd = gridDim.x;  // NSGD, or fewer for a small parameter group
+  const int64_t p0 = P * b / nsgd, p1 = P * (b + 1) / nsgd;
   auto upd = [&](float xp, float gr, float mp, float& mo, float& xo) {
     float gp = gr * c;
     if (wd != 0.0f) gp = __builtin_fmaf(wd, xp, gp);
@@ -427,6 +428,21 @@ extern "C" int flr_clip_sgd_step_blocked_src(float* const* x_blocks, const float
                                              const uint8_t* block_normed, const double* extra_sq, int64_t n_extra,
                                              const float* x_src, const int64_t* src_offsets, float* norms_out,
                                              void* workspace, size_t workspace_bytes, void* stream) {
+  return flr_clip_sgd_step_phase(x_blocks, g_blocks, m_blocks, block_numel, block_client_stride, nblocks, K, lr,
+                                 momentum, weight_decay, max_norm, first_step, x_out, out_offsets, out_ld, nneg,
+                                 block_normed, extra_sq, n_extra, x_src, src_offsets, norms_out, FLR_SGD_PHASE_ALL,
+                                 workspace, workspace_bytes, stream);
+}
+
+extern "C" int flr_clip_sgd_step_phase(float* const* x_blocks, const float* const* g_blocks, float* const* m_blocks,
+                                       const int64_t* block_numel, const int64_t* block_client_stride,
+                                       int64_t nblocks, int64_t K, float lr, float momentum, float weight_decay,
+                                       float max_norm, int first_step, float* x_out, const int64_t* out_offsets,
+                                       int64_t out_ld, int64_t nneg, const uint8_t* block_normed,
+                                       const double* extra_sq, int64_t n_extra, const float* x_src,
+                                       const int64_t* src_offsets, float* norms_out, int phase, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
+  if (phase < FLR_SGD_PHASE_NORM || phase > FLR_SGD_PHASE_ALL) return FLR_ERR_ARG;
   if (n_extra < 0 || (n_extra > 0 && !extra_sq)) return FLR_ERR_ARG;
   // the first step's shared parameter source: block j at x_src + src_offsets[j] (< 0: none)
   const float* xsrc = (first_step & 1) ? x_src : nullptr;
@@ -511,9 +527,11 @@ extern "C" int flr_clip_sgd_step_blocked_src(float* const* x_blocks, const float
   float* coef = nullptr;
   int rc;
   if (max_norm > 0) {
-    double* partial = static_cast<double*>(workspace);
     coef = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                     align_up((size_t)train::MAX_PARTS * K * train::NBLK * sizeof(double), 256));
+  }
+  if (max_norm > 0 && (phase & FLR_SGD_PHASE_NORM)) {
+    double* partial = static_cast<double*>(workspace);
     for (int c = 0; c < nsq; ++c) {
       hipLaunchKernelGGL(train::sumsq_blocked_kernel, dim3(train::NBLK, (unsigned)K), dim3(train::THREADS), 0, st,
                          sqt[c], sqt[c].pre[sqt[c].nb], partial + (int64_t)c * K * train::NBLK);
@@ -527,6 +545,7 @@ extern "C" int flr_clip_sgd_step_blocked_src(float* const* x_blocks, const float
                          coef, norms_out, nsq);
     if ((rc = launch_status("clip_coef_kernel")) != FLR_OK) return rc;
   }
+  if (!(phase & FLR_SGD_PHASE_UPDATE)) return FLR_OK;
   static const int unroll = [] {
     const char* e = getenv("FLR_SGD_U");
     const int u = e ? atoi(e) : 0;
@@ -535,7 +554,11 @@ extern "C" int flr_clip_sgd_step_blocked_src(float* const* x_blocks, const float
   for (int c = 0; c < nparts; ++c) {
     auto kern = unroll == 8 ? train::sgd_blocked_kernel<8>
                             : (unroll == 4 ? train::sgd_blocked_kernel<4> : train::sgd_blocked_kernel<2>);
-    hipLaunchKernelGGL(kern, dim3(train::NSGD, (unsigned)K), dim3(train::THREADS), 0, st, tbs[c],
+    // workgroups per client: NSGD, fewer for a small group (each takes >= 8192 elements: one
+    // iteration of the 8-deep float4 loop); the update is elementwise, so the split changes nothing
+    const int64_t pc = tbs[c].pre[tbs[c].nb];
+    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(train::NSGD, (pc + 8191) / 8192));
+    hipLaunchKernelGGL(kern, dim3(gx, (unsigned)K), dim3(train::THREADS), 0, st, tbs[c],
                        tbs[c].pre[tbs[c].nb], coef, lr, momentum, weight_decay, first_step & 3, xout, out_ld,
                        (int)std::min<int64_t>(nneg, K), xsrc);
     if ((rc = launch_status("sgd_blocked_kernel")) != FLR_OK) return rc;

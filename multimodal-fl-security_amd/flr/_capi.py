@@ -70,6 +70,10 @@ SIGNATURES = {
                                              ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _int,
                                              _c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64,
                                              _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "flr_clip_sgd_step_phase": (_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
+                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _int,
+                                       _c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64,
+                                       _c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _size_t, _c_void_p]),
     "flr_conv2d_workspace": (_size_t, [_i64] * 10),
     "flr_resnet_gru_num_params": (_i64, [_c_void_p]),
     "flr_train_clients_workspace": (_size_t, [_c_void_p, _i64, _i64, _i64]),
