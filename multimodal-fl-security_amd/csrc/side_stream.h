@@ -10,7 +10,14 @@
 // The stream and events are created once per device, outside any capture
 // (flr_*_workspace queries create them; a call that finds none while its
 // stream is capturing runs the update on the caller's stream instead — same
-// results, no overlap).  FLR_SGD_OVERLAP=0 turns the overlap off (A/B timing).
+// results, no overlap).
+//
+// Off by default (FLR_SGD_OVERLAP=1 turns it on).  Measured at C3 on MI355X
+// (tools/gpu_r3_k.sh, gpu_r3_l.sh): 79 % of the optimizer's kernel time does
+// run concurrently with the forward's kernels, but both slow down by as much
+// (summed kernel time 59.3 -> 69.1 ms per round) and the round time is
+// unchanged (61.6 vs 61.8-62.2 ms); a side stream created with a priority
+// (either end of the range) made the round 50 % slower.
 #pragma once
 
 #include <cstdlib>
@@ -29,7 +36,7 @@ struct SideStream {
 inline bool side_overlap_enabled() {
   static const bool on = [] {
     const char* e = getenv("FLR_SGD_OVERLAP");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
