@@ -334,7 +334,10 @@ int flr_conv2d_bwd_data_t(const float* dy, const float* w_t, float* dx, int64_t 
 /* dx = dgrad + add (one rounding per element; add in dx's layout, NULL: none):
  * the residual block's two input-gradient paths summed in the dgrad epilogue,
  * the value autograd's accumulation of the conv path and the shortcut path
- * gives (the reference's BasicBlock backward, torchvision resnet18). */
+ * gives (the reference's BasicBlock backward, torchvision resnet18).  add may
+ * be dx itself (in-place accumulation, dx += dgrad): the stride-parity classes
+ * no kernel tap reaches are then skipped (a strided 1x1 shortcut writes only
+ * its one class instead of zeros over the other three). */
 int flr_conv2d_bwd_data_t_add(const float* dy, const float* w_t, const float* add,
                               float* dx, int64_t K, int64_t B, int64_t Cin, int64_t H,
                               int64_t W, int64_t Cout, int64_t KH, int64_t KW,

@@ -62,7 +62,7 @@ constexpr int RHDR = 1 + RMAX;              // refine header: count, row list (a
 constexpr int RBLK = RHDR + RMAX * RMAX;    // fp64 per slice: header + [RMAX][RMAX] sums
 constexpr int PREC = 2 + RMAX;              // pivot record (int32): pivot, count, rows
 constexpr double COND_FLAG = 16.0;
-constexpr int RSEG_MAX = 64;                // refine segments per slice
+constexpr int RSEG_MAX = 160;               // refine segments per slice (x 8 slices: 1280 workgroups, ~5 per CU)
 constexpr int MAXK_PIVOT = 1024;
 
 template <int I, int N, typename F>
@@ -421,14 +421,25 @@ __global__ void reduce_splits_kernel(const double* __restrict__ stage1, int nrec
 
 // ---- refine: exact differences for the flagged rows (see COND_FLAG) ----
 // grid (nseg, 3 block pairs (0,0) (0,1) (1,1) of the row list, slices).  Each
-// workgroup sums (x_i - x_j)^2 over its segment of the slice's chunks: fp32
-// within a 64-coordinate chunk, fp64 across chunks.
+// workgroup sums (x_i - x_j)^2 over its segment of the slice's chunks for the
+// 32 x 32 pairs of its block pair.  The 32 rows of each block are staged per
+// 64-coordinate chunk in LDS ([row][64 + 4]: conflict-free ds_read_b128 under
+// the lane map below); a diagonal block pair stages them once and reads both
+// operands from that image.  Wave w takes coordinates 16w .. 16w+15 of every
+// chunk; lane (bi = lane >> 3, bj = lane & 7) the 4 x 4 pairs (bi + 8u, bj + 8v),
+// reading 4-coordinate runs of its 8 rows as float4 (two LDS reads per 4 pairs
+// per coordinate pair of rows, instead of four scalar reads per 4 pairs):
+// fp32 sums over the 16 coordinates, fp64 across chunks, the four waves'
+// partials added in wave order at the end.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr int RPAD = CW + 4;
 __global__ __launch_bounds__(256) void refine_partials_kernel(const float* __restrict__ X, int64_t ldx,
                                                               int64_t nch_total, int q_base, int64_t chunk0,
                                                               const int* __restrict__ prec, int nseg,
                                                               double* __restrict__ rpart) {
-  __shared__ float A[32][CW + 1];
-  __shared__ float B[32][CW + 1];
+  __shared__ __attribute__((aligned(16))) float A[32][RPAD];
+  __shared__ __attribute__((aligned(16))) float B[32][RPAD];
+  __shared__ double red[1024];
   const int c = prec[1];
   const int pr = blockIdx.y;
   const int a = pr == 2 ? 1 : 0, b = pr == 0 ? 0 : 1;
@@ -437,47 +448,97 @@ __global__ __launch_bounds__(256) void refine_partials_kernel(const float* __res
   const int q = q_base + (int)blockIdx.z;
   const int64_t s0 = slice_chunk(nch_total, q) - chunk0, s1 = slice_chunk(nch_total, q + 1) - chunk0;
   const int64_t c_begin = s0 + (s1 - s0) * seg / nseg, c_end = s0 + (s1 - s0) * (seg + 1) / nseg;
-  const int tid = threadIdx.x;
-  const int ia = 2 * (tid >> 4), jb = 2 * (tid & 15);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int bi = lane >> 3, bj = lane & 7;
   // the 32 rows of each block this workgroup stages (positions past the count repeat row 0)
   const int rr = tid >> 3, cc0 = 8 * (tid & 7);
   const int pa = 32 * a + rr, pb = 32 * b + rr;
   const float* ra = X + (int64_t)prec[2 + (pa < c ? pa : 0)] * ldx;
   const float* rb = X + (int64_t)prec[2 + (pb < c ? pb : 0)] * ldx;
-  double d00 = 0.0, d01 = 0.0, d10 = 0.0, d11 = 0.0;
-  for (int64_t ch = c_begin; ch < c_end; ++ch) {
-    const int64_t p0 = ch * CW + cc0;
-    const f32x4 va0 = *reinterpret_cast<const f32x4*>(ra + p0), va1 = *reinterpret_cast<const f32x4*>(ra + p0 + 4);
-    const f32x4 vb0 = *reinterpret_cast<const f32x4*>(rb + p0), vb1 = *reinterpret_cast<const f32x4*>(rb + p0 + 4);
+  const bool diag = a == b;
+  const float(*Bi)[RPAD] = diag ? A : B;
+  double d[4][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      A[rr][cc0 + e] = va0[e];
-      A[rr][cc0 + 4 + e] = va1[e];
-      B[rr][cc0 + e] = vb0[e];
-      B[rr][cc0 + 4 + e] = vb1[e];
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) d[u][v] = 0.0;
+  // chunk ch+1's values are loaded into registers before chunk ch's compute
+  f32x4 na0 = {}, na1 = {}, nb0 = {}, nb1 = {};
+  auto fetch = [&](int64_t ch) {
+    const int64_t p0 = ch * CW + cc0;
+    na0 = *reinterpret_cast<const f32x4*>(ra + p0);
+    na1 = *reinterpret_cast<const f32x4*>(ra + p0 + 4);
+    if (!diag) {
+      nb0 = *reinterpret_cast<const f32x4*>(rb + p0);
+      nb1 = *reinterpret_cast<const f32x4*>(rb + p0 + 4);
+    }
+  };
+  if (c_begin < c_end) fetch(c_begin);
+  for (int64_t ch = c_begin; ch < c_end; ++ch) {
+    *reinterpret_cast<f32x4*>(&A[rr][cc0]) = na0;
+    *reinterpret_cast<f32x4*>(&A[rr][cc0 + 4]) = na1;
+    if (!diag) {
+      *reinterpret_cast<f32x4*>(&B[rr][cc0]) = nb0;
+      *reinterpret_cast<f32x4*>(&B[rr][cc0 + 4]) = nb1;
     }
     __syncthreads();
-    float s00 = 0.f, s01 = 0.f, s10 = 0.f, s11 = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < CW; ++k) {
-      const float a0 = A[ia][k], a1 = A[ia + 1][k], b0 = B[jb][k], b1 = B[jb + 1][k];
-      float d;
-      d = a0 - b0; s00 = __builtin_fmaf(d, d, s00);
-      d = a0 - b1; s01 = __builtin_fmaf(d, d, s01);
-      d = a1 - b0; s10 = __builtin_fmaf(d, d, s10);
-      d = a1 - b1; s11 = __builtin_fmaf(d, d, s11);
+    if (ch + 1 < c_end) fetch(ch + 1);
+    // pairs (u, 2w) and (u, 2w+1) share one packed accumulator: v_pk_add_f32 /
+    // v_pk_fma_f32 do both pairs' sub + fma, each pair's own fp32 chain unchanged
+    f32x2 sacc[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int w2 = 0; w2 < 2; ++w2) sacc[u][w2] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+      const int k = 16 * wave + 4 * k4;
+      f32x4 av[4], bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        av[u] = *reinterpret_cast<const f32x4*>(&A[bi + 8 * u][k]);
+        bv[u] = *reinterpret_cast<const f32x4*>(&Bi[bj + 8 * u][k]);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int w2 = 0; w2 < 2; ++w2) {
+            const f32x2 a2 = {av[u][e], av[u][e]};
+            const f32x2 b2 = {bv[2 * w2][e], bv[2 * w2 + 1][e]};
+            const f32x2 df = a2 - b2;
+            sacc[u][w2] = __builtin_elementwise_fma(df, df, sacc[u][w2]);
+          }
     }
-    d00 += (double)s00;
-    d01 += (double)s01;
-    d10 += (double)s10;
-    d11 += (double)s11;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) d[u][v] += (double)sacc[u][v >> 1][v & 1];
     __syncthreads();
   }
-  double* rec = rpart + (((int64_t)blockIdx.z * 3 + pr) * nseg + seg) * 1024;
-  rec[ia * 32 + jb] = d00;
-  rec[ia * 32 + jb + 1] = d01;
-  rec[(ia + 1) * 32 + jb] = d10;
-  rec[(ia + 1) * 32 + jb + 1] = d11;
+  // the four waves' partials, added in wave order (one 8-KB exchange per wave)
+  for (int w = 1; w < 4; ++w) {
+    if (wave == w)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) red[(bi + 8 * u) * 32 + bj + 8 * v] = d[u][v];
+    __syncthreads();
+    if (wave == 0)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) d[u][v] += red[(bi + 8 * u) * 32 + bj + 8 * v];
+    __syncthreads();
+  }
+  if (wave == 0) {
+    double* rec = rpart + (((int64_t)blockIdx.z * 3 + pr) * nseg + seg) * 1024;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) rec[(bi + 8 * u) * 32 + bj + 8 * v] = d[u][v];
+  }
 }
 
 // Per slice: the segments summed in order into the slice's refine block
@@ -495,7 +556,8 @@ __global__ __launch_bounds__(256) void refine_reduce_kernel(const double* __rest
   for (int e = threadIdx.x; e < 1024; e += 256) {
     const double* p = rpart + ((int64_t)z * 3 + pr) * nseg * 1024 + e;
     double s = 0.0;
-    for (int k = 0; k < nseg; ++k) s += p[(int64_t)k * 1024];
+#pragma unroll 16
+    for (int k = 0; k < nseg; ++k) s += p[(int64_t)k * 1024];  // independent loads, 16 in flight
     blk[RHDR + (32 * a + (e >> 5)) * RMAX + 32 * b + (e & 31)] = s;
   }
 }

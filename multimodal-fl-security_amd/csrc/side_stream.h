@@ -33,12 +33,9 @@ struct SideStream {
   hipEvent_t ev[NEV] = {};
 };
 
-inline bool side_overlap_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("FLR_SGD_OVERLAP");
-    return e && e[0] == '1';
-  }();
-  return on;
+inline bool side_overlap_enabled() {  // read per call: a test flips it within one process
+  const char* e = getenv("FLR_SGD_OVERLAP");
+  return e && e[0] == '1';
 }
 
 // The current device's side stream; created on first use when create is set

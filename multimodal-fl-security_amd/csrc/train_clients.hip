@@ -557,6 +557,14 @@ class Net {
       const float* other = bk.d_res;  // identity shortcut: the residual gradient itself
       if (bk.has_ds) {
         FLR_TRY(bn_bwd(bk.bds, bk.d_res, bk.yd, nullptr, false, bk.d_yd, nullptr, st));
+        if (ps_[bk.c1.p].tap && ps_[bk.ds.p].tap && fuse_res_) {
+          // d_in = dgrad(c1), then the strided 1x1 shortcut's dgrad added in place
+          // (its epilogue: dx = dgrad(ds) + dx, the same one fp32 add); the parity
+          // classes no shortcut tap reaches are skipped instead of written as zeros
+          FLR_TRY(conv_bwd(bk.c1, bk.x_in, bk.d_y1, bk.d_in, st));
+          FLR_TRY(conv_bwd(bk.ds, bk.x_in, bk.d_yd, bk.d_in, st, bk.d_in));
+          continue;
+        }
         FLR_TRY(conv_bwd(bk.ds, bk.x_in, bk.d_yd, bk.d_xd, st));
         other = bk.d_xd;
       }

@@ -2611,6 +2611,8 @@ extern "C" int flr_conv2d_bwd_data_t_ex(const float* dy, const float* w_t, int64
   convt::DgradT cls[convt::MAX_CLASSES];
   const int nc = convt::dgrad_classes(g, cls);
   for (int c = 0; c < nc; ++c) {
+    // in-place accumulation (add == dx): a class no tap reaches adds nothing
+    if (add == dx && cls[c].R() == 0) continue;
     cls[c].dy = dy; cls[c].w = w_t; cls[c].dx = dx; cls[c].add = add; cls[c].wsk = w_stride;
     const int rc = convt::launch(cls[c], ws, ws_bytes, as_stream(stream), "conv bwd data (tap-major)");
     if (rc != FLR_OK) return rc;

@@ -235,3 +235,9 @@ def test_dgrad_addend_bit_identical(cuda, shape, form, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(got, want)
 
+    # in place (add == dx): dx += dgrad, the classes no tap reaches left untouched
+    inplace = add.clone()
+    _capi.call("flr_conv2d_bwd_data_t_add", dy.data_ptr(), wt.data_ptr(), inplace.data_ptr(), inplace.data_ptr(),
+               *geom, wsp, nb, _stream(dy))
+    torch.cuda.synchronize()
+    assert torch.equal(inplace, want)

@@ -18,10 +18,16 @@ pytestmark = pytest.mark.gpu
 # c3_b128: batch 128 gives the 128 x 128 weight-gradient tiles a deeper split-K
 # than the smaller tiles (the workspace and the fused clip-norm slots
 # must follow the tile the launch takes)
-@pytest.mark.parametrize("spec_name,B,nneg", [("tiny", 4, 1), ("c3", 8, 1), ("c3_b40", 40, 0), ("c3_b128", 128, 0)])
-def test_native_trainer_bit_identical_to_python_trainer(cuda, spec_name, B, nneg):
+# c3_overlap: the optimizer update on the side stream under the next step's forward
+# (FLR_SGD_OVERLAP=1, side_stream.h), three steps so two updates overlap a forward
+@pytest.mark.parametrize("spec_name,B,nneg", [("tiny", 4, 1), ("c3", 8, 1), ("c3_b40", 40, 0), ("c3_b128", 128, 0),
+                                              ("c3_overlap", 8, 1)])
+def test_native_trainer_bit_identical_to_python_trainer(cuda, spec_name, B, nneg, monkeypatch):
     spec = TINY if spec_name == "tiny" else ModelSpec()
     K, steps = 3, 2
+    if spec_name == "c3_overlap":
+        monkeypatch.setenv("FLR_SGD_OVERLAP", "1")
+        steps = 3
     cfg = TrainConfig(local_steps=steps)
     glob = initial_global(spec, 42, cuda)
     batches = synthetic_batches(spec, steps, range(K), B, cuda)
