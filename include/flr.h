@@ -488,6 +488,23 @@ int flr_batchnorm_bwd(const float* dy, const float* x, const float* y,
                       const float* gamma, const float* mean, const float* invstd,
                       float* dx, float* dgamma, float* dbeta, float* dresidual,
                       int64_t B, int64_t KC, int64_t HW, int relu, void* stream);
+/* The ResNet stem's BatchNorm + ReLU + 3x3/2 pad-1 max-pool as one kernel each
+ * way (torchvision resnet18 stem: bn1 -> relu -> maxpool), per (client,
+ * channel) plane of NI images of H x W: the same values as flr_batchnorm_fwd
+ * (relu, no residual) followed by flr_maxpool2d_fwd, and as flr_maxpool2d_bwd
+ * followed by flr_batchnorm_bwd (relu; the mask recomputed from x, beta and
+ * the saved statistics), without the BN output / its gradient in HBM.
+ * y_pool / dy_pool: [KC][NI][H/2][W/2], argmax: 1-byte window offsets as
+ * flr_maxpool2d_fwd's.  Shapes: H = W = 16, NI = 16 or 32 (the stem at 32 x 32
+ * inputs, batch 16 / 32); else FLR_ERR_UNSUPPORTED (use the two-kernel form). */
+int flr_batchnorm_relu_maxpool_fwd(const float* x, const float* gamma, const float* beta,
+                                   float* y_pool, uint8_t* argmax, float* mean, float* invstd,
+                                   int64_t KC, int64_t NI, int64_t H, int64_t W, float eps,
+                                   void* stream);
+int flr_maxpool_relu_batchnorm_bwd(const float* dy_pool, const uint8_t* argmax, const float* x,
+                                   const float* gamma, const float* beta, const float* mean,
+                                   const float* invstd, float* dx, float* dgamma, float* dbeta,
+                                   int64_t KC, int64_t NI, int64_t H, int64_t W, void* stream);
 
 /* ---- a3 / a4: batched dense GEMM (text branch, late-fusion MLP) ------------
  * Replaces the nn.Linear / nn.GRU matrix products of the text branch and the

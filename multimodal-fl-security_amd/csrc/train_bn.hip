@@ -340,6 +340,179 @@ bool bwd_fast(const float* dy, const float* x, const float* y, const float* gamm
   return false;
 }
 
+// ---- the ResNet stem's BatchNorm + ReLU + 3x3/2/1 max-pool, fused -------------
+// One workgroup per (client, channel) plane of NI images of 16 x 16 (NI = 16 or
+// 32: the fast path's L = 256 lanes, V = NI / 4 float4s per lane; lane l's float4
+// i is image 4i + l/64, row (l/4) % 16, columns 4 (l % 4) .. +3).  Forward: the
+// fast kernel's BatchNorm + ReLU in registers, the activated plane staged in LDS,
+// the pool evaluated from LDS exactly as pool::fwd_kernel (first in-bounds max,
+// NaN wins, 1-byte argmax) — the BN output never goes to HBM.  Backward: the
+// pooled gradient and argmax staged in LDS, each lane gathers its four pixels'
+// gradients in window-raster order (pool::bwd_k3s2p1_kernel's order), the ReLU
+// mask recomputed from x (t = x alpha + shift > 0, the forward's arithmetic),
+// then bwd_fast_kernel's BatchNorm backward.  Bit-identical to the three-kernel
+// composition (flr_batchnorm_fwd + flr_maxpool2d_fwd, flr_maxpool2d_bwd +
+// flr_batchnorm_bwd) and two HBM round trips of the plane lighter each way.
+constexpr int SP_H = 16, SP_W = 16, SP_HO = 8, SP_WO = 8;
+
+template <int V>
+__global__ __launch_bounds__(THREADS) void stem_bn_pool_fwd_kernel(const float* __restrict__ x,
+                                                                   const float* __restrict__ gamma,
+                                                                   const float* __restrict__ beta,
+                                                                   float* __restrict__ yp, uint8_t* __restrict__ arg,
+                                                                   float* __restrict__ mean_out,
+                                                                   float* __restrict__ invstd_out, int KC, float eps) {
+  constexpr int L = 256, NI = 4 * V;
+  __shared__ float red[THREADS / 64];
+  __shared__ __attribute__((aligned(16))) float xs[NI * SP_H * SP_W];
+  const FastPlane<L, V> pl(KC);
+  const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+  f32x4 v[V];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    v[i] = pl.valid ? x4[pl.at(i)] : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  }
+  const float n = (float)(4 * L * V);
+  const float mean = plane_sum<L>(s, red) / n;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[i][e] - mean;
+      q += d * d;
+    }
+  const float var = plane_sum<L>(q, red) / n;
+  if (!pl.valid) return;  // one plane per workgroup: uniform
+  const float invstd = 1.0f / sqrtf(var + eps);
+  const float alpha = invstd * gamma[pl.kc];
+  const float shift = beta[pl.kc] - mean * alpha;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = fmaxf(v[i][e] * alpha + shift, 0.f);
+    reinterpret_cast<f32x4*>(xs)[i * L + pl.lane] = o;
+  }
+  if (pl.lane == 0) {
+    mean_out[pl.kc] = mean;
+    invstd_out[pl.kc] = invstd;
+  }
+  __syncthreads();
+  float* yb = yp + (int64_t)pl.kc * NI * SP_HO * SP_WO;
+  uint8_t* ab = arg + (int64_t)pl.kc * NI * SP_HO * SP_WO;
+  for (int o = threadIdx.x; o < NI * SP_HO * SP_WO; o += THREADS) {
+    const int b = o / (SP_HO * SP_WO), qq = o % (SP_HO * SP_WO);
+    const int oh = qq / SP_WO, ow = qq % SP_WO;
+    const float* xp = xs + b * SP_H * SP_W;
+    const int ih0 = 2 * oh - 1, iw0 = 2 * ow - 1;
+    float best = -__builtin_huge_valf();
+    int bi = -1;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = ih0 + kh;
+      if (ih < 0 || ih >= SP_H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = iw0 + kw;
+        if (iw < 0 || iw >= SP_W) continue;
+        const float val = xp[ih * SP_W + iw];
+        if (bi < 0) bi = kh * 3 + kw;  // torch's initial maxindex: the first in-bounds element
+        if (val > best || val != val) {
+          best = val;
+          bi = kh * 3 + kw;
+        }
+      }
+    }
+    yb[o] = best;
+    ab[o] = (uint8_t)bi;
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(THREADS) void stem_pool_bn_bwd_kernel(
+    const float* __restrict__ dyp, const uint8_t* __restrict__ arg, const float* __restrict__ x,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean_in,
+    const float* __restrict__ invstd_in, float* __restrict__ dx, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, int KC) {
+  constexpr int L = 256, NI = 4 * V, NO = NI * SP_HO * SP_WO;
+  __shared__ float red[THREADS / 64];
+  __shared__ __attribute__((aligned(16))) float ds[NO];
+  __shared__ __attribute__((aligned(16))) uint8_t as[NO];
+  const FastPlane<L, V> pl(KC);
+  if (!pl.valid) return;  // one plane per workgroup: uniform
+  const float* dyb = dyp + (int64_t)pl.kc * NO;
+  const uint8_t* ab = arg + (int64_t)pl.kc * NO;
+  for (int o = threadIdx.x; o < NO / 4; o += THREADS) {
+    reinterpret_cast<f32x4*>(ds)[o] = reinterpret_cast<const f32x4*>(dyb)[o];
+    reinterpret_cast<uint32_t*>(as)[o] = reinterpret_cast<const uint32_t*>(ab)[o];
+  }
+  __syncthreads();
+  const float mean = mean_in[pl.kc];
+  const float invstd = invstd_in[pl.kc];
+  const float alpha = invstd * gamma[pl.kc];
+  const float shift = beta[pl.kc] - mean * alpha;
+  const int r = (pl.lane >> 2) & 15, c0 = 4 * (pl.lane & 3);
+  const int m = r >> 1, dh = r & 1;
+  f32x4 g[V], xc[V];
+  float s = 0.f, d = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int b = 4 * i + (pl.lane >> 6);
+    const float* dp = ds + b * SP_HO * SP_WO;
+    const uint8_t* ap = as + b * SP_HO * SP_WO;
+    // this lane's four pixels: 2x2 blocks n = c0/2 and c0/2 + 1, row dh of each
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int nn = (c0 >> 1) + nb;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {  // windows in raster order
+        const int oh = m + (w >> 1), ow = nn + (w & 1);
+        if (oh >= SP_HO || ow >= SP_WO) continue;
+        const int a = ap[oh * SP_WO + ow];
+        const int kh = a / 3, kw = a - 3 * kh;
+        const int rh = 2 * oh - 1 + kh - 2 * m, rw = 2 * ow - 1 + kw - 2 * nn;  // argmax relative to the block
+        if (rh != dh || rw < 0 || rw > 1) continue;
+        acc[2 * nb + rw] = add_rn(acc[2 * nb + rw], dp[oh * SP_WO + ow]);
+      }
+    }
+    f32x4 xv = reinterpret_cast<const f32x4*>(x)[pl.at(i)];
+    f32x4 gv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float t = xv[e] * alpha + shift;  // the forward's pre-ReLU value
+      gv[e] = fmaxf(t, 0.f) > 0.f ? acc[e] : 0.f;
+      xv[e] = xv[e] - mean;
+      s += gv[e];
+      d += xv[e] * gv[e];
+    }
+    g[i] = gv;
+    xc[i] = xv;
+  }
+  s = plane_sum<L>(s, red);
+  d = plane_sum<L>(d, red);
+  const float n = (float)(4 * L * V);
+  const float kk = d * invstd * invstd / n;
+  const float mdy = s / n;
+  const float wscale = invstd * gamma[pl.kc];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (g[i][e] - mdy - xc[i][e] * kk) * wscale;
+    reinterpret_cast<f32x4*>(dx)[pl.at(i)] = o;
+  }
+  if (pl.lane == 0) {
+    dgamma[pl.kc] = d * invstd;
+    dbeta[pl.kc] = s;
+  }
+}
+
+inline bool stem_fused_ok(int64_t NI, int64_t H, int64_t W) { return H == SP_H && W == SP_W && (NI == 16 || NI == 32); }
+
 inline int seg_log2_of(int HW) {
   int l = 0;
   while (l < 6 && (1 << (l + 1)) <= HW) ++l;
@@ -411,4 +584,43 @@ extern "C" int flr_batchnorm_bwd(const float* dy, const float* x, const float* y
   else FLR_BN_BWD(false, false);
 #undef FLR_BN_BWD
   return launch_status("batchnorm bwd");
+}
+
+extern "C" int flr_batchnorm_relu_maxpool_fwd(const float* x, const float* gamma, const float* beta, float* y_pool,
+                                              uint8_t* argmax, float* mean, float* invstd, int64_t KC, int64_t NI,
+                                              int64_t H, int64_t W, float eps, void* stream) {
+  if (!x || !gamma || !beta || !y_pool || !argmax || !mean || !invstd || KC < 1 || NI < 1 ||
+      KC * NI * H * W >= ((int64_t)1 << 31))
+    return FLR_ERR_ARG;
+  if (!bn::stem_fused_ok(NI, H, W) || !bn::aligned16(x) || !bn::aligned16(y_pool) ||
+      (reinterpret_cast<uintptr_t>(argmax) & 3) != 0)
+    return FLR_ERR_UNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  if (NI == 32)
+    hipLaunchKernelGGL(bn::stem_bn_pool_fwd_kernel<8>, dim3((unsigned)KC), dim3(bn::THREADS), 0, st, x, gamma, beta,
+                       y_pool, argmax, mean, invstd, (int)KC, eps);
+  else
+    hipLaunchKernelGGL(bn::stem_bn_pool_fwd_kernel<4>, dim3((unsigned)KC), dim3(bn::THREADS), 0, st, x, gamma, beta,
+                       y_pool, argmax, mean, invstd, (int)KC, eps);
+  return launch_status("batchnorm + relu + maxpool fwd");
+}
+
+extern "C" int flr_maxpool_relu_batchnorm_bwd(const float* dy_pool, const uint8_t* argmax, const float* x,
+                                              const float* gamma, const float* beta, const float* mean,
+                                              const float* invstd, float* dx, float* dgamma, float* dbeta, int64_t KC,
+                                              int64_t NI, int64_t H, int64_t W, void* stream) {
+  if (!dy_pool || !argmax || !x || !gamma || !beta || !mean || !invstd || !dx || !dgamma || !dbeta || KC < 1 ||
+      NI < 1 || KC * NI * H * W >= ((int64_t)1 << 31))
+    return FLR_ERR_ARG;
+  if (!bn::stem_fused_ok(NI, H, W) || !bn::aligned16(x) || !bn::aligned16(dx) || !bn::aligned16(dy_pool) ||
+      (reinterpret_cast<uintptr_t>(argmax) & 3) != 0)
+    return FLR_ERR_UNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  if (NI == 32)
+    hipLaunchKernelGGL(bn::stem_pool_bn_bwd_kernel<8>, dim3((unsigned)KC), dim3(bn::THREADS), 0, st, dy_pool, argmax,
+                       x, gamma, beta, mean, invstd, dx, dgamma, dbeta, (int)KC);
+  else
+    hipLaunchKernelGGL(bn::stem_pool_bn_bwd_kernel<4>, dim3((unsigned)KC), dim3(bn::THREADS), 0, st, dy_pool, argmax,
+                       x, gamma, beta, mean, invstd, dx, dgamma, dbeta, (int)KC);
+  return launch_status("maxpool + relu + batchnorm bwd");
 }

@@ -135,6 +135,11 @@ class Net {
     Hs_ = stem_.Ho;
     stem_bn_ = BnOp{pbw, pbb, w0, B_ * Hs_ * Hs_};
     Hp_ = (Hs_ + 2 - 3) / 2 + 1;  // the 3x3/2/1 max pool
+    // the fused stem BN + ReLU + pool kernels' shapes (FLR_STEM_FUSED=0: the three-kernel form)
+    {
+      const char* e = getenv("FLR_STEM_FUSED");
+      stem_fused_ = !(e && e[0] == '0') && Hs_ == 16 && (B_ == 16 || B_ == 32);
+    }
     int64_t cin = w0, Hc = Hp_;
     for (int li = 0; li < 4; ++li) {
       const int64_t cout = s.widths[li];
@@ -474,8 +479,13 @@ class Net {
     int seg = 0;  // the previous step's update of each trunk segment's parameters (side stream)
     FLR_TRY(wait_group(seg++, st));
     FLR_TRY(conv_fwd(stem_, ximg_, y0_, st));
-    FLR_TRY(bn_fwd(stem_bn_, y0_, nullptr, a0_, true, st));
-    FLR_TRY(flr_maxpool2d_fwd(a0_, p0_, arg0_, K_ * s.widths[0] * B_, Hs_, Hs_, 3, 3, 2, 1, st));
+    if (stem_fused_) {  // bn1 + relu + maxpool in one pass: the BN output never reaches HBM
+      FLR_TRY(flr_batchnorm_relu_maxpool_fwd(y0_, ps_[stem_bn_.pg].w, ps_[stem_bn_.pb].w, p0_, arg0_, stem_bn_.mean,
+                                             stem_bn_.invstd, K_ * s.widths[0], B_, Hs_, Hs_, 1e-5f, st));
+    } else {
+      FLR_TRY(bn_fwd(stem_bn_, y0_, nullptr, a0_, true, st));
+      FLR_TRY(flr_maxpool2d_fwd(a0_, p0_, arg0_, K_ * s.widths[0] * B_, Hs_, Hs_, 3, 3, 2, 1, st));
+    }
     for (auto& bk : blocks_) {
       const float* idt = bk.x_in;
       FLR_TRY(wait_group(seg++, st));
@@ -579,8 +589,14 @@ class Net {
         FLR_TRY(launch_status("train_clients: gradient sum"));
       }
     }
-    FLR_TRY(flr_maxpool2d_bwd(d_p0_, arg0_, d_a0_, K_ * s.widths[0] * B_, Hs_, Hs_, 3, 3, 2, 1, st));
-    FLR_TRY(bn_bwd(stem_bn_, d_a0_, y0_, a0_, true, d_y0_, nullptr, st));
+    if (stem_fused_) {
+      FLR_TRY(flr_maxpool_relu_batchnorm_bwd(d_p0_, arg0_, y0_, ps_[stem_bn_.pg].w, ps_[stem_bn_.pb].w, stem_bn_.mean,
+                                             stem_bn_.invstd, d_y0_, ps_[stem_bn_.pg].g, ps_[stem_bn_.pb].g,
+                                             K_ * s.widths[0], B_, Hs_, Hs_, st));
+    } else {
+      FLR_TRY(flr_maxpool2d_bwd(d_p0_, arg0_, d_a0_, K_ * s.widths[0] * B_, Hs_, Hs_, 3, 3, 2, 1, st));
+      FLR_TRY(bn_bwd(stem_bn_, d_a0_, y0_, a0_, true, d_y0_, nullptr, st));
+    }
     FLR_TRY(conv_bwd(stem_, ximg_, d_y0_, nullptr, st));
     // ---------------- clip + SGD-momentum ----------------
     std::vector<float*> xb, mb;
@@ -822,6 +838,7 @@ class Net {
   int gtext_ = 0, ghead_ = 0;
  public:
   SideStream* side_ = nullptr;  // the optimizer's side stream (nullptr: the update runs on the caller's stream)
+  bool stem_fused_ = false;     // bn1 + relu + maxpool fused (flr_batchnorm_relu_maxpool_fwd / _bwd)
  private:
   bool pending_ = false;        // a side-stream update the next forward must wait for
   char *sgd_ws_ = nullptr, *gws_ = nullptr, *rws_ = nullptr, *ews_ = nullptr, *cws_ = nullptr;

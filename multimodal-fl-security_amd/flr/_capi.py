@@ -74,6 +74,8 @@ SIGNATURES = {
                                        ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _int,
                                        _c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64,
                                        _c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _size_t, _c_void_p]),
+    "flr_batchnorm_relu_maxpool_fwd": (_int, [_c_void_p] * 7 + [_i64] * 4 + [ctypes.c_float, _c_void_p]),
+    "flr_maxpool_relu_batchnorm_bwd": (_int, [_c_void_p] * 10 + [_i64] * 4 + [_c_void_p]),
     "flr_conv2d_workspace": (_size_t, [_i64] * 10),
     "flr_resnet_gru_num_params": (_i64, [_c_void_p]),
     "flr_train_clients_workspace": (_size_t, [_c_void_p, _i64, _i64, _i64]),

@@ -20,8 +20,9 @@ pytestmark = pytest.mark.gpu
 # must follow the tile the launch takes)
 # c3_overlap: the optimizer update on the side stream under the next step's forward
 # (FLR_SGD_OVERLAP=1, side_stream.h), three steps so two updates overlap a forward
-@pytest.mark.parametrize("spec_name,B,nneg", [("tiny", 4, 1), ("c3", 8, 1), ("c3_b40", 40, 0), ("c3_b128", 128, 0),
-                                              ("c3_overlap", 8, 1)])
+# c3_b32: batch 32 takes the fused stem BN + ReLU + max-pool kernels (flr_batchnorm_relu_maxpool_fwd / _bwd)
+@pytest.mark.parametrize("spec_name,B,nneg", [("tiny", 4, 1), ("c3", 8, 1), ("c3_b32", 32, 1), ("c3_b40", 40, 0),
+                                              ("c3_b128", 128, 0), ("c3_overlap", 8, 1)])
 def test_native_trainer_bit_identical_to_python_trainer(cuda, spec_name, B, nneg, monkeypatch):
     spec = TINY if spec_name == "tiny" else ModelSpec()
     K, steps = 3, 2
