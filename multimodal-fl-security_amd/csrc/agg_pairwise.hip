@@ -38,8 +38,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int CW = 64;          // coordinates per chunk = 256 B per row
 constexpr int THREADS = 256;    // 4 waves; wave w owns k-step w of the chunk
 constexpr int SUPER = 128;      // rows of a diagonal group (4 client blocks)
-constexpr int REC_TILES = 10;   // max tiles per group
-constexpr int REC_DIAG = 6 * 32;
+constexpr int REC_TILES = 16;   // max tiles per group (the K > 128 cross groups: 4 x 4)
+constexpr int REC_DIAG = 8 * 32;  // max rows per group
 constexpr int REC = REC_TILES * 1024 + REC_DIAG;   // floats per partial record
 constexpr int MAX_SEG = 512;
 // Gram workgroups per full call (all slices and groups): one round of the
@@ -78,17 +78,28 @@ __device__ __forceinline__ void static_for(F&& f) {
 // P = 3.3e7.  CROSS_NJ = 2 (NL = 4, 64 KB, two per CU, so one wave's bf16 split
 // can overlap the other's MFMAs) measured 67 ms: the extra split work (one block
 // per tile instead of 0.75) costs more than the overlap gains.
+//
+// Round 3: CROSS_NI = 4 (the default): all four blocks of I against the four of
+// J — one cross group per super-block pair, 16 tiles, NL = 8 (128 KB of LDS,
+// one workgroup per CU).  Each chunk's bf16 split per wave then feeds 64 MFMAs
+// per 8 blocks instead of 32 per 6, and the cross stage streams each pair's 256
+// rows once (4x the matrix over all groups, diagonal included) instead of
+// 5.5x.  FLR_GRAM_CROSS_NI=2 at build time: the 2 x 4 groups (A/B).
+#ifndef FLR_GRAM_CROSS_NI
+#define FLR_GRAM_CROSS_NI 4
+#endif
+constexpr int CROSS_NI = FLR_GRAM_CROSS_NI;
 constexpr int CROSS_NJ = 4;
-constexpr int CROSS_NL = 2 + CROSS_NJ;
-constexpr int CROSS_PER_PAIR = 2 * (4 / CROSS_NJ);  // cross groups per super-block pair
+constexpr int CROSS_NL = CROSS_NI + CROSS_NJ;
+constexpr int CROSS_PER_PAIR = (4 / CROSS_NI) * (4 / CROSS_NJ);  // cross groups per super-block pair
 
 // Tile enumeration.  DIAG: every (a <= b) over NL loaded blocks, a-major.
-// CROSS: a in {0,1} (rows of super-block I), b in {2..NL-1} (rows of J).
+// CROSS: a in {0..CROSS_NI-1} (rows of super-block I), b in {CROSS_NI..NL-1} (rows of J).
 template <int NL, bool CROSS>
 struct TileSet {
-  static constexpr int N = CROSS ? 2 * (NL - 2) : NL * (NL + 1) / 2;
+  static constexpr int N = CROSS ? CROSS_NI * (NL - CROSS_NI) : NL * (NL + 1) / 2;
   __host__ __device__ static constexpr int a(int t) {
-    if (CROSS) return t / (NL - 2);
+    if (CROSS) return t / (NL - CROSS_NI);
     int r = t;
     for (int i = 0; i < NL; ++i) {
       if (r < NL - i) return i;
@@ -97,7 +108,7 @@ struct TileSet {
     return -1;
   }
   __host__ __device__ static constexpr int b(int t) {
-    if (CROSS) return 2 + t % (NL - 2);
+    if (CROSS) return CROSS_NI + t % (NL - CROSS_NI);
     int r = t;
     for (int i = 0; i < NL; ++i) {
       if (r < NL - i) return i + r;
@@ -143,6 +154,19 @@ __device__ __forceinline__ void lds_read_blocks(uint32_t a0, uint32_t a1, f32x4 
                  : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[2][0]), "=&v"(v[2][1]),
                    "=&v"(v[3][0]), "=&v"(v[3][1])
                  : "v"(a0), "v"(a1) : "memory");
+  } else if constexpr (NL == 8) {
+    asm volatile("ds_read_b128 %0, %16\n\tds_read_b128 %1, %17\n\t"
+                 "ds_read_b128 %2, %16 offset:8192\n\tds_read_b128 %3, %17 offset:8192\n\t"
+                 "ds_read_b128 %4, %16 offset:16384\n\tds_read_b128 %5, %17 offset:16384\n\t"
+                 "ds_read_b128 %6, %16 offset:24576\n\tds_read_b128 %7, %17 offset:24576\n\t"
+                 "ds_read_b128 %8, %16 offset:32768\n\tds_read_b128 %9, %17 offset:32768\n\t"
+                 "ds_read_b128 %10, %16 offset:40960\n\tds_read_b128 %11, %17 offset:40960\n\t"
+                 "ds_read_b128 %12, %16 offset:49152\n\tds_read_b128 %13, %17 offset:49152\n\t"
+                 "ds_read_b128 %14, %16 offset:57344\n\tds_read_b128 %15, %17 offset:57344\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[2][0]), "=&v"(v[2][1]),
+                   "=&v"(v[3][0]), "=&v"(v[3][1]), "=&v"(v[4][0]), "=&v"(v[4][1]), "=&v"(v[5][0]), "=&v"(v[5][1]),
+                   "=&v"(v[6][0]), "=&v"(v[6][1]), "=&v"(v[7][0]), "=&v"(v[7][1])
+                 : "v"(a0), "v"(a1) : "memory");
   } else {
     static_assert(NL == 6, "unsupported block count");
     asm volatile("ds_read_b128 %0, %12\n\tds_read_b128 %1, %13\n\t"
@@ -158,7 +182,7 @@ __device__ __forceinline__ void lds_read_blocks(uint32_t a0, uint32_t a1, f32x4 
 }
 
 struct GroupDesc {
-  int blk[6];
+  int blk[8];
 };
 
 // Group -> list of global client blocks it loads.
@@ -166,13 +190,13 @@ __device__ __forceinline__ GroupDesc group_desc(int g, int K, bool cross) {
   GroupDesc d;
   const int nb = cdiv(K, 32);
   if (K <= SUPER) {
-    for (int i = 0; i < 6; ++i) d.blk[i] = i;
+    for (int i = 0; i < 8; ++i) d.blk[i] = i;
     (void)nb;
     return d;
   }
   const int nsb = cdiv(K, SUPER);
   if (!cross) {
-    for (int i = 0; i < 6; ++i) d.blk[i] = 4 * g + i;
+    for (int i = 0; i < 8; ++i) d.blk[i] = 4 * g + i;
     return d;
   }
   const int q = (g - nsb) / CROSS_PER_PAIR, w = (g - nsb) % CROSS_PER_PAIR;
@@ -180,9 +204,8 @@ __device__ __forceinline__ GroupDesc group_desc(int g, int K, bool cross) {
   int I = 0, rem = q;
   while (rem >= nsb - 1 - I) { rem -= nsb - 1 - I; ++I; }
   const int J = I + 1 + rem;
-  d.blk[0] = 4 * I + 2 * hi;
-  d.blk[1] = 4 * I + 2 * hi + 1;
-  for (int i = 0; i < CROSS_NJ; ++i) d.blk[2 + i] = 4 * J + CROSS_NJ * hj + i;
+  for (int i = 0; i < CROSS_NI; ++i) d.blk[i] = 4 * I + CROSS_NI * hi + i;
+  for (int i = 0; i < CROSS_NJ; ++i) d.blk[CROSS_NI + i] = 4 * J + CROSS_NJ * hj + i;
   return d;
 }
 
@@ -648,9 +671,9 @@ __global__ void assemble_kernel(const double* __restrict__ gsum, int ngroups, in
       int q = 0;
       for (int a = 0; a < I; ++a) q += nsb - 1 - a;
       q += J - I - 1;
-      g = nsb + CROSS_PER_PAIR * q + (bi >> 1) * (4 / CROSS_NJ) + bj / CROSS_NJ;
-      lb_i = bi & 1;
-      lb_j = 2 + bj % CROSS_NJ;
+      g = nsb + CROSS_PER_PAIR * q + (bi / CROSS_NI) * (4 / CROSS_NJ) + bj / CROSS_NJ;
+      lb_i = bi % CROSS_NI;
+      lb_j = CROSS_NI + bj % CROSS_NJ;
       t = lb_i * CROSS_NJ + bj % CROSS_NJ;
     }
   }
