@@ -204,13 +204,19 @@ __device__ __forceinline__ float bload1(rsrc_t r, bool ok, int64_t off) {
 
 // forward step t: gh = h_t W_hh^T + b_hh for the units [j0, j0+32) of all three
 // gates, then the gate math of fwd_step_kernel for those units.
-template <bool V8, int NW, int G>
-__global__ __launch_bounds__(64 * NW) void fwd_fused_kernel(const float* __restrict__ gi,
+// SEQ: the waves' partial sums added in wave order through ONE LDS slot (wave w
+// adds its partials to the slot in turn: the same sums in the same order as
+// the NW-slot form, bit-identical), 12 KB instead of 96 KB of LDS, and the
+// kernel held to 128 VGPRs, so two workgroups share a CU and one's W_hh
+// stream overlaps the other's reduction and gate math (the NW-slot form runs
+// one workgroup per CU: 1024 workgroups in four serial rounds at C3).
+template <bool V8, int NW, int G, bool SEQ = false>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(SEQ ? 4 : 1))) void fwd_fused_kernel(const float* __restrict__ gi,
                                                             const float* __restrict__ whhP,
                                                             const float* __restrict__ bhh, float* __restrict__ hseq,
                                                             float* __restrict__ gates, const Dims d, int nub) {
   constexpr int EPT = 16 / NW;  // epilogue elements per thread
-  __shared__ float red[NW][3][16][64];
+  __shared__ float red[SEQ ? 1 : NW][3][16][64];
   int k, ub;
   block_coords(nub, k, ub);
   const int j0 = ub * 32;
@@ -223,19 +229,24 @@ __global__ __launch_bounds__(64 * NW) void fwd_fused_kernel(const float* __restr
   const rsrc_t rbias = make_rsrc(bhh + (int64_t)k * 3 * H, (int64_t)3 * H);
   // epilogue operands: element p = tid + 64 NW i -> (e, ln) of the MFMA tile
   float pgi[EPT][3], php[EPT], pbh[EPT][3];
+  auto load_epi = [&]() {
 #pragma unroll
-  for (int i = 0; i < EPT; ++i) {
-    const int p = threadIdx.x + 64 * NW * i, e = p >> 6, ln = p & 63;
-    const int b = (e & 3) + 8 * (e >> 2) + 4 * (ln >> 5), j = j0 + (ln & 31);
-    const bool ok = b < B && j < H;
-    const int64_t go = ((int64_t)b * d.T + d.t) * 3 * H + j;
+    for (int i = 0; i < EPT; ++i) {
+      const int p = threadIdx.x + 64 * NW * i, e = p >> 6, ln = p & 63;
+      const int b = (e & 3) + 8 * (e >> 2) + 4 * (ln >> 5), j = j0 + (ln & 31);
+      const bool ok = b < B && j < H;
+      const int64_t go = ((int64_t)b * d.T + d.t) * 3 * H + j;
 #pragma unroll
-    for (int g = 0; g < 3; ++g) {
-      pgi[i][g] = bload1(rg, ok, go + g * H);
-      pbh[i][g] = bload1(rbias, ok, g * H + j);
+      for (int g = 0; g < 3; ++g) {
+        pgi[i][g] = bload1(rg, ok, go + g * H);
+        pbh[i][g] = bload1(rbias, ok, g * H + j);
+      }
+      php[i] = bload1(rh, ok, (int64_t)b * H + j);
     }
-    php[i] = bload1(rh, ok, (int64_t)b * H + j);
-  }
+  };
+  // SEQ: the epilogue operands are loaded after the MFMAs (their latency under the
+  // ordered reduction), keeping them out of the loads' register peak
+  if constexpr (!SEQ) load_epi();
   const bool aok = l32 < B;
   f32x16 acc[3];
 #pragma unroll
@@ -266,11 +277,23 @@ __global__ __launch_bounds__(64 * NW) void fwd_fused_kernel(const float* __restr
       }
     }
   }
+  if constexpr (SEQ) {
+    load_epi();
+    for (int w = 0; w < NW; ++w) {
+      if (wave == w)
 #pragma unroll
-  for (int g = 0; g < 3; ++g)
+        for (int g = 0; g < 3; ++g)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) red[wave][g][e][lane] = acc[g][e];
-  __syncthreads();
+          for (int e = 0; e < 16; ++e) red[0][g][e][lane] = w == 0 ? acc[g][e] : red[0][g][e][lane] + acc[g][e];
+      __syncthreads();
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) red[wave][g][e][lane] = acc[g][e];
+    __syncthreads();
+  }
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int p = threadIdx.x + 64 * NW * i, e = p >> 6, ln = p & 63;
@@ -280,8 +303,9 @@ __global__ __launch_bounds__(64 * NW) void fwd_fused_kernel(const float* __restr
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
       float x = red[0][g][e][ln];
+      if constexpr (!SEQ)
 #pragma unroll
-      for (int w = 1; w < NW; ++w) x += red[w][g][e][ln];
+        for (int w = 1; w < NW; ++w) x += red[w][g][e][ln];
       v[g] = x;
     }
     const int64_t hrw = (((int64_t)k * (d.T + 1) + d.t) * B + b) * H;
@@ -301,14 +325,14 @@ __global__ __launch_bounds__(64 * NW) void fwd_fused_kernel(const float* __restr
 // backward step t >= 1: dh_t = dh_direct + dgh_t W_hh for the units [i0, i0+32)
 // (W_hh^T rows), then the element backward of step t - 1 for those units
 // (d.t = t - 1).  dh_direct is read and rewritten in place by the same thread.
-template <bool V8, int NW, int G>
-__global__ __launch_bounds__(64 * NW) void bwd_fused_kernel(const float* __restrict__ whhTP,
+template <bool V8, int NW, int G, bool SEQ = false>  // SEQ: as fwd_fused_kernel's
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(SEQ ? 6 : 1))) void bwd_fused_kernel(const float* __restrict__ whhTP,
                                                             const float* __restrict__ gates,
                                                             const float* __restrict__ hseq, float* __restrict__ dgh,
                                                             float* __restrict__ dgi, float* __restrict__ dh_direct,
                                                             float* __restrict__ dh0, const Dims d, int nub) {
   constexpr int EPT = 16 / NW;
-  __shared__ float red[NW][16][64];
+  __shared__ float red[SEQ ? 1 : NW][16][64];
   int k, ub;
   block_coords(nub, k, ub);
   const int i0 = ub * 32;
@@ -325,16 +349,19 @@ __global__ __launch_bounds__(64 * NW) void bwd_fused_kernel(const float* __restr
   const rsrc_t rgt = make_rsrc(gates + ((int64_t)k * d.T + tg) * B * 4 * H, (int64_t)B * 4 * H);
   const rsrc_t rhp = make_rsrc(hseq + ((int64_t)k * (d.T + 1) + tg) * B * H, (int64_t)B * H);
   float pdd[EPT], pg[EPT][4], php[EPT];
+  auto load_epi = [&]() {
 #pragma unroll
-  for (int i = 0; i < EPT; ++i) {
-    const int p = threadIdx.x + 64 * NW * i, e = p >> 6, ln = p & 63;
-    const int b = (e & 3) + 8 * (e >> 2) + 4 * (ln >> 5), j = i0 + (ln & 31);
-    const bool ok = b < B && j < H;
-    pdd[i] = bload1(rdd, ok, (int64_t)b * H + j);
+    for (int i = 0; i < EPT; ++i) {
+      const int p = threadIdx.x + 64 * NW * i, e = p >> 6, ln = p & 63;
+      const int b = (e & 3) + 8 * (e >> 2) + 4 * (ln >> 5), j = i0 + (ln & 31);
+      const bool ok = b < B && j < H;
+      pdd[i] = bload1(rdd, ok, (int64_t)b * H + j);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) pg[i][q] = bload1(rgt, ok && elem, (int64_t)b * 4 * H + q * H + j);
-    php[i] = bload1(rhp, ok && elem, (int64_t)b * H + j);
-  }
+      for (int q = 0; q < 4; ++q) pg[i][q] = bload1(rgt, ok && elem, (int64_t)b * 4 * H + q * H + j);
+      php[i] = bload1(rhp, ok && elem, (int64_t)b * H + j);
+    }
+  };
+  if constexpr (!SEQ) load_epi();
   const bool aok = l32 < B;
   f32x16 acc;
 #pragma unroll
@@ -358,17 +385,28 @@ __global__ __launch_bounds__(64 * NW) void bwd_fused_kernel(const float* __restr
       acc = mfma6(ah, am, al, bh, bm, bl, acc);
     }
   }
+  if constexpr (SEQ) {
+    load_epi();
+    for (int w = 0; w < NW; ++w) {
+      if (wave == w)
 #pragma unroll
-  for (int e = 0; e < 16; ++e) red[wave][e][lane] = acc[e];
-  __syncthreads();
+        for (int e = 0; e < 16; ++e) red[0][e][lane] = w == 0 ? acc[e] : red[0][e][lane] + acc[e];
+      __syncthreads();
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[wave][e][lane] = acc[e];
+    __syncthreads();
+  }
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int p = threadIdx.x + 64 * NW * i, e = p >> 6, ln = p & 63;
     const int b = (e & 3) + 8 * (e >> 2) + 4 * (ln >> 5), j = i0 + (ln & 31);
     if (b >= B || j >= H) continue;
     float x = red[0][e][ln];
+    if constexpr (!SEQ)
 #pragma unroll
-    for (int w = 1; w < NW; ++w) x += red[w][e][ln];
+      for (int w = 1; w < NW; ++w) x += red[w][e][ln];
     const int64_t kb = (int64_t)k * B + b;
     const int64_t idx = kb * H + j;
     const float dy = pdd[i] + x;  // dL/dh_t
@@ -460,10 +498,10 @@ namespace gru {
 // (waves per workgroup, k-steps per load group); FLR_GRU_FW / FLR_GRU_BW = "NW,G" for A/B timing
 // (tools/gru_bench.py); default 8 waves x 2 k-steps for both (C3: fwd 29 us, bwd 27 us per step)
 inline int cfg_index(const char* env, int dflt) {
-  static const char* names[] = {"4,4", "8,2", "2,8", "", "8,6", "4,12", "16,3", ""};
+  static const char* names[] = {"4,4", "8,2", "2,8", "8,2s", "8,6", "4,12", "16,3", "", "8,2s"};
   const char* v = getenv(env);
   if (v)
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 9; ++i)
         if (names[i][0] && !strcmp(v, names[i])) return i;
   return dflt;
 }
@@ -473,6 +511,7 @@ inline void launch_fwd(int cfg, dim3 grid, hipStream_t st, const float* gi, cons
   switch (cfg) {
     case 0: hipLaunchKernelGGL((fwd_fused_kernel<V8, 4, 4>), grid, dim3(256), 0, st, gi, whh, bhh, hseq, gates, d, nub); break;
     case 2: hipLaunchKernelGGL((fwd_fused_kernel<V8, 2, 8>), grid, dim3(128), 0, st, gi, whh, bhh, hseq, gates, d, nub); break;
+    case 3: hipLaunchKernelGGL((fwd_fused_kernel<V8, 8, 1, true>), grid, dim3(512), 0, st, gi, whh, bhh, hseq, gates, d, nub); break;
     default: hipLaunchKernelGGL((fwd_fused_kernel<V8, 8, 2>), grid, dim3(512), 0, st, gi, whh, bhh, hseq, gates, d, nub);
   }
 }
@@ -483,6 +522,7 @@ inline void launch_bwd(int cfg, dim3 grid, hipStream_t st, const float* whhT, co
     case 5: hipLaunchKernelGGL((bwd_fused_kernel<V8, 4, 12>), grid, dim3(256), 0, st, whhT, gates, hseq, dgh, dgi, dh_direct, dh0, d, nub); break;
     case 6: hipLaunchKernelGGL((bwd_fused_kernel<V8, 16, 3>), grid, dim3(1024), 0, st, whhT, gates, hseq, dgh, dgi, dh_direct, dh0, d, nub); break;
     case 4: hipLaunchKernelGGL((bwd_fused_kernel<V8, 8, 6>), grid, dim3(512), 0, st, whhT, gates, hseq, dgh, dgi, dh_direct, dh0, d, nub); break;
+    case 3: hipLaunchKernelGGL((bwd_fused_kernel<V8, 8, 2, true>), grid, dim3(512), 0, st, whhT, gates, hseq, dgh, dgi, dh_direct, dh0, d, nub); break;
     default: hipLaunchKernelGGL((bwd_fused_kernel<V8, 8, 2>), grid, dim3(512), 0, st, whhT, gates, hseq, dgh, dgi, dh_direct, dh0, d, nub);
   }
 }

@@ -17,7 +17,7 @@ namespace flr {
 namespace train {
 
 constexpr int THREADS = 256;
-constexpr int NBLK = 128;  // norm partial blocks per client row
+constexpr int NBLK = 32;   // norm partial blocks per client row (>= 8 float4 per lane at C3's unfused blocks)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -187,17 +187,36 @@ __global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable
     const int64_t hi = p1 < tb.pre[j + 1] ? p1 : tb.pre[j + 1];
     if (lo >= hi || (tb.vec[j] & 2)) continue;
     const float* g = tb.g[j] + (int64_t)k * tb.cs[j] - tb.pre[j];
-    visit_range(
-        lo, hi, tb.pre[j], (tb.vec[j] & 1) != 0,
-        [&](int64_t e) {
-          const double v = (double)g[e];
-          acc += v * v;
-        },
-        [&](int64_t e) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(g + e);
+    auto f1 = [&](int64_t e) {
+      const double v = (double)g[e];
+      acc += v * v;
+    };
+    if (!(tb.vec[j] & 1)) {
+      for (int64_t e = lo + threadIdx.x; e < hi; e += THREADS) f1(e);
+      continue;
+    }
+    // visit_range's order, with 8 float4 loads in flight per lane before they are summed
+    const int64_t pre = tb.pre[j];
+    int64_t vlo = pre + ((lo - pre + 3) & ~(int64_t)3);
+    if (vlo > hi) vlo = hi;
+    const int64_t vhi = pre + ((hi - pre) & ~(int64_t)3);
+    for (int64_t e = lo + threadIdx.x; e < vlo; e += THREADS) f1(e);
+    int64_t e = vlo + 4 * (int64_t)threadIdx.x;
+    for (; e + 7 * 4 * THREADS < vhi; e += 8 * 4 * THREADS) {
+      f32x4 v[8];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) acc += (double)v[q] * (double)v[q];
-        });
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(g + e + u * 4 * THREADS);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc += (double)v[u][q] * (double)v[u][q];
+    }
+    for (; e < vhi; e += 4 * THREADS) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(g + e);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc += (double)v[q] * (double)v[q];
+    }
+    for (int64_t t = (vhi > vlo ? vhi : vlo) + threadIdx.x; t < hi; t += THREADS) f1(t);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);

@@ -17,6 +17,7 @@ def main():
     from flr.nn import _gru_packed
     whhP, whhT = r(K, _gru_packed(3, H, H)), r(K, _gru_packed(1, H, 3 * H))
     dgh, dgi, dd = r(K, T, B, 3 * H), r(K, B, T, 3 * H), r(K, B, H)
+    dd0 = dd.clone()
     lib = _capi.lib()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     P = lambda x: ctypes.c_void_p(x.data_ptr())
@@ -40,12 +41,23 @@ def main():
     for name, fn in [("pack W_hh", pack), ("pack W_hh^T", packT)]:
         us = timeit(fn)
         print(f"{name:12s} {us:8.2f} us  {2 * wbytes / us / 1e6:6.2f} TB/s (read + write)", flush=True)
+    outs = {"fwd": lambda: (hseq[:, 6].clone(), gates[:, 5].clone()),
+            "bwd": lambda: (dgh[:, 5].clone(), dgi[:, :, 5].clone(), dd.clone())}
     for var, env, fn in [("fwd", "FLR_GRU_FW", fwd), ("bwd", "FLR_GRU_BW", bwd)]:
-        cfgs = ["4,4", "8,2", "2,8"] if var == "fwd" else ["8,6", "4,12", "16,3", "8,2"]
+        cfgs = ["8,2", "8,2s", "4,4", "2,8"] if var == "fwd" else ["8,2", "8,2s", "8,6", "4,12", "16,3"]
+        ref = None
         for c in cfgs:
             os.environ[env] = c
+            if var == "bwd":
+                dd.copy_(dd0)  # the bwd step rewrites dh_direct in place: same input for every variant
+            assert fn() == 0
+            torch.cuda.synchronize()
+            o = outs[var]()
+            same = "" if ref is None else ("  bit-identical" if all(torch.equal(a, b) for a, b in zip(o, ref))
+                                            else "  DIFFERS")
+            ref = ref if ref is not None else o
             us = timeit(fn)
-            print(f"{var} NW,G={c:5s} {us:8.2f} us  W_hh stream {wbytes / us / 1e6:6.2f} TB/s", flush=True)
+            print(f"{var} NW,G={c:5s} {us:8.2f} us  W_hh stream {wbytes / us / 1e6:6.2f} TB/s{same}", flush=True)
         os.environ.pop(env)
 
 
