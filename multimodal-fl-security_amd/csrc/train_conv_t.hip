@@ -1656,7 +1656,13 @@ template <int A, int B> struct has_k8<BGemm<A, B>> : std::true_type {};
 // during tile t's MFMAs, one workgroup per CU by LDS) were measured 20-35 %
 // slower than this one-stage form at two workgroups per CU (C3 conv and C4
 // GEMM shapes, profiles/r3_sgemm_db.txt).
-template <class Plan, int MS, int NS, int D>
+//
+// Producer / consumer waves (8 consumer waves over a 128 x 256 tile + 4 waves that
+// only stash into the other of two LDS stages, one barrier per K-tile; or 4 + 4 over
+// 128 x 128) were measured, bit-identical, 7-40 % slower than this loop on the C4
+// GEMM and C3 conv shapes (profiles/r3_gemm_loop/pc8_*): the consumer waves, which
+// wait for their fragment reads after every barrier, set the pace.
+template <class Plan, int MS, int NS, int D, int ABL = 0>
 __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restrict__ part, int remap) {
   constexpr int NST = 1;
   __shared__ __attribute__((aligned(16))) __bf16 Ls[NST][MS + NS][3][TERM_B];
@@ -1758,11 +1764,15 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
       // t+D-1 into the set just freed (clamped past the last tile: duplicates)
       auto tile_body = [&](int t, auto qc) {
         const int r0 = rbeg + t * BK;
-        compute_tile(Q0{});
-        split_all(qc);
-        __syncthreads();  // every wave's fragment reads of tile t are done
-        write_all(Q0{});
-        load(std::min(r0 + D * BK, rlast), qc);
+        // ABL (tools build only, timing ablations with wrong results): 1 no global loads,
+        // 2 no stash writes, 4 no first barrier, 8 no split, 16 no MFMAs / fragment reads
+        // (profiles/r3_gemm_loop/: without the stash writes the loop is 36 % shorter; with
+        // only the fragment reads and MFMAs it runs at ~0.55 of the bf16x6 ceiling)
+        if constexpr (!(ABL & 16)) compute_tile(Q0{});
+        if constexpr (!(ABL & 8)) split_all(qc);
+        if constexpr (!(ABL & 4)) __syncthreads();  // every wave's fragment reads of tile t are done
+        if constexpr (!(ABL & 2)) write_all(Q0{});
+        if constexpr (!(ABL & 1)) load(std::min(r0 + D * BK, rlast), qc);
         __syncthreads();
       };
       if constexpr (D == 3) {
@@ -1845,10 +1855,10 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
     }
 }
 
-template <class Plan, int MS, int NS, int D>
+template <class Plan, int MS, int NS, int D, int ABL = 0>
 __global__ __launch_bounds__(THREADS, FLR_SG_OCC) void sgemm_kernel(const Plan pl, int S, float* __restrict__ part,
                                                                      int remap) {
-  sgemm_body<Plan, MS, NS, D>(pl, S, part, remap);
+  sgemm_body<Plan, MS, NS, D, ABL>(pl, S, part, remap);
 }
 
 // ---- the weight gradient on split-at-stash images, transposed ----------------
@@ -2281,6 +2291,21 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
     }
   }
   if constexpr (has_k8<Plan>::value) {
+#ifdef FLR_ABLATION
+    if constexpr (MS == 2 && NS == 2) {
+      const char* ae = getenv("FLR_SG_ABL");  // timing ablations of the main loop (tools build only)
+      const int abl = ae ? atoi(ae) : 0;
+#define FLR_SG_ABL_CASE(A)                                                                                  \
+  if (form == 5 && abl == A) {                                                                               \
+    hipLaunchKernelGGL((sgemm_kernel<Plan, MS, NS, 2, A>), grid, dim3(THREADS), 0, st, pl, S,               \
+                       static_cast<float*>(ws), xcd_remap());                                                \
+    form = -1;                                                                                               \
+  }
+      FLR_SG_ABL_CASE(1) FLR_SG_ABL_CASE(2) FLR_SG_ABL_CASE(3) FLR_SG_ABL_CASE(4) FLR_SG_ABL_CASE(8)
+      FLR_SG_ABL_CASE(10) FLR_SG_ABL_CASE(16) FLR_SG_ABL_CASE(11) FLR_SG_ABL_CASE(15) FLR_SG_ABL_CASE(23)
+#undef FLR_SG_ABL_CASE
+    }
+#endif
     if (form == 5) {
       hipLaunchKernelGGL((sgemm_kernel<Plan, MS, NS, 2>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
                          xcd_remap());
