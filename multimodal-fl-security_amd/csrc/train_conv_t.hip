@@ -1662,8 +1662,14 @@ template <int A, int B> struct has_k8<BGemm<A, B>> : std::true_type {};
 // 128 x 128) were measured, bit-identical, 7-40 % slower than this loop on the C4
 // GEMM and C3 conv shapes (profiles/r3_gemm_loop/pc8_*): the consumer waves, which
 // wait for their fragment reads after every barrier, set the pace.
-template <class Plan, int MS, int NS, int D, int ABL = 0>
+// NAR (narrow N, the l4 convolutions' N = B * 1 * 1 = 32 pixels): NS = 1 and the four
+// waves stacked along M over MS 64-row A sub-tiles, each wave MS / 2 MFMA blocks of
+// 32 x 32 on the first 32 columns of the B image — a 64-wide N tile would leave half
+// its MFMAs on empty columns.  Same products per output: bit-identical.
+template <class Plan, int MS, int NS, int D, int ABL = 0, bool NAR = false>
 __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restrict__ part, int remap) {
+  static_assert(!NAR || (NS == 1 && (MS == 2 || MS == 4)), "narrow tiles: 128 or 256 x 32");
+  constexpr int MSW = NAR ? MS / 2 : MS;  // MFMA blocks per wave along M (NAR), or A sub-tiles
   constexpr int NST = 1;
   __shared__ __attribute__((aligned(16))) __bf16 Ls[NST][MS + NS][3][TERM_B];
   int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
@@ -1691,13 +1697,20 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
   // C3 conv and C4 GEMM shapes — the loop is not load-latency-bound; D == 2 is the one instantiated)
   float ra[2][MS][8], rb[2][NS][8];
   bf16x8 pa[MS][3], pb[NS][3];
-  f32x16 acc[MS][NS];
+  f32x16 acc[MSW][NS];
 #pragma unroll
-  for (int i = 0; i < MS; ++i)
+  for (int i = 0; i < MSW; ++i)
 #pragma unroll
     for (int j = 0; j < NS; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // this wave's MFMA block i: A sub-tile and row band (NAR: wave-stacked), and its
+  // row / column offset from (m0, n0)
+  auto a_sub = [&](int i) { return NAR ? (wave * MSW + i) >> 1 : i; };
+  auto a_row = [&](int i) { return NAR ? 32 * ((wave * MSW + i) & 1) + l32 : 32 * wm + l32; };
+  auto b_row = [&]() { return NAR ? l32 : 32 * wn + l32; };
+  auto m_off = [&](int i) { return NAR ? 32 * (wave * MSW + i) : BM * i + 32 * wm; };
+  auto n_off = [&](int j) { return NAR ? 0 : BN * j + 32 * wn; };
   auto load = [&](int r, auto qc) {
     constexpr int Q = decltype(qc)::value;
 #pragma unroll
@@ -1727,20 +1740,20 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
       constexpr int ST = decltype(stc)::value;
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
-        bf16x8 fa[MS][3], fb[NS][3];
+        bf16x8 fa[MSW][3], fb[NS][3];
         const int ko = 16 * s + 8 * h;
 #pragma unroll
-        for (int i = 0; i < MS; ++i)
+        for (int i = 0; i < MSW; ++i)
 #pragma unroll
           for (int q = 0; q < 3; ++q)
-            fa[i][q] = *reinterpret_cast<const bf16x8*>(&Ls[ST][i][q][zimg(32 * wm + l32, ko >> 3)]);
+            fa[i][q] = *reinterpret_cast<const bf16x8*>(&Ls[ST][a_sub(i)][q][zimg(a_row(i), ko >> 3)]);
 #pragma unroll
         for (int j = 0; j < NS; ++j)
 #pragma unroll
           for (int q = 0; q < 3; ++q)
-            fb[j][q] = *reinterpret_cast<const bf16x8*>(&Ls[ST][MS + j][q][zimg(32 * wn + l32, ko >> 3)]);
+            fb[j][q] = *reinterpret_cast<const bf16x8*>(&Ls[ST][MS + j][q][zimg(b_row(), ko >> 3)]);
 #define FLR_SX(TA, TB)                                                                              \
-  _Pragma("unroll") for (int i = 0; i < MS; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
+  _Pragma("unroll") for (int i = 0; i < MSW; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
       acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][TA], fb[j][TB], acc[i][j], 0, 0, 0);
         // product-major, small terms first (term 0 = hi, 1 = mid, 2 = lo)
         FLR_SX(1, 1) FLR_SX(0, 2) FLR_SX(2, 0) FLR_SX(0, 1) FLR_SX(1, 0) FLR_SX(0, 0)
@@ -1787,14 +1800,15 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
   }
   // C/D map of the 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
 #pragma unroll
-  for (int i = 0; i < MS; ++i)
+  for (int i = 0; i < MSW; ++i)
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-      const int tm0 = m0 + BM * i, tn0 = n0 + BN * j;
+      // (tm0, tn0): this wave's 32 x 32 block; offsets inside it below
+      const int tm0 = m0 + m_off(i), tn0 = n0 + n_off(j);
       if (S == 1 && pl.linear()) {
         float* base = pl.out() + pl.tile_base(k, tm0, tn0);
         const int64_t ldm = pl.ldm();
-        const int nl = 32 * wn + l32;
+        const int nl = l32;
         if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
           if (pl.bias) {  // the batched GEMM's bias: one value per lane column, bias + v
             const float bv = tn0 + nl < N ? pl.bias[k * pl.bias_k + tn0 + nl] : 0.f;
@@ -1807,7 +1821,7 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
           float av[16];
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            const int ml = 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int ml = (e & 3) + 8 * (e >> 2) + 4 * h;
             av[e] = (tm0 + ml < M && tn0 + nl < N) ? abase[ml * ldm + nl] : 0.f;
           }
 #pragma unroll
@@ -1815,7 +1829,7 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
         }
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int ml = 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const int ml = (e & 3) + 8 * (e >> 2) + 4 * h;
           if (tm0 + ml < M && tn0 + nl < N) base[ml * ldm + nl] = acc[i][j][e];
         }
         continue;
@@ -1826,8 +1840,8 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
           float av[16];
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            const int m = tm0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
-            const int n = tn0 + 32 * wn + l32;
+            const int m = tm0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int n = tn0 + l32;
             ix[e] = (m < M && n < N) ? pl.index(k, m, n) : -1;
             av[e] = ix[e] >= 0 ? pl.add[ix[e]] : 0.f;
           }
@@ -1839,14 +1853,14 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
       }
       if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
         if (S == 1) {
-          pl.store_tile(k, tm0, tn0, 32 * wm + 4 * h, 32 * wn + l32, acc[i][j], M, N);
+          pl.store_tile(k, tm0, tn0, 4 * h, l32, acc[i][j], M, N);
           continue;
         }
       }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int m = tm0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int n = tn0 + 32 * wn + l32;
+        const int m = tm0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int n = tn0 + l32;
         if (m < M && n < N) {
           if (S == 1) pl.store(k, m, n, acc[i][j][e]);
           else part[(((int64_t)split * pl.g.Kc + k) * M + m) * N + n] = acc[i][j][e];
@@ -1855,10 +1869,10 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
     }
 }
 
-template <class Plan, int MS, int NS, int D, int ABL = 0>
+template <class Plan, int MS, int NS, int D, int ABL = 0, bool NAR = false>
 __global__ __launch_bounds__(THREADS, FLR_SG_OCC) void sgemm_kernel(const Plan pl, int S, float* __restrict__ part,
                                                                      int remap) {
-  sgemm_body<Plan, MS, NS, D, ABL>(pl, S, part, remap);
+  sgemm_body<Plan, MS, NS, D, ABL, NAR>(pl, S, part, remap);
 }
 
 // ---- the weight gradient on split-at-stash images, transposed ----------------
@@ -2395,9 +2409,36 @@ int sq_slots(const Plan& pl) {
   return (int)(((int64_t)M * N + 255) / 256);
 }
 
+// Narrow-N tiles (sgemm_body NAR) for the conv forward / data gradient whose GEMM has
+// at most 32 columns (the l4 layers at 32 x 32 inputs: B * 1 * 1); FLR_CONV_NARROW=0:
+// the 64-wide tiles (A/B, read per launch).
+inline bool conv_narrow() {
+  const char* e = getenv("FLR_CONV_NARROW");
+  return !(e && e[0] == '0');
+}
+template <class Plan>
+int launch_narrow(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
+  const int M = pl.M(), N = pl.N(), R = pl.R(), K = pl.g.Kc;
+  int S = choose_splits(M, N, R, K, 2, plan_min_kt(pl));
+  if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) S = 1;
+  const dim3 grid((unsigned)cdiv(N, BN), (unsigned)cdiv(M, 2 * BM), (unsigned)(K * S));
+  hipLaunchKernelGGL((sgemm_kernel<Plan, 2, 1, 2, 0, true>), grid, dim3(THREADS), 0, st, pl, S,
+                     static_cast<float*>(ws), xcd_remap());
+  int rc = launch_status(name);
+  if (rc != FLR_OK || S == 1) return rc;
+  const int64_t mn = (int64_t)M * N;
+  hipLaunchKernelGGL(treduce_kernel<Plan>, dim3((unsigned)((mn + 255) / 256), (unsigned)K), dim3(256), 0, st, pl, S,
+                     static_cast<const float*>(ws));
+  return launch_status(name);
+}
+
 template <class Plan>
 int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   if (pl.R() == 0 && !std::is_same<Plan, DgradT>::value) return FLR_OK;  // a dgrad class with no tap stores zeros
+  if constexpr (std::is_same<Plan, FwdT>::value || std::is_same<Plan, DgradT>::value) {
+    if (pl.N() <= 32 && pl.M() % (2 * BM) == 0 && pl.R() > 0 && gemm_form() == 5 && conv_narrow())
+      return launch_narrow(pl, ws, ws_bytes, st, name);
+  }
   const int tile = plan_tile(pl);
   if constexpr (wide_tiles<Plan>()) {
     switch (tile) {

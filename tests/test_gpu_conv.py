@@ -241,3 +241,39 @@ def test_dgrad_addend_bit_identical(cuda, shape, form, monkeypatch):
                *geom, wsp, nb, _stream(dy))
     torch.cuda.synchronize()
     assert torch.equal(inplace, want)
+
+
+@pytest.mark.parametrize("shape", [(32, 32, 512, 1, 1, 512, 3, 1, 1), (8, 8, 256, 2, 2, 512, 3, 2, 1),
+                                   (5, 24, 256, 1, 1, 256, 1, 1, 0), (3, 32, 256, 2, 2, 512, 1, 2, 0)],
+                         ids=["l4b", "l4a", "1x1-n24", "l4ds"])
+def test_narrow_tiles_bit_identical(cuda, shape, monkeypatch):
+    """The l4 convolutions' narrow-N tiles (N = B*Ho*Wo <= 32: four waves stacked
+    along M) give the 64 x 64-tile kernels' bits: forward, data gradient (incl.
+    the strided classes and the in-place addend) and split-K."""
+    from flr import _capi
+    from flr.nn import _stream, _workspace_t
+    K, B, Cin, H, W, Cout, KS, stride, pad = shape
+    g = torch.Generator(device="cpu").manual_seed(sum(shape))
+    Ho, Wo = (H + 2 * pad - KS) // stride + 1, (W + 2 * pad - KS) // stride + 1
+    x = torch.randn(K * Cin, B, H, W, generator=g).to(cuda)
+    dy = torch.randn(K * Cout, B, Ho, Wo, generator=g).to(cuda)
+    wt = (torch.randn(K, KS, KS, Cin, Cout, generator=g) * 0.1).to(cuda)
+    add = torch.randn(K * Cin, B, H, W, generator=g).to(cuda)
+    geom = (K, B, Cin, H, W, Cout, KS, KS, stride, pad)
+    ws, nb = _workspace_t(geom, cuda)
+    wsp = None if ws is None else ws.data_ptr()
+    outs = []
+    for narrow in ("1", "0"):
+        monkeypatch.setenv("FLR_CONV_NARROW", narrow)
+        y = torch.full((K * Cout, B, Ho, Wo), float("nan"), device=cuda)
+        _capi.call("flr_conv2d_fwd_t", x.data_ptr(), wt.data_ptr(), y.data_ptr(), *geom, wsp, nb, _stream(x))
+        dx = torch.full_like(x, float("nan"))
+        _capi.call("flr_conv2d_bwd_data_t", dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), *geom, wsp, nb, _stream(x))
+        acc = add.clone()
+        _capi.call("flr_conv2d_bwd_data_t_add", dy.data_ptr(), wt.data_ptr(), acc.data_ptr(), acc.data_ptr(), *geom,
+                   wsp, nb, _stream(x))
+        torch.cuda.synchronize()
+        outs.append((y.cpu(), dx.cpu(), acc.cpu()))
+    for a, b in zip(*outs):
+        assert not torch.isnan(a).any()
+        assert torch.equal(a, b)
