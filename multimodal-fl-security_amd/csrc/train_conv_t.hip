@@ -1662,6 +1662,12 @@ template <int A, int B> struct has_k8<BGemm<A, B>> : std::true_type {};
 // 128 x 128) were measured, bit-identical, 7-40 % slower than this loop on the C4
 // GEMM and C3 conv shapes (profiles/r3_gemm_loop/pc8_*): the consumer waves, which
 // wait for their fragment reads after every barrier, set the pace.
+//
+// A half-phase schedule (one barrier per 16-deep k-step; waves 0-1 stash k-step 0's
+// half of the next tile beside k-step 1's MFMAs, waves 2-3 k-step 1's half beside
+// the next k-step 0; lane pairs instead of quads on k-contiguous rows) was
+// bit-identical and 0-25 % slower per conv layer, 8-27 % on the C4 GEMMs, C3 round
+// 60.0 -> 61.5 ms (profiles/r3_gemm_loop/half_phase.txt): twice the barriers per MFMA.
 // NAR (narrow N, the l4 convolutions' N = B * 1 * 1 = 32 pixels): NS = 1 and the four
 // waves stacked along M over MS 64-row A sub-tiles, each wave MS / 2 MFMA blocks of
 // 32 x 32 on the first 32 columns of the B image — a 64-wide N tile would leave half
