@@ -1668,6 +1668,8 @@ template <int A, int B> struct has_k8<BGemm<A, B>> : std::true_type {};
 // the next k-step 0; lane pairs instead of quads on k-contiguous rows) was
 // bit-identical and 0-25 % slower per conv layer, 8-27 % on the C4 GEMMs, C3 round
 // 60.0 -> 61.5 ms (profiles/r3_gemm_loop/half_phase.txt): twice the barriers per MFMA.
+// Issuing tile t+2's global loads before the first barrier instead of after the
+// stash: neutral on the GEMMs, C3 round 58.7 -> 59.6 ms (same file).
 // NAR (narrow N, the l4 convolutions' N = B * 1 * 1 = 32 pixels): NS = 1 and the four
 // waves stacked along M over MS 64-row A sub-tiles, each wave MS / 2 MFMA blocks of
 // 32 x 32 on the first 32 columns of the B image — a 64-wide N tile would leave half
