@@ -358,24 +358,24 @@ __host__ __device__ inline int att_ldr(int T) {
 }
 
 // s[a][c] = sum_d A[ra][d] * B[rc][d] over d < 64 (16-B LDS reads)
-template <int NT>
-__device__ __forceinline__ void att_dot(const float* A, const float* Bm, int ldr, const int (&ra)[NT],
-                                        const int (&rc)[NT], float (&s)[NT][NT]) {
+template <int NA, int NC>
+__device__ __forceinline__ void att_dot(const float* A, const float* Bm, int ldr, const int (&ra)[NA],
+                                        const int (&rc)[NC], float (&s)[NA][NC]) {
 #pragma unroll
-  for (int a = 0; a < NT; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int c = 0; c < NT; ++c) s[a][c] = 0.f;
+    for (int c = 0; c < NC; ++c) s[a][c] = 0.f;
 #pragma unroll 2
   for (int d = 0; d < DH; d += 4) {
-    f32x4 av[NT], bv[NT];
+    f32x4 av[NA], bv[NC];
 #pragma unroll
-    for (int a = 0; a < NT; ++a) av[a] = *reinterpret_cast<const f32x4*>(A + ra[a] * ldr + d);
+    for (int a = 0; a < NA; ++a) av[a] = *reinterpret_cast<const f32x4*>(A + ra[a] * ldr + d);
 #pragma unroll
-    for (int c = 0; c < NT; ++c) bv[c] = *reinterpret_cast<const f32x4*>(Bm + rc[c] * ldr + d);
+    for (int c = 0; c < NC; ++c) bv[c] = *reinterpret_cast<const f32x4*>(Bm + rc[c] * ldr + d);
 #pragma unroll
-    for (int a = 0; a < NT; ++a)
+    for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int c = 0; c < NT; ++c)
+      for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int e = 0; e < 4; ++e) s[a][c] = __builtin_fmaf(av[a][e], bv[c][e], s[a][c]);
   }
@@ -418,15 +418,15 @@ __device__ __forceinline__ float group16_sum(float v) {
 // src[s]) into LDS regions [T4][ldr]; rows T..T4-1 zeroed.  Every global load
 // is issued before the first LDS store: at two workgroups per CU nothing else
 // hides a serial chain of HBM latencies.
-constexpr int ATT_LOAD_IT = (((ATT_MAXT + 3) & ~3) * 16 + 255) / 256;
-template <int NS>
+template <int NS, int THR>
 __device__ __forceinline__ void att_load(float* const (&dst)[NS], const float* const (&src)[NS],
                                          const int64_t (&ld)[NS], int T, int ldr) {
+  constexpr int ATT_LOAD_IT = (((ATT_MAXT + 3) & ~3) * 16 + THR - 1) / THR;
   const int T4 = att_t4(T);
   f32x4 v[NS][ATT_LOAD_IT];
 #pragma unroll
   for (int it = 0; it < ATT_LOAD_IT; ++it) {
-    const int e = threadIdx.x + 256 * it;
+    const int e = threadIdx.x + THR * it;
     const int i = e >> 4, q = e & 15;
 #pragma unroll
     for (int k = 0; k < NS; ++k)
@@ -434,7 +434,7 @@ __device__ __forceinline__ void att_load(float* const (&dst)[NS], const float* c
   }
 #pragma unroll
   for (int it = 0; it < ATT_LOAD_IT; ++it) {
-    const int e = threadIdx.x + 256 * it;
+    const int e = threadIdx.x + THR * it;
     const int i = e >> 4, q = e & 15;
     if (e < T4 * 16) {
 #pragma unroll
@@ -443,15 +443,27 @@ __device__ __forceinline__ void att_load(float* const (&dst)[NS], const float* c
   }
 }
 
-template <int NT>
-__device__ __forceinline__ void att_rows(int T, int t, int (&r)[NT]) {
+template <int N>
+__device__ __forceinline__ void att_rows(int T, int t, int step, int (&r)[N]) {
 #pragma unroll
-  for (int a = 0; a < NT; ++a) r[a] = min(t + 16 * a, T - 1);
+  for (int a = 0; a < N; ++a) r[a] = min(t + step * a, T - 1);
 }
 
-template <int NT>
-__global__ __launch_bounds__(256) void att_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
+// THR threads per (sequence, head): thread (ti, tj) = (tid / 16, tid % 16) owns
+// score rows ti + RS a (RS = THR / 16, a < NA) and columns tj + 16 c (c < NT);
+// every score, softmax sum and output element is computed by one thread in the
+// same order whatever THR is (bit-identical); 512 threads put four waves on each
+// SIMD at two workgroups per CU instead of two (att_threads).
+template <int NT, int THR>
+struct AttShape {
+  static constexpr int RS = THR / 16;
+  static constexpr int NA = (NT * 16 + RS - 1) / RS;
+};
+
+template <int NT, int THR>
+__global__ __launch_bounds__(THR) void att_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
                                                       float* __restrict__ lse, int T, int H) {
+  constexpr int RS = AttShape<NT, THR>::RS, NA = AttShape<NT, THR>::NA;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int ldr = att_ldr(T), T4 = att_t4(T);
   const int region = T4 * ldr;
@@ -466,20 +478,20 @@ __global__ __launch_bounds__(256) void att_fwd_kernel(const float* __restrict__ 
     float* const dst[3] = {Qs, Ks, Vs};
     const float* const src[3] = {base, base + D, base + 2 * D};
     const int64_t ld[3] = {3 * D, 3 * D, 3 * D};
-    att_load<3>(dst, src, ld, T, ldr);
+    att_load<3, THR>(dst, src, ld, T, ldr);
   }
   __syncthreads();
   const int tid = threadIdx.x, ti = tid >> 4, tj = tid & 15;
-  int ra[NT], rc[NT];
-  att_rows<NT>(T, ti, ra);
-  att_rows<NT>(T, tj, rc);
-  float s[NT][NT];
-  att_dot<NT>(Qs, Ks, ldr, ra, rc, s);
+  int ra[NA], rc[NT];
+  att_rows<NA>(T, ti, RS, ra);
+  att_rows<NT>(T, tj, 16, rc);
+  float s[NA][NT];
+  att_dot<NA, NT>(Qs, Ks, ldr, ra, rc, s);
   __syncthreads();  // Q is dead: its region takes P
   float* Ps = Qs;
 #pragma unroll
-  for (int a = 0; a < NT; ++a) {
-    const int i = ti + 16 * a;
+  for (int a = 0; a < NA; ++a) {
+    const int i = ti + RS * a;
     float m = -__builtin_huge_valf();
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
@@ -506,11 +518,11 @@ __global__ __launch_bounds__(256) void att_fwd_kernel(const float* __restrict__ 
     }
   }
   __syncthreads();
-  f32x4 o[NT];
-  att_mat<NT>(Ps, Vs, ldr, T4, ra, tj, o);
+  f32x4 o[NA];
+  att_mat<NA>(Ps, Vs, ldr, T4, ra, tj, o);
 #pragma unroll
-  for (int a = 0; a < NT; ++a) {
-    const int i = ti + 16 * a;
+  for (int a = 0; a < NA; ++a) {
+    const int i = ti + RS * a;
     if (i < T) *reinterpret_cast<f32x4*>(ctx + (row0 + i) * D + h * DH + 4 * tj) = o[a];
   }
 }
@@ -519,10 +531,11 @@ __global__ __launch_bounds__(256) void att_fwd_kernel(const float* __restrict__ 
 // Drow_i = sum_d dO[i][d] O[i][d]; dS = P (dP - Drow) / 8;
 // dQ = dS K; dK = dS^T Q.  dqkv rows [rows][3D] (overwritten).
 // Four LDS regions: Q, K, V (-> P^T -> dS), dO (-> dS^T).
-template <int NT>
-__global__ __launch_bounds__(256) void att_bwd_kernel(const float* __restrict__ qkv, const float* __restrict__ ctx,
+template <int NT, int THR>
+__global__ __launch_bounds__(THR) void att_bwd_kernel(const float* __restrict__ qkv, const float* __restrict__ ctx,
                                                       const float* __restrict__ dctx, const float* __restrict__ lse,
                                                       float* __restrict__ dqkv, int T, int H) {
+  constexpr int RS = AttShape<NT, THR>::RS, NA = AttShape<NT, THR>::NA;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int ldr = att_ldr(T), T4 = att_t4(T);
   const int region = T4 * ldr;
@@ -535,15 +548,15 @@ __global__ __launch_bounds__(256) void att_bwd_kernel(const float* __restrict__ 
   const int64_t row0 = (int64_t)kb * T;
   const float* base = qkv + row0 * 3 * D + h * DH;
   const int tid = threadIdx.x, ti = tid >> 4, tj = tid & 15;
-  int ra[NT], rc[NT];
-  att_rows<NT>(T, ti, ra);
-  att_rows<NT>(T, tj, rc);
-  // Drow for rows ti + 16a (16 lanes split the 64 columns, 4 each) and the
+  int ra[NA], rc[NT];
+  att_rows<NA>(T, ti, RS, ra);
+  att_rows<NT>(T, tj, 16, rc);
+  // Drow for rows ti + RS a (16 lanes split the 64 columns, 4 each) and the
   // rows' lse: loads issued ahead of the LDS fill
-  f32x4 gv[NT], ov[NT];
-  float lrow[NT];
+  f32x4 gv[NA], ov[NA];
+  float lrow[NA];
 #pragma unroll
-  for (int a = 0; a < NT; ++a) {
+  for (int a = 0; a < NA; ++a) {
     const int64_t off = (row0 + ra[a]) * D + h * DH + 4 * tj;
     gv[a] = *reinterpret_cast<const f32x4*>(dctx + off);
     ov[a] = *reinterpret_cast<const f32x4*>(ctx + off);
@@ -553,31 +566,31 @@ __global__ __launch_bounds__(256) void att_bwd_kernel(const float* __restrict__ 
     float* const dst[4] = {Qs, Ks, Vs, dOs};
     const float* const src[4] = {base, base + D, base + 2 * D, dctx + row0 * D + h * DH};
     const int64_t ld[4] = {3 * D, 3 * D, 3 * D, D};
-    att_load<4>(dst, src, ld, T, ldr);
+    att_load<4, THR>(dst, src, ld, T, ldr);
   }
-  float drow[NT];
+  float drow[NA];
 #pragma unroll
-  for (int a = 0; a < NT; ++a) {
+  for (int a = 0; a < NA; ++a) {
     float acc = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc = __builtin_fmaf(gv[a][e], ov[a][e], acc);
     drow[a] = group16_sum(acc);
   }
   __syncthreads();
-  float p[NT][NT], dp[NT][NT];
-  att_dot<NT>(Qs, Ks, ldr, ra, rc, p);
-  att_dot<NT>(dOs, Vs, ldr, ra, rc, dp);
+  float p[NA][NT], dp[NA][NT];
+  att_dot<NA, NT>(Qs, Ks, ldr, ra, rc, p);
+  att_dot<NA, NT>(dOs, Vs, ldr, ra, rc, dp);
 #pragma unroll
-  for (int a = 0; a < NT; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
     for (int c = 0; c < NT; ++c) p[a][c] = tj + 16 * c < T ? expf(p[a][c] * 0.125f - lrow[a]) : 0.f;
   __syncthreads();  // V is dead: its region takes P^T
   float* Pt = Vs;
-  for (int e = tid; e < T4 * ldr; e += 256) Pt[e] = 0.f;
+  for (int e = tid; e < T4 * ldr; e += THR) Pt[e] = 0.f;
   __syncthreads();
 #pragma unroll
-  for (int a = 0; a < NT; ++a) {
-    const int i = ti + 16 * a;
+  for (int a = 0; a < NA; ++a) {
+    const int i = ti + RS * a;
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
       const int j = tj + 16 * c;
@@ -587,25 +600,25 @@ __global__ __launch_bounds__(256) void att_bwd_kernel(const float* __restrict__ 
   __syncthreads();
   float* dq = dqkv + row0 * 3 * D + h * DH;
   {  // dV[j][4tj..] = sum_i P^T[j][i] dO[i][4tj..]
-    f32x4 o[NT];
-    att_mat<NT>(Pt, dOs, ldr, T4, ra, tj, o);
+    f32x4 o[NA];
+    att_mat<NA>(Pt, dOs, ldr, T4, ra, tj, o);
 #pragma unroll
-    for (int a = 0; a < NT; ++a) {
-      const int j = ti + 16 * a;
+    for (int a = 0; a < NA; ++a) {
+      const int j = ti + RS * a;
       if (j < T) *reinterpret_cast<f32x4*>(dq + (int64_t)j * 3 * D + 2 * D + 4 * tj) = o[a];
     }
   }
   __syncthreads();  // P^T and dO are dead: dS into V's region, dS^T into dO's
   float* dS = Vs;
   float* dSt = dOs;
-  for (int e = tid; e < T4 * ldr; e += 256) {
+  for (int e = tid; e < T4 * ldr; e += THR) {
     dS[e] = 0.f;
     dSt[e] = 0.f;
   }
   __syncthreads();
 #pragma unroll
-  for (int a = 0; a < NT; ++a) {
-    const int i = ti + 16 * a;
+  for (int a = 0; a < NA; ++a) {
+    const int i = ti + RS * a;
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
       const int j = tj + 16 * c;
@@ -618,12 +631,12 @@ __global__ __launch_bounds__(256) void att_bwd_kernel(const float* __restrict__ 
   }
   __syncthreads();
   {
-    f32x4 oq[NT], ok[NT];
-    att_mat<NT>(dS, Ks, ldr, T4, ra, tj, oq);   // dQ[i] = sum_j dS[i][j] K[j]
-    att_mat<NT>(dSt, Qs, ldr, T4, ra, tj, ok);  // dK[j] = sum_i dS^T[j][i] Q[i]
+    f32x4 oq[NA], ok[NA];
+    att_mat<NA>(dS, Ks, ldr, T4, ra, tj, oq);   // dQ[i] = sum_j dS[i][j] K[j]
+    att_mat<NA>(dSt, Qs, ldr, T4, ra, tj, ok);  // dK[j] = sum_i dS^T[j][i] Q[i]
 #pragma unroll
-    for (int a = 0; a < NT; ++a) {
-      const int r = ti + 16 * a;
+    for (int a = 0; a < NA; ++a) {
+      const int r = ti + RS * a;
       if (r < T) {
         *reinterpret_cast<f32x4*>(dq + (int64_t)r * 3 * D + 4 * tj) = oq[a];
         *reinterpret_cast<f32x4*>(dq + (int64_t)r * 3 * D + D + 4 * tj) = ok[a];
@@ -801,17 +814,36 @@ extern "C" int flr_layernorm_bwd(const float* dy, int64_t lddy, const float* s, 
 }
 
 namespace {
+// 512 threads per (sequence, head) for T > 80 (AttShape; T = 96: fwd 28.2 -> 15.4 us,
+// bwd 35.8 -> 32.3 at KB = 64, H = 2, bit-identical).  At T = 65 (ViT-S/4) the 512-thread
+// form computes 96 score rows instead of 80 and measured slower (fwd 263 -> 293 us, bwd
+// 492 -> 678 at KB = 1024, H = 6), so T <= 80 stays on 256.  FLR_ATT_THREADS=256 / 512
+// forces a form (A/B, read per launch; tools/att_bench.py).
+inline int att_threads(int NT) {
+  const char* e = getenv("FLR_ATT_THREADS");
+  if (e && atoi(e) == 256) return 256;
+  if (e && atoi(e) == 512) return 512;
+  return NT >= 6 ? 512 : 256;
+}
 template <int NT>
 int att_fwd_launch(const float* qkv, float* ctx, float* lse, int64_t KB, int T, int H, hipStream_t st) {
-  hipLaunchKernelGGL(xf::att_fwd_kernel<NT>, dim3((unsigned)H, (unsigned)KB), dim3(256), xf::att_fwd_lds(T), st, qkv,
-                     ctx, lse, T, H);
+  const dim3 grid((unsigned)H, (unsigned)KB);
+  if (att_threads(NT) == 512)
+    hipLaunchKernelGGL((xf::att_fwd_kernel<NT, 512>), grid, dim3(512), xf::att_fwd_lds(T), st, qkv, ctx, lse, T, H);
+  else
+    hipLaunchKernelGGL((xf::att_fwd_kernel<NT, 256>), grid, dim3(256), xf::att_fwd_lds(T), st, qkv, ctx, lse, T, H);
   return launch_status("att_fwd_kernel");
 }
 template <int NT>
 int att_bwd_launch(const float* qkv, const float* ctx, const float* dctx, const float* lse, float* dqkv, int64_t KB,
                    int T, int H, hipStream_t st) {
-  hipLaunchKernelGGL(xf::att_bwd_kernel<NT>, dim3((unsigned)H, (unsigned)KB), dim3(256), xf::att_bwd_lds(T), st, qkv,
-                     ctx, dctx, lse, dqkv, T, H);
+  const dim3 grid((unsigned)H, (unsigned)KB);
+  if (att_threads(NT) == 512)
+    hipLaunchKernelGGL((xf::att_bwd_kernel<NT, 512>), grid, dim3(512), xf::att_bwd_lds(T), st, qkv, ctx, dctx, lse,
+                       dqkv, T, H);
+  else
+    hipLaunchKernelGGL((xf::att_bwd_kernel<NT, 256>), grid, dim3(256), xf::att_bwd_lds(T), st, qkv, ctx, dctx, lse,
+                       dqkv, T, H);
   return launch_status("att_bwd_kernel");
 }
 }  // namespace

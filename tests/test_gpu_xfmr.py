@@ -106,6 +106,24 @@ def test_attention_fwd_bwd(cuda, T, H):
     assert _rel(dq, dref) < 1e-5, _rel(dq, dref)
 
 
+@pytest.mark.parametrize("T", [65, 96])
+def test_attention_thread_forms_bit_identical(cuda, T, monkeypatch):
+    """The 256- and 512-thread attention forms (FLR_ATT_THREADS) compute every
+    score and output in the same order: bit-identical outputs and gradients."""
+    K, B, H, dh = 2, 3, 2, 64
+    g = torch.Generator().manual_seed(T)
+    qkv = torch.randn(K, B, T, 3 * H * dh, generator=g).to(cuda)
+    dctx = torch.randn(K, B, T, H * dh, generator=g).to(cuda)
+    outs = []
+    for thr in ("256", "512"):
+        monkeypatch.setenv("FLR_ATT_THREADS", thr)
+        q_ = qkv.clone().requires_grad_(True)
+        ctx = fnn.client_attention(q_, H)
+        (dq,) = torch.autograd.grad(ctx, q_, dctx)
+        outs.append((ctx.detach(), dq))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("act", ["relu", "gelu", "tanh"])
 def test_bgemm_ex_epilogues(cuda, act):
     K, M, N, R = 3, 70, 96, 130

@@ -7,7 +7,12 @@ import torch
 from flr import _capi
 
 
-def bench(KB, T, H, reps=20):
+def bench(KB, T, H, reps=20, threads=None):
+    if threads:
+        os.environ["FLR_ATT_THREADS"] = str(threads)
+    else:
+        os.environ.pop("FLR_ATT_THREADS", None)
+    torch.manual_seed(0)
     D = H * 64
     qkv = torch.randn(KB * T, 3 * D, device="cuda")
     ctx = torch.empty(KB * T, D, device="cuda")
@@ -31,10 +36,18 @@ def bench(KB, T, H, reps=20):
         us = e0.elapsed_time(e1) / reps * 1e3
         flops = KB * H * nprod * 2.0 * T * T * 64
         out.append((us, flops / us / 1e6))
-    print(f"KB={KB} T={T} H={H}: fwd {out[0][0]:8.1f} us {out[0][1]:6.1f} TF/s | bwd {out[1][0]:8.1f} us "
+    print(f"[threads {threads or 'default'}] KB={KB} T={T} H={H}: fwd {out[0][0]:8.1f} us {out[0][1]:6.1f} TF/s | bwd {out[1][0]:8.1f} us "
           f"{out[1][1]:6.1f} TF/s", flush=True)
+    f()
+    b()
+    torch.cuda.synchronize()
+    return ctx.cpu(), lse.cpu(), dqkv.cpu()
+
 
 
 if __name__ == "__main__":
-    bench(32 * 32, 65, 6)
-    bench(32 * 32, 16, 4)
+    for KB, T, H in ((32 * 32, 65, 6), (32 * 32, 16, 4), (64, 48, 2), (64, 96, 2)):
+        r0 = bench(KB, T, H, threads=256)
+        r1 = bench(KB, T, H, threads=512)
+        same = all(torch.equal(a, b) for a, b in zip(r0, r1))
+        print(f"  T={T}: 256- and 512-thread outputs bit-identical: {same}", flush=True)
