@@ -70,6 +70,40 @@ __global__ void from_tap_major_kernel(const float* __restrict__ src, float* __re
   }
 }
 
+// X's dead-tap ranges (training order) <- the global vector, every range of every
+// row in ONE launch (grid: slices x K): range r = [off[r], off[r] + n[r]) of both
+// g and each row; rows k < nneg negated.  g, X 16-B aligned and ld % 4 == 0 (the
+// caller checks), so g + o and X + k ld + o share their alignment: a scalar head
+// to the 16-B boundary, f32x4 body, scalar tail.  The body's stores are
+// non-temporal (the 3.6 GB of C3 rows are not re-read before the Gram streams
+// them from HBM): 926 -> 652 us per C3 round, 3.8 -> 5.5 TB/s
+// (profiles/r3_dead_ranges_nt.txt; plain stores from the client matrix's SGD
+// step measured no faster non-temporal).
+constexpr int DEAD_MAX = 96;
+struct DeadTable {
+  int64_t off[DEAD_MAX];
+  int64_t n[DEAD_MAX];
+  int cnt;
+};
+__global__ __launch_bounds__(THREADS) void dead_ranges_kernel(const DeadTable t, const float* __restrict__ g,
+                                                              float* __restrict__ X, int64_t ld, int nneg) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  float* d = X + (int64_t)blockIdx.y * ld;
+  const float sg = (int)blockIdx.y < nneg ? -1.f : 1.f;
+  const int64_t i0 = (int64_t)blockIdx.x * THREADS + threadIdx.x, stride = (int64_t)gridDim.x * THREADS;
+  for (int r = 0; r < t.cnt; ++r) {
+    const int64_t o = t.off[r], n = t.n[r];
+    const int64_t head = std::min<int64_t>(n, (4 - (o & 3)) & 3);
+    const int64_t nv = (n - head) / 4;
+    if (i0 < head) d[o + i0] = g[o + i0] * sg;
+    const f32x4* gs = reinterpret_cast<const f32x4*>(g + o + head);
+    f32x4* ds = reinterpret_cast<f32x4*>(d + o + head);
+    for (int64_t i = i0; i < nv; i += stride) __builtin_nontemporal_store(gs[i] * sg, ds + i);
+    const int64_t tl = o + head + 4 * nv, nt = n - head - 4 * nv;
+    if (i0 < nt) d[tl + i0] = g[tl + i0] * sg;
+  }
+}
+
 inline unsigned grid_for(int64_t n) {
   const int64_t g = (n + THREADS - 1) / THREADS;
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 4096));
@@ -407,9 +441,41 @@ class Net {
     return flush();
   }
 
-  // X's dead-tap ranges (training order) <- gtrain, rows k < nneg negated
+  // X's dead-tap ranges (training order) <- gtrain, rows k < nneg negated: one
+  // launch over the range table when it fits and the rows are 16-B aligned
+  // (was one broadcast per range: 57 launches per C3 round), else per range.
   int dead_ranges(const float* gtrain, float* X, int64_t ld, int64_t nneg, hipStream_t st) {
     int rc;
+    DeadTable t;
+    t.cnt = 0;
+    int64_t total = 0;
+    bool fits = (reinterpret_cast<uintptr_t>(gtrain) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
+                ld % 4 == 0 && K_ <= 65535;
+    for (size_t j = 0; j < ps_.size() && fits; ++j) {
+      const Param& p = ps_[j];
+      if (!p.dead) continue;
+      int64_t e = 0;
+      auto add = [&](int64_t a) {
+        if (a <= e) return;
+        if (t.cnt == DEAD_MAX) { fits = false; return; }
+        t.off[t.cnt] = p.off + e;
+        t.n[t.cnt++] = a - e;
+        total = std::max(total, a - e);
+      };
+      for (const auto& b : blocks_opt_) {
+        if (b.j != (int)j) continue;
+        add(b.o);
+        e = b.o + b.n;
+      }
+      add(p.n);
+    }
+    if (fits) {
+      if (t.cnt == 0) return FLR_OK;
+      const int64_t g = std::max<int64_t>(1, std::min<int64_t>(256, (total / 4 + THREADS - 1) / THREADS));
+      hipLaunchKernelGGL(dead_ranges_kernel, dim3((unsigned)g, (unsigned)K_), dim3(THREADS), 0, st, t, gtrain, X, ld,
+                         (int)std::min<int64_t>(nneg, K_));
+      return launch_status("train_clients: dead ranges");
+    }
     for (size_t j = 0; j < ps_.size(); ++j) {
       const Param& p = ps_[j];
       if (!p.dead) continue;
