@@ -217,7 +217,7 @@ __device__ __forceinline__ GroupDesc group_desc(int g, int K, bool cross) {
 // the single-GPU call computes for them.
 __host__ __device__ inline int64_t slice_chunk(int64_t nch, int q) { return nch * q / FLR_PW_SLICES; }
 
-template <int NL, bool CROSS, int TERMS, int ABLATE = 0>
+template <int NL, bool CROSS, int TERMS, int ABLATE = 0, bool NTL = false>
 // NL = 6 (96 KB of LDS) is limited to one workgroup per CU: give it the whole
 // register file (with the 2-per-CU bound it spilled to scratch).
 __global__ __launch_bounds__(THREADS, NL >= 6 ? 1 : 2) void gram_partials_kernel(
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(THREADS, NL >= 6 ? 1 : 2) void gram_partials_kernel
       const int inst = wave * 2 * NL + q;
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(src_row[q] + (int64_t)chunk * CW),
-          (__attribute__((address_space(3))) void*)(buf + inst * 256), 16, 0, 0);
+          (__attribute__((address_space(3))) void*)(buf + inst * 256), 16, 0, NTL ? 2 : 0);
     }
   };
 
@@ -886,9 +886,9 @@ int launch_gram(const GramArgs& a, const Plan& p, int group_base, int ngroups, h
   const size_t lds = (size_t)2 * 32 * NL * CW * sizeof(float);
   const int nseg = CROSS ? p.nseg_cross : p.nseg_diag;
   dim3 grid(nseg, ngroups, a.nsl);
-#define FLR_GRAM_LAUNCH(T, AB)                                                                              \
-  hipLaunchKernelGGL((gram_partials_kernel<NL, CROSS, T, AB>), grid, dim3(THREADS), lds, st, a.X, a.K, a.ldx, \
-                     p.nchunks, a.q0, a.chunk0, group_base, p.ngroups(), a.pivot, a.partials, nseg, p.nseg)
+#define FLR_GRAM_LAUNCH(T, AB, ...)                                                                      \
+  hipLaunchKernelGGL((gram_partials_kernel<NL, CROSS, T, AB, ##__VA_ARGS__>), grid, dim3(THREADS), lds, st, a.X, \
+                     a.K, a.ldx, p.nchunks, a.q0, a.chunk0, group_base, p.ngroups(), a.pivot, a.partials, nseg, p.nseg)
   if (gram_terms(a.P) == 3) {
     FLR_GRAM_LAUNCH(3, 0);
     return launch_status("gram_partials_kernel");
@@ -905,6 +905,20 @@ int launch_gram(const GramArgs& a, const Plan& p, int group_base, int ngroups, h
     }
   }
 #endif
+  // every row in one group (K <= 32 NL, no cross stage): each chunk of X is read
+  // once, so the DMA streams it non-temporally: C3 (K = 128) 1.044 -> 0.93 ms,
+  // 0.72 -> 0.81 of 8 TB/s.  Where groups re-read rows (K > 128) the default policy
+  // keeps their L2 / MALL hits (non-temporal there: C5 +9 %, C4 -1 %;
+  // profiles/r3_gram_nt.txt).  FLR_GRAM_NT=0: default policy everywhere, 2:
+  // non-temporal everywhere (A/B)
+  {
+    const char* e = getenv("FLR_GRAM_NT");
+    const int mode = e ? atoi(e) : 1;
+    if (mode == 2 || (mode == 1 && !CROSS && a.K <= 32 * NL)) {
+      FLR_GRAM_LAUNCH(2, 0, true);
+      return launch_status("gram_partials_kernel");
+    }
+  }
   FLR_GRAM_LAUNCH(2, 0);
 #undef FLR_GRAM_LAUNCH
   return launch_status("gram_partials_kernel");

@@ -38,7 +38,7 @@ def main():
         t = int(0.1 * K)
         runs = [("trimmed_mean", lambda: ops.trimmed_mean(X, t), 4.0 * K * P + 4.0 * P),
                 ("median", lambda: ops.median_lower(X), 4.0 * K * P + 4.0 * P)]
-        if cfg == "C5":
+        if cfg == "C5" or os.environ.get("GRAM_ALL"):
             runs.append(("krum_pairwise_gram", lambda: ops.pairwise_l2(X, "gram"), 4.0 * K * P + 8.0 * K * K))
         for name, fn, byts in runs:
             ms = timeit(fn)
