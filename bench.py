@@ -13,9 +13,16 @@ are generated on the device before timing.
 
 N = 1: python bench.py [--steps K --warmup W]
 N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  or   python bench.py --gpus N: with no torchrun environment (WORLD_SIZE
+       unset) the process starts the N ranks itself — a fresh
+       `python -m torch.distributed.run` child, before anything touches the
+       GPU — relays their output and exits with their status.
+Every rank checks that the process group's world size equals --gpus.
 Clients shard over ranks (K/N each), so the total work per round is fixed
 and the scaling is "strong".  Rank 0 prints one JSON line.
 --exchange allgather selects the whole-matrix all-gather instead.
+--backend gloo: the N-rank rehearsal on one GPU (collectives staged through
+the host; every rank on cuda:(local_rank mod device count)).
 """
 from __future__ import annotations
 
@@ -304,9 +311,39 @@ WORKLOAD = {
 }
 
 
+def launch_command(argv, n: int, port: int):
+    """The child command that starts n ranks of this script on one node
+    (torch.distributed.run, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def needs_launch(gpus: int, env=None) -> bool:
+    """True when --gpus asks for more ranks than this process's torchrun
+    environment provides and there is none: the parent then starts them.
+    A torchrun environment whose WORLD_SIZE differs from --gpus is an error."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" not in env:
+        return gpus > 1
+    if int(env["WORLD_SIZE"]) != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={env['WORLD_SIZE']} but --gpus {gpus}")
+    return False
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo = one-GPU rehearsal)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C3", choices=sorted(PRESETS),
@@ -323,6 +360,13 @@ def main() -> None:
                     help="rocprofv3 kernel_stats.csv (or the committed text summary) of THIS code's C3 bench, "
                          "for conv_mfma_from_profile (default: the newest committed profiles/*c3_kernel_stats*)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if needs_launch(args.gpus):
+        # fresh child processes (never exec: nothing here has touched the GPU yet)
+        import subprocess
+        rc = subprocess.run(launch_command(sys.argv[1:], args.gpus, _free_port())).returncode
+        sys.exit(rc)
 
     import torch
     from flr import dist as fdist
@@ -332,9 +376,19 @@ def main() -> None:
     from flr.train import TrainConfig
     from flr import ops
 
-    rank, world, local = fdist.init("nccl")
-    device = torch.device("cuda", local)
+    rank, world, local = fdist.init(args.backend)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: process group world size {world} != --gpus {args.gpus}")
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and local >= ndev:
+        raise SystemExit(f"bench.py: local rank {local} but only {ndev} GPUs visible (use --backend gloo "
+                         "to rehearse N ranks on fewer GPUs)")
+    device = torch.device("cuda", local % max(1, ndev))
     torch.cuda.set_device(device)
+    pg = None
+    if world > 1:
+        import torch.distributed as tdist
+        pg = {"backend": tdist.get_backend(), "world_size": tdist.get_world_size()}
     model, K, defense, dcfg, attack, afrac = PRESETS[args.config]
     custom = any(v is not None for v in (args.clients, args.defense, args.model))
     model = args.model or model
@@ -409,6 +463,9 @@ def main() -> None:
     if krum:
         eng.defense.publish()
         attackers_selected = sorted(set(eng.defense.selected_clients) & set(range(f)))
+    # the global model after warmup + steps rounds (bit-identical at every N)
+    import hashlib
+    global_sha256 = hashlib.sha256(eng.global_flat.detach().cpu().numpy().tobytes()).hexdigest()
 
     out = {
         "metric": METRIC,
@@ -438,6 +495,8 @@ def main() -> None:
                  "; local updates = one flr_train_clients_ex call") if eng.native else
                 "; local updates = the Python autograd composition of the kernels"),
         },
+        "process_group": pg,
+        "global_sha256": global_sha256,
         "aggregate_ms": aggregate_ms,
         "train_ms_per_round": train_ms,
         "attackers_selected": attackers_selected,

@@ -96,6 +96,18 @@ int flr_pairwise_tail(const float* X, int64_t K, int64_t ldx, int64_t p0, int64_
 int flr_pairwise_finish(const double* gsum, const double* tail, int64_t K, double* D,
                         void* stream);
 
+/* Reference-exact variant (opt-in parity mode, pairwise_method="reference"):
+ * D[i][j] bit-identical to the reference's fp32 torch.norm(flat_i - flat_j)
+ * .item() (krum.py:89-97) — per pair, 8 fp32 lanes of sequential
+ * fma(d, d, lane) over every 8th coordinate d = fl(x_i - x_j), the lanes
+ * summed 0..7 in order, the P mod 8 tail added as separate multiply + add,
+ * correctly rounded sqrt_f32 (oracle/norm_ref.c).  X in the
+ * reference's coordinate order (parameters() order); rows 16-B aligned and
+ * ldx % 4 == 0 (else FLR_ERR_ARG).  No workspace.  VALU / LDS bound: each
+ * pair's 8 chains run the whole vector sequentially. */
+int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx,
+                              double* D, void* stream);
+
 /* Direct-difference VALU variant (same contract, exact fp32 differences);
  * a slower second implementation used to cross-check the MFMA path. */
 size_t flr_pairwise_l2_direct_workspace(int64_t K, int64_t P);

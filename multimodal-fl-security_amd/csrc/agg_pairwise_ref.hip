@@ -1,0 +1,175 @@
+// a9, reference-exact mode — Krum distances bit-identical to the reference's
+// fp32 `torch.norm(flat_i - flat_j).item()` (src/defenses/krum.py:89-97).
+//
+// The reference's norm on an fp32 CPU tensor accumulates (SURVEY.md App. C,
+// probed on this image's torch; oracle/norm_ref.c restates it and
+// tests/test_oracle.py pins it against torch.norm):
+//   d = fl(x_i - x_j) elementwise;
+//   8 fp32 lanes, lane c = fma(d[8r+c], d[8r+c], lane c) sequentially over r;
+//   s = lane 0 + lane 1 + ... + lane 7 (in that order);
+//   s = s + fl(d[t] * d[t]) for each tail element t >= 8*floor(P/8);
+//   sqrt_f32(s) (correctly rounded), widened to fp64 by .item().
+// Every fp32 operation here is that operation, in that order, so D is the
+// reference's D bit for bit — no tolerance, no margin argument.
+//
+// The cost of exactness: each of the 8 lanes of a pair is ONE sequential
+// chain over P/8 coordinates (no split over coordinates, no reassociation),
+// so the parallelism is 8 chains per pair (65,024 at K = 128).  A thread owns
+// the chain pair (2cp, 2cp+1) of one client pair and advances both with one
+// v_pk_add_f32 + one v_pk_fma_f32 per 8 coordinates (the packed ops are two
+// IEEE fp32 ops each, rounding unchanged).  A 128-thread workgroup owns a
+// tile of 4 rows (I) x 8 rows (J) = 32 pairs; per 32-step chunk (256
+// coordinates) the 12 rows are staged into LDS by LDS-DMA (one 1-KB
+// global_load_lds_dwordx4 per row, double buffered) with a 1056-B row stride
+// (8 dwords of padding: the 8 rows x 4 chain pairs of a ds_read_b64 lane
+// group land on 64 distinct banks).  Per chain step a thread reads one float2
+// of each row (2 ds_read_b64): 16 B of LDS and 2 VALU instructions per two
+// chain steps.  Bound: VALU issue / LDS, not HBM (each tile re-reads its 12
+// rows from L2 / MALL).
+#include "flr_common.h"
+
+namespace flr {
+namespace pwref {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int TI = 4;                 // rows of a tile's I block
+constexpr int TJ = 8;                 // rows of a tile's J block
+constexpr int THREADS = TI * TJ * 4;  // 4 chain pairs per client pair: 128
+constexpr int CS = 32;                // chain steps per staged chunk
+constexpr int CW = 8 * CS;            // coordinates per chunk (1 KB per row)
+constexpr int RSTR = CW + 8;          // LDS row stride in floats (== 8 mod 64 dwords)
+constexpr int NROWS = TI + TJ;
+constexpr int BUF = NROWS * RSTR;     // floats per staging buffer
+
+// Tiles: J block jb (rows 8jb..8jb+7) with I blocks ib = 0 .. min(nI, 2jb+2)-1
+// (4 ib < 8 jb + 7: some i < some j).  Tiles are numbered jb-major.
+__host__ __device__ inline int64_t tiles_upto(int jb, int nI) {
+  // sum_{b < jb} min(nI, 2b + 2)
+  int64_t n = 0;
+  for (int b = 0; b < jb; ++b) n += (2 * b + 2 < nI ? 2 * b + 2 : nI);
+  return n;
+}
+
+__global__ __launch_bounds__(THREADS) void ref_norm_kernel(const float* __restrict__ X, int K, int64_t P,
+                                                           int64_t ldx, int ntiles, double* __restrict__ D) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
+  __shared__ f32x2 red[THREADS];
+  const int nI = cdiv(K, TI), nJ = cdiv(K, TJ);
+  // XCD-aware: consecutive workgroup ids go to different XCDs, so XCD x takes
+  // the contiguous tile range [x * per, (x + 1) * per) of the jb-major order
+  // (tiles sharing J rows share one L2)
+  const int per = cdiv(ntiles, 8);
+  const int tile = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (tile >= ntiles) return;  // uniform: the whole workgroup leaves
+  int jb = 0, base = 0;
+  for (; jb < nJ; ++jb) {
+    const int n = 2 * jb + 2 < nI ? 2 * jb + 2 : nI;
+    if (tile < base + n) break;
+    base += n;
+  }
+  const int ib = tile - base;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int pi = tid >> 5, pj = (tid >> 2) & 7, cp = tid & 3;
+  const int i = TI * ib + pi, j = TJ * jb + pj;
+
+  // staging: wave w DMAs rows w, w + 2, ... of the 12 (I rows 0..3, J rows 4..11)
+  const int64_t R = P / 8;  // full chain steps
+  const int64_t nch = (R + CS - 1) / CS;
+  const float* src[NROWS / 2];
+#pragma unroll
+  for (int q = 0; q < NROWS / 2; ++q) {
+    const int row = wave + 2 * q;
+    int g = row < TI ? TI * ib + row : TJ * jb + (row - TI);
+    g = g < K ? g : K - 1;
+    src[q] = X + (int64_t)g * ldx;
+  }
+  auto stage = [&](int64_t ch, float* buf) {
+    const int64_t off = ch * CW + 4 * lane;  // this lane's 4 floats of the row's chunk
+    const bool ok = off + 4 <= R * 8;        // past the last full step: any valid address (unused)
+#pragma unroll
+    for (int q = 0; q < NROWS / 2; ++q) {
+      const int row = wave + 2 * q;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src[q] + (ok ? off : 0)),
+          (__attribute__((address_space(3))) void*)(buf + row * RSTR), 16, 0, 0);
+    }
+  };
+
+  f32x2 acc = {0.f, 0.f};
+  const float* arow = lds + pi * RSTR + 2 * cp;
+  const float* brow = lds + (TI + pj) * RSTR + 2 * cp;
+  if (nch > 0) stage(0, lds);
+  for (int64_t ch = 0; ch < nch; ++ch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // chunk ch landed (every wave's DMA); chunk ch-1's buffer is free
+    const int cur = (int)(ch & 1);
+    if (ch + 1 < nch) stage(ch + 1, lds + (cur ^ 1) * BUF);
+    const float* a = arow + cur * BUF;
+    const float* b = brow + cur * BUF;
+    const int64_t left = R - ch * CS;
+    if (left >= CS) {
+#pragma unroll
+      for (int s = 0; s < CS; ++s) {
+        const f32x2 d = *reinterpret_cast<const f32x2*>(a + 8 * s) - *reinterpret_cast<const f32x2*>(b + 8 * s);
+        acc = __builtin_elementwise_fma(d, d, acc);
+      }
+    } else {
+      for (int s = 0; s < (int)left; ++s) {
+        const f32x2 d = *reinterpret_cast<const f32x2*>(a + 8 * s) - *reinterpret_cast<const f32x2*>(b + 8 * s);
+        acc = __builtin_elementwise_fma(d, d, acc);
+      }
+    }
+  }
+  // lane sum 0..7 in order, then the tail (separate multiply and add), sqrt
+  red[tid] = acc;
+  __syncthreads();
+  if (cp == 0 && i < j && j < K) {
+    const f32x2 l01 = red[tid], l23 = red[tid + 1], l45 = red[tid + 2], l67 = red[tid + 3];
+    float s = l01[0];
+    s = add_rn(s, l01[1]);
+    s = add_rn(s, l23[0]);
+    s = add_rn(s, l23[1]);
+    s = add_rn(s, l45[0]);
+    s = add_rn(s, l45[1]);
+    s = add_rn(s, l67[0]);
+    s = add_rn(s, l67[1]);
+    const float* xi = X + (int64_t)i * ldx;
+    const float* xj = X + (int64_t)j * ldx;
+    for (int64_t t = R * 8; t < P; ++t) {
+      const float d = xi[t] - xj[t];
+      s = add_rn(s, mul_rn(d, d));
+    }
+    const double v = (double)__fsqrt_rn(s);
+    D[(int64_t)i * K + j] = v;
+    D[(int64_t)j * K + i] = v;
+  }
+}
+
+__global__ void diag_zero_kernel(int K, double* __restrict__ D) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < K) D[(int64_t)i * K + i] = 0.0;
+}
+
+}  // namespace pwref
+}  // namespace flr
+
+using namespace flr;
+using namespace flr::pwref;
+
+extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx, double* D,
+                                         void* stream) {
+  if (K < 1 || P < 0 || ldx < P || !D || (K > 1 && P > 0 && !X)) return FLR_ERR_ARG;
+  if (K > (1 << 15)) return FLR_ERR_UNSUPPORTED;
+  // LDS-DMA reads 16-B pieces: rows must start 16-B aligned
+  if (K > 1 && P >= 8 && (((reinterpret_cast<uintptr_t>(X) & 15) != 0) || (ldx % 4) != 0)) return FLR_ERR_ARG;
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(diag_zero_kernel, dim3(cdiv((int)K, 256)), dim3(256), 0, st, (int)K, D);
+  int rc = launch_status("diag_zero_kernel");
+  if (rc != FLR_OK || K == 1) return rc;
+  const int nI = cdiv((int)K, TI), nJ = cdiv((int)K, TJ);
+  const int64_t ntiles = tiles_upto(nJ, nI);
+  const int per = (int)((ntiles + 7) / 8);
+  hipLaunchKernelGGL(ref_norm_kernel, dim3(8 * per), dim3(THREADS), 0, st, X, (int)K, P, ldx, (int)ntiles, D);
+  return launch_status("ref_norm_kernel");
+}

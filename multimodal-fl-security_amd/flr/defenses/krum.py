@@ -52,8 +52,17 @@ class KrumDefense(BaseDefense):
             return cm.data[int(order[0].item()), : cm.P]
         return ops.rows_mean(cm.X, order[: min(self.multi_k, cm.K)], divisor=self.multi_k)
 
-    supports_sharded = True
-    order_free = True
+    # pairwise_method="reference" reproduces the reference's torch.norm
+    # accumulation, which runs over the whole vector in parameters() order:
+    # it needs whole rows (all-gather exchange) in torch order (no
+    # training-order rounds)
+    @property
+    def supports_sharded(self) -> bool:
+        return self.pairwise_method != "reference"
+
+    @property
+    def order_free(self) -> bool:
+        return self.pairwise_method != "reference"
 
     def aggregate_sharded(self, cs, num_examples: List[int], publish: bool = True, events=None) -> torch.Tensor:
         """Coordinate-sharded Krum (flr.shard): distances from the per-slice

@@ -3,11 +3,19 @@
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).
 GPU g owns the contiguous clients [g*K/G, (g+1)*K/G), so global client ids,
 attacker ids (0..f-1) and the row order of the client matrix mean the same at
-every G.  The round has exactly one exchange: after local training, one
-all-gather of the (K/G)×P row blocks gives every GPU the full K×P client
-matrix in global client order; aggregation then runs replicated with
-deterministic fixed-order kernels, so every GPU ends the round with the
-bit-identical global model and no second collective is needed.
+every G.  The round's data exchange after local training is one of two
+(flr.round, RoundConfig.exchange):
+* "alltoall" (the default for the coordinate-wise and Krum defenses,
+  flr.shard): one all-to-all hands GPU g all K clients' values of its
+  coordinate range; each GPU aggregates its range (Krum: plus small
+  collectives of the pivot sample, the tail term and the per-slice Gram
+  records) and one all-gather of the aggregated slices rebuilds the global
+  model;
+* "allgather" (defenses that need whole rows): one all-gather of the
+  (K/G)×P row blocks (allgather_rows below) gives every GPU the full K×P
+  matrix in global client order and the aggregation runs replicated.
+Both use deterministic fixed-order kernels, so every GPU ends the round with
+the bit-identical global model at every G.
 """
 from __future__ import annotations
 
@@ -67,6 +75,8 @@ def barrier() -> None:
 def max_over_ranks(value: float, device) -> float:
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    # gloo reduces host tensors; RCCL device tensors
+    t = torch.tensor([value], dtype=torch.float64,
+                     device="cpu" if dist.get_backend() == "gloo" else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

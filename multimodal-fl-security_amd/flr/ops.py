@@ -37,10 +37,21 @@ def _check_matrix(X: torch.Tensor, name: str = "X") -> Tuple[int, int, int]:
 def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None) -> torch.Tensor:
     """K×K float64 distances, D[i][j] = fp32 ||X_i - X_j|| (krum.py:73-99).
 
+    method: "gram" (centred Gram on MFMA, the production path), "direct"
+    (exact fp32 differences, fp32/fp64 partial sums) or "reference" (the
+    reference's own torch.norm accumulation, bit-identical D; X must then be
+    in the reference's coordinate order).
     events: optional (begin, end) raw hipEvent_t handles recorded around the
     main MFMA kernel (flr.timing.HipEventPair)."""
     K, P, ldx = _check_matrix(X)
     D = torch.empty((K, K), dtype=torch.float64, device=X.device)
+    if method == "reference":
+        if X.data_ptr() % 16 or ldx % 4:  # the kernel stages 16-B pieces of 16-B aligned rows
+            Xa = torch.zeros((K, (P + 63) // 64 * 64), dtype=torch.float32, device=X.device)
+            Xa[:, :P].copy_(X)
+            X, ldx = Xa, Xa.stride(0)
+        _capi.call("flr_pairwise_l2_reference", X.data_ptr(), K, P, ldx, D.data_ptr(), _stream(X))
+        return D
     if method == "gram":
         ws_fn, fn = "flr_pairwise_l2_workspace", "flr_pairwise_l2"
     elif method == "direct":

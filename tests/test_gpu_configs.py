@@ -28,6 +28,8 @@ import torch
 
 from oracle import aggregation as orc
 from oracle import training as otrain
+from flr import ops
+from flr.matrix import padded_ld
 from flr.models.multimodal import VIT_BERT, ModelSpec, model_class
 from flr.round import RoundConfig, RoundEngine
 from flr.train import TrainConfig, make_dropout_masks, synthetic_batches
@@ -132,10 +134,23 @@ def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
     D64 = fp64_distances(X, P)
     t0 = time.perf_counter()
     rows = []
+    Xt = torch.zeros((K, padded_ld(P)), dtype=torch.float32, device=cuda)  # torch-order device copy
     for k in range(K):  # the reference's flattened updates: torch (parameters()) order
         r = eng.trainer.to_torch_order(X[k]) if eng.train_order else X[k]
+        Xt[k, :P].copy_(r)
         rows.append(r.cpu())
     t_copy = time.perf_counter() - t0
+    # the reference-exact mode (pairwise_method="reference") on the same rows
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()  # the op's kernels run on torch's current stream
+    D_mode = ops.pairwise_l2(Xt[:, :P], "reference")
+    ev1.record()
+    torch.cuda.synchronize()
+    mode_ms = ev0.elapsed_time(ev1)
+    _, order_mode = ops.krum_select(D_mode, f)
+    order_mode = order_mode.cpu().tolist()
+    D_mode = D_mode.cpu().numpy()
+    del Xt
     t0 = time.perf_counter()
     D_ref = reference_distances(rows)
     t_ref = time.perf_counter() - t0
@@ -163,16 +178,21 @@ def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
         "selected_set_identical": set(eng.defense.selected_clients) == set(sel_ref),
         "attackers_selected": sorted(set(eng.defense.selected_clients) & set(range(f))),
         "host_copy_s": t_copy, "reference_norms_s": t_ref, **rep,
+        "reference_mode_D_bit_identical": bool(np.array_equal(D_mode, D_ref)),
+        "reference_mode_D_max_abs_diff": float(np.abs(D_mode - D_ref).max()),
+        "reference_mode_selected_identical": order_mode[:mk] == sel_ref,
+        "reference_mode_rejected_identical": order_mode[mk:] == rej_ref,
+        "reference_mode_kernel_ms": mode_ms,
         "selected_reference": sel_ref, "selected_gpu": eng.defense.selected_clients,
     }
-    conditioned = rep["boundary_well_conditioned"]
     _record("c3_krum_trained_round.json", payload)
+    # the reference-exact mode: the reference's D bit for bit, so its whole order
+    assert np.array_equal(D_mode, D_ref)
+    assert order_mode[:mk] == sel_ref and order_mode[mk:] == rej_ref
+    # the production (centred Gram) path: the selected clients, in order
+    assert eng.defense.selected_clients == sel_ref
     assert not set(eng.defense.selected_clients) & set(range(f))
     assert rep["differences_within_error"], rep["positions_differing"]
-    if conditioned:
-        assert set(eng.defense.selected_clients) == set(sel_ref)
-    if not rep["positions_differing"]:
-        assert eng.defense.selected_clients == sel_ref and eng.defense.rejected_clients == rej_ref
 
 
 def _strided(P: int, n: int = 1_100_000) -> torch.Tensor:

@@ -1,0 +1,104 @@
+"""GPU: the reference-exact Krum distance mode (pairwise_method="reference",
+flr_pairwise_l2_reference) against the reference's own per-pair fp32
+``torch.norm(fi - fj).item()`` (krum.py:89-97) — BIT-identical D, hence
+identical scores, selected and rejected lists (krum.py:101-131, 174-176).
+
+Oracles: oracle.aggregation.distance_matrix (torch.norm per pair, the
+reference's op), oracle.normref (its C restatement, pinned against torch.norm
+in tests/test_oracle.py; used where the torch loop would take minutes), and the
+C3-shaped golden fixtures (their `dist` field is the oracle's torch.norm D)."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_files, load_golden
+from oracle import aggregation as orc
+from oracle import normref
+from flr import ops
+from flr.defenses import KrumDefense
+from flr.matrix import ClientMatrix, padded_ld
+from flr.workload import update_matrix
+
+pytestmark = pytest.mark.gpu
+
+
+def _matrix(K, P, seed, device):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(K, P, generator=g) * 0.05
+    X[: K // 5] = -X[: K // 5]
+    X += 1e-3 * torch.randn(K, P, generator=g) * torch.exp(torch.randn(K, P, generator=g))
+    data = torch.zeros((K, padded_ld(P)), dtype=torch.float32)
+    data[:, :P] = X
+    return X, data.to(device)
+
+
+@pytest.mark.parametrize("K,P", [(2, 0), (2, 1), (3, 7), (5, 8), (7, 9), (9, 255), (12, 256), (13, 257),
+                                 (16, 4099), (33, 2053), (40, 65537), (1, 100)])
+def test_reference_mode_equals_torch_norm(cuda, K, P):
+    X, data = _matrix(K, P, K * 1000 + P, cuda)
+    D = ops.pairwise_l2(data[:, :P], "reference").cpu().numpy()
+    want = orc.distance_matrix([[X[k]] for k in range(K)])
+    assert np.array_equal(D, want), np.abs(D - want).max()
+
+
+def test_reference_mode_unaligned_view(cuda):
+    """A row view starting 4 B into the buffer (not 16-B aligned): the op
+    re-pads it; D unchanged."""
+    K, P = 10, 3001
+    X, _ = _matrix(K, P, 77, cuda)
+    buf = torch.zeros((K, P + 1), dtype=torch.float32, device=cuda)
+    buf[:, 1:] = X.to(cuda)
+    D = ops.pairwise_l2(buf[:, 1:], "reference").cpu().numpy()
+    assert np.array_equal(D, orc.distance_matrix([[X[k]] for k in range(K)]))
+
+
+@pytest.mark.parametrize("K,P", [(128, 1 << 20), (64, 3_000_017), (300, 20_011)])
+def test_reference_mode_large_vs_c_oracle(cuda, K, P):
+    """Longer chains and K > 128 (more tiles than CUs) against the C restatement."""
+    X, data = _matrix(K, P, 5 + K, cuda)
+    D = ops.pairwise_l2(data[:, :P], "reference").cpu().numpy()
+    assert np.array_equal(D, normref.distance_matrix(X.numpy()))
+
+
+@pytest.mark.parametrize("path", golden_files("c3krum"), ids=lambda p: p.split("/")[-1])
+def test_reference_mode_c3_fixtures(cuda, path):
+    """The C3-shaped fixtures (K = 128, f = 25 sign-flipped, multi_k = 64):
+    D equals the fixture's reference fp32 norms bit for bit, and the Krum
+    outputs (selected, rejected, the Multi-Krum mean) are the fixture's."""
+    fx = load_golden(path)
+    K, P, f, mk = (int(fx[k]) for k in ("K", "P", "f", "multi_k"))
+    X = update_matrix(K, P, f=f, seed=int(fx["seed"]), device="cpu")[:, :P]
+    data = torch.zeros((K, padded_ld(P)), dtype=torch.float32, device=cuda)
+    data[:, :P] = X.to(cuda)
+    d = KrumDefense({"num_malicious": f, "multi_k": mk, "pairwise_method": "reference"})
+    flat = d.aggregate_flat(ClientMatrix(data, P, [(P,)]), [1] * K)
+    assert np.array_equal(d.distances.cpu().numpy(), fx["dist"])
+    assert d.client_scores == fx["scores"].tolist()
+    assert d.selected_clients == fx["selected"].tolist()
+    assert d.rejected_clients == fx["rejected"].tolist()
+    assert hashlib.sha256(flat.cpu().numpy().tobytes()).hexdigest() == str(fx["agg_sha256"])
+
+
+def test_reference_mode_round_engine(cuda):
+    """A round with Krum in the reference mode: the engine hands the defense
+    whole rows in the reference's coordinate order (all-gather exchange, no
+    training-order rows), and D / selection / rejection equal the oracle's
+    torch.norm loop on those rows."""
+    from flr.models.multimodal import TINY
+    from flr.round import RoundConfig, RoundEngine
+    from flr.train import TrainConfig
+    K, f = 12, 2
+    rc = RoundConfig(num_clients=K, batch=4, defense="krum", num_attackers=f,
+                     defense_cfg={"pairwise_method": "reference"})
+    eng = RoundEngine(TINY, rc, TrainConfig(local_steps=2), cuda)
+    assert eng.exchange == "allgather" and not eng.train_order
+    eng.run_round()
+    eng.defense.publish()
+    P = eng.trainer.P
+    rows = [eng.trainer.X.data[k, :P].cpu() for k in range(K)]
+    _, scores, sel, rej, dist = orc.krum([[r] for r in rows], f, K // 2)
+    assert np.array_equal(eng.defense.distances.cpu().numpy(), dist)
+    assert eng.defense.client_scores == [float(s) for s in scores]
+    assert eng.defense.selected_clients == sel and eng.defense.rejected_clients == rej

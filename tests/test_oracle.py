@@ -146,3 +146,49 @@ def test_golden_krum_margins_recorded():
     for path in golden_files("krum"):
         fx = load_golden(path)
         assert float(fx["margin"]) > 0  # no exact tie at the selection boundary
+
+
+# ---- the reference's per-pair norm (krum.py:95) restated in C (oracle/norm_ref.c) ----
+
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 9, 63, 1000, 4099, 65537, 1 << 20, 3_000_001])
+def test_norm_ref_model_equals_torch_norm(n):
+    """SURVEY App. C's accumulation model of fp32 torch.norm (8 sequential-fma
+    lanes, lanes summed in order, tail mul + add, sqrt_f32) reproduces
+    torch.norm(a - b).item() bit for bit, at every length and magnitude mix
+    (several seeds per length; the heavy-tailed cases make order matter)."""
+    from oracle import normref
+    for seed in range(6):
+        g = torch.Generator().manual_seed(1000 * n + seed)
+        a = torch.randn(n, generator=g) * (10.0 ** (seed - 3))
+        b = a + torch.randn(n, generator=g) * 1e-3 * torch.exp(2 * torch.randn(n, generator=g))
+        want = torch.norm(a - b).item()
+        got = normref.norm_diff(a.numpy(), b.numpy())
+        assert got == want, (n, seed, got, want)
+
+
+def test_norm_ref_model_thread_independent():
+    """A single-output fp32 norm is one sequential reduction whatever the
+    intra-op thread count (C3's P = 11,800,394)."""
+    from oracle import normref
+    g = torch.Generator().manual_seed(5)
+    n = 11_800_394
+    a = torch.randn(n, generator=g) * 0.05
+    b = a + 0.01 * torch.randn(n, generator=g)
+    got = normref.norm_diff(a.numpy(), b.numpy())
+    prev = torch.get_num_threads()
+    try:
+        for th in (1, max(2, prev)):
+            torch.set_num_threads(th)
+            assert torch.norm(a - b).item() == got
+    finally:
+        torch.set_num_threads(prev)
+
+
+def test_norm_ref_distance_matrix_equals_oracle():
+    """The OpenMP pair matrix == oracle.aggregation.distance_matrix (torch.norm per pair)."""
+    from oracle import normref
+    g = torch.Generator().manual_seed(9)
+    X = torch.randn(9, 3001, generator=g)
+    X[:3] = -X[:3]
+    want = orc.distance_matrix([[X[k]] for k in range(9)])
+    assert np.array_equal(normref.distance_matrix(X.numpy()), want)
