@@ -155,14 +155,39 @@ def round_roofline(K: int, P: int, P_live: int, steps: int, ms_per_round: float,
     }
 
 
-def cpu_baseline(spec, P, K, f, multi_k, steps, batch, budget_s: float = 20.0):
-    """Time the oracle (the reference's CPU path restated) on a bounded sample
-    and extrapolate one round: K clients x local update + K(K-1)/2 pair norms +
-    the Multi-Krum mean."""
+def _median_time(fn, n: int, budget_s: float):
+    """Median wall time of up to n calls of fn (at least one), stopping early
+    once budget_s is spent; returns (median seconds, samples taken)."""
+    import statistics
+    ts = []
+    t_all = time.perf_counter()
+    while len(ts) < n:
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_all > budget_s:
+            break
+    return statistics.median(ts), len(ts)
+
+
+def cpu_baseline(spec, P, K, defense, f, multi_k, steps, batch, budget_s: float = 20.0, trim_ratio: float = 0.1):
+    """The reference's CPU path (the oracle: run_experiments.py:195-240 loop,
+    krum.py:55-192, trimmed_mean.py:48-166, base_defense.py:80-97 restated
+    with the same torch/numpy calls) on this host's cores, BASELINE.md §2:
+    (a) one client's local update (`steps` batches), (b) aggregate-ms of every
+    hot-path aggregator at this K, (c) rounds/s of this config's defense =
+    1 / (K * (a) + (b)[defense]).  Each figure is the median of up to 5 timed
+    calls after one warm-up, inside a time budget (the sample text says how
+    many were taken).  Bounded samples, stated: Krum's K(K-1)/2 pair norms are
+    priced from pair norms at the full P; FedAvg, the trimmed mean, the median
+    and the Multi-Krum mean from a reduced coordinate count P_s, scaled by
+    P / P_s (each is linear in P)."""
+    import numpy as np
     import torch
     sys.path.insert(0, ROOT)
+    from oracle import aggregation as orc
     from oracle import training as otrain
-    from flr.models.multimodal import MultimodalNet
+    from flr.models.multimodal import model_class
 
     # the box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool; os.cpu_count()
     # reports the whole host there, whose other cores belong to other jobs)
@@ -174,42 +199,69 @@ def cpu_baseline(spec, P, K, f, multi_k, steps, batch, budget_s: float = 20.0):
                 torch.randint(0, spec.vocab, (batch, spec.seq_len), generator=g),
                 torch.randint(0, spec.num_classes, (batch,), generator=g)) for _ in range(steps)]
     torch.manual_seed(42)
-    glob = torch.cat([p.detach().reshape(-1) for p in MultimodalNet(spec).parameters()])
-    otrain.local_update(MultimodalNet, spec, glob, batches[:1])  # warm-up
-    t0 = time.perf_counter()
-    n_clients = 0
-    while True:
-        otrain.local_update(MultimodalNet, spec, glob, batches)
-        n_clients += 1
-        if time.perf_counter() - t0 > budget_s * 0.5 or n_clients >= 4:
-            break
-    t_client = (time.perf_counter() - t0) / n_clients
+    cls = model_class(spec)
+    glob = torch.cat([p.detach().reshape(-1) for p in cls(spec).parameters()])
+    otrain.local_update(cls, spec, glob, batches[:1])  # warm-up
+    t_client, n_client = _median_time(lambda: otrain.local_update(cls, spec, glob, batches), 5, budget_s * 0.4)
+
+    # (b) aggregation inputs: X[i] = g + sigma_i N(0,1), f sign-flipped
+    P_s = min(P, 1 << 17)
+    gs = torch.Generator().manual_seed(7)
+    base = 0.05 * torch.randn(P_s, generator=gs)
+    rows = []
+    for i in range(K):
+        r = base + 0.01 * (1 + 0.5 * i / K) * torch.randn(P_s, generator=gs)
+        rows.append([-r if i < f else r])
+    scale = P / P_s
+    per = budget_s * 0.1
+    nex = [steps * batch] * K
+    agg = {}
+    orc.fedavg(rows[:2], nex[:2])
+    t, n_fa = _median_time(lambda: orc.fedavg(rows, nex), 5, per)
+    agg["fedavg"] = t * scale
+    orc.trimmed_mean(rows[:8], trim_ratio)
+    t, n_tm = _median_time(lambda: orc.trimmed_mean(rows, trim_ratio), 5, per)
+    agg["trimmed_mean"] = t * scale
+    orc.median(rows[:8])
+    t, n_md = _median_time(lambda: orc.median(rows), 5, per)
+    agg["median"] = t * scale
+    # Krum: pair norms at the full P (krum.py:95), scores + argsort on a K x K
+    # matrix (krum.py:126-129, 174), the Multi-Krum mean of multi_k rows (:182-192)
     a = glob + 0.01 * torch.randn(P, generator=g)
     b = glob + 0.01 * torch.randn(P, generator=g)
     torch.norm(a - b).item()
-    t0 = time.perf_counter()
-    n_pairs = 0
-    while True:
-        torch.norm(a - b).item()  # krum.py:95, one pair
-        n_pairs += 1
-        if time.perf_counter() - t0 > budget_s * 0.3 or n_pairs >= 200:
-            break
-    t_pair = (time.perf_counter() - t0) / n_pairs
-    rows = [glob + 0.01 * torch.randn(P, generator=g) for _ in range(4)]
-    t0 = time.perf_counter()
-    s = sum(r for r in rows)  # krum.py:189 over 4 rows
-    _ = s / multi_k
-    t_mean = (time.perf_counter() - t0) / 4 * multi_k
-    round_s = K * t_client + K * (K - 1) / 2 * t_pair + t_mean
+    t_pair, n_pair = _median_time(lambda: torch.norm(a - b).item(), 5, per)
+    del a, b
+    D = np.abs(np.random.default_rng(0).standard_normal((K, K)))
+    D = D + D.T
+    np.fill_diagonal(D, 0.0)
+    t_sel, _ = _median_time(lambda: np.argsort(orc.krum_scores(D, K - f - 2)), 5, per)
+    mk = max(1, min(multi_k or K // 2, K))
+    chosen = rows[:mk]
+    t_mean, _ = _median_time(lambda: [sum(u[0] for u in chosen) / mk], 5, per)
+    krum_s = K * (K - 1) / 2 * t_pair + t_sel + t_mean * scale
+    agg["krum"] = krum_s
+    mk_tm = max(1, int(mk * trim_ratio))
+    sub = rows[:mk]
+    t_ktm, _ = _median_time(lambda: orc.trimmed_mean(sub, trim_ratio), 3, per)
+    agg["krum_trimmed_mean"] = K * (K - 1) / 2 * t_pair + t_sel + t_ktm * scale
+    key = {"multi_krum": "krum", "none": "fedavg"}.get(defense, defense)
+    agg_s = agg.get(key)
+    round_s = K * t_client + (agg_s if agg_s is not None else 0.0)
     return {
         "value": 1.0 / round_s, "unit": "rounds/s", "cores": threads, "kind": "port",
         "cpu_model": cpu_model(), "host_cpus": host_cpus,
+        "local_update_s_per_client": t_client, "local_update_s_all_clients": K * t_client,
+        "aggregate_ms": {k: v * 1e3 for k, v in agg.items()},
+        "aggregate_ms_this_defense": None if agg_s is None else agg_s * 1e3,
+        "round_s": round_s,
         "sample": (f"oracle (reference loop restated, torch CPU fp32, {threads} threads = this job's CPU share "
-                   f"(OMP_NUM_THREADS) of the host's {host_cpus} CPUs): {n_clients} client "
-                   f"local update(s) x {steps} steps timed ({t_client:.3f} s/client), {n_pairs} Krum pair "
-                   f"norms at P={P} ({t_pair * 1e3:.1f} ms/pair), 4-row mean ({t_mean / multi_k * 1e3:.1f} "
-                   f"ms/row); round = {K}*client + {K * (K - 1) // 2}*pair + {multi_k}*row = {round_s:.1f} s"),
-        "round_s": round_s, "t_client_s": t_client, "t_pair_ms": t_pair * 1e3,
+                   f"(OMP_NUM_THREADS) of the host's {host_cpus} CPUs), medians after one warm-up: one client's "
+                   f"local update x {steps} steps at batch {batch} ({n_client} timed, {t_client:.3f} s); "
+                   f"FedAvg / trimmed mean (t = max(1, int({trim_ratio} K))) / median over K={K} rows at "
+                   f"P_s={P_s} ({n_fa}/{n_tm}/{n_md} timed) scaled x{scale:.1f} to P={P}; Krum = "
+                   f"{K * (K - 1) // 2} pair norms at the full P ({n_pair} timed, {t_pair * 1e3:.2f} ms/pair) + "
+                   f"scores/argsort + the {mk}-row mean; round = K*client + aggregate({key}) = {round_s:.1f} s"),
     }
 
 
@@ -434,6 +486,24 @@ def main() -> None:
     ev1.record()
     torch.cuda.synchronize()
     aggregate_ms = ev0.elapsed_time(ev1) / reps
+    # every hot-path aggregator on this round's client matrix
+    from flr.defenses import get_defense
+    aggregate_ms_all = {}
+    for name in ("fedavg", "krum", "trimmed_mean", "median"):
+        cfg = ({"num_malicious": f if krum else int(0.2 * K), "multi_k": max(1, K // 2)} if name == "krum" else
+               {"trim_ratio": dcfg.get("trim_ratio", 0.1)} if name == "trimmed_mean" else {})
+        d = get_defense(name, cfg)
+        kwd = {"publish": False} if hasattr(d, "publish") else {}
+        run = ((lambda: eng.slice.gather_vector(d.aggregate_sharded(eng.slice, eng.num_examples, **kwd),
+                                                torch.empty_like(eng.global_flat))) if sharded else
+               (lambda: d.aggregate_flat(eng.full, eng.num_examples, **kwd)))
+        run()
+        ev0.record()
+        for _ in range(reps):
+            run()
+        ev1.record()
+        torch.cuda.synchronize()
+        aggregate_ms_all[name] = ev0.elapsed_time(ev1) / reps
     # the dominant aggregation kernel of the headline config: centred-Gram pairwise
     # (HIP events around its launch, on the stream it runs on); sharded: this
     # GPU's coordinates.  Timed for every config (the Krum roofline line).
@@ -498,6 +568,7 @@ def main() -> None:
         "process_group": pg,
         "global_sha256": global_sha256,
         "aggregate_ms": aggregate_ms,
+        "aggregate_ms_by_defense": aggregate_ms_all,
         "train_ms_per_round": train_ms,
         "attackers_selected": attackers_selected,
         "round_roofline": round_roofline(K, P, eng.trainer.live_params, args.local_steps,
@@ -517,8 +588,9 @@ def main() -> None:
             "kernel_ms": kernel_ms, "algorithmic_bytes": pair_bytes, "coords_per_gpu": n_coords,
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and defense == "krum" and model == "resnet_gru":
-        out["cpu_baseline"] = cpu_baseline(spec, P, K, f, multi_k, args.local_steps, rcfg.batch, args.cpu_budget)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(spec, P, K, defense, f, multi_k, args.local_steps, rcfg.batch,
+                                           args.cpu_budget, dcfg.get("trim_ratio", 0.1))
     if rank == 0:
         print(json.dumps(out), flush=True)
 

@@ -45,8 +45,10 @@ const char* flr_last_error(void);
  * fixed-order fp64 reduction of per-segment partials.  Any K >= 1.
  * Pairs the centring cannot condition (two rows close to each other but far
  * from the medoid pivot, e.g. a cluster of sign-flipped updates) are flagged
- * from the pivot sample and recomputed from exact fp32 differences (at most 64
- * such rows per call).
+ * from the pivot sample and recomputed from exact fp32 differences (up to 128
+ * such rows per call: every row at K <= 128).  More flagged rows than that
+ * (K > 128 only) makes every off-diagonal D entry NaN: a loud failure, never a
+ * silently inaccurate distance.
  */
 size_t flr_pairwise_l2_workspace(int64_t K, int64_t P);
 int flr_pairwise_l2(const float* X, int64_t K, int64_t P, int64_t ldx,
@@ -100,8 +102,10 @@ int flr_pairwise_finish(const double* gsum, const double* tail, int64_t K, doubl
  * D[i][j] bit-identical to the reference's fp32 torch.norm(flat_i - flat_j)
  * .item() (krum.py:89-97) — per pair, 8 fp32 lanes of sequential
  * fma(d, d, lane) over every 8th coordinate d = fl(x_i - x_j), the lanes
- * summed 0..7 in order, the P mod 8 tail added as separate multiply + add,
- * correctly rounded sqrt_f32 (oracle/norm_ref.c).  X in the
+ * summed 0..7 in order, the P mod 8 tail added in order (a first group of 4
+ * as separate multiply + add, the last 0..3 as fma), correctly rounded
+ * sqrt_f32 (tail probed in tools/diag_norm_host.py;
+ * oracle/norm_ref.c).  X in the
  * reference's coordinate order (parameters() order); rows 16-B aligned and
  * ldx % 4 == 0 (else FLR_ERR_ARG).  No workspace.  VALU / LDS bound: each
  * pair's 8 chains run the whole vector sequentially. */

@@ -53,14 +53,21 @@ constexpr int TARGET_BLOCKS = 512;
 // e.g. the sign-flipped attackers of a trained round (|x| ~ 1e3 |x_i - x_j|)
 // — cancels catastrophically.  The pivot prepass estimates each pair's
 // cancellation factor (|y_i|^2 + |y_j|^2) / |y_i - y_j|^2 from the exact sample
-// distances; rows in any pair above COND_FLAG (at most RMAX of them, lowest
-// index first) get their mutual distances from exact fp32 differences over the
+// distances; rows in any pair above COND_FLAG (lowest index first, at most
+// RMAX, see below) get their mutual distances from exact fp32 differences over the
 // whole vector instead ("refine" records, kept per canonical slice next to the
 // Gram records so the sharded composition stays bit-identical).
-constexpr int RMAX = 64;                    // refined rows per call
-constexpr int RHDR = 1 + RMAX;              // refine header: count, row list (as doubles)
+// Up to RMAX flagged rows are refined (4 blocks of 32 rows: every row at
+// K <= 128).  More flagged rows than that (K > 128 only, e.g. over 128
+// duplicated clients) is an overflow: the pivot record counts it and every
+// off-diagonal distance of that call is NaN — loud, never silently inaccurate
+// (KrumDefense.publish raises on it).
+constexpr int RMAX = 128;                   // refined rows per call
+constexpr int RNB = RMAX / 32;              // row blocks of the refine list
+constexpr int RNBP = RNB * (RNB + 1) / 2;   // block pairs (a <= b)
+constexpr int RHDR = 2 + RMAX;              // refine header: count, row list, total flagged (as doubles)
 constexpr int RBLK = RHDR + RMAX * RMAX;    // fp64 per slice: header + [RMAX][RMAX] sums
-constexpr int PREC = 2 + RMAX;              // pivot record (int32): pivot, count, rows
+constexpr int PREC = 3 + RMAX;              // pivot record (int32): pivot, count, rows, total flagged
 constexpr double COND_FLAG = 16.0;
 constexpr int RSEG_MAX = 160;               // refine segments per slice (x 8 slices: 1280 workgroups, ~5 per CU)
 constexpr int MAXK_PIVOT = 1024;
@@ -443,7 +450,7 @@ __global__ void reduce_splits_kernel(const double* __restrict__ stage1, int nrec
 }
 
 // ---- refine: exact differences for the flagged rows (see COND_FLAG) ----
-// grid (nseg, 3 block pairs (0,0) (0,1) (1,1) of the row list, slices).  Each
+// grid (nseg, RNBP block pairs (a <= b) of the row list, slices).  Each
 // workgroup sums (x_i - x_j)^2 over its segment of the slice's chunks for the
 // 32 x 32 pairs of its block pair.  The 32 rows of each block are staged per
 // 64-coordinate chunk in LDS ([row][64 + 4]: conflict-free ds_read_b128 under
@@ -456,6 +463,17 @@ __global__ void reduce_splits_kernel(const double* __restrict__ stage1, int nrec
 // partials added in wave order at the end.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int RPAD = CW + 4;
+// block pair index -> (a, b), a <= b, a-major: (0,0) (0,1) .. (0,RNB-1) (1,1) ..
+__host__ __device__ inline int bp_a(int pr) {
+  int a = 0;
+  while (pr >= RNB - a) { pr -= RNB - a; ++a; }
+  return a;
+}
+__host__ __device__ inline int bp_b(int pr) {
+  int a = 0;
+  while (pr >= RNB - a) { pr -= RNB - a; ++a; }
+  return a + pr;
+}
 __global__ __launch_bounds__(256) void refine_partials_kernel(const float* __restrict__ X, int64_t ldx,
                                                               int64_t nch_total, int q_base, int64_t chunk0,
                                                               const int* __restrict__ prec, int nseg,
@@ -465,7 +483,7 @@ __global__ __launch_bounds__(256) void refine_partials_kernel(const float* __res
   __shared__ double red[1024];
   const int c = prec[1];
   const int pr = blockIdx.y;
-  const int a = pr == 2 ? 1 : 0, b = pr == 0 ? 0 : 1;
+  const int a = bp_a(pr), b = bp_b(pr);
   if (32 * b >= c) return;  // an empty block of the row list (uniform: the whole workgroup leaves)
   const int seg = blockIdx.x;
   const int q = q_base + (int)blockIdx.z;
@@ -556,7 +574,7 @@ __global__ __launch_bounds__(256) void refine_partials_kernel(const float* __res
     __syncthreads();
   }
   if (wave == 0) {
-    double* rec = rpart + (((int64_t)blockIdx.z * 3 + pr) * nseg + seg) * 1024;
+    double* rec = rpart + (((int64_t)blockIdx.z * RNBP + pr) * nseg + seg) * 1024;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -572,12 +590,12 @@ __global__ __launch_bounds__(256) void refine_reduce_kernel(const double* __rest
   const int z = blockIdx.y, pr = blockIdx.x;
   double* blk = gsum + (int64_t)z * glen + (int64_t)ngroups * REC;
   const int c = prec[1];
-  if (pr == 0)
+  if (pr == 0)  // header: count, the RMAX row slots, the total flagged count
     for (int t = threadIdx.x; t < RHDR; t += 256) blk[t] = t == 0 ? (double)c : (double)prec[1 + t];
-  const int a = pr == 2 ? 1 : 0, b = pr == 0 ? 0 : 1;
+  const int a = bp_a(pr), b = bp_b(pr);
   if (32 * b >= c) return;
   for (int e = threadIdx.x; e < 1024; e += 256) {
-    const double* p = rpart + ((int64_t)z * 3 + pr) * nseg * 1024 + e;
+    const double* p = rpart + ((int64_t)z * RNBP + pr) * nseg * 1024 + e;
     double s = 0.0;
 #pragma unroll 16
     for (int k = 0; k < nseg; ++k) s += p[(int64_t)k * 1024];  // independent loads, 16 in flight
@@ -588,7 +606,8 @@ __global__ __launch_bounds__(256) void refine_reduce_kernel(const double* __rest
 // Rows to refine, from the exact sample distances Ds and the pivot (one
 // workgroup): row i is flagged when some j has
 //   Ds[i][j]^2 * COND_FLAG < Ds[i][p]^2 + Ds[j][p]^2.
-// The first RMAX flagged rows in index order go to prec[2..], their count to prec[1].
+// The first RMAX flagged rows in index order go to prec[2..], their count to
+// prec[1], the number of flagged rows (may exceed RMAX) to prec[2 + RMAX].
 __global__ __launch_bounds__(256) void flag_rows_kernel(const double* __restrict__ Ds, int K, int* __restrict__ prec) {
   __shared__ unsigned char flag[MAXK_PIVOT];
   const int p = prec[0];
@@ -604,11 +623,15 @@ __global__ __launch_bounds__(256) void flag_rows_kernel(const double* __restrict
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int c = 0;
-    for (int i = 0; i < K && c < RMAX; ++i)
-      if (flag[i]) prec[2 + c++] = i;
+    int c = 0, total = 0;
+    for (int i = 0; i < K; ++i)
+      if (flag[i]) {
+        if (c < RMAX) prec[2 + c++] = i;
+        ++total;
+      }
     prec[1] = c;
     for (int t = c; t < RMAX; ++t) prec[2 + t] = 0;
+    prec[2 + RMAX] = total;
   }
 }
 
@@ -680,6 +703,10 @@ __global__ void assemble_kernel(const double* __restrict__ gsum, int ngroups, in
   // a refined pair (both rows in the refine list): the exact-difference sums
   const double* hdr = gsum + (int64_t)ngroups * REC;  // slice 0's header (every slice holds the same)
   const int c = (int)hdr[0];
+  if ((int)hdr[1 + RMAX] > c) {  // more flagged rows than the refine list holds: loud, not inaccurate
+    D[idx] = __builtin_nan("");
+    return;
+  }
   int pi = -1, pj = -1;
   for (int u = 0; u < c; ++u) {
     const int row = (int)hdr[1 + u];
@@ -841,7 +868,7 @@ inline Layout layout(int64_t K, int64_t P, int nsl = FLR_PW_SLICES) {
   l.spart = take((size_t)direct_npairs(K) * SAMPLE_NSEG * 1024 * sizeof(float));
   l.ds = take((size_t)K * K * sizeof(double));
   l.pivot = take(PREC * sizeof(int));
-  l.rpart = take((size_t)nsl * 3 * refine_nseg(P) * 1024 * sizeof(double));
+  l.rpart = take((size_t)nsl * RNBP * refine_nseg(P) * 1024 * sizeof(double));
   l.total = off;
   return l;
 }
@@ -1058,10 +1085,10 @@ int gram_phase(const GramArgs& a, double* stage1, double* gsum, double* rpart, h
   // the flagged rows' exact-difference records of these slices (workgroups of an
   // empty row-list block leave at once)
   const int rseg = refine_nseg(a.P);
-  hipLaunchKernelGGL(refine_partials_kernel, dim3(rseg, 3, a.nsl), dim3(256), 0, st, a.X, a.ldx, p.nchunks, a.q0,
-                     a.chunk0, a.pivot, rseg, rpart);
+  hipLaunchKernelGGL(refine_partials_kernel, dim3(rseg, RNBP, a.nsl), dim3(256), 0, st, a.X, a.ldx, p.nchunks,
+                     a.q0, a.chunk0, a.pivot, rseg, rpart);
   if ((rc = launch_status("refine_partials_kernel")) != FLR_OK) return rc;
-  hipLaunchKernelGGL(refine_reduce_kernel, dim3(3, a.nsl), dim3(256), 0, st, rpart, rseg, a.pivot, p.ngroups(),
+  hipLaunchKernelGGL(refine_reduce_kernel, dim3(RNBP, a.nsl), dim3(256), 0, st, rpart, rseg, a.pivot, p.ngroups(),
                      glen, gsum);
   return launch_status("refine_reduce_kernel");
 }

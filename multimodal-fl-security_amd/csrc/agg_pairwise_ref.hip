@@ -7,7 +7,9 @@
 //   d = fl(x_i - x_j) elementwise;
 //   8 fp32 lanes, lane c = fma(d[8r+c], d[8r+c], lane c) sequentially over r;
 //   s = lane 0 + lane 1 + ... + lane 7 (in that order);
-//   s = s + fl(d[t] * d[t]) for each tail element t >= 8*floor(P/8);
+//   the tail t >= 8*floor(P/8): while 4 or more remain, the next 4 as
+//   s = s + fl(d[t] * d[t]) (separate multiply and add), then the last
+//   0..3 as s = fma(d[t], d[t], s);
 //   sqrt_f32(s) (correctly rounded), widened to fp64 by .item().
 // Every fp32 operation here is that operation, in that order, so D is the
 // reference's D bit for bit — no tolerance, no margin argument.
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(THREADS) void ref_norm_kernel(const float* __restri
       }
     }
   }
-  // lane sum 0..7 in order, then the tail (separate multiply and add), sqrt
+  // lane sum 0..7 in order, then the tail, correctly rounded sqrt
   red[tid] = acc;
   __syncthreads();
   if (cp == 0 && i < j && j < K) {
@@ -136,11 +138,17 @@ __global__ __launch_bounds__(THREADS) void ref_norm_kernel(const float* __restri
     s = add_rn(s, l67[1]);
     const float* xi = X + (int64_t)i * ldx;
     const float* xj = X + (int64_t)j * ldx;
-    for (int64_t t = R * 8; t < P; ++t) {
+    int64_t t = R * 8;
+    if (t + 4 <= P)
+      for (const int64_t e = t + 4; t < e; ++t) {
+        const float d = xi[t] - xj[t];
+        s = add_rn(s, mul_rn(d, d));
+      }
+    for (; t < P; ++t) {
       const float d = xi[t] - xj[t];
-      s = add_rn(s, mul_rn(d, d));
+      s = __builtin_fmaf(d, d, s);
     }
-    const double v = (double)__fsqrt_rn(s);
+    const double v = (double)sqrt_rn(s);
     D[(int64_t)i * K + j] = v;
     D[(int64_t)j * K + i] = v;
   }

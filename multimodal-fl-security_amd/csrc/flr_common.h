@@ -34,4 +34,22 @@ __device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, 
 __device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }
 __device__ __forceinline__ float div_rn(float a, float b) { return __fdiv_rn(a, b); }
 
+// Correctly rounded fp32 sqrt (std::sqrt / torch's sqrt on the CPU).  HIP's
+// __fsqrt_rn is the native v_sqrt_f32 (up to 1 ulp off) unless the OCML
+// rounded operations are enabled, so the candidate is checked against the
+// rounding midpoints in fp64 (exact: a midpoint has 25 significant bits, its
+// square at most 50) and moved by one ulp when needed.
+__device__ __forceinline__ float sqrt_rn(float s) {
+  float r = __builtin_sqrtf(s);
+  if (!(s > 0.f) || !(r < __builtin_huge_valf())) return r;  // 0, negative, NaN, inf
+  const uint32_t u = __float_as_uint(r);
+  const float up = __uint_as_float(u + 1), dn = __uint_as_float(u - 1);
+  const double sd = (double)s, rd = (double)r;
+  const double hi = 0.5 * (rd + (double)up);
+  if (sd > hi * hi) return up;
+  const double lo = 0.5 * (rd + (double)dn);
+  if (sd < lo * lo) return dn;
+  return r;
+}
+
 }  // namespace flr

@@ -81,9 +81,17 @@ class KrumDefense(BaseDefense):
         return ops.rows_mean(cs.X, self.order_device[: min(self.multi_k, n)], divisor=self.multi_k)
 
     def publish(self) -> None:
-        """Host copies of scores / selected / rejected (krum.py:171-176)."""
+        """Host copies of scores / selected / rejected (krum.py:171-176).
+        NaN scores from finite distances cannot arise; a NaN distance matrix is
+        the Gram path's loud refine-capacity overflow (include/flr.h) or NaN
+        client updates — raised here rather than published as a selection."""
         order_host = self.order_device.cpu().tolist()
         self.client_scores = self.scores_device.cpu().tolist()
+        if any(s != s for s in self.client_scores):
+            from .._capi import FlrError
+            raise FlrError("KrumDefense", -3, "NaN Krum scores: NaN client updates, or more far-cluster rows "
+                                              "than the Gram path refines (use pairwise_method='direct' or "
+                                              "'reference')")
         self.selected_clients = order_host[: self.multi_k]
         self.rejected_clients = order_host[self.multi_k:]
 

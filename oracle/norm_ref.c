@@ -4,7 +4,11 @@
  * (tests/test_oracle.py pins this file against torch.norm
  * itself on random vectors of many lengths):
  *   d = fl(a - b); 8 fp32 lanes, lane c = fma(d[8r+c], d[8r+c], lane c) over r;
- *   s = lane 0 + ... + lane 7 in order; s = s + fl(d[t]*d[t]) for the tail;
+ *   s = lane 0 + ... + lane 7 in order;
+ *   tail (the P mod 8 last elements): while 4 or more remain, the next 4 as
+ *   s = s + fl(d[t]*d[t]) (separate multiply and add), the last 0..3 as
+ *   s = fma(d[t], d[t], s) — the compiled scalar tail loop of torch's norm
+ *   kernel (probed: tools/diag_norm_host.py, tests/test_oracle.py);
  *   sqrt_f32(s).
  * Built by oracle/Makefile with -ffp-contract=off (no implicit contraction). */
 #include <math.h>
@@ -20,10 +24,16 @@ float flr_oracle_norm_diff(const float* a, const float* b, int64_t n) {
     }
   float s = lane[0];
   for (int c = 1; c < 8; ++c) s = s + lane[c];
-  for (int64_t t = nf; t < n; ++t) {
+  int64_t t = nf;
+  if (t + 4 <= n)
+    for (const int64_t e = t + 4; t < e; ++t) {
+      const float d = a[t] - b[t];
+      const float q = d * d;
+      s = s + q;
+    }
+  for (; t < n; ++t) {
     const float d = a[t] - b[t];
-    const float q = d * d;
-    s = s + q;
+    s = fmaf(d, d, s);
   }
   return sqrtf(s);
 }

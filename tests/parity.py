@@ -1,0 +1,79 @@
+"""Per-tensor training parity on the UPDATE.
+
+A whole-vector bound max|a - b| / max|b| is set by the largest weight (the
+N(0,1) embedding table, ~4.4) and would not notice a zeroed conv weight
+gradient (one clipped step moves a conv weight by ~5e-6).  These helpers
+compare, parameter tensor by parameter tensor in parameters() order
+(param_layout), the update Δ = trained - global of the engine's row against
+the oracle's Δ (run_experiments.py:206-238 restated by oracle.training):
+
+* delta_rel      = max|Δ_gpu - Δ_ref| / max|Δ_ref|  (the raw figure)
+* delta_rel_ulp  = max over elements of (|w_gpu - w_ref| - 2 ulp(w_ref))_+ /
+                   max|Δ_ref|: the same, after forgiving the last two fp32
+                   roundings of the stored weight itself.  Both trainers store
+                   fl(w - lr * buf) every step; where |w| >> |Δ| (the embedding
+                   table: ulp(4) = 4.8e-7 against updates ~1e-5) one ulp of the
+                   stored weight is a percent of Δ, so the raw figure measures
+                   fp32 storage, not the gradient.  A wrong or missing gradient
+                   still shows at full size (Δ_gpu - Δ_ref ~ Δ_ref, thousands
+                   of ulps for a conv weight).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _ulp(x: np.ndarray) -> np.ndarray:
+    a = np.abs(x.astype(np.float32))
+    return (np.nextafter(a, np.float32(np.inf)) - a).astype(np.float64)
+
+
+def delta_report(got: torch.Tensor, ref: torch.Tensor, glob: torch.Tensor,
+                 layout: List[Tuple[str, torch.Size]]) -> Dict:
+    """got / ref / glob: flat fp32 vectors in torch (parameters()) order."""
+    g = got.detach().cpu().numpy().astype(np.float64)
+    r = ref.detach().cpu().numpy().astype(np.float64)
+    w0 = glob.detach().cpu().numpy().astype(np.float64)
+    ulp = _ulp(ref.detach().cpu().numpy())
+    out, off = {}, 0
+    for name, shape in layout:
+        n = int(np.prod(shape)) if len(shape) else 1
+        sl = slice(off, off + n)
+        off += n
+        dg, dr = g[sl] - w0[sl], r[sl] - w0[sl]
+        scale = float(np.abs(dr).max()) if n else 0.0
+        diff = np.abs(g[sl] - r[sl])
+        if scale == 0.0:
+            out[name] = {"max_delta_ref": 0.0, "max_abs_diff": float(diff.max()) if n else 0.0,
+                         "delta_rel": 0.0 if not n or diff.max() == 0 else float("inf"), "delta_rel_ulp": 0.0}
+            continue
+        out[name] = {"max_delta_ref": scale, "max_abs_diff": float(diff.max()),
+                     "delta_rel": float(np.abs(dg - dr).max() / scale),
+                     "delta_rel_ulp": float(np.maximum(diff - 2.0 * ulp[sl], 0.0).max() / scale)}
+    assert off == g.size, (off, g.size)
+    worst = max(out, key=lambda k: out[k]["delta_rel_ulp"])
+    worst_raw = max(out, key=lambda k: out[k]["delta_rel"])
+    return {"per_tensor": out, "worst_tensor": worst, "worst_delta_rel_ulp": out[worst]["delta_rel_ulp"],
+            "worst_raw_tensor": worst_raw, "worst_delta_rel": out[worst_raw]["delta_rel"]}
+
+
+def record(name: str, payload: Dict) -> None:
+    d = os.environ.get("FLR_RECORD_DIR", os.path.join(ROOT, "gpurun_out", "records"))
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, name), "w") as fh:
+        json.dump(payload, fh, indent=1)
+    print(f"\n[record {name}] " + json.dumps({k: v for k, v in payload.items() if not isinstance(v, (list, dict))}))
+
+
+def check_delta(reports: Dict[str, Dict], bound: float = 1e-5) -> None:
+    """Assert every tensor of every report within `bound` (delta_rel_ulp)."""
+    bad = {(c, t): r["per_tensor"][t]["delta_rel_ulp"] for c, r in reports.items()
+           for t in r["per_tensor"] if r["per_tensor"][t]["delta_rel_ulp"] > bound}
+    assert not bad, bad

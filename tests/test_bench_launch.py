@@ -64,3 +64,18 @@ def test_bench_two_gloo_ranks_equal_one(cuda):
     assert two["process_group"] == {"backend": "gloo", "world_size": 2}
     assert two["global_sha256"] == one["global_sha256"]
     assert two["attackers_selected"] == one["attackers_selected"] == []
+
+
+def test_cpu_baseline_every_aggregator():
+    """cpu_baseline reports a local-update time and the
+    aggregate-ms of every hot-path aggregator, for any defense (TINY model,
+    small budget)."""
+    from flr.models.multimodal import TINY, num_params
+    P = num_params(TINY)
+    out = bench.cpu_baseline(TINY, P, 8, "trimmed_mean", 1, 4, 2, 4, budget_s=2.0)
+    assert set(out["aggregate_ms"]) == {"fedavg", "krum", "trimmed_mean", "median", "krum_trimmed_mean"}
+    assert all(v > 0 for v in out["aggregate_ms"].values())
+    assert out["aggregate_ms_this_defense"] == out["aggregate_ms"]["trimmed_mean"]
+    assert out["value"] == pytest.approx(1.0 / (8 * out["local_update_s_per_client"]
+                                                + out["aggregate_ms"]["trimmed_mean"] * 1e-3))
+    assert out["kind"] == "port" and out["cores"] >= 1

@@ -30,7 +30,8 @@ from oracle import aggregation as orc
 from oracle import training as otrain
 from flr import ops
 from flr.matrix import padded_ld
-from flr.models.multimodal import VIT_BERT, ModelSpec, model_class
+from flr.models.multimodal import VIT_BERT, ModelSpec, model_class, param_layout
+from parity import check_delta, delta_report
 from flr.round import RoundConfig, RoundEngine
 from flr.train import TrainConfig, make_dropout_masks, synthetic_batches
 
@@ -212,18 +213,27 @@ def _sample_rows(eng, clients, idx: torch.Tensor) -> torch.Tensor:
     return torch.stack(out)
 
 
-def _check_clients(eng, spec, glob, clients, batches_dev, masks_dev, negate=()):
+def _check_clients(eng, spec, glob, clients, batches_dev, masks_dev, negate=(), losses=False):
+    """Sampled clients' rows vs the oracle loop: whole vector at 1e-5 and the
+    per-tensor update report (tests/parity.py); returns the reports."""
+    reps = {}
     for k in clients:
         j = k - eng.lo
         cb = [(im[j].cpu(), tk[j].cpu(), lb[j].cpu()) for im, tk, lb in batches_dev]
         cm = None if masks_dev is None else [m[j].cpu() for m in masks_dev]
-        upd, _ = otrain.local_update(model_class(spec), spec, glob, cb, masks=cm)
+        upd, ref_loss = otrain.local_update(model_class(spec), spec, glob, cb, masks=cm)
         ref = torch.cat([u.reshape(-1) for u in upd])
-        if k in negate:
-            ref = -ref
         row = eng.trainer.X.data[j, : eng.trainer.P]
         row = eng.trainer.to_torch_order(row) if eng.train_order else row
+        reps[f"client{k}"] = delta_report(-row if k in negate else row, ref, glob, param_layout(spec))
+        if losses:
+            got = eng.losses[j].item()
+            reps[f"client{k}"]["loss_rel_err"] = abs(got - ref_loss) / max(1.0, abs(ref_loss))
+            assert reps[f"client{k}"]["loss_rel_err"] <= 1e-5
+        if k in negate:
+            ref = -ref
         assert _rel(row.cpu(), ref) < 1e-5, (k, _rel(row.cpu(), ref))
+    return reps
 
 
 @pytest.mark.timeout(600)
@@ -239,7 +249,9 @@ def test_c4_round_trimmed_mean_vit_bert(cuda):
     new = eng.run_round().clone()
     torch.cuda.synchronize()
     assert eng.defense.num_trimmed_per_end == 25
-    _check_clients(eng, spec, glob, [0, 77, 200, 255], eng.batches, eng.masks)
+    reps = _check_clients(eng, spec, glob, [0, 77, 200, 255], eng.batches, eng.masks)
+    _record("c4_update_parity_b8_1step.json", {"config": "C4 round, B=8, 1 step", **reps})
+    check_delta(reps)
     P = eng.trainer.P
     idx = _strided(P)
     sub = _sample_rows(eng, range(K), idx)
@@ -272,7 +284,10 @@ def test_c5_round_backdoor_krum_trimmed_mean(cuda):
     new = eng.run_round().clone()
     eng.defense.publish()
     torch.cuda.synchronize()
-    _check_clients(eng, spec, glob, [0, 101, 102, 511], eng.batches, eng.masks)
+    reps = _check_clients(eng, spec, glob, [0, 101, 102, 511], eng.batches, eng.masks)
+    _record("c5_update_parity_b32_1step.json", {"config": "C5 round, B=32, 1 step (backdoor clients 0, 101)",
+                                                **reps})
+    check_delta(reps)
     P = eng.trainer.P
     X = eng.trainer.X.data[:, :P]
     D_gpu = eng.defense.distances.double()
@@ -300,3 +315,31 @@ def test_c5_round_backdoor_krum_trimmed_mean(cuda):
         "P": P, "distance_rel_err_gpu_vs_fp64": dist_err, "coords_checked": int(idx.numel()),
         "aggregate_rel_err": err, "backdoor_clients_selected": sorted(set(sel) & set(range(f))), **rep})
     assert err < 1e-5, err
+
+
+@pytest.mark.timeout(900)
+def test_c4_round_bench_shape_update_parity(cuda):
+    """C4 at the bench's own training shape (B = 32, 5 local steps, K = 256
+    trimmed mean, ViT-S/4 + BERT-mini): two sampled clients' updates per
+    tensor and their losses against the oracle loop (run_experiments.py:
+    206-238), and the aggregate against oracle.trimmed_mean on a strided
+    sample."""
+    spec = VIT_BERT
+    K, B, steps = 256, 32, 5
+    rc = RoundConfig(num_clients=K, batch=B, defense="trimmed_mean", defense_cfg={"trim_ratio": 0.1},
+                     attack="none", num_attackers=0)
+    eng = RoundEngine(spec, rc, TrainConfig(local_steps=steps), cuda)
+    glob = eng.global_flat.clone().cpu()
+    new = eng.run_round().clone()
+    torch.cuda.synchronize()
+    reps = _check_clients(eng, spec, glob, [3, 250], eng.batches, eng.masks, losses=True)
+    P = eng.trainer.P
+    idx = _strided(P, 400_000)
+    sub = _sample_rows(eng, range(K), idx)
+    want, t = orc.trimmed_mean([[sub[k]] for k in range(K)], 0.1)
+    err = _rel(new[idx.to(cuda)].cpu(), want[0])
+    _record("c4_update_parity_bench_shape.json", {"config": "C4 round at the bench shape: K=256 trimmed mean, "
+                                                            "ViT-S/4 + BERT-mini, B=32, 5 local steps",
+                                                  "aggregate_rel_err": err, **reps})
+    assert err < 1e-5, err
+    check_delta(reps)

@@ -7,8 +7,9 @@ import pytest
 import torch
 
 from oracle import training as otrain
+from parity import check_delta, delta_report, record
 from flr import native_trainer as nt
-from flr.models.multimodal import TINY, ModelSpec, MultimodalNet
+from flr.models.multimodal import TINY, ModelSpec, MultimodalNet, param_layout
 from flr.round import initial_global
 from flr.train import ClientBatchTrainer, TrainConfig, make_dropout_masks, synthetic_batches
 
@@ -53,6 +54,7 @@ def test_native_trainer_matches_reference_loop(cuda):
     batches = synthetic_batches(spec, steps, range(K), B, cuda)
     masks = make_dropout_masks(spec, steps, K, B, cuda, seed=3)
     X, loss, _ = nt.train_clients(spec, glob, batches, TrainConfig(local_steps=steps), masks)
+    reps = {}
     for k in range(K):
         cb = [(im[k].cpu(), tk[k].cpu(), lb[k].cpu()) for im, tk, lb in batches]
         upd, ref_loss = otrain.local_update(MultimodalNet, spec, glob.cpu(), cb, masks=[m[k].cpu() for m in masks])
@@ -60,6 +62,10 @@ def test_native_trainer_matches_reference_loop(cuda):
         err = ((X[k].cpu().double() - ref.double()).abs().max() / ref.abs().max()).item()
         assert err < 1e-5, err
         assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+        reps[f"client{k}"] = delta_report(X[k], ref, glob, param_layout(spec))
+    record("native_resnet_gru_update_parity.json",
+           {"config": "flr_train_clients, ResNet-18 + GRU, K=2, B=8, 2 steps, dropout masks", **reps})
+    check_delta(reps)
 
 
 def _vit_python(spec, glob, batches, masks, K, steps, chunk, nneg, cuda):
@@ -106,6 +112,7 @@ def test_native_vit_bert_matches_reference_loop(cuda):
     tr = nt.NativeRoundTrainer(spec, K, cuda, TrainConfig(local_steps=steps), batch=B)
     tr.load_global(glob)
     loss = tr.local_update(batches, masks).cpu()
+    reps = {}
     for k in range(K):
         cb = [(im[k].cpu(), tk[k].cpu(), lb[k].cpu()) for im, tk, lb in batches]
         upd, ref_loss = otrain.local_update(model_class(spec), spec, glob.cpu(), cb, masks=[m[k].cpu() for m in masks])
@@ -114,3 +121,7 @@ def test_native_vit_bert_matches_reference_loop(cuda):
         err = ((got.double() - ref.double()).abs().max() / ref.abs().max()).item()
         assert err < 1e-5, err
         assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+        reps[f"client{k}"] = delta_report(got, ref, glob, param_layout(spec))
+    record("native_vit_bert_tiny_update_parity.json",
+           {"config": "flr_train_vit_bert, ViT/BERT tiny, K=3, B=8, 3 steps, dropout masks", **reps})
+    check_delta(reps)

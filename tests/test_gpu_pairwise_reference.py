@@ -34,7 +34,7 @@ def _matrix(K, P, seed, device):
     return X, data.to(device)
 
 
-@pytest.mark.parametrize("K,P", [(2, 0), (2, 1), (3, 7), (5, 8), (7, 9), (9, 255), (12, 256), (13, 257),
+@pytest.mark.parametrize("K,P", [(2, 0), (2, 1), (3, 7), (5, 8), (7, 9), (9, 255), (12, 256), (13, 257), (5, 12), (6, 13), (7, 15), (4, 4), (4, 6),
                                  (16, 4099), (33, 2053), (40, 65537), (1, 100)])
 def test_reference_mode_equals_torch_norm(cuda, K, P):
     X, data = _matrix(K, P, K * 1000 + P, cuda)

@@ -4,9 +4,11 @@ trained parameters within 1e-5 (north_star)."""
 import pytest
 import torch
 
+from parity import check_delta, delta_report, record
+
 from oracle import training as otrain
 from flr.client import Client
-from flr.models.multimodal import CUB, TINY, ModelSpec, MultimodalNet, model_class, num_params
+from flr.models.multimodal import CUB, TINY, ModelSpec, MultimodalNet, model_class, num_params, param_layout
 from flr.round import initial_global
 from flr.train import ClientBatchTrainer, TrainConfig, make_dropout_masks, synthetic_batches
 
@@ -265,6 +267,15 @@ def test_c2_round_fedavg_matches_reference(cuda):
         losses.append(ref_loss)
     ref = torch.cat([t.reshape(-1) for t in orc.fedavg(ups, [steps * B] * K)])
     assert _rel(new, ref) < 1e-5, _rel(new, ref)
+    layout = param_layout(spec)
+    reps = {"aggregate": delta_report(new, ref, glob, layout)}
+    X = eng.trainer.X.data[:, : eng.trainer.P]
+    for k in (0, 31):
+        row = eng.trainer.to_torch_order(X[k]) if eng.train_order else X[k]
+        reps[f"client{k}"] = delta_report(row, torch.cat([u.reshape(-1) for u in ups[k]]), glob, layout)
+    record("c2_update_parity.json", {"config": "C2: FedAvg K=32, ResNet-18 + GRU, B=32, 2 local steps",
+                                     **{c: r for c, r in reps.items()}})
+    check_delta(reps)
     got_loss = eng.losses.cpu()
     err = max(abs(got_loss[k].item() - losses[k]) / max(1.0, abs(losses[k])) for k in range(K))
     print(f"\n[C2 round] weights rel err {_rel(new, ref):.2e}, max loss rel err {err:.2e}")
@@ -291,14 +302,20 @@ def test_c3_round_multikrum_signflip(cuda):
     X = eng.trainer.X.data[:, : eng.trainer.P]
     batches = synthetic_batches(spec, steps, [0, 24, 25, 127], B, "cpu")
     masks = make_dropout_masks(spec, steps, [0, 24, 25, 127], B, "cpu", seed=rc.seed + 7919)
+    reps = {}
     for j, k in enumerate([0, 24, 25, 127]):
         cb = [(im[j], tk[j], lb[j]) for im, tk, lb in batches]
         upd, _ = otrain.local_update(MultimodalNet, spec, glob, cb, masks=[m[j] for m in masks])
         ref = torch.cat([u.reshape(-1) for u in upd])
+        row = eng.trainer.to_torch_order(X[k]) if eng.train_order else X[k]  # X is in training order
+        # the update is compared before the sign flip (the attackers submit -row)
+        reps[f"client{k}"] = delta_report(-row if k < f else row, ref, glob, param_layout(spec))
         if k < f:
             ref = -ref
-        row = eng.trainer.to_torch_order(X[k]) if eng.train_order else X[k]  # X is in training order
         assert _rel(row.cpu(), ref) < 1e-5, (k, _rel(row.cpu(), ref))
+    record("c3_update_parity_1step.json", {"config": "C3 round: K=128 Multi-Krum sign flip, B=8, 1 local step",
+                                           **reps})
+    check_delta(reps)
     D = eng.defense.distances.cpu().numpy()
     scores = orc.krum_scores(D, K - f - 2)
     import numpy as np

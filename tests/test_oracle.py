@@ -166,6 +166,18 @@ def test_norm_ref_model_equals_torch_norm(n):
         assert got == want, (n, seed, got, want)
 
 
+@pytest.mark.parametrize("n", list(range(1, 17)) + [20, 23, 100, 1001, 4099])
+def test_norm_ref_model_tail_lengths(n):
+    """The P mod 8 tail (every length 0..7 after 0..N full 8-lane steps), 200
+    seeds each: a 4-element group as separate multiply + add, the rest fma."""
+    from oracle import normref
+    for seed in range(200):
+        g = torch.Generator().manual_seed(n * 1000 + seed)
+        a = torch.randn(n, generator=g) * 3
+        b = torch.randn(n, generator=g)
+        assert normref.norm_diff(a.numpy(), b.numpy()) == torch.norm(a - b).item(), (n, seed)
+
+
 def test_norm_ref_model_thread_independent():
     """A single-output fp32 norm is one sequential reduction whatever the
     intra-op thread count (C3's P = 11,800,394)."""
