@@ -288,7 +288,7 @@ def gemm_flops_per_sample(spec) -> float:
     return 2.0 * (3 * sum(macs) - (macs[0] if macs else 0))
 
 
-def gemm_utilisation(spec, K: int, batch: int, steps: int, stats_path=None):
+def gemm_utilisation(spec, K: int, batch: int, steps: int, stats_path=None, chunk: int = 32):
     """Batched-GEMM MFMA utilisation for the encoder family (C4/C5): useful GEMM
     FLOPs per round (gemm_flops_per_sample) over the BGemm kernels' summed time
     per round in a rocprofv3 summary of that config's bench (--kernel-stats; the
@@ -305,8 +305,8 @@ def gemm_utilisation(spec, K: int, batch: int, steps: int, stats_path=None):
             calls_ce += calls
     if not calls_ce or not ms:
         return None
-    # the cross-entropy kernel runs once per client chunk (32 clients) and local step
-    rounds = calls_ce / (steps * max(1, -(-K // 32)))
+    # the cross-entropy kernel runs once per client chunk and local step (K = this GPU's clients)
+    rounds = calls_ce / (steps * max(1, -(-K // max(1, chunk))))
     per_round = ms / rounds
     achieved = flops / (per_round * 1e-3) / 1e12
     peak = 2500.0 / 6.0
@@ -576,9 +576,9 @@ def main() -> None:
         "conv_mfma_from_profile": conv_utilisation(spec, K, rcfg.batch, args.local_steps, args.kernel_stats)
         if args.config == "C3" and not custom else None,
         "gemm_mfma_from_profile": gemm_utilisation(
-            spec, K, rcfg.batch, args.local_steps,
+            spec, K // world, rcfg.batch, args.local_steps,
             args.kernel_stats or (os.path.join(ROOT, COMMITTED_C4_STATS) if args.config == "C4" and not custom
-                                  else None))
+                                  else None), chunk=eng.trainer.chunks[0][1] - eng.trainer.chunks[0][0])
         if model == "vit_bert" else None,
         "collectives": round_collectives(eng, defense, K, P, world),
         "roofline": {

@@ -12,6 +12,12 @@
 // stream is capturing runs the update on the caller's stream instead — same
 // results, no overlap).
 //
+// One stream and one event set per device, shared by every trainer of the
+// process: with FLR_SGD_OVERLAP=1 at most one training call may be in flight
+// per device at a time (two concurrent callers would record and wait on the
+// same events).  A model with more parameter groups than NEV - 1 updates on
+// the caller's stream (no overlap, same results).
+//
 // Off by default (FLR_SGD_OVERLAP=1 turns it on).  Measured at C3 on MI355X
 // (tools/gpu_r3_k.sh, gpu_r3_l.sh): 79 % of the optimizer's kernel time does
 // run concurrently with the forward's kernels, but both slow down by as much

@@ -232,7 +232,6 @@ class Net {
     gorder_.assign(1, gtext_);
     for (int g = 0; g < gtext_; ++g) gorder_.push_back(g);
     gorder_.push_back(ghead_);
-    if ((int)gthr_.size() + 1 > SideStream::NEV) return FLR_ERR_UNSUPPORTED;
     // tap-major convs and their dead taps (flr.train.ClientBatchTrainer)
     mark_conv(stem_);
     for (auto& bk : blocks_) {
@@ -687,7 +686,9 @@ class Net {
     if (src)
       for (const auto& b : blocks_opt_) soffs.push_back(ps_[b.j].tap ? ps_[b.j].off + b.o : -1);
     const int flags = int(first) | (int(last) << 1);
-    if (last || !side_) {  // the last step writes X: nothing after it in the call to overlap
+    // the last step writes X: nothing after it in the call to overlap; a model with
+    // more parameter groups than the side stream has events updates on the caller's stream
+    if (last || !side_ || (int)gthr_.size() + 1 > SideStream::NEV) {
       FLR_TRY(flr_clip_sgd_step_blocked_src(xb.data(), gb.data(), mb.data(), nb.data(), cs.data(),
                                             (int64_t)xb.size(), K_, lr, mom, wd_, clip_, flags, last ? xout_ : nullptr,
                                             last && xout_ ? xoffs.data() : nullptr, xld_, xneg_,

@@ -48,6 +48,10 @@ class RoundConfig:
     exchange: str = "auto"               # "alltoall" | "allgather" | "auto" (alltoall when the defense shards)
     graph: bool = True                   # replay the training phase as one captured HIP graph (FLR_GRAPH=0: eager)
     fallback_fedavg: bool = False        # defense raises -> FedAvg of the round (robust_server.py:120-122)
+    # with fallback_fedavg: also fall back on library / device errors (FlrError,
+    # out of memory), as the reference's `except Exception` does (True, the
+    # default); False re-raises them and falls back on defense-logic errors only
+    fallback_device_errors: bool = True
 
 
 def initial_global(spec: ModelSpec, seed: int, device) -> torch.Tensor:
@@ -196,11 +200,13 @@ class RoundEngine:
 
     def _fallback(self, err: Exception, X: torch.Tensor) -> torch.Tensor:
         """robust_server.py:120-122: a failing defense falls back to FedAvg
-        (only with RoundConfig.fallback_fedavg; otherwise the error propagates)."""
+        (only with RoundConfig.fallback_fedavg; otherwise the error propagates).
+        The reference catches every Exception; RoundConfig.fallback_device_errors
+        = False keeps device / library failures (kernel launch, workspace, HIP or
+        RCCL errors, out of memory) loud instead."""
         from ._capi import FlrError
-        # device / library failures (kernel launch, workspace, HIP or RCCL errors)
-        # are real faults, not defense-logic errors: never hidden behind FedAvg
-        if not self.rcfg.fallback_fedavg or isinstance(err, (FlrError, torch.cuda.OutOfMemoryError)):
+        device_error = isinstance(err, (FlrError, torch.cuda.OutOfMemoryError))
+        if not self.rcfg.fallback_fedavg or (device_error and not self.rcfg.fallback_device_errors):
             raise err
         logging.getLogger(__name__).error("Defense aggregation failed: %s, falling back to FedAvg", err)
         self.fell_back = True

@@ -47,17 +47,23 @@ def test_fedavg_fallback_when_defense_raises(cuda):
     strict = RoundEngine(TINY, RoundConfig(defense="krum", **kw), TrainConfig(local_steps=1), cuda)
     with pytest.raises(ValueError):
         strict.run_round()
-    # a device / library failure is never hidden behind the fallback
+    # a device / library failure: the reference's `except Exception` falls back
+    # (the default); fallback_device_errors=False keeps it loud
     from flr._capi import FlrError
-    boom = RoundEngine(TINY, RoundConfig(defense="fedavg", fallback_fedavg=True, **kw), TrainConfig(local_steps=1),
-                       cuda)
 
     def _fail(*a, **k):
         raise FlrError("flr_fedavg", -3, "injected")
-    boom.defense.aggregate_flat = _fail
-    boom.defense.aggregate_sharded = _fail
-    with pytest.raises(FlrError):
-        boom.run_round()
+    for loud in (False, True):
+        boom = RoundEngine(TINY, RoundConfig(defense="fedavg", fallback_fedavg=True,
+                                             fallback_device_errors=not loud, **kw),
+                           TrainConfig(local_steps=1), cuda)
+        boom.defense.aggregate_flat = _fail
+        boom.defense.aggregate_sharded = _fail
+        if loud:
+            with pytest.raises(FlrError):
+                boom.run_round()
+        else:
+            assert torch.equal(boom.run_round(), ref) and boom.fallback_error == "FlrError"
 
 
 def test_fltrust_round(cuda):
