@@ -474,16 +474,42 @@ __host__ __device__ inline int bp_b(int pr) {
   while (pr >= RNB - a) { pr -= RNB - a; ++a; }
   return a + pr;
 }
+// Staging (round 4): RSC chunks (256 coordinates = 1 KB per row) per stage,
+// fetched by LDS-DMA (one global_load_lds_dwordx4 per row: no VGPR round trip,
+// no per-chunk barrier), double buffered, the next stage in flight during this
+// one's compute.  Row images are unpadded 1-KB rows with the 16-B slots
+// XOR-swizzled by (row & 7) on the SOURCE address (the DMA writes lane-
+// linearly), so the 8 rows of a ds_read_b128 lane group hit 8 distinct bank
+// groups.  Per chunk the arithmetic is the same as before (wave w: coordinates
+// 16w .. 16w+15 of every chunk, fp32 over those 16, fp64 across chunks in
+// chunk order): the records are bit-identical to the register-staged form.
+// Diagonal block pairs stage 32 rows (64 KB of LDS, two workgroups per CU),
+// off-diagonal pairs 64 (128 KB): separate launches.
+constexpr int RSC = 4;                 // chunks per stage
+constexpr int RSW = RSC * CW;          // floats per staged row (1 KB)
+template <bool DIAG>
 __global__ __launch_bounds__(256) void refine_partials_kernel(const float* __restrict__ X, int64_t ldx,
                                                               int64_t nch_total, int q_base, int64_t chunk0,
                                                               const int* __restrict__ prec, int nseg,
                                                               double* __restrict__ rpart) {
-  __shared__ __attribute__((aligned(16))) float A[32][RPAD];
-  __shared__ __attribute__((aligned(16))) float B[32][RPAD];
+  constexpr int NR = DIAG ? 32 : 64;   // staged rows: block a (and block b)
+  extern __shared__ __attribute__((aligned(16))) float rl[];  // [2][NR][RSW]
   __shared__ double red[1024];
   const int c = prec[1];
-  const int pr = blockIdx.y;
-  const int a = bp_a(pr), b = bp_b(pr);
+  int a, b, pr;
+  if constexpr (DIAG) {  // blockIdx.y = a
+    a = b = (int)blockIdx.y;
+    pr = 0;
+    for (int t = 0; t < a; ++t) pr += RNB - t;
+  } else {  // blockIdx.y = the off-diagonal pairs (a < b) in a-major order
+    int r = (int)blockIdx.y;
+    a = 0;
+    while (r >= RNB - 1 - a) { r -= RNB - 1 - a; ++a; }
+    b = a + 1 + r;
+    pr = 0;
+    for (int t = 0; t < a; ++t) pr += RNB - t;
+    pr += b - a;
+  }
   if (32 * b >= c) return;  // an empty block of the row list (uniform: the whole workgroup leaves)
   const int seg = blockIdx.x;
   const int q = q_base + (int)blockIdx.z;
@@ -491,72 +517,80 @@ __global__ __launch_bounds__(256) void refine_partials_kernel(const float* __res
   const int64_t c_begin = s0 + (s1 - s0) * seg / nseg, c_end = s0 + (s1 - s0) * (seg + 1) / nseg;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int bi = lane >> 3, bj = lane & 7;
-  // the 32 rows of each block this workgroup stages (positions past the count repeat row 0)
-  const int rr = tid >> 3, cc0 = 8 * (tid & 7);
-  const int pa = 32 * a + rr, pb = 32 * b + rr;
-  const float* ra = X + (int64_t)prec[2 + (pa < c ? pa : 0)] * ldx;
-  const float* rb = X + (int64_t)prec[2 + (pb < c ? pb : 0)] * ldx;
-  const bool diag = a == b;
-  const float(*Bi)[RPAD] = diag ? A : B;
+  // staged rows of this wave: rows wave + 4 i (i < NR / 4); row t < 32 is list
+  // position 32a + t, row 32 + t position 32b + t (past the count: row 0)
+  const float* src[NR / 4];
+#pragma unroll
+  for (int i = 0; i < NR / 4; ++i) {
+    const int t = wave + 4 * i;
+    const int pos = t < 32 ? 32 * a + t : 32 * b + (t - 32);
+    src[i] = X + (int64_t)prec[2 + (pos < c ? pos : 0)] * ldx;
+  }
+  const int64_t nst = (c_end - c_begin + RSC - 1) / RSC;
+  auto stage = [&](int64_t st, float* buf) {
+#pragma unroll
+    for (int i = 0; i < NR / 4; ++i) {
+      const int t = wave + 4 * i;
+      // lane l fills LDS slot l of row t with the row's global slot l ^ (t & 7)
+      int64_t ch0 = c_begin + st * RSC;
+      const int gslot = lane ^ (t & 7);
+      int64_t ch = ch0 + (gslot >> 4);
+      ch = ch < c_end ? ch : c_begin;  // past the segment: any valid chunk (not computed)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src[i] + ch * CW + 4 * (gslot & 15)),
+          (__attribute__((address_space(3))) void*)(buf + t * RSW), 16, 0, 0);
+    }
+  };
   double d[4][4];
 #pragma unroll
   for (int u = 0; u < 4; ++u)
 #pragma unroll
     for (int v = 0; v < 4; ++v) d[u][v] = 0.0;
-  // chunk ch+1's values are loaded into registers before chunk ch's compute
-  f32x4 na0 = {}, na1 = {}, nb0 = {}, nb1 = {};
-  auto fetch = [&](int64_t ch) {
-    const int64_t p0 = ch * CW + cc0;
-    na0 = *reinterpret_cast<const f32x4*>(ra + p0);
-    na1 = *reinterpret_cast<const f32x4*>(ra + p0 + 4);
-    if (!diag) {
-      nb0 = *reinterpret_cast<const f32x4*>(rb + p0);
-      nb1 = *reinterpret_cast<const f32x4*>(rb + p0 + 4);
-    }
-  };
-  if (c_begin < c_end) fetch(c_begin);
-  for (int64_t ch = c_begin; ch < c_end; ++ch) {
-    *reinterpret_cast<f32x4*>(&A[rr][cc0]) = na0;
-    *reinterpret_cast<f32x4*>(&A[rr][cc0 + 4]) = na1;
-    if (!diag) {
-      *reinterpret_cast<f32x4*>(&B[rr][cc0]) = nb0;
-      *reinterpret_cast<f32x4*>(&B[rr][cc0 + 4]) = nb1;
-    }
-    __syncthreads();
-    if (ch + 1 < c_end) fetch(ch + 1);
-    // pairs (u, 2w) and (u, 2w+1) share one packed accumulator: v_pk_add_f32 /
-    // v_pk_fma_f32 do both pairs' sub + fma, each pair's own fp32 chain unchanged
-    f32x2 sacc[4][2];
+  if (nst > 0) stage(0, rl);
+  for (int64_t st = 0; st < nst; ++st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage st landed (every wave's DMA); stage st-1's buffer is free
+    float* buf = rl + (st & 1) * NR * RSW;
+    if (st + 1 < nst) stage(st + 1, rl + ((st + 1) & 1) * NR * RSW);
+    const float* Ab = buf;
+    const float* Bb = DIAG ? buf : buf + 32 * RSW;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int cc = 0; cc < RSC; ++cc) {
+      if (c_begin + st * RSC + cc >= c_end) break;  // uniform
+      // pairs (u, 2w) and (u, 2w+1) share one packed accumulator: v_pk_add_f32 /
+      // v_pk_fma_f32 do both pairs' sub + fma, each pair's own fp32 chain unchanged
+      f32x2 sacc[4][2];
 #pragma unroll
-      for (int w2 = 0; w2 < 2; ++w2) sacc[u][w2] = f32x2{0.f, 0.f};
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4) {
-      const int k = 16 * wave + 4 * k4;
-      f32x4 av[4], bv[4];
+        for (int w2 = 0; w2 < 2; ++w2) sacc[u][w2] = f32x2{0.f, 0.f};
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        av[u] = *reinterpret_cast<const f32x4*>(&A[bi + 8 * u][k]);
-        bv[u] = *reinterpret_cast<const f32x4*>(&Bi[bj + 8 * u][k]);
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const int slot = 16 * cc + 4 * wave + k4;  // 16-B slot of coordinates 16 wave + 4 k4 .. +3 of chunk cc
+        f32x4 av[4], bv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int ra = bi + 8 * u, rb = bj + 8 * u;
+          av[u] = *reinterpret_cast<const f32x4*>(Ab + ra * RSW + 4 * (slot ^ (ra & 7)));
+          bv[u] = *reinterpret_cast<const f32x4*>(Bb + rb * RSW + 4 * (slot ^ (rb & 7)));
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int w2 = 0; w2 < 2; ++w2) {
+              const f32x2 a2 = {av[u][e], av[u][e]};
+              const f32x2 b2 = {bv[2 * w2][e], bv[2 * w2 + 1][e]};
+              const f32x2 df = a2 - b2;
+              sacc[u][w2] = __builtin_elementwise_fma(df, df, sacc[u][w2]);
+            }
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int w2 = 0; w2 < 2; ++w2) {
-            const f32x2 a2 = {av[u][e], av[u][e]};
-            const f32x2 b2 = {bv[2 * w2][e], bv[2 * w2 + 1][e]};
-            const f32x2 df = a2 - b2;
-            sacc[u][w2] = __builtin_elementwise_fma(df, df, sacc[u][w2]);
-          }
+        for (int v = 0; v < 4; ++v) d[u][v] += (double)sacc[u][v >> 1][v & 1];
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) d[u][v] += (double)sacc[u][v >> 1][v & 1];
-    __syncthreads();
   }
   // the four waves' partials, added in wave order (one 8-KB exchange per wave)
   for (int w = 1; w < 4; ++w) {
@@ -1085,9 +1119,12 @@ int gram_phase(const GramArgs& a, double* stage1, double* gsum, double* rpart, h
   // the flagged rows' exact-difference records of these slices (workgroups of an
   // empty row-list block leave at once)
   const int rseg = refine_nseg(a.P);
-  hipLaunchKernelGGL(refine_partials_kernel, dim3(rseg, RNBP, a.nsl), dim3(256), 0, st, a.X, a.ldx, p.nchunks,
-                     a.q0, a.chunk0, a.pivot, rseg, rpart);
-  if ((rc = launch_status("refine_partials_kernel")) != FLR_OK) return rc;
+  hipLaunchKernelGGL(refine_partials_kernel<true>, dim3(rseg, RNB, a.nsl), dim3(256), 2 * 32 * RSW * sizeof(float),
+                     st, a.X, a.ldx, p.nchunks, a.q0, a.chunk0, a.pivot, rseg, rpart);
+  if ((rc = launch_status("refine_partials_kernel<diag>")) != FLR_OK) return rc;
+  hipLaunchKernelGGL(refine_partials_kernel<false>, dim3(rseg, RNBP - RNB, a.nsl), dim3(256),
+                     2 * 64 * RSW * sizeof(float), st, a.X, a.ldx, p.nchunks, a.q0, a.chunk0, a.pivot, rseg, rpart);
+  if ((rc = launch_status("refine_partials_kernel<cross>")) != FLR_OK) return rc;
   hipLaunchKernelGGL(refine_reduce_kernel, dim3(RNBP, a.nsl), dim3(256), 0, st, rpart, rseg, a.pivot, p.ngroups(),
                      glen, gsum);
   return launch_status("refine_reduce_kernel");

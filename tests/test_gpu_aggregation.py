@@ -113,11 +113,13 @@ def _fp64_dist(X):
 
 
 @pytest.mark.parametrize("K,P,f", [(40, 64 * 1000 + 7, 8), (128, 200_000, 25), (128, 70_000, 40),
-                                   (130, 64 * 900, 30), (300, 64 * 700, 60)])
+                                   (130, 64 * 900, 30), (300, 64 * 700, 60), (300, 64 * 700 + 5, 80),
+                                   (320, 64 * 500, 100), (128, 64 * 300, 60)])
 def test_pairwise_far_cluster_refined(cuda, K, P, f):
     """Pairs inside a cluster far from the medoid pivot (cancellation factor ~1e8
     here) come from the exact-difference refine, every pair within 2e-5 of
-    fp64 — including the 33..64-row lists (two row-list blocks) and K > 128."""
+    fp64 — including row lists of 33..128 rows (two to four row-list blocks,
+    diagonal and off-diagonal block pairs) and K > 128."""
     X = _far_cluster_matrix(K, P, f, seed=K + f, device=cuda)
     D = ops.pairwise_l2(X[:, :P], "gram")
     ref = _fp64_dist(X[:, :P])
@@ -128,6 +130,24 @@ def test_pairwise_far_cluster_refined(cuda, K, P, f):
     from test_gpu_shard import _phases
     for world in (2, 8):
         assert torch.equal(_phases(X, K, P, world), D)
+
+
+def test_pairwise_far_cluster_overflow_is_loud(cuda):
+    """More far-cluster rows than the refine list holds (140 > 128, only
+    possible at K > 128): every off-diagonal distance is NaN and Krum's
+    publish raises — never a silently inaccurate selection."""
+    from flr._capi import FlrError
+    K, P, f = 300, 64 * 200, 140
+    X = _far_cluster_matrix(K, P, f, seed=3, device=cuda)
+    D = ops.pairwise_l2(X[:, :P], "gram")
+    off = ~torch.eye(K, dtype=torch.bool, device=cuda)
+    assert torch.isnan(D[off]).all() and (D.diagonal() == 0).all()
+    d = KrumDefense({"num_malicious": f, "multi_k": K // 2})
+    with pytest.raises(FlrError):
+        d.aggregate_flat(ClientMatrix(X, P, [(P,)]), [1] * K)
+    # the exact paths have no such limit
+    Dd = ops.pairwise_l2(X[:, :P], "direct")
+    assert not torch.isnan(Dd).any()
 
 
 def test_pairwise_large_offset_centering(cuda):
