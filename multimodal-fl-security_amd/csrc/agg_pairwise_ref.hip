@@ -22,7 +22,10 @@
 // IEEE fp32 ops each, rounding unchanged).  A 128-thread workgroup owns a
 // tile of 4 rows (I) x 8 rows (J) = 32 pairs; per 32-step chunk (256
 // coordinates) the 12 rows are staged into LDS by LDS-DMA (one 1-KB
-// global_load_lds_dwordx4 per row, double buffered) with a 1056-B row stride
+// global_load_lds_dwordx4 per row) into a ring of NSTAGE buffers, NSTAGE - 1
+// chunks in flight (a chunk's compute is ~0.3 us, an L2 / HBM round trip
+// 1-2 us: with two buffers the kernel waited on every chunk, 54 ms at C3),
+// counted vmcnt waits and a raw s_barrier, with a 1056-B row stride
 // (8 dwords of padding: the 8 rows x 4 chain pairs of a ds_read_b64 lane
 // group land on 64 distinct banks).  Per chain step a thread reads one float2
 // of each row (2 ds_read_b64): 16 B of LDS and 2 VALU instructions per two
@@ -43,6 +46,8 @@ constexpr int CW = 8 * CS;            // coordinates per chunk (1 KB per row)
 constexpr int RSTR = CW + 8;          // LDS row stride in floats (== 8 mod 64 dwords)
 constexpr int NROWS = TI + TJ;
 constexpr int BUF = NROWS * RSTR;     // floats per staging buffer
+constexpr int NSTAGE = 4;             // ring of staging buffers (NSTAGE - 1 chunks in flight)
+constexpr int DMA_PER_WAVE = NROWS / 2;  // one DMA per staged row, two waves
 
 // Tiles: J block jb (rows 8jb..8jb+7) with I blocks ib = 0 .. min(nI, 2jb+2)-1
 // (4 ib < 8 jb + 7: some i < some j).  Tiles are numbered jb-major.
@@ -55,8 +60,11 @@ __host__ __device__ inline int64_t tiles_upto(int jb, int nI) {
 
 __global__ __launch_bounds__(THREADS) void ref_norm_kernel(const float* __restrict__ X, int K, int64_t P,
                                                            int64_t ldx, int ntiles, double* __restrict__ D) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
-  __shared__ f32x2 red[THREADS];
+  // ONE __shared__ array (a second __shared__ object makes hipcc wait vmcnt(0)
+  // before the LDS reads, draining the DMA ring): the staging ring, then the
+  // lane partials of the final sum
+  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * BUF + 2 * THREADS];
+  f32x2* red = reinterpret_cast<f32x2*>(lds + NSTAGE * BUF);
   const int nI = cdiv(K, TI), nJ = cdiv(K, TJ);
   // XCD-aware: consecutive workgroup ids go to different XCDs, so XCD x takes
   // the contiguous tile range [x * per, (x + 1) * per) of the jb-major order
@@ -101,12 +109,22 @@ __global__ __launch_bounds__(THREADS) void ref_norm_kernel(const float* __restri
   f32x2 acc = {0.f, 0.f};
   const float* arow = lds + pi * RSTR + 2 * cp;
   const float* brow = lds + (TI + pj) * RSTR + 2 * cp;
-  if (nch > 0) stage(0, lds);
+  for (int64_t c = 0; c < NSTAGE - 1 && c < nch; ++c) stage(c, lds + c * BUF);
   for (int64_t ch = 0; ch < nch; ++ch) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // chunk ch landed (every wave's DMA); chunk ch-1's buffer is free
-    const int cur = (int)(ch & 1);
-    if (ch + 1 < nch) stage(ch + 1, lds + (cur ^ 1) * BUF);
+    // chunk ch landed: this wave's DMAs of the chunks after it may stay in flight
+    if (ch + NSTAGE - 2 < nch) {
+      static_assert(DMA_PER_WAVE * (NSTAGE - 2) == 12, "vmcnt immediate below");
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // every wave's DMA of chunk ch landed and every wave's reads of chunk ch-1
+    // are done (their buffer is restaged below): raw barrier, no vmcnt(0) drain
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int cur = (int)(ch % NSTAGE);
+    if (ch + NSTAGE - 1 < nch) stage(ch + NSTAGE - 1, lds + ((ch + NSTAGE - 1) % NSTAGE) * BUF);
     const float* a = arow + cur * BUF;
     const float* b = brow + cur * BUF;
     const int64_t left = R - ch * CS;
@@ -124,6 +142,7 @@ __global__ __launch_bounds__(THREADS) void ref_norm_kernel(const float* __restri
     }
   }
   // lane sum 0..7 in order, then the tail, correctly rounded sqrt
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   red[tid] = acc;
   __syncthreads();
   if (cp == 0 && i < j && j < K) {
