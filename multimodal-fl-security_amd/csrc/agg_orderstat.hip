@@ -79,10 +79,15 @@ __device__ __forceinline__ int nan_to_inf(float* v) {
   return n;
 }
 
+template <int N>
+__device__ __forceinline__ void reg_fence(float* v) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k]));
+}
+
 // MODE 0: trimmed mean over ranks [t, K-t); MODE 1: lower median.
+// 3 waves/SIMD: the NP = 128 network fits the 168 VGPRs available.
 template <int NP, int MODE>
-// 3 waves/SIMD: the NP=128 network needs ~150 VGPRs; the bound stops the
-// trimmed sum from pushing the kernel over the 168-VGPR occupancy step.
 __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __restrict__ X, int K, int64_t P,
                                                             int64_t ldx, int t, float* __restrict__ out,
                                                             const int32_t* __restrict__ rows, uint32_t rmax) {
@@ -96,8 +101,16 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
 #pragma unroll
     for (int k = 0; k < NP; ++k) v[k] = k < K ? X[(int64_t)k * ldx + p] : __builtin_huge_valf();
   }
+  // Empty asm fences pin all NP values in VGPRs at the phase boundaries, so
+  // the compiler cannot stretch load, sort and sum live ranges into one
+  // another: without them ROCm 7.2 spilled 237-283 VGPRs of the NP = 128
+  // trimmed mean to scratch (5.7 ms at C3's K = 128, P = 11.8 M, against
+  // 1.6 ms for the median); with them 5 (the output address and NaN count,
+  // stored once).
+  reg_fence<NP>(v);
   const int nnan = nan_to_inf<NP>(v);
   oem_sort<0, NP>(v);
+  if constexpr (MODE == 0) reg_fence<NP>(v);
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (MODE == 1) {
     const int med = (K - 1) / 2;
@@ -106,20 +119,22 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
     for (int k = 1; k < NP; ++k) r = (k == med) ? v[k] : r;
     out[p] = nnan > 0 ? __builtin_nanf("") : r;
   } else {
-    const int R = K - 2 * t;
+    // t, R wave-uniform (SGPRs): the rank tests are scalar compares and uniform
+    // branches, no per-rank lane masks
+    const int tu = __builtin_amdgcn_readfirstlane(t);
+    const int R = __builtin_amdgcn_readfirstlane(K - 2 * tu);
     const int nfull = R & ~15;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int pos = k - t;
-      // branch-free (selects keep the live ranges short; t, R are wave-uniform)
-      const bool in = (unsigned)pos < (unsigned)R;
-      const float n0 = add_rn(a0, v[k]);
-      a0 = in ? n0 : a0;
-      const bool blk = in && pos < nfull && ((pos + 1) & 15) == 0;
-      const float n1 = add_rn(a1, a0);
-      a1 = blk ? n1 : a1;
-      a0 = blk ? 0.f : a0;
+      const int pos = k - tu;
+      if ((unsigned)pos < (unsigned)R) {
+        a0 = add_rn(a0, v[k]);
+        if (pos < nfull && ((pos + 1) & 15) == 0) {
+          a1 = add_rn(a1, a0);
+          a0 = 0.f;
+        }
+      }
       // NP <= 128: a block end i = pos + 1 is at most 128, never a multiple of
       // 256, so the level-2/3 folds (i & 0xF0 == 0, i & 0xF00 == 0) never fire.
       static_assert(NP <= 128, "level-2 cascade folds not implemented");

@@ -462,7 +462,6 @@ __global__ void reduce_splits_kernel(const double* __restrict__ stage1, int nrec
 // fp32 sums over the 16 coordinates, fp64 across chunks, the four waves'
 // partials added in wave order at the end.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-constexpr int RPAD = CW + 4;
 // block pair index -> (a, b), a <= b, a-major: (0,0) (0,1) .. (0,RNB-1) (1,1) ..
 __host__ __device__ inline int bp_a(int pr) {
   int a = 0;
@@ -541,6 +540,28 @@ __global__ __launch_bounds__(256) void refine_partials_kernel(const float* __res
           (__attribute__((address_space(3))) void*)(buf + t * RSW), 16, 0, 0);
     }
   };
+  // Compact mapping (diagonal block pairs with at most 28 rows, e.g. the 25
+  // sign-flipped clients of C3): only the 4 x 4 sub-blocks (p <= q) of the upper
+  // triangle over the valid rows are computed, two lanes per sub-block (8 of the
+  // wave's 16 coordinates each) — 28 sub-blocks for 25 rows instead of the full
+  // mapping's 32 x 32 pair slots, both triangles and the padding rows (the kernel
+  // is VALU-bound: 0.58 ms at C3 with the full mapping).  Otherwise lane (bi, bj)
+  // takes the strided 4 x 4 block (bi + 8u, bj + 8v) over the wave's 16 coordinates.
+  const int ca = DIAG ? std::min(32, c - 32 * a) : 32;
+  const int np = (ca + 3) / 4;
+  const bool compact = DIAG && np * (np + 1) / 2 <= 32;  // uniform
+  int t_p = 0, t_q = 0;
+  bool t_ok = true;
+  if (compact) {
+    int t = lane >> 1, pp = 0;
+    while (pp < np && t >= np - pp) { t -= np - pp; ++pp; }
+    t_ok = pp < np;
+    t_p = t_ok ? pp : 0;
+    t_q = t_ok ? pp + t : 0;
+  }
+  const int half = lane & 1;
+  auto arow = [&](int u) { return compact ? 4 * t_p + u : bi + 8 * u; };
+  auto brow = [&](int v) { return compact ? 4 * t_q + v : bj + 8 * v; };
   double d[4][4];
 #pragma unroll
   for (int u = 0; u < 4; ++u)
@@ -564,13 +585,12 @@ __global__ __launch_bounds__(256) void refine_partials_kernel(const float* __res
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int w2 = 0; w2 < 2; ++w2) sacc[u][w2] = f32x2{0.f, 0.f};
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
+      auto k4_step = [&](int k4) {
         const int slot = 16 * cc + 4 * wave + k4;  // 16-B slot of coordinates 16 wave + 4 k4 .. +3 of chunk cc
         f32x4 av[4], bv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int ra = bi + 8 * u, rb = bj + 8 * u;
+          const int ra = arow(u), rb = brow(u);
           av[u] = *reinterpret_cast<const f32x4*>(Ab + ra * RSW + 4 * (slot ^ (ra & 7)));
           bv[u] = *reinterpret_cast<const f32x4*>(Bb + rb * RSW + 4 * (slot ^ (rb & 7)));
         }
@@ -585,12 +605,36 @@ __global__ __launch_bounds__(256) void refine_partials_kernel(const float* __res
               const f32x2 df = a2 - b2;
               sacc[u][w2] = __builtin_elementwise_fma(df, df, sacc[u][w2]);
             }
+      };
+      if (compact) {
+        k4_step(2 * half);
+        k4_step(2 * half + 1);
+      } else {
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) k4_step(k4);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int v = 0; v < 4; ++v) d[u][v] += (double)sacc[u][v >> 1][v & 1];
     }
+  }
+  if (compact) {
+    // the eight partials of a pair (wave w, half h) added in (w, h) order into
+    // red, the record's [32][32] image (entries of no sub-block stay 0)
+    for (int e = tid; e < 1024; e += 256) red[e] = 0.0;
+    __syncthreads();
+    for (int ph = 0; ph < 8; ++ph) {
+      if (t_ok && wave == (ph >> 1) && half == (ph & 1))
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) red[(4 * t_p + u) * 32 + 4 * t_q + v] += d[u][v];
+      __syncthreads();
+    }
+    double* rec = rpart + (((int64_t)blockIdx.z * RNBP + pr) * nseg + seg) * 1024;
+    for (int e = tid; e < 1024; e += 256) rec[e] = red[e];
+    return;
   }
   // the four waves' partials, added in wave order (one 8-KB exchange per wave)
   for (int w = 1; w < 4; ++w) {
