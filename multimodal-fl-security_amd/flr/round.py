@@ -154,7 +154,7 @@ class RoundEngine:
         self.round_index += 1
         return self.global_flat
 
-    def _capture(self) -> None:
+    def _capture(self, keep_graph: bool = False) -> None:
         """Capture the training phase (~2.4k kernel launches per round at C3)
         as one HIP graph: replay removes the host launch cost, which dominates
         once a GPU holds few clients (K/G = 16 at 8 GPUs).  Inputs (global
@@ -165,7 +165,7 @@ class RoundEngine:
         with torch.cuda.stream(side):  # warm-up on a side stream: library handles and workspaces
             self._train_phase()
         torch.cuda.current_stream(self.device).wait_stream(side)
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=keep_graph)  # keep_graph: the raw graph stays queryable (tools)
         with torch.cuda.graph(g):
             self._graph_losses = self._train_phase()
         self._graph = g

@@ -24,11 +24,23 @@ def main():
     rc = RoundConfig(num_clients=K, defense=defense, defense_cfg=dict(dcfg), num_attackers=int(afrac * K),
                      attack=attack)
     eng = RoundEngine(spec, rc, TrainConfig(local_steps=5), torch.device("cuda:0"))
-    eng._capture()
+    eng._capture(keep_graph=True)
     hip = ctypes.CDLL("libamdhip64.so.7")
     n = ctypes.c_size_t(0)
     st = hip.hipGraphGetNodes(ctypes.c_void_p(eng._graph.raw_cuda_graph()), None, ctypes.byref(n))
-    print(f"{cfg} K={K}: graph nodes {n.value} (status {st})", flush=True)
+    nodes = (ctypes.c_void_p * n.value)()
+    st2 = hip.hipGraphGetNodes(ctypes.c_void_p(eng._graph.raw_cuda_graph()), nodes, ctypes.byref(n))
+    kinds = {}
+    for i in range(n.value):
+        t = ctypes.c_int(-1)
+        hip.hipGraphNodeGetType(ctypes.c_void_p(nodes[i]), ctypes.byref(t))
+        kinds[t.value] = kinds.get(t.value, 0) + 1
+    # hipGraphNodeType: 0 kernel, 1 memcpy, 2 memset, 3 host, 4 graph, 5 empty, 6 wait event, 7 event record
+    print(f"{cfg} K={K}: graph nodes {n.value} (status {st}/{st2}) by type {kinds}", flush=True)
+    eng._graph.instantiate()
+    eng.run_round()
+    torch.cuda.synchronize()
+    print(f"{cfg} K={K}: replay ok", flush=True)
 
 
 if __name__ == "__main__":
