@@ -256,16 +256,16 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
   float* y;
   int64_t wsk;  // weight floats between clients (KK*Cin*Cout; 0: every client reads one shared copy)
   static constexpr int LA = KR_VEC, LB = KR_GATHER;
-  __host__ __device__ int M() const { return g.Cout; }
-  __host__ __device__ int N() const { return g.B * g.Ho * g.Wo; }
-  __host__ __device__ int R() const { return g.ntaps * g.Cin; }
+  __host__ __device__ __forceinline__ int M() const { return g.Cout; }
+  __host__ __device__ __forceinline__ int N() const { return g.B * g.Ho * g.Wo; }
+  __host__ __device__ __forceinline__ int R() const { return g.ntaps * g.Cin; }
   struct State {
     rsrc_t ra, rb;
     unsigned a0;            // byte offset of (k-row tid/16, m 4*(tid%16)) at tap 0, ci 0
     int ih0, iw0, xoff;     // this thread's output pixel (B operand)
     bool nok;
   };
-  __device__ State init(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ State init(int k, int m0, int n0, int tid) const {
     State s;
     const int KK = g.KH * g.KW;
     s.ra = make_rsrc(w + (int64_t)k * wsk, (int64_t)KK * g.Cin * g.Cout);
@@ -280,7 +280,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
     s.xoff = (int)(bb * g.sxb + (tid / 64) * g.sxc);
     return s;
   }
-  __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
+  __device__ __forceinline__ void load_a(const State& s, int r0, float (&a)[8]) const {
     const int slot = uni(r0 / g.Cin), ci0 = r0 - slot * g.Cin;
     int kh, kw;
     slot_tap(g, slot, kh, kw);
@@ -294,7 +294,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
       for (int e = 0; e < 4; ++e) a[4 * i + e] = q[e];
     }
   }
-  __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
+  __device__ __forceinline__ void load_b(const State& s, int r0, float (&b)[8]) const {
     const int slot = uni(r0 / g.Cin), ci0 = r0 - slot * g.Cin;
     int kh, kw;
     slot_tap(g, slot, kh, kw);
@@ -311,11 +311,11 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
     for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, cb + i * 4 * HW * 4);
   }
   // y[k][m][n]: n = b*Ho*Wo + p is linear in the [K][C][B][Ho][Wo] layout
-  __device__ void store(int k, int m, int n, float v) const { y[k * g.syk + m * g.syc + n] = v; }
-  __device__ bool linear() const { return true; }
-  __device__ float* out() const { return y; }
-  __device__ int64_t tile_base(int k, int m0, int n0) const { return k * g.syk + m0 * g.syc + n0; }
-  __device__ int64_t ldm() const { return g.syc; }
+  __device__ __forceinline__ void store(int k, int m, int n, float v) const { y[k * g.syk + m * g.syc + n] = v; }
+  __device__ __forceinline__ bool linear() const { return true; }
+  __device__ __forceinline__ float* out() const { return y; }
+  __device__ __forceinline__ int64_t tile_base(int k, int m0, int n0) const { return k * g.syk + m0 * g.syc + n0; }
+  __device__ __forceinline__ int64_t ldm() const { return g.syc; }
   // ---- k-contiguous loads for the split-at-stash kernel: thread (row = tid & 63,
   // k = 8 (tid >> 6) .. +7) of a 64 x 32 sub-tile
   struct State8 {
@@ -324,7 +324,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
     int ih0, iw0, xoff;
     bool nok;
   };
-  __device__ State8 init8(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ State8 init8(int k, int m0, int n0, int tid) const {
     State8 s;
     const int KK = g.KH * g.KW;
     const int row = tid & 63, k0 = 8 * (tid >> 6);
@@ -340,7 +340,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
     s.xoff = (int)(bb * g.sxb + k0 * g.sxc);
     return s;
   }
-  __device__ void load_a8(const State8& s, int r0, float (&a)[8]) const {  // A(co, ci): lanes along co
+  __device__ __forceinline__ void load_a8(const State8& s, int r0, float (&a)[8]) const {  // A(co, ci): lanes along co
     const int slot = uni((int)udiv((uint32_t)r0, g.d_cin)), ci0 = r0 - slot * g.Cin;
     int kh, kw;
     slot_tap(g, slot, kh, kw);
@@ -348,7 +348,7 @@ struct FwdT {  // y = conv(x, W_t): M = Cout, N = B*Ho*Wo, R = ntaps*Cin
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[e] = ld1(s.ra, s.a0, arow + e * g.Cout * 4);
   }
-  __device__ void load_b8(const State8& s, int r0, float (&b)[8]) const {  // B(pixel, ci): 8 channels
+  __device__ __forceinline__ void load_b8(const State8& s, int r0, float (&b)[8]) const {  // B(pixel, ci): 8 channels
     const int slot = uni((int)udiv((uint32_t)r0, g.d_cin)), ci0 = r0 - slot * g.Cin;
     int kh, kw;
     slot_tap(g, slot, kh, kw);
@@ -384,16 +384,16 @@ struct DgradT {
   int8_t ckh[conv::MAXTAPS], ckw[conv::MAXTAPS];
   conv::TapRect crect;  // the class taps: a rectangle of step = stride
   static constexpr int LA = RK_VEC, LB = KR_GATHER;
-  __host__ __device__ int M() const { return g.Cin; }
-  __host__ __device__ int N() const { return g.B * Hc * Wc; }
-  __host__ __device__ int R() const { return ntc * g.Cout; }
+  __host__ __device__ __forceinline__ int M() const { return g.Cin; }
+  __host__ __device__ __forceinline__ int N() const { return g.B * Hc * Wc; }
+  __host__ __device__ __forceinline__ int R() const { return ntc * g.Cout; }
   struct State {
     rsrc_t ra, rb;
     unsigned a0;
     int ih, iw, yoff;  // ih, iw: this lane's input pixel + pad
     bool nok;
   };
-  __device__ State init(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ State init(int k, int m0, int n0, int tid) const {
     State s;
     const int KK = g.KH * g.KW;
     s.ra = make_rsrc(w + (int64_t)k * wsk, (int64_t)KK * g.Cin * g.Cout);
@@ -408,7 +408,7 @@ struct DgradT {
     s.yoff = (int)(bb * g.syb + (tid / 64) * g.syc);
     return s;
   }
-  __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
+  __device__ __forceinline__ void load_a(const State& s, int r0, float (&a)[8]) const {
     const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
     int kh, kw;
     conv::rect_tap(crect, slot, kh, kw);
@@ -422,7 +422,7 @@ struct DgradT {
       for (int e = 0; e < 4; ++e) a[4 * i + e] = q[e];
     }
   }
-  __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
+  __device__ __forceinline__ void load_b(const State& s, int r0, float (&b)[8]) const {
     const int slot = uni(r0 / g.Cout), co0 = r0 - slot * g.Cout;
     int kh, kw;
     conv::rect_tap(crect, slot, kh, kw);
@@ -439,31 +439,31 @@ struct DgradT {
 #pragma unroll
     for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, cb0 + i * 4 * cs * 4);
   }
-  __device__ void store(int k, int m, int n, float v) const {
+  __device__ __forceinline__ void store(int k, int m, int n, float v) const {
     const uint32_t bb = udiv(n, d_hcwc), p = n - bb * Hc * Wc;
     const uint32_t ihc = udiv(p, d_wc), iwc = p - ihc * Wc;
     const int ih = ca + (int)ihc * g.stride, iw = cb + (int)iwc * g.stride;
     const int64_t i = k * g.sxk + m * g.sxc + bb * g.sxb + ih * g.W + iw;
     dx[i] = add ? __fadd_rn(v, add[i]) : v;
   }
-  __device__ int64_t index(int k, int m, int n) const {  // dx offset of output (m, n) of client k
+  __device__ __forceinline__ int64_t index(int k, int m, int n) const {  // dx offset of output (m, n) of client k
     const uint32_t bb = udiv(n, d_hcwc), p = n - bb * Hc * Wc;
     const uint32_t ihc = udiv(p, d_wc), iwc = p - ihc * Wc;
     const int ih = ca + (int)ihc * g.stride, iw = cb + (int)iwc * g.stride;
     return k * g.sxk + m * g.sxc + bb * g.sxb + ih * g.W + iw;
   }
   // stride 1 (the one class is every pixel): dx[k][m][n] is linear in n
-  __device__ bool linear() const { return g.stride == 1; }
-  __device__ float* out() const { return dx; }
-  __device__ int64_t tile_base(int k, int m0, int n0) const { return k * g.sxk + m0 * g.sxc + n0; }
-  __device__ int64_t ldm() const { return g.sxc; }
+  __device__ __forceinline__ bool linear() const { return g.stride == 1; }
+  __device__ __forceinline__ float* out() const { return dx; }
+  __device__ __forceinline__ int64_t tile_base(int k, int m0, int n0) const { return k * g.sxk + m0 * g.sxc + n0; }
+  __device__ __forceinline__ int64_t ldm() const { return g.sxc; }
   struct State8 {
     rsrc_t ra, rb;
     unsigned a0;
     int ih, iw, yoff;
     bool nok;
   };
-  __device__ State8 init8(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ State8 init8(int k, int m0, int n0, int tid) const {
     State8 s;
     const int KK = g.KH * g.KW;
     const int row = tid & 63, k0 = 8 * (tid >> 6);
@@ -480,7 +480,7 @@ struct DgradT {
     s.yoff = (int)(bb * g.syb + k0 * g.syc);
     return s;
   }
-  __device__ void load_a8(const State8& s, int r0, float (&a)[8]) const {  // A(ci, co): 8 consecutive co
+  __device__ __forceinline__ void load_a8(const State8& s, int r0, float (&a)[8]) const {  // A(ci, co): 8 consecutive co
     const int slot = uni((int)udiv((uint32_t)r0, g.d_cout)), co0 = r0 - slot * g.Cout;
     int kh, kw;
     conv::rect_tap(crect, slot, kh, kw);
@@ -492,7 +492,7 @@ struct DgradT {
       a[4 + e] = q1[e];
     }
   }
-  __device__ void load_b8(const State8& s, int r0, float (&b)[8]) const {  // B(input pixel, co): 8 channels
+  __device__ __forceinline__ void load_b8(const State8& s, int r0, float (&b)[8]) const {  // B(input pixel, co): 8 channels
     const int slot = uni((int)udiv((uint32_t)r0, g.d_cout)), co0 = r0 - slot * g.Cout;
     int kh, kw;
     conv::rect_tap(crect, slot, kh, kw);
@@ -553,14 +553,14 @@ struct WgtT {
   double* sq = nullptr;
   int sq_ld = 0;
   static constexpr int LA = RK_GATHER, LB = BVEC ? RK_VEC : RK_GATHER;
-  __host__ __device__ int M() const { return g.ntaps * g.Cin; }
-  __host__ __device__ int N() const { return g.Cout; }
-  __host__ __device__ int R() const { return g.B * g.Ho * g.Wo; }
+  __host__ __device__ __forceinline__ int M() const { return g.ntaps * g.Cin; }
+  __host__ __device__ __forceinline__ int N() const { return g.Cout; }
+  __host__ __device__ __forceinline__ int R() const { return g.B * g.Ho * g.Wo; }
   struct State {
     rsrc_t ra, rb;
     int kh, kw, aoff, boff;
   };
-  __device__ State init(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ State init(int k, int m0, int n0, int tid) const {
     State s;
     s.ra = make_rsrc(x + k * g.sxk, g.xext);
     s.rb = make_rsrc(dy + k * g.syk, g.yext);
@@ -573,7 +573,7 @@ struct WgtT {
     s.boff = (int)((BVEC ? (n0 + tid / 8) : (n0 + tid / 32)) * g.syc);
     return s;
   }
-  __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
+  __device__ __forceinline__ void load_a(const State& s, int r0, float (&a)[8]) const {
     const int tid = threadIdx.x;
     const int HoWo = g.Ho * g.Wo, R = this->R();
     {  // A: x gathered at q = r0 + tid % 32
@@ -589,7 +589,7 @@ struct WgtT {
     }
   }
   // B: dy[co][q] with q = b*Ho*Wo + p contiguous per channel ([K][C][B][Ho][Wo])
-  __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
+  __device__ __forceinline__ void load_b(const State& s, int r0, float (&b)[8]) const {
     const int tid = threadIdx.x, R = this->R();
     if constexpr (BVEC) {  // q = r0 + 4 (tid % 8) .. +3
       const int q = r0 + 4 * (tid % 8);
@@ -607,23 +607,23 @@ struct WgtT {
       for (int i = 0; i < 8; ++i) b[i] = ld1(s.rb, vb, i * 8 * (int)g.syc * 4);
     }
   }
-  __device__ void store(int k, int m, int n, float v) const {
+  __device__ __forceinline__ void store(int k, int m, int n, float v) const {
     const int slot = (int)udiv(m, g.d_cin), ci = m - slot * g.Cin;
     dw[(((int64_t)k * g.KH * g.KW + tap_index(g, slot)) * g.Cin + ci) * g.Cout + n] = v;
   }
-  __device__ bool linear() const { return true; }
-  __device__ float* out() const { return dw; }
-  __device__ int64_t tile_base(int k, int m0, int n0) const {
+  __device__ __forceinline__ bool linear() const { return true; }
+  __device__ __forceinline__ float* out() const { return dw; }
+  __device__ __forceinline__ int64_t tile_base(int k, int m0, int n0) const {
     const int slot = m0 / g.Cin, ci0 = m0 - slot * g.Cin;
     return (((int64_t)k * g.KH * g.KW + tap_index(g, slot)) * g.Cin + ci0) * g.Cout + n0;
   }
-  __device__ int64_t ldm() const { return g.Cout; }
+  __device__ __forceinline__ int64_t ldm() const { return g.Cout; }
   struct State8 {
     rsrc_t ra, rb;
     int kh, kw, k0;
     unsigned aoff, boff;
   };
-  __device__ State8 init8(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ State8 init8(int k, int m0, int n0, int tid) const {
     State8 s;
     s.ra = make_rsrc(x + k * g.sxk, g.xext);
     s.rb = make_rsrc(dy + k * g.syk, g.yext);
@@ -640,7 +640,7 @@ struct WgtT {
   }
   // A(ci, pixel q): the 8 pixels of the wave's k-group are wave-uniform, so their
   // decomposition and padding test run on the scalar unit (soffset per pixel)
-  __device__ void load_a8(const State8& s, int r0, float (&a)[8]) const {
+  __device__ __forceinline__ void load_a8(const State8& s, int r0, float (&a)[8]) const {
     const int R = this->R(), HoWo = g.Ho * g.Wo;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -654,7 +654,7 @@ struct WgtT {
     }
   }
   // B(co, q): dy[co][q], q contiguous per channel
-  __device__ void load_b8(const State8& s, int r0, float (&b)[8]) const {
+  __device__ __forceinline__ void load_b8(const State8& s, int r0, float (&b)[8]) const {
     const int R = this->R();
     const int q0 = r0 + s.k0;
     if constexpr (BVEC) {  // syc % 4 == 0, R % 4 == 0
@@ -679,7 +679,7 @@ struct WgtT {
     int kh, kw;
     unsigned arow, brow;
   };
-  __device__ StateT initT(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ StateT initT(int k, int m0, int n0, int tid) const {
     StateT s;
     s.ra = make_rsrc(x + k * g.sxk, g.xext);
     s.rb = make_rsrc(dy + k * g.syk, g.yext);
@@ -693,7 +693,7 @@ struct WgtT {
     s.brow = (unsigned)((n0 + 8 * rg) * g.syc * 4);
     return s;
   }
-  __device__ void load_at8(const StateT& s, int r0, float (&a)[8]) const {  // x(ci, pixel q of tap (kh, kw))
+  __device__ __forceinline__ void load_at8(const StateT& s, int r0, float (&a)[8]) const {  // x(ci, pixel q of tap (kh, kw))
     const int q = r0 + (int)(threadIdx.x & 31), HoWo = g.Ho * g.Wo;
     const uint32_t bb = udiv(q, g.d_howo), p = q - bb * HoWo;
     const uint32_t oh = udiv(p, g.d_wo), ow = p - oh * g.Wo;
@@ -703,7 +703,7 @@ struct WgtT {
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = ld1(s.ra, va, i * (int)g.sxc * 4);
   }
-  __device__ void load_bt8(const StateT& s, int r0, float (&b)[8]) const {  // dy(co, q), q contiguous
+  __device__ __forceinline__ void load_bt8(const StateT& s, int r0, float (&b)[8]) const {  // dy(co, q), q contiguous
     const int q = r0 + (int)(threadIdx.x & 31);
     const unsigned vb = q < R() ? s.brow + (unsigned)(q * 4) : SENT;
 #pragma unroll
@@ -723,15 +723,15 @@ struct DenseFwd {  // y[co][pix] = sum_r wp[co][r] col[pix][r]: M = Cout, N = B*
   const float* wp;
   float* y;
   static constexpr int LA = RK_VEC, LB = RK_VEC;
-  __host__ __device__ int M() const { return g.Cout; }
-  __host__ __device__ int N() const { return g.B * g.Ho * g.Wo; }
-  __host__ __device__ int R() const { return RP; }
+  __host__ __device__ __forceinline__ int M() const { return g.Cout; }
+  __host__ __device__ __forceinline__ int N() const { return g.B * g.Ho * g.Wo; }
+  __host__ __device__ __forceinline__ int R() const { return RP; }
   struct State {
     rsrc_t ra, rb;
     unsigned a0, b0;
     bool aok[2], bok[2];
   };
-  __device__ State init(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ State init(int k, int m0, int n0, int tid) const {
     State s;
     s.ra = make_rsrc(wp + (int64_t)k * g.Cout * RP, (int64_t)g.Cout * RP);
     s.rb = make_rsrc(col + (int64_t)k * N() * RP, (int64_t)N() * RP);
@@ -744,7 +744,7 @@ struct DenseFwd {  // y[co][pix] = sum_r wp[co][r] col[pix][r]: M = Cout, N = B*
     }
     return s;
   }
-  __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
+  __device__ __forceinline__ void load_a(const State& s, int r0, float (&a)[8]) const {
     const bool kok = r0 + 4 * (int)(threadIdx.x % 8) < RP;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -753,7 +753,7 @@ struct DenseFwd {  // y[co][pix] = sum_r wp[co][r] col[pix][r]: M = Cout, N = B*
       for (int e = 0; e < 4; ++e) a[4 * i + e] = qa[e];
     }
   }
-  __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
+  __device__ __forceinline__ void load_b(const State& s, int r0, float (&b)[8]) const {
     const bool kok = r0 + 4 * (int)(threadIdx.x % 8) < RP;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -763,11 +763,11 @@ struct DenseFwd {  // y[co][pix] = sum_r wp[co][r] col[pix][r]: M = Cout, N = B*
     }
   }
   // y[k][m][n]: n = b*Ho*Wo + p is linear in the [K][C][B][Ho][Wo] layout
-  __device__ void store(int k, int m, int n, float v) const { y[k * g.syk + m * g.syc + n] = v; }
-  __device__ bool linear() const { return true; }
-  __device__ float* out() const { return y; }
-  __device__ int64_t tile_base(int k, int m0, int n0) const { return k * g.syk + m0 * g.syc + n0; }
-  __device__ int64_t ldm() const { return g.syc; }
+  __device__ __forceinline__ void store(int k, int m, int n, float v) const { y[k * g.syk + m * g.syc + n] = v; }
+  __device__ __forceinline__ bool linear() const { return true; }
+  __device__ __forceinline__ float* out() const { return y; }
+  __device__ __forceinline__ int64_t tile_base(int k, int m0, int n0) const { return k * g.syk + m0 * g.syc + n0; }
+  __device__ __forceinline__ int64_t ldm() const { return g.syc; }
 };
 
 struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N = RP, R = B*Ho*Wo (HoWo % 4 == 0)
@@ -777,16 +777,16 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
   const float* dy;
   float* dwp;
   static constexpr int LA = RK_VEC, LB = KR_VEC;
-  __host__ __device__ int M() const { return g.Cout; }
-  __host__ __device__ int N() const { return RP; }
-  __host__ __device__ int R() const { return g.B * g.Ho * g.Wo; }
+  __host__ __device__ __forceinline__ int M() const { return g.Cout; }
+  __host__ __device__ __forceinline__ int N() const { return RP; }
+  __host__ __device__ __forceinline__ int R() const { return g.B * g.Ho * g.Wo; }
   struct State {
     rsrc_t ra, rb;
     int arow;
     bool aok[2], nok;
     unsigned b0;
   };
-  __device__ State init(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ State init(int k, int m0, int n0, int tid) const {
     State s;
     s.ra = make_rsrc(dy + k * g.syk, g.yext);
     s.rb = make_rsrc(col + (int64_t)k * R() * RP, (int64_t)R() * RP);
@@ -798,7 +798,7 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
     s.b0 = (unsigned)(((tid / 16) * RP + n) * 4);
     return s;
   }
-  __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
+  __device__ __forceinline__ void load_a(const State& s, int r0, float (&a)[8]) const {
     const int tid = threadIdx.x, R = this->R();
     const int q = r0 + 4 * (tid % 8);  // dy[co][q]: q = b*Ho*Wo + p contiguous per channel
     const unsigned va = (unsigned)((s.arow + q) * 4);
@@ -809,7 +809,7 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
       for (int e = 0; e < 4; ++e) a[4 * i + e] = qa[e];
     }
   }
-  __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
+  __device__ __forceinline__ void load_b(const State& s, int r0, float (&b)[8]) const {
     const int tid = threadIdx.x, R = this->R();
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -819,11 +819,11 @@ struct DenseWgt {  // dwp[co][r] = sum_pix dy[co][pix] col[pix][r]: M = Cout, N 
       for (int e = 0; e < 4; ++e) b[4 * i + e] = qb[e];
     }
   }
-  __device__ void store(int k, int m, int n, float v) const { dwp[((int64_t)k * g.Cout + m) * RP + n] = v; }
-  __device__ bool linear() const { return true; }
-  __device__ float* out() const { return dwp; }
-  __device__ int64_t tile_base(int k, int m0, int n0) const { return ((int64_t)k * g.Cout + m0) * RP + n0; }
-  __device__ int64_t ldm() const { return RP; }
+  __device__ __forceinline__ void store(int k, int m, int n, float v) const { dwp[((int64_t)k * g.Cout + m) * RP + n] = v; }
+  __device__ __forceinline__ bool linear() const { return true; }
+  __device__ __forceinline__ float* out() const { return dwp; }
+  __device__ __forceinline__ int64_t tile_base(int k, int m0, int n0) const { return ((int64_t)k * g.Cout + m0) * RP + n0; }
+  __device__ __forceinline__ int64_t ldm() const { return RP; }
 };
 
 // The same two GEMMs with the im2col operand gathered on the fly from x
@@ -838,16 +838,16 @@ struct StemFwd {  // y[co][pix] = sum_r wp[co][r] x(pix; r): M = Cout, N = B*Ho*
   const float* wp;
   float* y;
   static constexpr int LA = RK_VEC, LB = KR_GATHER;
-  __host__ __device__ int M() const { return g.Cout; }
-  __host__ __device__ int N() const { return g.B * g.Ho * g.Wo; }
-  __host__ __device__ int R() const { return RP; }
+  __host__ __device__ __forceinline__ int M() const { return g.Cout; }
+  __host__ __device__ __forceinline__ int N() const { return g.B * g.Ho * g.Wo; }
+  __host__ __device__ __forceinline__ int R() const { return RP; }
   struct State {
     rsrc_t ra, rb;
     unsigned a0;
     bool aok[2], nok;
     int ih0, iw0, xoff;
   };
-  __device__ State init(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ State init(int k, int m0, int n0, int tid) const {
     State s;
     s.ra = make_rsrc(wp + (int64_t)k * g.Cout * RP, (int64_t)g.Cout * RP);
     s.a0 = (unsigned)(((m0 + tid / 8) * RP + 4 * (tid % 8)) * 4);
@@ -863,7 +863,7 @@ struct StemFwd {  // y[co][pix] = sum_r wp[co][r] x(pix; r): M = Cout, N = B*Ho*
     s.xoff = (int)(bb * g.sxb);
     return s;
   }
-  __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
+  __device__ __forceinline__ void load_a(const State& s, int r0, float (&a)[8]) const {
     const bool kok = r0 + 4 * (int)(threadIdx.x % 8) < RP;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -873,7 +873,7 @@ struct StemFwd {  // y[co][pix] = sum_r wp[co][r] x(pix; r): M = Cout, N = B*Ho*
     }
   }
   // k-row tid/64 + 4i is the wave's: (ci, kh, kw) are wave-uniform (SGPRs)
-  __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
+  __device__ __forceinline__ void load_b(const State& s, int r0, float (&b)[8]) const {
     const int KK = g.KH * g.KW;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -887,11 +887,11 @@ struct StemFwd {  // y[co][pix] = sum_r wp[co][r] x(pix; r): M = Cout, N = B*Ho*
       b[i] = ld1(s.rb, vb, uni(ci * (int)g.sxc * 4));
     }
   }
-  __device__ void store(int k, int m, int n, float v) const { y[k * g.syk + m * g.syc + n] = v; }
-  __device__ bool linear() const { return true; }
-  __device__ float* out() const { return y; }
-  __device__ int64_t tile_base(int k, int m0, int n0) const { return k * g.syk + m0 * g.syc + n0; }
-  __device__ int64_t ldm() const { return g.syc; }
+  __device__ __forceinline__ void store(int k, int m, int n, float v) const { y[k * g.syk + m * g.syc + n] = v; }
+  __device__ __forceinline__ bool linear() const { return true; }
+  __device__ __forceinline__ float* out() const { return y; }
+  __device__ __forceinline__ int64_t tile_base(int k, int m0, int n0) const { return k * g.syk + m0 * g.syc + n0; }
+  __device__ __forceinline__ int64_t ldm() const { return g.syc; }
 };
 
 struct StemWgt {  // dwp[co][r] = sum_pix dy[co][pix] x(pix; r): M = Cout, N = RP, R = B*Ho*Wo (HoWo % 4 == 0)
@@ -902,9 +902,9 @@ struct StemWgt {  // dwp[co][r] = sum_pix dy[co][pix] x(pix; r): M = Cout, N = R
   const float* dy;
   float* dwp;
   static constexpr int LA = RK_VEC, LB = KR_VEC;
-  __host__ __device__ int M() const { return g.Cout; }
-  __host__ __device__ int N() const { return RP; }
-  __host__ __device__ int R() const { return g.B * g.Ho * g.Wo; }
+  __host__ __device__ __forceinline__ int M() const { return g.Cout; }
+  __host__ __device__ __forceinline__ int N() const { return RP; }
+  __host__ __device__ __forceinline__ int R() const { return g.B * g.Ho * g.Wo; }
   struct State {
     rsrc_t ra, rb;
     int arow;
@@ -912,7 +912,7 @@ struct StemWgt {  // dwp[co][r] = sum_pix dy[co][pix] x(pix; r): M = Cout, N = R
     int roff[4];          // this thread's 4 reduction columns r: ci*sxc + kh*W + kw
     int8_t kh[4], kw[4];  // (kh = -128: r past R)
   };
-  __device__ State init(int k, int m0, int n0, int tid) const {
+  __device__ __forceinline__ State init(int k, int m0, int n0, int tid) const {
     State s;
     s.ra = make_rsrc(dy + k * g.syk, g.yext);
     s.arow = (int)((m0 + tid / 8) * g.syc);
@@ -932,7 +932,7 @@ struct StemWgt {  // dwp[co][r] = sum_pix dy[co][pix] x(pix; r): M = Cout, N = R
     }
     return s;
   }
-  __device__ void load_a(const State& s, int r0, float (&a)[8]) const {
+  __device__ __forceinline__ void load_a(const State& s, int r0, float (&a)[8]) const {
     const int tid = threadIdx.x, R = this->R();
     const int q = r0 + 4 * (tid % 8);  // dy[co][q]: q = b*Ho*Wo + p contiguous per channel
     const unsigned va = (unsigned)((s.arow + q) * 4);
@@ -944,7 +944,7 @@ struct StemWgt {  // dwp[co][r] = sum_pix dy[co][pix] x(pix; r): M = Cout, N = R
     }
   }
   // KR_VEC image: pixel k-rows tid/16 + 16i, columns r = n0 + 4 (tid % 16) + e
-  __device__ void load_b(const State& s, int r0, float (&b)[8]) const {
+  __device__ __forceinline__ void load_b(const State& s, int r0, float (&b)[8]) const {
     const int tid = threadIdx.x, R = this->R(), HoWo = g.Ho * g.Wo;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -962,11 +962,11 @@ struct StemWgt {  // dwp[co][r] = sum_pix dy[co][pix] x(pix; r): M = Cout, N = R
       }
     }
   }
-  __device__ void store(int k, int m, int n, float v) const { dwp[((int64_t)k * g.Cout + m) * RP + n] = v; }
-  __device__ bool linear() const { return true; }
-  __device__ float* out() const { return dwp; }
-  __device__ int64_t tile_base(int k, int m0, int n0) const { return ((int64_t)k * g.Cout + m0) * RP + n0; }
-  __device__ int64_t ldm() const { return RP; }
+  __device__ __forceinline__ void store(int k, int m, int n, float v) const { dwp[((int64_t)k * g.Cout + m) * RP + n] = v; }
+  __device__ __forceinline__ bool linear() const { return true; }
+  __device__ __forceinline__ float* out() const { return dwp; }
+  __device__ __forceinline__ int64_t tile_base(int k, int m0, int n0) const { return ((int64_t)k * g.Cout + m0) * RP + n0; }
+  __device__ __forceinline__ int64_t ldm() const { return RP; }
 };
 
 // col[k][pix][RP] (grid: pixel blocks x K).  A workgroup builds IM_PB whole
@@ -1042,19 +1042,20 @@ __device__ __forceinline__ float apply_act(int act, float v, const float* aux, i
 
 template <int AM, int BMD>
 struct BGemm : BGemmArgs {
+  static constexpr int AMODE = AM, BMODE = BMD;
   static constexpr bool QUAD_A = FLR_QUAD != 0 && AM == BM_RK, QUAD_B = FLR_QUAD != 0 && BMD == BM_RK;
   static constexpr int LA = AM == BM_RK ? RK_VEC : (AM == BM_KR ? KR_VEC : RK_GATHER);
   static constexpr int LB = BMD == BM_RK ? RK_VEC : (BMD == BM_KR ? KR_VEC : RK_GATHER);
-  __host__ __device__ int M() const { return m; }
-  __host__ __device__ int N() const { return n; }
-  __host__ __device__ int R() const { return r; }
+  __host__ __device__ __forceinline__ int M() const { return m; }
+  __host__ __device__ __forceinline__ int N() const { return n; }
+  __host__ __device__ __forceinline__ int R() const { return r; }
   struct State {
     rsrc_t ra, rb;
     int arow, brow;
   };
   // one operand (rows = m or n) of a 64 x 32 tile, in the layout its mode stashes
   template <int MODE>
-  __device__ static void load_op(rsrc_t rs, int base_row, int rows, int r0, int R, int64_t s_row, int64_t s_r,
+  __device__ __forceinline__ static void load_op(rsrc_t rs, int base_row, int rows, int r0, int R, int64_t s_row, int64_t s_r,
                                  float (&v)[8]) {
     const int tid = threadIdx.x;
     if constexpr (MODE == BM_RK) {  // rows tid/8 + 32 i, k = r0 + 4 (tid % 8) .. +3
@@ -1090,7 +1091,7 @@ struct BGemm : BGemmArgs {
       }
     }
   }
-  __device__ State init(int k, int m0, int n0, int) const {
+  __device__ __forceinline__ State init(int k, int m0, int n0, int) const {
     State s;
     s.ra = make_rsrc(a + k * a_k, a_ext);
     s.rb = make_rsrc(b + k * b_k, b_ext);
@@ -1098,13 +1099,13 @@ struct BGemm : BGemmArgs {
     s.brow = n0;
     return s;
   }
-  __device__ void load_a(const State& s, int r0, float (&v)[8]) const {
+  __device__ __forceinline__ void load_a(const State& s, int r0, float (&v)[8]) const {
     load_op<AM>(s.ra, s.arow, m, r0, r, a_m, a_r, v);
   }
-  __device__ void load_b(const State& s, int r0, float (&v)[8]) const {
+  __device__ __forceinline__ void load_b(const State& s, int r0, float (&v)[8]) const {
     load_op<BMD>(s.rb, s.brow, n, r0, r, b_n, b_r, v);
   }
-  __device__ void store(int k, int mm, int nn, float v) const {
+  __device__ __forceinline__ void store(int k, int mm, int nn, float v) const {
     const int64_t i = k * c_k + mm * c_m + nn * c_n;
     if (bias) v = bias[k * bias_k + nn] + v;
     if (add) v = add[i] + v;
@@ -1118,7 +1119,8 @@ struct BGemm : BGemmArgs {
   // first store.  Per value, store()'s load -> store chain serialised on memory
   // latency (the stores may alias the operands): the bias epilogue cost 141 us
   // of 252 on the GRU input projection.  Same operations in the same order.
-  __device__ void store_tile(int k, int tm0, int tn0, int ml0, int nl, const f32x16& acc, int M, int N) const {
+  __device__ __forceinline__ void store_tile(int k, int tm0, int tn0, int ml0, int nl, const f32x16& acc, int M,
+                                             int N) const {
     // the plain epilogue's addressing: one uniform tile base, per value the
     // offset ml c_m + nl c_n (ml = ml0 + r, r = (e & 3) + 8 (e >> 2)), bounds as
     // predicates (no early exit)
@@ -1152,13 +1154,13 @@ struct BGemm : BGemmArgs {
     }
   }
   // the plain epilogue (row-major output, at most a bias: added there as bias + v)
-  __device__ bool linear() const { return c_n == 1 && !add && !act && !mul && !pre; }
-  __device__ float* out() const { return c; }
-  __device__ int64_t tile_base(int k, int m0, int n0) const { return k * c_k + m0 * c_m + n0; }
-  __device__ int64_t ldm() const { return c_m; }
+  __device__ __forceinline__ bool linear() const { return c_n == 1 && !add && !act && !mul && !pre; }
+  __device__ __forceinline__ float* out() const { return c; }
+  __device__ __forceinline__ int64_t tile_base(int k, int m0, int n0) const { return k * c_k + m0 * c_m + n0; }
+  __device__ __forceinline__ int64_t ldm() const { return c_m; }
   using State8 = State;
   template <int MODE>
-  __device__ static void load_op8(rsrc_t rs, int base_row, int rows, int r0, int R, int64_t s_row, int64_t s_r,
+  __device__ __forceinline__ static void load_op8(rsrc_t rs, int base_row, int rows, int r0, int R, int64_t s_row, int64_t s_r,
                                   float (&v)[8]) {
     const int tid = threadIdx.x;
     constexpr bool Q = FLR_QUAD != 0 && MODE == BM_RK;
@@ -1182,18 +1184,18 @@ struct BGemm : BGemmArgs {
       }
     }
   }
-  __device__ State8 init8(int k, int m0, int n0, int tid) const { return init(k, m0, n0, tid); }
-  __device__ void load_a8(const State8& s, int r0, float (&v)[8]) const {
+  __device__ __forceinline__ State8 init8(int k, int m0, int n0, int tid) const { return init(k, m0, n0, tid); }
+  __device__ __forceinline__ void load_a8(const State8& s, int r0, float (&v)[8]) const {
     load_op8<AM>(s.ra, s.arow, m, r0, r, a_m, a_r, v);
   }
-  __device__ void load_b8(const State8& s, int r0, float (&v)[8]) const {
+  __device__ __forceinline__ void load_b8(const State8& s, int r0, float (&v)[8]) const {
     load_op8<BMD>(s.rb, s.brow, n, r0, r, b_n, b_r, v);
   }
   // transposed-image loads of a k-contiguous (RK) operand (wsgemm_kernel): thread t
   // reads k = r0 + (t & 31) of rows 8 (t >> 5) .. +7 — a half-wave covers 128 B of a row
   using StateT = State;
-  __device__ StateT initT(int k, int m0, int n0, int tid) const { return init(k, m0, n0, tid); }
-  __device__ static void load_opT(rsrc_t rs, int base_row, int rows, int r0, int R, int64_t s_row, float (&v)[8]) {
+  __device__ __forceinline__ StateT initT(int k, int m0, int n0, int tid) const { return init(k, m0, n0, tid); }
+  __device__ __forceinline__ static void load_opT(rsrc_t rs, int base_row, int rows, int r0, int R, int64_t s_row, float (&v)[8]) {
     const int kk = r0 + (int)(threadIdx.x & 31);
     const int row0 = base_row + 8 * (int)(threadIdx.x >> 5);
     const unsigned base = (unsigned)((row0 * s_row + kk) * 4);
@@ -1203,11 +1205,49 @@ struct BGemm : BGemmArgs {
       v[i] = ld1(rs, ok ? base + (unsigned)(i * s_row * 4) : SENT, 0);
     }
   }
-  __device__ void load_at8(const StateT& s, int r0, float (&v)[8]) const {
+  __device__ __forceinline__ void load_at8(const StateT& s, int r0, float (&v)[8]) const {
     load_opT(s.ra, s.arow, m, r0, r, a_m, v);
   }
-  __device__ void load_bt8(const StateT& s, int r0, float (&v)[8]) const {
+  __device__ __forceinline__ void load_bt8(const StateT& s, int r0, float (&v)[8]) const {
     load_opT(s.rb, s.brow, n, r0, r, b_n, v);
+  }
+  // LDS-DMA fill of one 128-row x 32-k operand image (dsgemm_kernel): 16 pieces of
+  // 1 KB, one buffer_load_dwordx4 ... lds each, pieces 4 wave .. 4 wave + 3 issued by
+  // this wave.  The destination is lane-linear, so the images' swizzles are applied
+  // to the SOURCE address (lane -> the logical chunk its physical slot holds):
+  //   RK [128 rows][32 k]: physical 16-B chunk of (row, q) = q ^ ((row >> 1) & 7)
+  //      (a ds_read_b128 group of 16 rows hits 16 distinct bank groups);
+  //   KR [32 k][128 rows]: physical 4-row chunk of (k, c) = c ^ (8 ((k >> 3) & 1))
+  //      (the two half-waves' ds_read_b32, k and k + 8, on disjoint bank halves).
+  // Out-of-range rows / reductions read 0 (raw buffer bounds), as the register loads.
+  template <int MODE>
+  __device__ __forceinline__ static void dma_op(rsrc_t rs, float* img, int base_row, int rows, int r0, int R, int64_t s_row,
+                                int64_t s_r, int wave, int lane) {
+    static_assert(MODE == BM_RK || MODE == BM_KR, "LDS-DMA images hold RK or KR operands");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int piece = 4 * wave + i;  // wave-uniform: the LDS base goes to M0
+      unsigned voff;
+      if constexpr (MODE == BM_RK) {  // 8 rows x 128 B per piece
+        const int rl = 8 * piece + (lane >> 3);
+        const int q = (lane & 7) ^ ((rl >> 1) & 7);
+        const int row = base_row + rl, kk = r0 + 4 * q;
+        voff = ((row < rows) & (kk < R)) ? (unsigned)((row * s_row + kk) * 4) : SENT;
+      } else {  // 2 k-rows x 512 B per piece
+        const int kl = 2 * piece + (lane >> 5);
+        const int q = (lane & 31) ^ (((kl >> 3) & 1) << 3);
+        const int row = base_row + 4 * q, kk = r0 + kl;
+        voff = ((row < rows) & (kk < R)) ? (unsigned)((kk * s_r + row) * 4) : SENT;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + piece * 256), 16,
+                                               voff, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void dma_a(const State& s, float* img, int r0, int wave, int lane) const {
+    dma_op<AM>(s.ra, img, s.arow, m, r0, r, a_m, a_r, wave, lane);
+  }
+  __device__ __forceinline__ void dma_b(const State& s, float* img, int r0, int wave, int lane) const {
+    dma_op<BMD>(s.rb, img, s.brow, n, r0, r, b_n, b_r, wave, lane);
   }
 };
 
@@ -1652,6 +1692,89 @@ template <> struct has_k8<DgradT> : std::true_type {};
 // cache line per lane): l1 wgrad 202 -> 366 us measured.
 template <int A, int B> struct has_k8<BGemm<A, B>> : std::true_type {};
 
+// The epilogue of the split-at-stash and LDS-DMA forms: this wave's MSW x NS
+// accumulator tiles (32 x 32 each, at (m0 + m_off(i), n0 + n_off(j))) to the
+// plan's output (S == 1: epilogue operands loaded before the stores) or to the
+// split-K partials.
+template <int MSW, int NS>
+struct TileOffs {
+  int m[MSW], n[NS];  // the wave's 32 x 32 blocks' row / column offsets from (m0, n0)
+};
+template <class Plan, int MSW, int NS>
+__device__ __forceinline__ void sg_store(const Plan& pl, int S, float* __restrict__ part, int k, int split, int m0,
+                                         int n0, int h, int l32, int M, int N, f32x16 (&acc)[MSW][NS],
+                                         const TileOffs<MSW, NS> off) {
+  // C/D map of the 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < MSW; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      // (tm0, tn0): this wave's 32 x 32 block; offsets inside it below
+      const int tm0 = m0 + off.m[i], tn0 = n0 + off.n[j];
+      if (S == 1 && pl.linear()) {
+        float* base = pl.out() + pl.tile_base(k, tm0, tn0);
+        const int64_t ldm = pl.ldm();
+        const int nl = l32;
+        if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
+          if (pl.bias) {  // the batched GEMM's bias: one value per lane column, bias + v
+            const float bv = tn0 + nl < N ? pl.bias[k * pl.bias_k + tn0 + nl] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = bv + acc[i][j][e];
+          }
+        }
+        if (const float* abase = plan_add(pl)) {  // all 16 addends in flight before the first store
+          abase += pl.tile_base(k, tm0, tn0);
+          float av[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int ml = (e & 3) + 8 * (e >> 2) + 4 * h;
+            av[e] = (tm0 + ml < M && tn0 + nl < N) ? abase[ml * ldm + nl] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] = __fadd_rn(acc[i][j][e], av[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int ml = (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (tm0 + ml < M && tn0 + nl < N) base[ml * ldm + nl] = acc[i][j][e];
+        }
+        continue;
+      }
+      if constexpr (std::is_same<Plan, DgradT>::value) {
+        if (S == 1 && pl.add) {  // parity-class stores: the addends loaded before any store
+          int64_t ix[16];
+          float av[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int m = tm0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int n = tn0 + l32;
+            ix[e] = (m < M && n < N) ? pl.index(k, m, n) : -1;
+            av[e] = ix[e] >= 0 ? pl.add[ix[e]] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (ix[e] >= 0) pl.dx[ix[e]] = __fadd_rn(acc[i][j][e], av[e]);
+          continue;
+        }
+      }
+      if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
+        if (S == 1) {
+          pl.store_tile(k, tm0, tn0, 4 * h, l32, acc[i][j], M, N);
+          continue;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = tm0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int n = tn0 + l32;
+        if (m < M && n < N) {
+          if (S == 1) pl.store(k, m, n, acc[i][j][e]);
+          else part[(((int64_t)split * pl.g.Kc + k) * M + m) * N + n] = acc[i][j][e];
+        }
+      }
+    }
+}
+
 // Two LDS stages (one barrier per K-tile, tile t+1 stashed into the other stage
 // during tile t's MFMAs, one workgroup per CU by LDS) were measured 20-35 %
 // slower than this one-stage form at two workgroups per CU (C3 conv and C4
@@ -1806,75 +1929,12 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
       }
     }
   }
-  // C/D map of the 32x32 MFMA: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+  TileOffs<MSW, NS> off;
 #pragma unroll
-  for (int i = 0; i < MSW; ++i)
+  for (int i = 0; i < MSW; ++i) off.m[i] = m_off(i);
 #pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      // (tm0, tn0): this wave's 32 x 32 block; offsets inside it below
-      const int tm0 = m0 + m_off(i), tn0 = n0 + n_off(j);
-      if (S == 1 && pl.linear()) {
-        float* base = pl.out() + pl.tile_base(k, tm0, tn0);
-        const int64_t ldm = pl.ldm();
-        const int nl = l32;
-        if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
-          if (pl.bias) {  // the batched GEMM's bias: one value per lane column, bias + v
-            const float bv = tn0 + nl < N ? pl.bias[k * pl.bias_k + tn0 + nl] : 0.f;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = bv + acc[i][j][e];
-          }
-        }
-        if (const float* abase = plan_add(pl)) {  // all 16 addends in flight before the first store
-          abase += pl.tile_base(k, tm0, tn0);
-          float av[16];
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int ml = (e & 3) + 8 * (e >> 2) + 4 * h;
-            av[e] = (tm0 + ml < M && tn0 + nl < N) ? abase[ml * ldm + nl] : 0.f;
-          }
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[i][j][e] = __fadd_rn(acc[i][j][e], av[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int ml = (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (tm0 + ml < M && tn0 + nl < N) base[ml * ldm + nl] = acc[i][j][e];
-        }
-        continue;
-      }
-      if constexpr (std::is_same<Plan, DgradT>::value) {
-        if (S == 1 && pl.add) {  // parity-class stores: the addends loaded before any store
-          int64_t ix[16];
-          float av[16];
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int m = tm0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            const int n = tn0 + l32;
-            ix[e] = (m < M && n < N) ? pl.index(k, m, n) : -1;
-            av[e] = ix[e] >= 0 ? pl.add[ix[e]] : 0.f;
-          }
-#pragma unroll
-          for (int e = 0; e < 16; ++e)
-            if (ix[e] >= 0) pl.dx[ix[e]] = __fadd_rn(acc[i][j][e], av[e]);
-          continue;
-        }
-      }
-      if constexpr (std::is_base_of<BGemmArgs, Plan>::value) {
-        if (S == 1) {
-          pl.store_tile(k, tm0, tn0, 4 * h, l32, acc[i][j], M, N);
-          continue;
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = tm0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int n = tn0 + l32;
-        if (m < M && n < N) {
-          if (S == 1) pl.store(k, m, n, acc[i][j][e]);
-          else part[(((int64_t)split * pl.g.Kc + k) * M + m) * N + n] = acc[i][j][e];
-        }
-      }
-    }
+  for (int j = 0; j < NS; ++j) off.n[j] = n_off(j);
+  sg_store<Plan, MSW, NS>(pl, S, part, k, split, m0, n0, h, l32, M, N, acc, off);
 }
 
 template <class Plan, int MS, int NS, int D, int ABL = 0, bool NAR = false>
@@ -1882,6 +1942,125 @@ __global__ __launch_bounds__(THREADS, FLR_SG_OCC) void sgemm_kernel(const Plan p
                                                                      int remap) {
   sgemm_body<Plan, MS, NS, D, ABL, NAR>(pl, S, part, remap);
 }
+
+// ---- the LDS-DMA form (FLR_BGEMM_DMA=1, batched GEMMs with RK / KR operands) ---
+// 128 x 128 tiles, four waves of 64 x 64.  The fp32 operand tiles go global ->
+// LDS by buffer_load_dwordx4 ... lds (BGemm::dma_op): no VGPR staging and no
+// ds_write pass (the split-at-stash form spends 36 % of its loop in the stash
+// writes, profiles/r3_gemm_loop/).  Two LDS stages of 32 KB, one barrier per
+// K-tile: tile t+1's DMA runs under tile t's MFMAs.  Each wave splits its own
+// fragments into bf16 hi / mid / lo at read time (twice the split work of the
+// stash form, on the VALU beside the MFMAs).  Every accumulator sees the same
+// bf16 products in the same order as sgemm_body: bit-identical.
+constexpr int DG_IMG = 128 * BK;  // floats per operand image
+template <class Plan>
+__global__ __launch_bounds__(THREADS, 2) void dsgemm_kernel(const Plan pl, int S, float* __restrict__ part,
+                                                            int remap) {
+  constexpr int MSW = 2, NS = 2;
+  __shared__ __attribute__((aligned(16))) float Lf[2][2][DG_IMG];  // [stage][A, B]
+  int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
+  if (remap) xcd_tile(bx, by, bz);
+  const int k = bz / S, split = bz % S;
+  const int M = pl.M(), N = pl.N(), R = pl.R();
+  const int ktiles = cdiv(R, BK);
+  const int rbeg = (int)((int64_t)ktiles * split / S) * BK;
+  const int rend = std::min(R, (int)((int64_t)ktiles * (split + 1) / S) * BK);
+  const int m0 = by * 128, n0 = bx * 128;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, l32 = lane & 31;
+  const typename Plan::State8 st = pl.init8(k, m0, n0, tid);
+  f32x16 acc[MSW][NS];
+#pragma unroll
+  for (int i = 0; i < MSW; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  auto dma = [&](int r0, int sg) {
+    pl.dma_a(st, &Lf[sg][0][0], r0, wave, lane);
+    pl.dma_b(st, &Lf[sg][1][0], r0, wave, lane);
+  };
+  // lane (l32, h): row `row` of the image, k = 16 s + 8 h .. +7
+  auto frag = [&](const float* img, auto modec, int row, int s, float (&v)[8]) {
+    constexpr int MODE = decltype(modec)::value;
+    if constexpr (MODE == BM_RK) {
+      const int f = (row >> 1) & 7, q0 = 4 * s + 2 * h;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(img + row * BK + 4 * (q0 ^ f));
+      const f32x4 b = *reinterpret_cast<const f32x4*>(img + row * BK + 4 * ((q0 + 1) ^ f));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = a[e];
+        v[4 + e] = b[e];
+      }
+    } else {
+      const float* p = img + (16 * s + 8 * h) * 128 + 4 * ((row >> 2) ^ (h << 3)) + (row & 3);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = p[e * 128];
+    }
+  };
+  using MA = std::integral_constant<int, Plan::AMODE>;
+  using MB = std::integral_constant<int, Plan::BMODE>;
+  auto compute = [&](int sg) {
+    const float* ia = &Lf[sg][0][0];
+    const float* ib = &Lf[sg][1][0];
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 fa[MSW][3], fb[NS][3];
+#pragma unroll
+      for (int i = 0; i < MSW; ++i) {
+        float v[8];
+        frag(ia, MA{}, 64 * i + 32 * wm + l32, s, v);
+        split3(v, fa[i][0], fa[i][1], fa[i][2]);
+      }
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        float v[8];
+        frag(ib, MB{}, 64 * j + 32 * wn + l32, s, v);
+        split3(v, fb[j][0], fb[j][1], fb[j][2]);
+      }
+#define FLR_DX(TA, TB)                                                                              \
+  _Pragma("unroll") for (int i = 0; i < MSW; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][TA], fb[j][TB], acc[i][j], 0, 0, 0);
+      // product-major, small terms first: sgemm_body's order
+      FLR_DX(1, 1) FLR_DX(0, 2) FLR_DX(2, 0) FLR_DX(0, 1) FLR_DX(1, 0) FLR_DX(0, 0)
+#undef FLR_DX
+    }
+  };
+  const int ntile = rend > rbeg ? (rend - rbeg + BK - 1) / BK : 0;
+  if (ntile > 0) {
+    dma(rbeg, 0);
+    for (int t = 0; t < ntile; ++t) {
+      // this wave's DMA of tile t landed; after the barrier every wave's has, and
+      // every wave's fragment reads of tile t-1 (the stage refilled next) are done
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t + 1 < ntile) dma(rbeg + (t + 1) * BK, (t + 1) & 1);
+      compute(t & 1);
+    }
+  }
+  auto m_off = [&](int i) { return 64 * i + 32 * wm; };
+  auto n_off = [&](int j) { return 64 * j + 32 * wn; };
+  TileOffs<MSW, NS> off;
+#pragma unroll
+  for (int i = 0; i < MSW; ++i) off.m[i] = m_off(i);
+#pragma unroll
+  for (int j = 0; j < NS; ++j) off.n[j] = n_off(j);
+  sg_store<Plan, MSW, NS>(pl, S, part, k, split, m0, n0, h, l32, M, N, acc, off);
+}
+
+// FLR_BGEMM_DMA=1 selects the LDS-DMA form (read per launch).  Off by default:
+// bit-identical, but 0-18 % SLOWER than split-at-stash at every C4 encoder shape
+// (vit.qkv 461 vs 391 us, vit.fc1 519 vs 489, vit.fc2 480 vs 455 at 32 clients;
+// profiles/r4_bgemm_dma_ab.txt): the per-wave split doubles the VALU split work
+// of the stash form, which costs more than the ds_write pass it removes.
+inline bool bgemm_dma() {
+  const char* e = getenv("FLR_BGEMM_DMA");
+  return e && e[0] == '1';
+}
+template <class P> struct dma_ok : std::false_type {};
+template <int A, int B> struct dma_ok<BGemm<A, B>> : std::integral_constant<bool, A != BM_G && B != BM_G> {};
 
 // ---- the weight gradient on split-at-stash images, transposed ----------------
 // Both operands of dW are contiguous along the reduction (pixels), so the loads
@@ -2309,6 +2488,13 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
     if (form == 5 && bgemm_timg()) {
       hipLaunchKernelGGL((wsgemm_kernel<Plan, MS, NS, 2, is_bgemm_t<Plan>::ta, is_bgemm_t<Plan>::tb>), grid,
                          dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws), xcd_remap());
+      form = -1;
+    }
+  }
+  if constexpr (dma_ok<Plan>::value && MS == 2 && NS == 2) {
+    if (form == 5 && bgemm_dma()) {
+      hipLaunchKernelGGL((dsgemm_kernel<Plan>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
+                         xcd_remap());
       form = -1;
     }
   }

@@ -44,10 +44,11 @@ def main():
         for var in variants:
             old = {k: os.environ.get(k) for k in var}
             os.environ.update(var)
-            fnn.bgemm(A, B, bias=bias, add=addt, out=out)
+            for _ in range(3):
+                fnn.bgemm(A, B, bias=bias, add=addt, out=out)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            reps = 10
+            reps = 20
             e0.record()
             for _ in range(reps):
                 fnn.bgemm(A, B, bias=bias, add=addt, out=out)
