@@ -68,4 +68,44 @@ inline SideStream* side_stream(bool create, hipStream_t st = nullptr) {
   return &ss;
 }
 
+// The text-branch stream of the ResNet + GRU trainer (train_clients.hip): the
+// embedding + GRU forward and backward run on it beside the image trunk (the
+// recurrence is a chain of small latency-bound launches that leaves most of the
+// chip idle), forked from and joined to the caller's stream by events (graph-
+// capturable).  One per device, created outside any capture; one training
+// call per device at a time.  FLR_TEXT_STREAM=0: everything on the caller's
+// stream (A/B, read per call).
+struct TextStream {
+  static constexpr int NEV = 4;  // forward fork / join, backward fork / join
+  hipStream_t s = nullptr;
+  hipEvent_t ev[NEV] = {};
+};
+
+inline bool text_stream_enabled() {
+  const char* e = getenv("FLR_TEXT_STREAM");
+  return !(e && e[0] == '0');
+}
+
+inline TextStream* text_stream(bool create, hipStream_t st = nullptr) {
+  if (!text_stream_enabled()) return nullptr;
+  static TextStream pool[64];
+  static bool made[64] = {};
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (made[dev]) return &pool[dev];
+  if (!create) return nullptr;
+  if (st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  }
+  TextStream& ts = pool[dev];
+  if (hipStreamCreateWithFlags(&ts.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  for (int i = 0; i < TextStream::NEV; ++i)
+    if (hipEventCreateWithFlags(&ts.ev[i], hipEventDisableTiming) != hipSuccess) return nullptr;
+  made[dev] = true;
+  return &ts;
+}
+
 }  // namespace flr

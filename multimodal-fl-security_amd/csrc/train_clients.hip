@@ -520,27 +520,33 @@ class Net {
     // side-stream update of the trunk (HBM-bound) runs under it (side_stream.h)
     const Param &emb = ps_[p_emb_], &wih = ps_[p_wih_], &whh = ps_[p_whh_], &bih = ps_[p_bih_],
                 &bhh = ps_[p_bhh_], &w1 = ps_[p_w1_], &b1 = ps_[p_b1_], &w2 = ps_[p_w2_], &b2 = ps_[p_b2_];
-    FLR_TRY(wait_group(gtext_, st));
+    // the text branch on its own stream beside the trunk (text_stream, side_stream.h);
+    // its workspaces (gws_, rws_, ews_) are not used by the trunk
+    const bool conc = text_ != nullptr && side_ == nullptr;
+    const hipStream_t ts = conc ? text_->s : st;
+    if (conc) FLR_TRY(fork(st, ts, 0));
+    FLR_TRY(wait_group(gtext_, ts));
     FLR_TRY(flr_embedding_fwd(emb.w, s.vocab * E_, s.vocab, tokens, N, nullptr, 0, 0, nullptr, 0, nullptr, 0, 0,
-                              nullptr, 0, K_, N, E_, emb_, st));
+                              nullptr, 0, K_, N, E_, emb_, ts));
     const int64_t H3 = 3 * H_;
-    FLR_TRY(gemm(emb_, N * E_, E_, 1, wih.w, H3 * E_, E_, 1, gi_, N * H3, H3, 1, bih.w, H3, nullptr, N, H3, E_, st));
+    FLR_TRY(gemm(emb_, N * E_, E_, 1, wih.w, H3 * E_, E_, 1, gi_, N * H3, H3, 1, bih.w, H3, nullptr, N, H3, E_, ts));
     const bool fused = B_ <= 32;
     // first step in training order: one packed copy of the global W_hh for every client
     const bool wsh = first_ && gshared_ != nullptr;
     if (fused) {
-      FLR_TRY(flr_fill(hseq_, K_ * (T_ + 1) * B_ * H_, 0.f, st));
-      FLR_TRY(flr_gru_pack(wsh ? gshared_ + whh.off : whh.w, wsh ? 1 : K_, 3, H_, H_, 0, whhP_, st));
+      FLR_TRY(flr_fill(hseq_, K_ * (T_ + 1) * B_ * H_, 0.f, ts));
+      FLR_TRY(flr_gru_pack(wsh ? gshared_ + whh.off : whh.w, wsh ? 1 : K_, 3, H_, H_, 0, whhP_, ts));
       for (int64_t t = 0; t < T_; ++t)
-        FLR_TRY(flr_gru_fwd_fused_ex(gi_, whhP_, wsh ? 1 : 0, bhh.w, hseq_, gates_, K_, B_, T_, H_, t, st));
+        FLR_TRY(flr_gru_fwd_fused_ex(gi_, whhP_, wsh ? 1 : 0, bhh.w, hseq_, gates_, K_, B_, T_, H_, t, ts));
     } else {
-      FLR_TRY(flr_fill(hseq_, K_ * (T_ + 1) * B_ * H_, 0.f, st));
+      FLR_TRY(flr_fill(hseq_, K_ * (T_ + 1) * B_ * H_, 0.f, ts));
       for (int64_t t = 0; t < T_; ++t) {
         FLR_TRY(gemm(hseq_ + t * B_ * H_, (T_ + 1) * B_ * H_, H_, 1, whh.w, H3 * H_, H_, 1, gh_, B_ * H3, H3, 1,
-                     bhh.w, H3, nullptr, B_, H3, H_, st));
-        FLR_TRY(flr_gru_fwd_step(gi_, gh_, hseq_, gates_, K_, B_, T_, H_, t, st));
+                     bhh.w, H3, nullptr, B_, H3, H_, ts));
+        FLR_TRY(flr_gru_fwd_step(gi_, gh_, hseq_, gates_, K_, B_, T_, H_, t, ts));
       }
     }
+    if (conc) FLR_TRY(fork(ts, st, 1));  // joined before the head (event recorded here, waited there)
     int seg = 0;  // the previous step's update of each trunk segment's parameters (side stream)
     FLR_TRY(wait_group(seg++, st));
     FLR_TRY(conv_fwd(stem_, ximg_, y0_, st));
@@ -568,6 +574,8 @@ class Net {
     const float* hT = hseq_ + T_ * B_ * H_;  // [K][B][H] at client stride (T+1)*B*H
     const int64_t hk = (T_ + 1) * B_ * H_, DI = Dimg_ + H_;
     // fc1 over the column blocks [img | h] (never concatenated), ReLU + dropout mask in the epilogue
+    if (conc && hipStreamWaitEvent(st, text_->ev[1], 0) != hipSuccess)
+      return launch_status("train_clients: text-stream join");
     FLR_TRY(wait_group(ghead_, st));
     pending_ = false;  // every side-stream update of the previous step is joined
     FLR_TRY(flr_bgemm_ex(x4, Dimg_ * B_, 1, B_, w1.w, F_ * DI, DI, 1, h1_, B_ * F_, F_, 1, b1.w, F_, nullptr,
@@ -595,33 +603,35 @@ class Net {
     FLR_TRY(gemm(dpre_, B_ * F_, 1, F_, hT, hk, 1, H_, w1.g + Dimg_, F_ * DI, DI, 1, nullptr, 0, nullptr, F_, H_, B_,
                  st));
     FLR_TRY(rowsum(dpre_, B_ * F_, F_, B_, F_, b1.g, st));
+    if (conc) FLR_TRY(fork(st, ts, 2));
     // GRU (ClientGRU.backward)
     if (fused) {
-      FLR_TRY(flr_gru_pack(wsh ? gshared_ + whh.off : whh.w, wsh ? 1 : K_, 1, H_, H3, 1, whhT_, st));
-      FLR_TRY(flr_gru_bwd_step(dh_, gates_, hseq_, dgh_, dgi_, dh_direct_, K_, B_, T_, H_, T_ - 1, st));
+      FLR_TRY(flr_gru_pack(wsh ? gshared_ + whh.off : whh.w, wsh ? 1 : K_, 1, H_, H3, 1, whhT_, ts));
+      FLR_TRY(flr_gru_bwd_step(dh_, gates_, hseq_, dgh_, dgi_, dh_direct_, K_, B_, T_, H_, T_ - 1, ts));
       for (int64_t t = T_ - 1; t > 0; --t)
         FLR_TRY(flr_gru_bwd_fused_ex(whhT_, wsh ? 1 : 0, gates_, hseq_, dgh_, dgi_, dh_direct_, nullptr, K_, B_, T_,
-                                     H_, t, st));
+                                     H_, t, ts));
     } else {
       const float* dh = dh_;
       for (int64_t t = T_ - 1; t >= 0; --t) {
-        FLR_TRY(flr_gru_bwd_step(dh, gates_, hseq_, dgh_, dgi_, dh_direct_, K_, B_, T_, H_, t, st));
+        FLR_TRY(flr_gru_bwd_step(dh, gates_, hseq_, dgh_, dgi_, dh_direct_, K_, B_, T_, H_, t, ts));
         if (t > 0) {
           float* out = dh == dh2_ ? dh_ : dh2_;
           FLR_TRY(gemm(dgh_ + t * B_ * H3, T_ * B_ * H3, H3, 1, whh.w, H3 * H_, 1, H_, out, B_ * H_, H_, 1, nullptr,
-                       0, dh_direct_, B_, H_, H3, st));
+                       0, dh_direct_, B_, H_, H3, ts));
           dh = out;
         }
       }
     }
     FLR_TRY(gemm(dgh_, T_ * B_ * H3, 1, H3, hseq_, hk, 1, H_, whh.g, H3 * H_, H_, 1, nullptr, 0, nullptr, H3, H_,
-                 T_ * B_, st));
-    FLR_TRY(rowsum(dgh_, T_ * B_ * H3, H3, T_ * B_, H3, bhh.g, st));
+                 T_ * B_, ts));
+    FLR_TRY(rowsum(dgh_, T_ * B_ * H3, H3, T_ * B_, H3, bhh.g, ts));
     // W_ih (ClientLinear.backward), then the embedding
-    FLR_TRY(gemm(dgi_, N * H3, H3, 1, wih.w, H3 * E_, 1, E_, demb_, N * E_, E_, 1, nullptr, 0, nullptr, N, E_, H3, st));
-    FLR_TRY(gemm(dgi_, N * H3, 1, H3, emb_, N * E_, 1, E_, wih.g, H3 * E_, E_, 1, nullptr, 0, nullptr, H3, E_, N, st));
-    FLR_TRY(rowsum(dgi_, N * H3, H3, N, H3, bih.g, st));
-    FLR_TRY(flr_embedding_bwd(demb_, tokens, N, K_, N, s.vocab, E_, emb.g, s.vocab * E_, 1, ews_, ews_n_, st));
+    FLR_TRY(gemm(dgi_, N * H3, H3, 1, wih.w, H3 * E_, 1, E_, demb_, N * E_, E_, 1, nullptr, 0, nullptr, N, E_, H3, ts));
+    FLR_TRY(gemm(dgi_, N * H3, 1, H3, emb_, N * E_, 1, E_, wih.g, H3 * E_, E_, 1, nullptr, 0, nullptr, H3, E_, N, ts));
+    FLR_TRY(rowsum(dgi_, N * H3, H3, N, H3, bih.g, ts));
+    FLR_TRY(flr_embedding_bwd(demb_, tokens, N, K_, N, s.vocab, E_, emb.g, s.vocab * E_, 1, ews_, ews_n_, ts));
+    if (conc) FLR_TRY(fork(ts, st, 3));
     // trunk, last block first
     for (int bi = (int)blocks_.size() - 1; bi >= 0; --bi) {
       Block& bk = blocks_[bi];
@@ -663,6 +673,8 @@ class Net {
       FLR_TRY(bn_bwd(stem_bn_, d_a0_, y0_, a0_, true, d_y0_, nullptr, st));
     }
     FLR_TRY(conv_bwd(stem_, ximg_, d_y0_, nullptr, st));
+    if (conc && hipStreamWaitEvent(st, text_->ev[3], 0) != hipSuccess)
+      return launch_status("train_clients: text-stream join");
     // ---------------- clip + SGD-momentum ----------------
     std::vector<float*> xb, mb;
     std::vector<const float*> gb;
@@ -733,6 +745,15 @@ class Net {
   }
 
   // the forward's wait for the previous step's side-stream update of group g
+  // record event e on `from`; with e even, `to` waits on it now (a fork); odd
+  // events are waited on later by the caller (a join)
+  int fork(hipStream_t from, hipStream_t to, int e) {
+    if (hipEventRecord(text_->ev[e], from) != hipSuccess) return launch_status("train_clients: text-stream event");
+    if (!(e & 1) && hipStreamWaitEvent(to, text_->ev[e], 0) != hipSuccess)
+      return launch_status("train_clients: text-stream fork");
+    return FLR_OK;
+  }
+
   int wait_group(int g, hipStream_t st) {
     if (!pending_) return FLR_OK;
     if (hipStreamWaitEvent(st, side_->ev[g], 0) != hipSuccess) return launch_status("train_clients: side-stream join");
@@ -905,6 +926,7 @@ class Net {
   int gtext_ = 0, ghead_ = 0;
  public:
   SideStream* side_ = nullptr;  // the optimizer's side stream (nullptr: the update runs on the caller's stream)
+  TextStream* text_ = nullptr;  // the text branch's stream (nullptr, or the side stream on: the caller's stream)
   bool stem_fused_ = false;     // bn1 + relu + maxpool fused (flr_batchnorm_relu_maxpool_fwd / _bwd)
  private:
   bool pending_ = false;        // a side-stream update the next forward must wait for
@@ -935,6 +957,7 @@ extern "C" size_t flr_train_clients_workspace(const flr_resnet_gru_spec* spec, i
                                               int64_t steps) {
   if (!spec || K < 1 || B < 1 || steps < 1) return 0;
   side_stream(true);  // created here, before any capture of the training call
+  text_stream(true);
   tc::Net net(*spec, K, B, 0.f, 1.f, nullptr);
   if (net.layout() != FLR_OK) return 0;
   return align_up(net.bytes(), 256) + align_up((size_t)steps * K * sizeof(float), 256) + 256;
@@ -979,6 +1002,7 @@ extern "C" int flr_train_clients_ex(const flr_resnet_gru_spec* spec, const float
   const bool train_order = (flags & FLR_TC_TRAIN_ORDER) != 0;
   hipStream_t st = as_stream(stream);
   net.side_ = side_stream(true, st);
+  net.text_ = text_stream(true, st);
   if (train_order) {
     net.xout_ = X;
     net.xld_ = ld;

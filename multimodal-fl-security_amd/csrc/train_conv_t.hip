@@ -2469,9 +2469,12 @@ inline bool bgemm_timg() {
 }
 
 template <class Plan, int MS, int NS>
-int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
+int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name, int split_sub = 0) {
   const int M = pl.M(), N = pl.N(), R = pl.R(), K = pl.g.Kc;
-  int S = choose_splits(M, N, R, K, MS * NS, plan_min_kt(pl));
+  // split_sub: the sub-tile count the split-K choice is made for (0: this tile's);
+  // a launch on smaller tiles with the default tile's split count computes the
+  // same sums in the same order (fill_tile below)
+  int S = choose_splits(M, N, R, K, split_sub > 0 ? split_sub : MS * NS, plan_min_kt(pl));
   if (S > 1 && (!ws || ws_bytes < (size_t)S * K * M * N * sizeof(float))) {
     // a clip-norm launch must write the slots sq_slots() promised: no silent fallback
     if constexpr (has_sq<Plan>::value) {
@@ -2626,6 +2629,34 @@ int launch_narrow(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, con
   return launch_status(name);
 }
 
+// Small client counts (K/G clients per GPU at G = 8: 16 at C3) leave the
+// default tiles' grids below one wave of the chip: layer2 / layer3 of ResNet-18
+// launch 4 workgroups of 128 x 128 per client.  Forward and data-gradient
+// launches whose grid would hold fewer than FILL_WG workgroups then run on
+// 64 x 64 tiles with the DEFAULT tile's split-K count: every output element is
+// the same K-tile / k-step / product sequence, so the result is bit-identical
+// to the default tiles (and the model to the one at G = 1).  The weight
+// gradients keep their tiles: their clip-norm partial slots follow the tile.
+// FLR_CONV_FILL=0: off (A/B, read per launch).
+constexpr int FILL_WG = 512;  // two 128 x 128 workgroups per CU on 256 CUs
+inline bool conv_fill() {
+  const char* e = getenv("FLR_CONV_FILL");
+  return !(e && e[0] == '0');
+}
+template <class Plan>
+bool fill_tile(const Plan& pl, int tile) {
+  if constexpr (!(std::is_same<Plan, FwdT>::value || std::is_same<Plan, DgradT>::value)) {
+    return false;
+  } else {
+    const int ms = tile / 10, ns = tile % 10;
+    if (ms * ns == 1 || !conv_fill()) return false;
+    const int M = pl.M(), N = pl.N(), R = pl.R();
+    const int S = choose_splits(M, N, R, pl.g.Kc, ms * ns, plan_min_kt(pl));
+    const int64_t wg = (int64_t)pl.g.Kc * cdiv(M, BM * ms) * cdiv(N, BN * ns) * S;
+    return wg < FILL_WG;
+  }
+}
+
 template <class Plan>
 int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   if (pl.R() == 0 && !std::is_same<Plan, DgradT>::value) return FLR_OK;  // a dgrad class with no tap stores zeros
@@ -2634,6 +2665,7 @@ int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char
       return launch_narrow(pl, ws, ws_bytes, st, name);
   }
   const int tile = plan_tile(pl);
+  if (fill_tile(pl, tile)) return launch_tiles<Plan, 1, 1>(pl, ws, ws_bytes, st, name, (tile / 10) * (tile % 10));
   if constexpr (wide_tiles<Plan>()) {
     switch (tile) {
       case 13: return launch_tiles<Plan, 1, 3>(pl, ws, ws_bytes, st, name);

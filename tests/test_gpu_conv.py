@@ -277,3 +277,42 @@ def test_narrow_tiles_bit_identical(cuda, shape, monkeypatch):
     for a, b in zip(*outs):
         assert not torch.isnan(a).any()
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("shape", [(16, 32, 128, 4, 4, 128, 3, 1, 1), (16, 32, 256, 2, 2, 256, 3, 1, 1),
+                                   (16, 32, 128, 4, 4, 256, 3, 2, 1), (16, 32, 64, 8, 8, 128, 3, 2, 1),
+                                   (4, 32, 64, 8, 8, 64, 3, 1, 1), (16, 32, 128, 4, 4, 256, 1, 2, 0)],
+                         ids=["l2b", "l3b", "l3a", "l2a", "l1-k4", "l3ds"])
+def test_fill_tiles_bit_identical(cuda, shape, monkeypatch):
+    """Small client counts (K/G per GPU) run the forward and data-gradient
+    launches whose default grid is under one wave of the chip on 64 x 64 tiles
+    with the default tile's split-K count (FLR_CONV_FILL): the same bits as
+    the default tiles — forward, data gradient (strided classes, split-K) and
+    the in-place addend."""
+    from flr import _capi
+    from flr.nn import _stream, _workspace_t
+    K, B, Cin, H, W, Cout, KS, stride, pad = shape
+    g = torch.Generator(device="cpu").manual_seed(sum(shape) + 11)
+    Ho, Wo = (H + 2 * pad - KS) // stride + 1, (W + 2 * pad - KS) // stride + 1
+    x = torch.randn(K * Cin, B, H, W, generator=g).to(cuda)
+    dy = torch.randn(K * Cout, B, Ho, Wo, generator=g).to(cuda)
+    wt = (torch.randn(K, KS, KS, Cin, Cout, generator=g) * 0.1).to(cuda)
+    add = torch.randn(K * Cin, B, H, W, generator=g).to(cuda)
+    geom = (K, B, Cin, H, W, Cout, KS, KS, stride, pad)
+    ws, nb = _workspace_t(geom, cuda)
+    wsp = None if ws is None else ws.data_ptr()
+    outs = []
+    for fill in ("1", "0"):
+        monkeypatch.setenv("FLR_CONV_FILL", fill)
+        y = torch.full((K * Cout, B, Ho, Wo), float("nan"), device=cuda)
+        _capi.call("flr_conv2d_fwd_t", x.data_ptr(), wt.data_ptr(), y.data_ptr(), *geom, wsp, nb, _stream(x))
+        dx = torch.full_like(x, float("nan"))
+        _capi.call("flr_conv2d_bwd_data_t", dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), *geom, wsp, nb, _stream(x))
+        acc = add.clone()
+        _capi.call("flr_conv2d_bwd_data_t_add", dy.data_ptr(), wt.data_ptr(), acc.data_ptr(), acc.data_ptr(), *geom,
+                   wsp, nb, _stream(x))
+        torch.cuda.synchronize()
+        outs.append((y.cpu(), dx.cpu(), acc.cpu()))
+    for a, b in zip(*outs):
+        assert not torch.isnan(a).any()
+        assert torch.equal(a, b)
