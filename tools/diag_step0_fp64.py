@@ -4,7 +4,8 @@ tensor, the GPU's and the fp32 reference's update error against the fp64 update
 (max over elements / max |update_64|), and where the GPU and fp32 reference
 differ most.  Tells a kernel error (GPU far from fp64, reference close) from the
 reference's own fp32 error (both off, or the reference further off).
-Usage: python tools/diag_step0_fp64.py [B] [k] [mask_seed]"""
+Usage: python tools/diag_step0_fp64.py [B] [k] [mask_seed] [steps]
+(steps: how many of the parity test's 2 generated steps to run, default 1)"""
 import os
 import sys
 
@@ -22,14 +23,15 @@ from flr.train import TrainConfig, make_dropout_masks, synthetic_batches  # noqa
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 mseed = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+nst = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 cuda = torch.device("cuda:0")
 spec = ModelSpec()
 K = 2
 glob = initial_global(spec, 42, cuda)
 # the native-trainer parity test's data (2 steps generated), its first step only
-batches = synthetic_batches(spec, 2, range(K), B, cuda)[:1]
-masks = make_dropout_masks(spec, 2, K, B, cuda, seed=mseed)[:1]
-X1, loss1, norms1 = nt.train_clients(spec, glob, batches, TrainConfig(local_steps=1), masks)
+batches = synthetic_batches(spec, 2, range(K), B, cuda)[:nst]
+masks = make_dropout_masks(spec, 2, K, B, cuda, seed=mseed)[:nst]
+X1, loss1, norms1 = nt.train_clients(spec, glob, batches, TrainConfig(local_steps=nst), masks)
 torch.cuda.synchronize()
 gl = glob.cpu()
 cb = [(im[k].cpu(), tk[k].cpu(), lb[k].cpu()) for im, tk, lb in batches]
@@ -53,7 +55,7 @@ w32 = torch.cat([u.reshape(-1) for u in upd32]).double()
 w64 = torch.cat([u.reshape(-1) for u in upd64]).double()
 wg = X1[k].cpu().double()
 g0 = gl.double()
-print(f"B={B} client {k}: loss gpu {loss1[k].item():.9g} ref32 {l32:.9g} ref64 {l64:.12g}; gpu clip norm {norms1[k].item():.9g}")
+print(f"B={B} client {k}, {nst} step(s): loss gpu {loss1[k].item():.9g} ref32 {l32:.9g} ref64 {l64:.12g}; gpu clip norm {norms1[k].item():.9g}")
 rows = []
 off = 0
 for name, shp in param_layout(spec):
@@ -64,8 +66,11 @@ for name, shp in param_layout(spec):
     sc = u64.abs().max().item()
     if sc == 0:
         continue
-    eg = (wg[sl] - w64[sl]).abs().max().item() / sc
-    er = (w32[sl] - w64[sl]).abs().max().item() / sc
+    # parity.py's figure: forgive 2 ulp of the stored fp32 weight (the fp64 weight rounded to fp32)
+    w64r = w64[sl].float()
+    ulp = (torch.nextafter(w64r.abs(), torch.tensor(float("inf"))) - w64r.abs()).double()
+    eg = ((wg[sl] - w64[sl]).abs() - 2 * ulp).clamp(min=0).max().item() / sc
+    er = ((w32[sl] - w64[sl]).abs() - 2 * ulp).clamp(min=0).max().item() / sc
     d = (wg[sl] - w32[sl]).abs()
     i = int(d.argmax())
     rows.append((max(eg, er), name, eg, er, i, d[i].item(), (wg[sl] - g0[sl])[i].item(), (w32[sl] - g0[sl])[i].item(),
