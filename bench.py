@@ -54,7 +54,7 @@ def gram_traffic(K: int, P: int):
     return (2.0 * t["fetch_kib"] + t["write_kib"]) * 1024.0
 
 
-COMMITTED_C3_STATS = "profiles/r4_c3_kernel_stats_final.txt"
+COMMITTED_C3_STATS = "profiles/r4_c3_kernel_stats_serial.txt"  # FLR_TEXT_STREAM=0: per-kernel durations without the text stream beside them
 # the C4 bench's rocprofv3 summary (gemm_mfma_from_profile of an unmodified C4 line)
 COMMITTED_C4_STATS = "profiles/r3_c4_kernel_stats.txt"
 
