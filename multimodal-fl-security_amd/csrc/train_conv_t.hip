@@ -2059,6 +2059,180 @@ inline bool bgemm_dma() {
   const char* e = getenv("FLR_BGEMM_DMA");
   return e && e[0] == '1';
 }
+// ---- the pre-split form (batched GEMMs with 128 x 128 tiles, FLR_BGEMM_PRESPLIT=1; measured slower) --
+// Each operand is split into bf16 hi / mid / lo ONCE per GEMM by presplit_kernel
+// (the same split3 as every other form) into k-contiguous planes in the
+// workspace, [3][K][rows_pad][R_pad] with rows padded to 128 and R to 32 by
+// zeros.  The GEMM (psgemm_kernel) is then a plain six-product bf16 loop: each
+// 16-deep k-step's three A and three B planes go global -> LDS by
+// buffer_load_dwordx4 ... lds into a ring of three 24-KB stages (two k-steps in
+// flight, counted vmcnt, raw barrier), fragments are one ds_read_b128 per term,
+// no VGPR staging, no ds_write, no split in the loop.  Same bf16 terms, same
+// products in the same order per accumulator: bit-identical to sgemm_body.
+constexpr int PS_ROWS = 128;                 // tile rows per operand
+constexpr int PS_PLANE = PS_ROWS * 16;       // bf16 per plane per stage (16 k per row)
+constexpr int PS_STAGE = 6 * PS_PLANE;       // A hi/mid/lo, B hi/mid/lo
+constexpr int PS_NST = 3;                    // ring stages
+constexpr int PS_PIECES = 6 * PS_PLANE * 2 / 1024;  // 1-KB DMA pieces per stage (24)
+static_assert(PS_PIECES % 4 == 0, "pieces split over four waves");
+
+inline int64_t ps_pad(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+inline size_t ps_plane_bytes(int64_t K, int64_t rows, int64_t R) {
+  return (size_t)3 * K * ps_pad(rows, PS_ROWS) * ps_pad(R, BK) * 2;
+}
+
+// planes[t][k][row][c] = term t of src(k, row, c) (0 outside rows x R)
+template <int MODE>
+__global__ __launch_bounds__(THREADS) void presplit_kernel(const float* __restrict__ src, int64_t s_k, int64_t s_row,
+                                                           int64_t s_r, int K, int rows, int R, int rows_pad,
+                                                           int R_pad, __bf16* __restrict__ planes) {
+  const int ngrp = R_pad / 8;  // 8-wide k groups per row
+  const int64_t per_k = (int64_t)rows_pad * ngrp;
+  const int64_t total = (int64_t)K * per_k;
+  for (int64_t i = (int64_t)blockIdx.x * THREADS + threadIdx.x; i < total; i += (int64_t)gridDim.x * THREADS) {
+    const int k = (int)(i / per_k);
+    const int64_t rem = i - (int64_t)k * per_k;
+    int row, grp;
+    if constexpr (MODE == BM_RK) {  // lanes along k: each reads 32 contiguous bytes
+      row = (int)(rem / ngrp);
+      grp = (int)(rem - (int64_t)row * ngrp);
+    } else {  // lanes along rows: each load instruction reads consecutive rows
+      grp = (int)(rem / rows_pad);
+      row = (int)(rem - (int64_t)grp * rows_pad);
+    }
+    float v[8];
+    const float* base = src + k * s_k + (int64_t)row * s_row;
+    if constexpr (MODE == BM_RK) {  // s_r == 1, R % 4 == 0, 16-B aligned rows: two float4 loads
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = 8 * grp + 4 * q;
+        const f32x4 x = (row < rows && c < R) ? *reinterpret_cast<const f32x4*>(base + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = x[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = 8 * grp + e;
+        v[e] = (row < rows && c < R) ? base[(int64_t)c * s_r] : 0.f;
+      }
+    }
+    bf16x8 t0, t1, t2;
+    split3(v, t0, t1, t2);
+    const int64_t plane = (int64_t)K * rows_pad * R_pad;
+    const int64_t o = ((int64_t)k * rows_pad + row) * R_pad + 8 * grp;
+    *reinterpret_cast<bf16x8*>(planes + o) = t0;
+    *reinterpret_cast<bf16x8*>(planes + plane + o) = t1;
+    *reinterpret_cast<bf16x8*>(planes + 2 * plane + o) = t2;
+  }
+}
+
+template <class Plan>
+__global__ __launch_bounds__(THREADS, 2) void psgemm_kernel(const Plan pl, int S, float* __restrict__ part, int remap,
+                                                            const __bf16* __restrict__ pa, const __bf16* __restrict__ pb,
+                                                            int Mp, int Np, int Rp) {
+  constexpr int MSW = 2, NS = 2;
+  __shared__ __attribute__((aligned(16))) __bf16 L[PS_NST * PS_STAGE];  // one array: no compiler vmcnt(0)
+  int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
+  if (remap) xcd_tile(bx, by, bz);
+  const int k = bz / S, split = bz % S;
+  const int M = pl.M(), N = pl.N(), R = pl.R();
+  const int ktiles = cdiv(R, BK);
+  const int rbeg = (int)((int64_t)ktiles * split / S) * BK;
+  const int rend = std::min(R, (int)((int64_t)ktiles * (split + 1) / S) * BK);
+  const int m0 = by * 128, n0 = bx * 128;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, l32 = lane & 31;
+  // plane (operand o, term t) of client k: rows from m0 / n0, all of R_pad
+  const int64_t pla = (int64_t)pl.g.Kc * Mp * Rp, plb = (int64_t)pl.g.Kc * Np * Rp;
+  const rsrc_t ra = make_rsrc(reinterpret_cast<const float*>(pa), 3 * pla / 2);
+  const rsrc_t rb = make_rsrc(reinterpret_cast<const float*>(pb), 3 * plb / 2);
+  f32x16 acc[MSW][NS];
+#pragma unroll
+  for (int i = 0; i < MSW; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // one 16-deep k-step into ring stage sg: piece p = (operand, term, 32-row block);
+  // lane: row (lane >> 1) of the block, its 16-B half (lane & 1) holds the k half
+  // (lane & 1) ^ ((row >> 3) & 1) (source-side swizzle)
+  auto dma = [&](int k0, int sg) {
+#pragma unroll
+    for (int q = 0; q < PS_PIECES / 4; ++q) {
+      const int piece = (PS_PIECES / 4) * wave + q;
+      const int op = piece / 12, t = (piece % 12) / 4, blk = piece % 4;
+      const int row = 32 * blk + (lane >> 1);
+      const int half = (lane & 1) ^ ((row >> 3) & 1);
+      const int64_t rows_pad = op ? Np : Mp;
+      const int64_t e = (int64_t)t * (op ? plb : pla) + ((int64_t)k * rows_pad + (op ? n0 : m0) + row) * Rp + k0 +
+                        8 * half;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? rb : ra,
+                                               (__attribute__((address_space(3))) void*)(L + sg * PS_STAGE +
+                                                                                        piece * 512),
+                                               16, (unsigned)(e * 2), 0, 0, 0);
+    }
+  };
+  auto frag = [&](int sg, int op, int t, int row) {
+    const int off = sg * PS_STAGE + (op * 3 + t) * PS_PLANE + row * 16 + 8 * (h ^ ((row >> 3) & 1));
+    return *reinterpret_cast<const bf16x8*>(L + off);
+  };
+  const int nstep = rend > rbeg ? 2 * ((rend - rbeg + BK - 1) / BK) : 0;
+  if (nstep > 0) {
+    dma(rbeg, 0);
+    if (nstep > 1) dma(rbeg + 16, 1);
+    for (int s = 0; s < nstep; ++s) {
+      // this wave's DMA of step s landed (step s+1's may still fly); after the
+      // barrier every wave's has, and every wave's reads of step s-1 are done
+      if (s + 1 < nstep) {
+        static_assert(PS_PIECES / 4 == 6, "vmcnt immediate below");
+        asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s + 2 < nstep) dma(rbeg + 16 * (s + 2), (s + 2) % PS_NST);
+      const int sg = s % PS_NST;
+      bf16x8 fa[MSW][3], fb[NS][3];
+#pragma unroll
+      for (int i = 0; i < MSW; ++i)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) fa[i][t] = frag(sg, 0, t, 64 * i + 32 * wm + l32);
+#pragma unroll
+      for (int j = 0; j < NS; ++j)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) fb[j][t] = frag(sg, 1, t, 64 * j + 32 * wn + l32);
+#define FLR_PX(TA, TB)                                                                              \
+  _Pragma("unroll") for (int i = 0; i < MSW; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][TA], fb[j][TB], acc[i][j], 0, 0, 0);
+      FLR_PX(1, 1) FLR_PX(0, 2) FLR_PX(2, 0) FLR_PX(0, 1) FLR_PX(1, 0) FLR_PX(0, 0)
+#undef FLR_PX
+    }
+  }
+  TileOffs<MSW, NS> off;
+#pragma unroll
+  for (int i = 0; i < MSW; ++i) off.m[i] = 64 * i + 32 * wm;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) off.n[j] = 64 * j + 32 * wn;
+  sg_store<Plan, MSW, NS>(pl, S, part, k, split, m0, n0, h, l32, M, N, acc, off);
+}
+
+// FLR_BGEMM_PRESPLIT=1 selects the pre-split form (read per launch and per
+// workspace query).  Off by default: bit-identical, but 1.6-3x SLOWER than
+// split-at-stash at the C4 encoder shapes (vit.qkv 624 vs 392 us, vit.fc1.dw 1484
+// vs 499 us at 32 clients; profiles/r4_bgemm_presplit_ab.txt).  Three bf16 planes
+// are 6 B per operand value against the stash form's 4 B of fp32: the 128 x 128
+// tiles re-read their operands from L2 once per opposite tile, so the loop moves
+// 1.5x the bytes (2.8 GB per vit.qkv GEMM at 32 clients), and the split pass
+// itself transposes the row-contiguous (KR) operands of the weight gradients.
+inline bool bgemm_presplit() {
+  const char* e = getenv("FLR_BGEMM_PRESPLIT");
+  return e && e[0] == '1';
+}
+
 template <class P> struct dma_ok : std::false_type {};
 template <int A, int B> struct dma_ok<BGemm<A, B>> : std::integral_constant<bool, A != BM_G && B != BM_G> {};
 
@@ -2494,6 +2668,29 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
       form = -1;
     }
   }
+  float* partp = static_cast<float*>(ws);  // split-K partials (after the planes in the pre-split form)
+  if constexpr (std::is_base_of<BGemmArgs, Plan>::value && MS == 2 && NS == 2) {
+    if (form == 5 && bgemm_presplit()) {
+      const size_t pa_b = (ps_plane_bytes(K, M, R) + 255) / 256 * 256;
+      const size_t pb_b = (ps_plane_bytes(K, N, R) + 255) / 256 * 256;
+      const size_t need = pa_b + pb_b + (S > 1 ? (size_t)S * K * M * N * sizeof(float) : 0);
+      // the planes' byte offsets must fit the 31-bit buffer voffset
+      if (ws && ws_bytes >= need && pa_b < (size_t(1) << 31) && pb_b < (size_t(1) << 31)) {
+        __bf16* pa = static_cast<__bf16*>(ws);
+        __bf16* pb = reinterpret_cast<__bf16*>(static_cast<char*>(ws) + pa_b);
+        partp = reinterpret_cast<float*>(static_cast<char*>(ws) + pa_b + pb_b);
+        const int Mp = (int)ps_pad(M, PS_ROWS), Np = (int)ps_pad(N, PS_ROWS), Rp = (int)ps_pad(R, BK);
+        auto pgrid = [](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384))); };
+        hipLaunchKernelGGL((presplit_kernel<Plan::AMODE>), pgrid((int64_t)K * Mp * Rp / 8), dim3(THREADS), 0, st, pl.a,
+                           pl.a_k, pl.a_m, pl.a_r, K, M, R, Mp, Rp, pa);
+        hipLaunchKernelGGL((presplit_kernel<Plan::BMODE>), pgrid((int64_t)K * Np * Rp / 8), dim3(THREADS), 0, st, pl.b,
+                           pl.b_k, pl.b_n, pl.b_r, K, N, R, Np, Rp, pb);
+        hipLaunchKernelGGL((psgemm_kernel<Plan>), grid, dim3(THREADS), 0, st, pl, S, partp, xcd_remap(), pa, pb, Mp,
+                           Np, Rp);
+        form = -1;
+      }
+    }
+  }
   if constexpr (dma_ok<Plan>::value && MS == 2 && NS == 2) {
     if (form == 5 && bgemm_dma()) {
       hipLaunchKernelGGL((dsgemm_kernel<Plan>), grid, dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws),
@@ -2560,7 +2757,7 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
   if (rc != FLR_OK || S == 1) return rc;
   const int64_t mn = (int64_t)M * N;
   hipLaunchKernelGGL(treduce_kernel<Plan>, dim3((unsigned)((mn + 255) / 256), (unsigned)K), dim3(256), 0, st, pl, S,
-                     static_cast<const float*>(ws));
+                     static_cast<const float*>(partp));
   return launch_status(name);
 }
 
@@ -3013,7 +3210,11 @@ extern "C" size_t flr_bgemm_workspace(int64_t batch, int64_t M, int64_t N, int64
   // the larger of the two tile shapes' split counts (sub-tile count 1 or 4)
   const int S = std::max(convt::choose_splits((int)M, (int)N, (int)R, (int)batch, 1, convt::bgemm_min_kt()),
                          convt::choose_splits((int)M, (int)N, (int)R, (int)batch, 4, convt::bgemm_min_kt()));
-  return S > 1 ? (size_t)S * batch * M * N * sizeof(float) : 0;
+  size_t n = S > 1 ? (size_t)S * batch * M * N * sizeof(float) : 0;
+  // the pre-split form's bf16 planes of both operands (128 x 128 tiles), before the partials
+  if (convt::bgemm_presplit() && bgemm_tile((int)M, (int)N, (int)R) == 22)
+    n += (convt::ps_plane_bytes(batch, M, R) + 255) / 256 * 256 + (convt::ps_plane_bytes(batch, N, R) + 255) / 256 * 256;
+  return n;
 }
 
 extern "C" int flr_bgemm(const float* A, int64_t a_k, int64_t a_m, int64_t a_r, const float* B, int64_t b_k,
