@@ -108,4 +108,42 @@ inline TextStream* text_stream(bool create, hipStream_t st = nullptr) {
   return &ts;
 }
 
+// The weight-gradient stream of the ResNet + GRU trainer: every tap-major
+// conv's weight gradient runs on it, forked after the layer's output gradient
+// is ready, while the caller's stream continues down the data-gradient chain
+// (the backward's critical path); joined before the clip + SGD step.  Per
+// device, created outside any capture; FLR_WGRAD_STREAM=0: off (A/B).
+struct WgradStream {
+  static constexpr int NEV = 48;
+  hipStream_t s = nullptr;
+  hipEvent_t ev[NEV] = {};
+};
+
+inline bool wgrad_stream_enabled() {
+  const char* e = getenv("FLR_WGRAD_STREAM");
+  return !(e && e[0] == '0');
+}
+
+inline WgradStream* wgrad_stream(bool create, hipStream_t st = nullptr) {
+  if (!wgrad_stream_enabled()) return nullptr;
+  static WgradStream pool[64];
+  static bool made[64] = {};
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (made[dev]) return &pool[dev];
+  if (!create) return nullptr;
+  if (st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  }
+  WgradStream& ws = pool[dev];
+  if (hipStreamCreateWithFlags(&ws.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  for (int i = 0; i < WgradStream::NEV; ++i)
+    if (hipEventCreateWithFlags(&ws.ev[i], hipEventDisableTiming) != hipSuccess) return nullptr;
+  made[dev] = true;
+  return &ws;
+}
+
 }  // namespace flr

@@ -368,6 +368,7 @@ class Net {
     ews_n_ = flr_embedding_bwd_workspace(K_, N);
     ews_ = alloc<char>(ews_n_);
     cws_ = alloc<char>(cws_n_);  // the largest convolution workspace (conv_ws)
+    cws2_ = alloc<char>(cws_n_);  // the weight-gradient stream's own (split-K partials)
     if (N > 4096) return FLR_ERR_UNSUPPORTED;
     return FLR_OK;
   }
@@ -587,6 +588,10 @@ class Net {
     FLR_TRY(flr_cross_entropy(logits_, labels, K_, B_, C_, loss_, dlogits_, rows_, st));
     FLR_TRY(flr_copy_rows(loss_, K_, K_, loss_row, K_, 1, st));
     // ---------------- backward ----------------
+    // the weight-gradient stream (with the side-stream optimizer off)
+    WgradStream* wgs_save = wgs_;
+    if (side_) wgs_ = nullptr;
+    wev_ = 0;
     // head (ClientMLP.backward): dpre = dlogits W2 * relu'(h1) * mask
     FLR_TRY(flr_bgemm_ex(dlogits_, B_ * C_, C_, 1, w2.w, C_ * F_, 1, F_, dpre_, B_ * F_, F_, 1, nullptr, 0, nullptr,
                          FLR_ACT_DRELU, mask, h1_, nullptr, K_, B_, F_, C_, gws_, gws_n_, st));
@@ -675,6 +680,12 @@ class Net {
     FLR_TRY(conv_bwd(stem_, ximg_, d_y0_, nullptr, st));
     if (conc && hipStreamWaitEvent(st, text_->ev[3], 0) != hipSuccess)
       return launch_status("train_clients: text-stream join");
+    if (wgs_ && wev_ > 0) {  // every weight gradient (and its clip-norm partials) before the clip
+      if (wev_ >= WgradStream::NEV) return FLR_ERR_UNSUPPORTED;
+      if (hipEventRecord(wgs_->ev[wev_], wgs_->s) != hipSuccess || hipStreamWaitEvent(st, wgs_->ev[wev_], 0) != hipSuccess)
+        return launch_status("train_clients: weight-gradient join");
+    }
+    wgs_ = wgs_save;
     // ---------------- clip + SGD-momentum ----------------
     std::vector<float*> xb, mb;
     std::vector<const float*> gb;
@@ -866,6 +877,9 @@ class Net {
     return flr_conv2d_fwd(x, p.w, y, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad, c.fws, c.fws_n, st);
   }
   // dx (when wanted) then dw, as ClientConv2d[T].backward
+  // With the weight-gradient stream (wgs_, wev_ < NEV), a tap-major conv's dW runs on
+  // it with the second workspace, forked here (dy ready on st), the data gradient
+  // on st.  The two write disjoint outputs; dy and x are not rewritten this step.
   int conv_bwd(const ConvOp& c, const float* x, const float* dy, float* dx, hipStream_t st,
                const float* add = nullptr) {
     const Param& p = ps_[c.p];
@@ -873,15 +887,24 @@ class Net {
     if (p.tap) {
       int64_t wst;
       const float* w = tap_w(p, wst);
+      hipStream_t ws = st;
+      char* wsp = cws_;
+      if (wgs_ && wev_ + 1 < WgradStream::NEV) {  // one event kept for the join
+        if (hipEventRecord(wgs_->ev[wev_], st) != hipSuccess || hipStreamWaitEvent(wgs_->s, wgs_->ev[wev_], 0) != hipSuccess)
+          return launch_status("train_clients: weight-gradient fork");
+        ++wev_;
+        ws = wgs_->s;
+        wsp = cws2_;
+      }
       if (dx && (rc = flr_conv2d_bwd_data_t_ex(dy, w, wst, add, dx, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k,
                                                c.stride, c.pad, cws_, cws_n_, st)) != FLR_OK)
         return rc;
       const int zero_dead = p.dead ? 0 : 1;
       if (p.sq_base >= 0)
         return flr_conv2d_bwd_weight_t_sq(x, dy, p.g, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad,
-                                          zero_dead, sq_ + p.sq_base, std::max<int64_t>(1, nsq_), cws_, cws_n_, st);
+                                          zero_dead, sq_ + p.sq_base, std::max<int64_t>(1, nsq_), wsp, cws_n_, ws);
       return flr_conv2d_bwd_weight_t(x, dy, p.g, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad, zero_dead,
-                                     cws_, cws_n_, st);
+                                     wsp, cws_n_, ws);
     }
     if (dx && (rc = flr_conv2d_bwd_data(dy, p.w, dx, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad, cws_,
                                         cws_n_, st)) != FLR_OK)
@@ -927,10 +950,12 @@ class Net {
  public:
   SideStream* side_ = nullptr;  // the optimizer's side stream (nullptr: the update runs on the caller's stream)
   TextStream* text_ = nullptr;  // the text branch's stream (nullptr, or the side stream on: the caller's stream)
+  WgradStream* wgs_ = nullptr;  // the weight-gradient stream (nullptr: on the caller's stream)
+  int wev_ = 0;                 // fork events used this step
   bool stem_fused_ = false;     // bn1 + relu + maxpool fused (flr_batchnorm_relu_maxpool_fwd / _bwd)
  private:
   bool pending_ = false;        // a side-stream update the next forward must wait for
-  char *sgd_ws_ = nullptr, *gws_ = nullptr, *rws_ = nullptr, *ews_ = nullptr, *cws_ = nullptr;
+  char *sgd_ws_ = nullptr, *gws_ = nullptr, *rws_ = nullptr, *ews_ = nullptr, *cws_ = nullptr, *cws2_ = nullptr;
   size_t sgd_ws_n_ = 0, gws_n_ = 0, rws_n_ = 0, ews_n_ = 0, cws_n_ = 0;
   float *ximg_ = nullptr, *y0_ = nullptr, *a0_ = nullptr, *d_a0_ = nullptr, *d_y0_ = nullptr, *p0_ = nullptr,
         *d_p0_ = nullptr, *d_x4_ = nullptr;
@@ -958,6 +983,7 @@ extern "C" size_t flr_train_clients_workspace(const flr_resnet_gru_spec* spec, i
   if (!spec || K < 1 || B < 1 || steps < 1) return 0;
   side_stream(true);  // created here, before any capture of the training call
   text_stream(true);
+  wgrad_stream(true);
   tc::Net net(*spec, K, B, 0.f, 1.f, nullptr);
   if (net.layout() != FLR_OK) return 0;
   return align_up(net.bytes(), 256) + align_up((size_t)steps * K * sizeof(float), 256) + 256;
@@ -1003,6 +1029,7 @@ extern "C" int flr_train_clients_ex(const flr_resnet_gru_spec* spec, const float
   hipStream_t st = as_stream(stream);
   net.side_ = side_stream(true, st);
   net.text_ = text_stream(true, st);
+  net.wgs_ = wgrad_stream(true, st);
   if (train_order) {
     net.xout_ = X;
     net.xld_ = ld;
