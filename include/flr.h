@@ -694,11 +694,12 @@ int flr_attention_bwd(const float* qkv, const float* ctx, const float* dctx, con
  * trainer (flr.train.ClientBatchTrainer), so both give the same bits.  All
  * state lives in the workspace (flr_train_clients_workspace); image_size must
  * bring the trunk to a 1x1 map (32 for the four stride-2 stages).  The text
- * branch (embedding + GRU, forward and backward) runs on a per-device second
- * stream, forked from and joined to `stream` by events inside the call (graph-
- * capturable; created by flr_train_clients_workspace, outside any capture):
- * one training call per device at a time.  FLR_TEXT_STREAM=0 keeps everything
- * on `stream`. */
+ * branch (embedding + GRU, forward and backward) and the convolutions' weight
+ * gradients run on two per-device streams, forked from and joined to `stream`
+ * by events inside the call (graph-capturable; created by
+ * flr_train_clients_workspace, outside any capture): one training call per
+ * device at a time.  FLR_TEXT_STREAM=0 / FLR_WGRAD_STREAM=0 keep that work on
+ * `stream`; the results are the same bits either way. */
 typedef struct flr_resnet_gru_spec {
   int64_t num_classes, image_size, in_channels;
   int64_t widths[4], blocks[4];  /* the four ResNet stages (BasicBlock) */
