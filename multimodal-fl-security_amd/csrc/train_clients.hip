@@ -523,7 +523,7 @@ class Net {
                 &bhh = ps_[p_bhh_], &w1 = ps_[p_w1_], &b1 = ps_[p_b1_], &w2 = ps_[p_w2_], &b2 = ps_[p_b2_];
     // the text branch on its own stream beside the trunk (text_stream, side_stream.h);
     // its workspaces (gws_, rws_, ews_) are not used by the trunk
-    const bool conc = text_ != nullptr && side_ == nullptr;
+    const bool conc = text_ != nullptr;
     const hipStream_t ts = conc ? text_->s : st;
     if (conc) FLR_TRY(fork(st, ts, 0));
     FLR_TRY(wait_group(gtext_, ts));
@@ -588,9 +588,9 @@ class Net {
     FLR_TRY(flr_cross_entropy(logits_, labels, K_, B_, C_, loss_, dlogits_, rows_, st));
     FLR_TRY(flr_copy_rows(loss_, K_, K_, loss_row, K_, 1, st));
     // ---------------- backward ----------------
-    // the weight-gradient stream (with the side-stream optimizer off)
+    // the weight-gradient stream: forks from here on (every side-stream update of
+    // the previous step was joined before the head, so no update still reads p.g)
     WgradStream* wgs_save = wgs_;
-    if (side_) wgs_ = nullptr;
     wev_ = 0;
     // head (ClientMLP.backward): dpre = dlogits W2 * relu'(h1) * mask
     FLR_TRY(flr_bgemm_ex(dlogits_, B_ * C_, C_, 1, w2.w, C_ * F_, 1, F_, dpre_, B_ * F_, F_, 1, nullptr, 0, nullptr,
@@ -949,7 +949,7 @@ class Net {
   int gtext_ = 0, ghead_ = 0;
  public:
   SideStream* side_ = nullptr;  // the optimizer's side stream (nullptr: the update runs on the caller's stream)
-  TextStream* text_ = nullptr;  // the text branch's stream (nullptr, or the side stream on: the caller's stream)
+  TextStream* text_ = nullptr;  // the text branch's stream (nullptr: the caller's stream)
   WgradStream* wgs_ = nullptr;  // the weight-gradient stream (nullptr: on the caller's stream)
   int wev_ = 0;                 // fork events used this step
   bool stem_fused_ = false;     // bn1 + relu + maxpool fused (flr_batchnorm_relu_maxpool_fwd / _bwd)
