@@ -558,17 +558,32 @@ class Net {
       FLR_TRY(bn_fwd(stem_bn_, y0_, nullptr, a0_, true, st));
       FLR_TRY(flr_maxpool2d_fwd(a0_, p0_, arg0_, K_ * s.widths[0] * B_, Hs_, Hs_, 3, 3, 2, 1, st));
     }
+    // a block's shortcut (strided 1x1 conv + BN) on the weight-gradient stream, idle in
+    // the forward, beside conv1 / bn1 / conv2; joined before bn2 adds it
+    int fev = 0;
     for (auto& bk : blocks_) {
       const float* idt = bk.x_in;
       FLR_TRY(wait_group(seg++, st));
+      const bool ds_side = bk.has_ds && wgs_ && fev + 2 <= WgradStream::NEV;
       if (bk.has_ds) {
-        FLR_TRY(conv_fwd(bk.ds, bk.x_in, bk.yd, st));
-        FLR_TRY(bn_fwd(bk.bds, bk.yd, nullptr, bk.ad, false, st));
+        const hipStream_t dst = ds_side ? wgs_->s : st;
+        if (ds_side && (hipEventRecord(wgs_->ev[fev], st) != hipSuccess ||
+                        hipStreamWaitEvent(dst, wgs_->ev[fev], 0) != hipSuccess))
+          return launch_status("train_clients: shortcut fork");
+        FLR_TRY(conv_fwd(bk.ds, bk.x_in, bk.yd, dst, ds_side ? cws2_ : nullptr));
+        FLR_TRY(bn_fwd(bk.bds, bk.yd, nullptr, bk.ad, false, dst));
+        if (ds_side && hipEventRecord(wgs_->ev[fev + 1], dst) != hipSuccess)
+          return launch_status("train_clients: shortcut event");
         idt = bk.ad;
       }
       FLR_TRY(conv_fwd(bk.c1, bk.x_in, bk.y1, st));
       FLR_TRY(bn_fwd(bk.b1, bk.y1, nullptr, bk.a1, true, st));
       FLR_TRY(conv_fwd(bk.c2, bk.a1, bk.y2, st));
+      if (ds_side) {
+        if (hipStreamWaitEvent(st, wgs_->ev[fev + 1], 0) != hipSuccess)
+          return launch_status("train_clients: shortcut join");
+        fev += 2;
+      }
       FLR_TRY(bn_fwd(bk.b2, bk.y2, idt, bk.out, true, st));
     }
     const float* x4 = blocks_.back().out;  // [K][Dimg][B]: img[k][b][c] = x4[k][c][b]
@@ -866,13 +881,13 @@ class Net {
     stride = shared ? 0 : p.n;
     return shared ? gshared_ + p.off : p.w;
   }
-  int conv_fwd(const ConvOp& c, const float* x, float* y, hipStream_t st) {
+  int conv_fwd(const ConvOp& c, const float* x, float* y, hipStream_t st, char* wsp = nullptr) {
     const Param& p = ps_[c.p];
     if (p.tap) {
       int64_t wst;
       const float* w = tap_w(p, wst);
-      return flr_conv2d_fwd_t_ex(x, w, wst, y, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad, cws_,
-                                 cws_n_, st);
+      return flr_conv2d_fwd_t_ex(x, w, wst, y, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad,
+                                 wsp ? wsp : cws_, cws_n_, st);
     }
     return flr_conv2d_fwd(x, p.w, y, K_, B_, c.Cin, c.H, c.H, c.Cout, c.k, c.k, c.stride, c.pad, c.fws, c.fws_n, st);
   }
