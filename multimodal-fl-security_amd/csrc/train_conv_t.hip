@@ -2858,8 +2858,14 @@ template <class Plan>
 int launch(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, const char* name) {
   if (pl.R() == 0 && !std::is_same<Plan, DgradT>::value) return FLR_OK;  // a dgrad class with no tap stores zeros
   if constexpr (std::is_same<Plan, FwdT>::value || std::is_same<Plan, DgradT>::value) {
-    if (pl.N() <= 32 && pl.M() % (2 * BM) == 0 && pl.R() > 0 && gemm_form() == 5 && conv_narrow())
+    if (pl.N() <= 32 && pl.M() % (2 * BM) == 0 && pl.R() > 0 && gemm_form() == 5 && conv_narrow()) {
+      // a narrow launch under one wave of the chip (few clients per GPU): the 64 x 64
+      // tiles with the narrow tiles' split count — twice the workgroups, the same bits
+      const int S = choose_splits(pl.M(), pl.N(), pl.R(), pl.g.Kc, 2, plan_min_kt(pl));
+      if (conv_fill() && (int64_t)pl.g.Kc * cdiv(pl.M(), 2 * BM) * S < FILL_WG / 2)
+        return launch_tiles<Plan, 1, 1>(pl, ws, ws_bytes, st, name, 2);
       return launch_narrow(pl, ws, ws_bytes, st, name);
+    }
   }
   const int tile = plan_tile(pl);
   if (fill_tile(pl, tile)) return launch_tiles<Plan, 1, 1>(pl, ws, ws_bytes, st, name, (tile / 10) * (tile % 10));

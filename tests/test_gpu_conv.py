@@ -281,14 +281,15 @@ def test_narrow_tiles_bit_identical(cuda, shape, monkeypatch):
 
 @pytest.mark.parametrize("shape", [(16, 32, 128, 4, 4, 128, 3, 1, 1), (16, 32, 256, 2, 2, 256, 3, 1, 1),
                                    (16, 32, 128, 4, 4, 256, 3, 2, 1), (16, 32, 64, 8, 8, 128, 3, 2, 1),
-                                   (4, 32, 64, 8, 8, 64, 3, 1, 1), (16, 32, 128, 4, 4, 256, 1, 2, 0)],
-                         ids=["l2b", "l3b", "l3a", "l2a", "l1-k4", "l3ds"])
+                                   (4, 32, 64, 8, 8, 64, 3, 1, 1), (16, 32, 128, 4, 4, 256, 1, 2, 0),
+                                   (16, 32, 512, 1, 1, 512, 3, 1, 1), (16, 32, 256, 2, 2, 512, 3, 2, 1)],
+                         ids=["l2b", "l3b", "l3a", "l2a", "l1-k4", "l3ds", "l4b-narrow", "l4a-narrow"])
 def test_fill_tiles_bit_identical(cuda, shape, monkeypatch):
     """Small client counts (K/G per GPU) run the forward and data-gradient
     launches whose default grid is under one wave of the chip on 64 x 64 tiles
     with the default tile's split-K count (FLR_CONV_FILL): the same bits as
     the default tiles — forward, data gradient (strided classes, split-K) and
-    the in-place addend."""
+    the in-place addend; the l4 layers' narrow tiles (N = 32) likewise."""
     from flr import _capi
     from flr.nn import _stream, _workspace_t
     K, B, Cin, H, W, Cout, KS, stride, pad = shape
