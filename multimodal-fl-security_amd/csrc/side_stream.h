@@ -108,13 +108,14 @@ inline TextStream* text_stream(bool create, hipStream_t st = nullptr) {
   return &ts;
 }
 
-// The weight-gradient stream of the ResNet + GRU trainer: every tap-major
-// conv's weight gradient runs on it, forked after the layer's output gradient
-// is ready, while the caller's stream continues down the data-gradient chain
-// (the backward's critical path); joined before the clip + SGD step.  Per
-// device, created outside any capture; FLR_WGRAD_STREAM=0: off (A/B).
+// The weight-gradient stream of the native trainers: every tap-major conv's
+// weight gradient (ResNet + GRU) and every ViT layer's weight / bias gradients
+// (ViT + BERT) run on it, forked after the layer's output gradient is ready,
+// while the caller's stream continues down the data-gradient chain (the
+// backward's critical path); joined before the clip + SGD step.  Per device,
+// created outside any capture; FLR_WGRAD_STREAM=0: off (A/B).
 struct WgradStream {
-  static constexpr int NEV = 48;
+  static constexpr int NEV = 128;
   hipStream_t s = nullptr;
   hipEvent_t ev[NEV] = {};
 };

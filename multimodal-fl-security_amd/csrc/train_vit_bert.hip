@@ -22,6 +22,7 @@
 // kernels' scratch.  The layout is computed by a dry run (base == nullptr)
 // that sums sizes; the scratch sizes come from a dry pass over the schedule.
 #include "flr_common.h"
+#include "side_stream.h"
 
 #include <algorithm>
 #include <string>
@@ -217,6 +218,12 @@ class Net {
     for (float*& p : vd_) p = alloc<float>(KC * Rv * Dv_);
     vdq_ = alloc<float>(KC * Rv * 3 * Dv_);
     vdp_ = alloc<float>(KC * Rv * Mv_);
+    // the weight-gradient stream's second copies: a ViT layer's side work reads them
+    // while the next layer writes the first (vd_[6]: the third buffer of the dL/dr ring)
+    vdq2_ = alloc<float>(KC * Rv * 3 * Dv_);
+    vdp2_ = alloc<float>(KC * Rv * Mv_);
+    vdx2b_ = alloc<float>(KC * Rv * Dv_);
+    vdr3_ = alloc<float>(KC * Rv * Dv_);
     dtok_ = alloc<float>(KC * B_ * NP_ * Dv_);
     for (float*& p : bd_) p = alloc<float>(KC * Rb * Db_);
     bdq_ = alloc<float>(KC * Rb * 3 * Db_);
@@ -229,6 +236,8 @@ class Net {
     if (rc != FLR_OK) return rc;
     gws_ = alloc<char>(gws_n_);
     rws_ = alloc<char>(rws_n_);
+    gws2_ = alloc<char>(gws_n_);  // the weight-gradient stream's own
+    rws2_ = alloc<char>(rws_n_);
     lws_ = alloc<char>(lws_n_);
     ews_ = alloc<char>(ews_n_);
     return FLR_OK;
@@ -270,6 +279,9 @@ class Net {
                                        last ? X + c0 * ld : nullptr, last ? xoffs.data() : nullptr, ld, neg, nullptr,
                                        nullptr, 0, norms ? norms + c0 : nullptr, sgd_ws_, sgd_ws_n_, st);
   }
+
+  // the weight-gradient stream of the ViT layers' backward (nullptr: all on the caller's)
+  void set_wgrad_stream(WgradStream* w) { wgs_ = w; }
 
  private:
   // ---- the forward + backward of one pass ----------------------------------
@@ -400,29 +412,57 @@ class Net {
     }
     // the final LayerNorm: its dx is the gradient of both s (x) and the last MLP branch r
     FLR_TRY(ln_bwd(vdm, sf_, p_nw_, p_nb_, meanf_, rstdf_, nullptr, vdA, Rv, Dv));
-    for (int i = (int)vl_.size() - 1; i >= 0; --i) {
+    // With the weight-gradient stream, layer i's weight / bias gradients run on it beside
+    // the data-gradient chain of layers i and i-1: the scratch they read (dL/dr in a ring
+    // of three, d(attn), dqkv, the MLP's dpre in two copies) is rewritten only two layers
+    // later, after the caller's stream waited on that layer's side events.
+    wev_ = 0;
+    side_ = wgs_ != nullptr && !dry_ && vl_.size() <= 64 && 5 * vl_.size() <= (size_t)WgradStream::NEV;
+    float* ring[3] = {vdA, vdB, vdr3_};
+    hipEvent_t done[64];
+    int it = 0;
+    for (int i = (int)vl_.size() - 1; i >= 0; --i, ++it) {
       const Layer& L = vl_[i];
       LayerAct& a = va_[i];
+      if (use_side() && it >= 2 && hipStreamWaitEvent(st_, done[(it - 2) & 63], 0) != hipSuccess)
+        return launch_status("train_vit_bert: weight-gradient join");
+      vdA = use_side() ? ring[it % 3] : vdA;
+      vdB = use_side() ? ring[(it + 1) % 3] : vdB;
+      float* vx2 = use_side() && (it & 1) ? vdx2b_ : vdx2;
+      float* vq = use_side() && (it & 1) ? vdq2_ : vdq_;
+      float* vp = use_side() && (it & 1) ? vdp2_ : vdp_;
       // vdA = dL/d(s2_i) = dL/d(r_i): the next LayerNorm's dx
-      FLR_TRY(mlp_bwd(vdA, Rv, Dv, Mv_, L, a.y2, a.pre, a.hm, vdp_, vdm));  // vdm = d(y2)
-      FLR_TRY(ln_bwd(vdm, a.s2, L.ln2w, L.ln2b, a.mean2, a.rstd2, vdA, vdx2, Rv, Dv));  // d(s_in) and d(attn)
-      FLR_TRY(dinput(vdx2, Rv, L.projw, Dv, vdc));
-      FLR_TRY(dweight(vdx2, Rv * Dv, Dv, Rv, a.ctx, Rv * Dv, Dv, G(L.projw), Dv, Dv));
-      FLR_TRY(rowsum(vdx2, Rv * Dv, Dv, Rv, Dv, G(L.projb)));
-      if (!dry_) FLR_TRY(flr_attention_bwd(a.qkv, a.ctx, vdc, a.lse, kc * B_, Tv_, s.vit_heads, 64, vdq_, st_));
-      FLR_TRY(dinput(vdq_, Rv, L.qkvw, Dv, vdh));
-      FLR_TRY(dweight(vdq_, Rv * 3 * Dv, 3 * Dv, Rv, a.h, Rv * Dv, Dv, G(L.qkvw), Dv, Dv));
-      FLR_TRY(rowsum(vdq_, Rv * 3 * Dv, 3 * Dv, Rv, 3 * Dv, G(L.qkvb)));
+      FLR_TRY(mlp_bwd(vdA, Rv, Dv, Mv_, L, a.y2, a.pre, a.hm, vp, vdm));  // vdm = d(y2)
+      FLR_TRY(ln_bwd(vdm, a.s2, L.ln2w, L.ln2b, a.mean2, a.rstd2, vdA, vx2, Rv, Dv));  // d(s_in) and d(attn)
+      if (use_side()) FLR_TRY(link(st_, wgs_->s));
+      FLR_TRY(dinput(vx2, Rv, L.projw, Dv, vdc));
+      FLR_TRY(dweight(vx2, Rv * Dv, Dv, Rv, a.ctx, Rv * Dv, Dv, G(L.projw), Dv, Dv));
+      FLR_TRY(rowsum(vx2, Rv * Dv, Dv, Rv, Dv, G(L.projb)));
+      if (!dry_) FLR_TRY(flr_attention_bwd(a.qkv, a.ctx, vdc, a.lse, kc * B_, Tv_, s.vit_heads, 64, vq, st_));
+      if (use_side()) FLR_TRY(link(st_, wgs_->s));
+      FLR_TRY(dinput(vq, Rv, L.qkvw, Dv, vdh));
+      FLR_TRY(dweight(vq, Rv * 3 * Dv, 3 * Dv, Rv, a.h, Rv * Dv, Dv, G(L.qkvw), Dv, Dv));
+      FLR_TRY(rowsum(vq, Rv * 3 * Dv, 3 * Dv, Rv, 3 * Dv, G(L.qkvb)));
+      if (use_side()) FLR_TRY(mark(&done[it & 63]));
       if (i > 0) {
         // LN1 with the residual: ds = vdx2 (s1 feeds LN2 only); dx -> d(s2_{i-1}) = d(r_{i-1})
-        FLR_TRY(ln_bwd(vdh, a.s1, L.ln1w, L.ln1b, a.mean1, a.rstd1, vdx2, vdB, Rv, Dv));
+        FLR_TRY(ln_bwd(vdh, a.s1, L.ln1w, L.ln1b, a.mean1, a.rstd1, vx2, vdB, Rv, Dv));
         std::swap(vdA, vdB);
       } else {
-        // block 0: x0 feeds LN1 (no residual) and LN2 (as x): the two paths summed
+        // block 0: x0 feeds LN1 (no residual) and LN2 (as x): the two paths summed (into
+        // vdA, which this layer's side work reads: joined first)
         FLR_TRY(ln_bwd(vdh, x0_, L.ln1w, L.ln1b, a.mean1, a.rstd1, nullptr, vdB, Rv, Dv));
-        FLR_TRY(launch(add_kernel, kc * Rv * Dv, vdB, vdx2, vdA, kc * Rv * Dv));
+        if (use_side() && hipStreamWaitEvent(st_, done[it & 63], 0) != hipSuccess)
+          return launch_status("train_vit_bert: weight-gradient join");
+        FLR_TRY(launch(add_kernel, kc * Rv * Dv, vdB, vx2, vdA, kc * Rv * Dv));
       }
     }
+    // every side event of the layers joined (the last two were not waited on yet)
+    if (use_side())
+      for (int j = std::max(0, it - 2); j < it; ++j)
+        if (hipStreamWaitEvent(st_, done[j & 63], 0) != hipSuccess)
+          return launch_status("train_vit_bert: weight-gradient join");
+    side_ = false;
     // ClientViTTokens.backward: dpos / dcls = sums over the batch rows, dtok = the patch rows
     if (!dry_) {
       FLR_TRY(flr_sum_rows(vdA, Rv * Dv, Tv_ * Dv, kc, B_, Tv_ * Dv, G(p_pos_), Tv_ * Dv, st_));
@@ -440,11 +480,13 @@ class Net {
   int mlp_bwd(const float* dy, int64_t M, int64_t D, int64_t Fh, const Layer& L, const float* x, const float* pre,
               const float* hm, float* dpre, float* dx) {
     int rc;
+    if (use_side() && (rc = link(st_, wgs_->s)) != FLR_OK) return rc;  // dy ready
     if ((rc = gemm(dy, M * D, D, 1, W(L.fc2w), D * Fh, 1, Fh, dpre, M * Fh, Fh, 1, nullptr, 0, nullptr,
                    FLR_ACT_DGELU, nullptr, pre, nullptr, M, Fh, D)) != FLR_OK)
       return rc;
     if ((rc = dweight(dy, M * D, D, M, hm, M * Fh, Fh, G(L.fc2w), Fh, Fh)) != FLR_OK) return rc;
     if ((rc = rowsum(dy, M * D, D, M, D, G(L.fc2b))) != FLR_OK) return rc;
+    if (use_side() && (rc = link(st_, wgs_->s)) != FLR_OK) return rc;  // dpre ready
     if ((rc = dinput(dpre, M, L.fc1w, D, dx)) != FLR_OK) return rc;
     if ((rc = dweight(dpre, M * Fh, Fh, M, x, M * D, D, G(L.fc1w), D, D)) != FLR_OK) return rc;
     return rowsum(dpre, M * Fh, Fh, M, Fh, G(L.fc1b));
@@ -471,6 +513,7 @@ class Net {
   int dweight(const float* dy, int64_t dyk, int64_t out, int64_t M, const float* x, int64_t xk, int64_t xm,
               float* dW, int64_t ldw, int64_t in) {
     // the gradient block's client stride: the parameter's numel (out x ldw)
+    if (use_side()) return gemm_side(dy, dyk, 1, out, x, xk, 1, xm, dW, out * ldw, ldw, 1, out, in, M);
     return gemm(dy, dyk, 1, out, x, xk, 1, xm, dW, out * ldw, ldw, 1, nullptr, 0, nullptr, FLR_ACT_NONE, nullptr,
                 nullptr, nullptr, out, in, M);
   }
@@ -484,11 +527,33 @@ class Net {
     return flr_bgemm_ex(A, ak, am, ar, Bm, bk, bn, br, C, ck, cm, cn, bias, bias_k, add, act, mul, aux, pre, kc_, M,
                         N, R, gws_, gws_n_, st_);
   }
+  // the weight-gradient stream's GEMM and row sums (its own workspaces)
+  int gemm_side(const float* A, int64_t ak, int64_t am, int64_t ar, const float* Bm, int64_t bk, int64_t bn,
+                int64_t br, float* C, int64_t ck, int64_t cm, int64_t cn, int64_t M, int64_t N, int64_t R) {
+    return flr_bgemm_ex(A, ak, am, ar, Bm, bk, bn, br, C, ck, cm, cn, nullptr, 0, nullptr, FLR_ACT_NONE, nullptr,
+                        nullptr, nullptr, kc_, M, N, R, gws2_, gws_n_, wgs_->s);
+  }
+  // event e recorded on `from`; `to` waits on it
+  int link(hipStream_t from, hipStream_t to) {
+    if (wev_ >= WgradStream::NEV) return FLR_ERR_UNSUPPORTED;
+    hipEvent_t e = wgs_->ev[wev_++];
+    if (hipEventRecord(e, from) != hipSuccess || hipStreamWaitEvent(to, e, 0) != hipSuccess)
+      return launch_status("train_vit_bert: weight-gradient stream event");
+    return FLR_OK;
+  }
+  // the layer's side work so far, as an event the caller waits on later
+  int mark(hipEvent_t* out) {
+    if (wev_ >= WgradStream::NEV) return FLR_ERR_UNSUPPORTED;
+    *out = wgs_->ev[wev_++];
+    return hipEventRecord(*out, wgs_->s) == hipSuccess ? FLR_OK : launch_status("train_vit_bert: side mark");
+  }
+  bool use_side() const { return side_ && wgs_ && !dry_; }
   int rowsum(const float* X, int64_t xk, int64_t xm, int64_t M, int64_t N, float* out) {
     if (dry_) {
       rws_n_ = std::max(rws_n_, flr_sum_rows_workspace(KC_, M, N));
       return FLR_OK;
     }
+    if (use_side()) return flr_sum_rows_ex(X, xk, xm, kc_, M, N, out, N, rws2_, rws_n_, wgs_->s);
     return flr_sum_rows_ex(X, xk, xm, kc_, M, N, out, N, rws_, rws_n_, st_);
   }
   int ln_fwd(const float* x, const float* res, int pg, int pb, float* y, float* s_out, float* mean, float* rstd,
@@ -577,6 +642,11 @@ class Net {
   float *dpre_h_ = nullptr, *dimg_ = nullptr, *dtxt_ = nullptr, *dpre_p_ = nullptr, *dxp_ = nullptr;
   float* vd_[6] = {};
   float *vdq_ = nullptr, *vdp_ = nullptr, *dtok_ = nullptr;
+  float *vdq2_ = nullptr, *vdp2_ = nullptr, *vdx2b_ = nullptr, *vdr3_ = nullptr;
+  char *gws2_ = nullptr, *rws2_ = nullptr;
+  WgradStream* wgs_ = nullptr;  // the weight-gradient stream (nullptr: everything on st_)
+  bool side_ = false;           // route dweight / rowsum to it (set around the ViT layers)
+  int wev_ = 0;                 // events used this pass
   float* bd_[6] = {};
   float *bdq_ = nullptr, *bdp_ = nullptr;
 };
@@ -598,6 +668,7 @@ extern "C" int64_t flr_vit_bert_num_params(const flr_vit_bert_spec* spec) {
 extern "C" size_t flr_train_vit_bert_workspace(const flr_vit_bert_spec* spec, int64_t K, int64_t B, int64_t steps,
                                                int64_t chunk) {
   if (!spec || K < 1 || B < 1 || steps < 1 || chunk < 0) return 0;
+  wgrad_stream(true);  // created here, before any capture of the training call
   tv::Net net(*spec, K, B, tv::auto_chunk(K, chunk), steps, nullptr);
   if (net.layout() != FLR_OK) return 0;
   return align_up(net.bytes(), 256) + align_up((size_t)steps * K * sizeof(float), 256) + 256;
@@ -622,6 +693,7 @@ extern "C" int flr_train_vit_bert(const flr_vit_bert_spec* spec, const float* gl
   if (ld < net.P()) return FLR_ERR_ARG;
   float* step_loss = reinterpret_cast<float*>(base + align_up(net.bytes(), 256));
   hipStream_t st = as_stream(stream);
+  net.set_wgrad_stream(wgrad_stream(true, st));
   // every client starts from the global model (run_experiments.py:203); the
   // family has no layout change, so training order is the parameters() order
   if ((rc = net.load_global(global, st)) != FLR_OK) return rc;
