@@ -158,7 +158,7 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
 //   (L = 4) a cross-lane half-cleaner between lanes g and g^1, same register;
 //   then a 7-stage in-lane half-cleaner (j = 64..1, ascending everywhere).
 // Rank e then sits in lane e/128, register e%128.  About half the VALU work of a
-// full 512-wide bitonic sort.  SPLIT (K = 128 * L, all rows): the same network with
+// full 512-wide bitonic sort.  SPLIT (K = 128 * L: every register a client): the same network with
 // the in-lane sort's two 64-register halves screened and sorted in turn, so the
 // first half's sort (≈ 1150 of ≈ 5250 compare-exchange instructions) runs while
 // the second half's loads are still in flight (C5 trimmed mean 23.7 -> 23.4 ms,
@@ -197,7 +197,7 @@ __device__ __forceinline__ void half_clean_lane(float* v) {
   }
 }
 
-template <int L, int MODE, bool SPLIT>
+template <int L, int MODE, bool SPLIT, bool ROWS>
 __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const float* __restrict__ X, int K,
                                                                          int64_t P, int64_t ldx, int t,
                                                                          float* __restrict__ out,
@@ -209,18 +209,28 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
   const bool active = p < P;  // inactive lanes still join the exchanges
   const int64_t pc = active ? p : 0;
   float v[128];
-  if constexpr (SPLIT) {
+  if constexpr (ROWS) {
+    // a row subset (e.g. the Multi-Krum selection): the workgroup stages the clamped
+    // indices in LDS once (padding entries repeat row 0), so a lane's 128 loads issue
+    // back to back instead of each waiting on its own index load
+    __shared__ int32_t srow[128 * L];
+    for (int i = threadIdx.x; i < 128 * L; i += THREADS) srow[i] = (int32_t)min((uint32_t)rows[i < K ? i : 0], rmax);
+    __syncthreads();
+    const int32_t* rg = srow + 128 * g;
+    const float* __restrict__ col = X + pc;
+#pragma unroll
+    for (int i = 0; i < 128; ++i) v[i] = col[(int64_t)rg[i] * ldx];
+    if constexpr (!SPLIT) {
+#pragma unroll
+      for (int i = 0; i < 128; ++i) v[i] = 128 * g + i < K ? v[i] : __builtin_huge_valf();
+    }
+  } else if constexpr (SPLIT) {
     const float* __restrict__ base = X + (int64_t)(128 * g) * ldx + pc;
 #pragma unroll
     for (int i = 0; i < 128; ++i) v[i] = base[(int64_t)i * ldx];
-  } else if (rows) {  // a row subset (e.g. the Multi-Krum selection)
-    const int32_t* rg = rows + 128 * g;
-#pragma unroll
-    for (int i = 0; i < 128; ++i)
-      v[i] = 128 * g + i < K ? X[(int64_t)min((uint32_t)rg[i], rmax) * ldx + pc] : __builtin_huge_valf();
   } else {
     const float* __restrict__ base = X + (int64_t)(128 * g) * ldx + pc;
-    if (K >= 128 * L) {  // wave-uniform: every register holds a client (K = 256, 512)
+    if (K >= 128 * L) {  // wave-uniform: every register holds a client
 #pragma unroll
       for (int i = 0; i < 128; ++i) v[i] = base[(int64_t)i * ldx];
     } else {
@@ -303,6 +313,17 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
   }
 }
 
+template <int L, int MODE>
+void launch_ml(bool full, bool has_rows, const float* X, int K, int64_t P, int64_t ldx, int t, float* out,
+               const int32_t* rows, uint32_t rmax, hipStream_t st) {
+  const dim3 grid((unsigned)((L * P + THREADS - 1) / THREADS));
+  auto k = full ? (has_rows ? orderstat_multilane_kernel<L, MODE, true, true>
+                            : orderstat_multilane_kernel<L, MODE, true, false>)
+                : (has_rows ? orderstat_multilane_kernel<L, MODE, false, true>
+                            : orderstat_multilane_kernel<L, MODE, false, false>);
+  hipLaunchKernelGGL(k, grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows, rmax);
+}
+
 template <int MODE>
 int launch(const float* X, int K, int64_t P, int64_t ldx, int t, float* out, hipStream_t st,
            const int32_t* rows = nullptr, int64_t nrows = 0) {
@@ -321,21 +342,13 @@ int launch(const float* X, int K, int64_t P, int64_t ldx, int t, float* out, hip
   else if (K <= 128)
     hipLaunchKernelGGL((orderstat_kernel<128, MODE>), grid, dim3(THREADS), 0, st, X, K, P, ldx, t, out, rows, rmax);
   else if (K <= 512) {
-    // K = 128 * L without a row subset: the split-load form (no load branch)
-    const bool split = !rows && (K == 256 || K == 512);
-    const dim3 g2((unsigned)((2 * P + THREADS - 1) / THREADS)), g4((unsigned)((4 * P + THREADS - 1) / THREADS));
-    if (K <= 256 && split)
-      hipLaunchKernelGGL((orderstat_multilane_kernel<2, MODE, true>), g2, dim3(THREADS), 0, st, X, K, P, ldx, t, out,
-                         rows, rmax);
-    else if (K <= 256)
-      hipLaunchKernelGGL((orderstat_multilane_kernel<2, MODE, false>), g2, dim3(THREADS), 0, st, X, K, P, ldx, t, out,
-                         rows, rmax);
-    else if (split)
-      hipLaunchKernelGGL((orderstat_multilane_kernel<4, MODE, true>), g4, dim3(THREADS), 0, st, X, K, P, ldx, t, out,
-                         rows, rmax);
+    // K = 128 * L (every register a client): the split-load form; a row subset: the
+    // LDS-staged index form
+    const bool full = K == 256 || K == 512;
+    if (K <= 256)
+      launch_ml<2, MODE>(full, rows != nullptr, X, K, P, ldx, t, out, rows, rmax, st);
     else
-      hipLaunchKernelGGL((orderstat_multilane_kernel<4, MODE, false>), g4, dim3(THREADS), 0, st, X, K, P, ldx, t, out,
-                         rows, rmax);
+      launch_ml<4, MODE>(full, rows != nullptr, X, K, P, ldx, t, out, rows, rmax, st);
   }
   else
     return FLR_ERR_UNSUPPORTED;

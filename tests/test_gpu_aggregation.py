@@ -331,7 +331,7 @@ def test_client_matrix_zero_copy_defense(cuda):
     assert not set(d.selected_clients) & set(range(4))  # sign-flipped clients rejected
 
 
-@pytest.mark.parametrize("K,m", [(40, 20), (200, 100), (512, 256), (300, 7)])
+@pytest.mark.parametrize("K,m", [(40, 20), (200, 100), (512, 256), (300, 7), (512, 200), (600, 400), (512, 512)])
 def test_order_stats_row_subset(cuda, K, m):
     P = 2049
     X = torch.randn(K, P, device=cuda)

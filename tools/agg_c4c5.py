@@ -38,6 +38,10 @@ def main():
         t = int(0.1 * K)
         runs = [("trimmed_mean", lambda: ops.trimmed_mean(X, t), 4.0 * K * P + 4.0 * P),
                 ("median", lambda: ops.median_lower(X), 4.0 * K * P + 4.0 * P)]
+        if cfg == "C5":  # the C5 defense's second half: the trimmed mean of the 256 Multi-Krum rows
+            rows = torch.randperm(K, generator=torch.Generator().manual_seed(5))[: K // 2].to(torch.int32).cuda()
+            runs.append(("trimmed_mean_rows256", lambda: ops.trimmed_mean(X, int(0.1 * (K // 2)), rows=rows),
+                         4.0 * (K // 2) * P + 4.0 * P))
         if cfg == "C5" or os.environ.get("GRAM_ALL"):
             runs.append(("krum_pairwise_gram", lambda: ops.pairwise_l2(X, "gram"), 4.0 * K * P + 8.0 * K * K))
         for name, fn, byts in runs:
