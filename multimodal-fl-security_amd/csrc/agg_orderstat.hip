@@ -159,10 +159,10 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
 //   then a 7-stage in-lane half-cleaner (j = 64..1, ascending everywhere).
 // Rank e then sits in lane e/128, register e%128.  About half the VALU work of a
 // full 512-wide bitonic sort.  SPLIT (K = 128 * L: every register a client): the same network with
-// the in-lane sort's two 64-register halves screened and sorted in turn, so the
-// first half's sort (≈ 1150 of ≈ 5250 compare-exchange instructions) runs while
-// the second half's loads are still in flight (C5 trimmed mean 23.7 -> 23.4 ms,
-// median 19.9 -> 19.4; C4 10.1 -> 9.8 and 8.5 -> 8.2; same box).  Trimmed sums are per-lane sequential in rank
+// the in-lane sort's 32-register quarters screened and sorted in turn, so ≈ 1600 of
+// its ≈ 5250 compare-exchange instructions run while later quarters' loads are
+// still in flight (C5 trimmed mean 23.7 -> 23.3 ms, median 19.9 -> 19.2; C4 10.1 ->
+// 9.8 and 8.5 -> 8.0; halves gave 23.4 / 19.4 / 9.9 / 8.2).  Trimmed sums are per-lane sequential in rank
 // order, combined in lane order (deterministic; 1e-5 vs torch, not bit-exact).
 template <int CTRL>
 __device__ __forceinline__ float dpp_swap(float x) {
@@ -240,16 +240,26 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
   }
   int nnan;
   if constexpr (SPLIT) {
-    // every lane holds K / L clients here (K = 128 * L, no row subset): the first
-    // half is screened and sorted while the second half's loads are in flight
-    nnan = nan_to_inf<64>(v);
-    oem_sort<0, 64>(v);
-    // volatile fences keep their order: the first half's (after its sort), then the
-    // second half's, which is where that half's load wait lands
+    // every lane holds K / L clients here (K = 128 * L): the in-lane sort's quarters
+    // are screened and sorted as their loads land; the ordered fences put each later
+    // quarter's load wait behind the sorts before it (vmcnt counts at most 63, so the
+    // first wait covers two quarters)
+    nnan = nan_to_inf<32>(v);
+    oem_sort<0, 32>(v);
+    reg_fence<32>(v);
+    reg_fence<32>(v + 32);
+    nnan += nan_to_inf<32>(v + 32);
+    oem_sort<32, 32>(v);
+    oem_merge<0, 64, 1>(v);
     reg_fence<64>(v);
-    reg_fence<64>(v + 64);
-    nnan += nan_to_inf<64>(v + 64);
-    oem_sort<64, 64>(v);
+    reg_fence<32>(v + 64);
+    nnan += nan_to_inf<32>(v + 64);
+    oem_sort<64, 32>(v);
+    reg_fence<32>(v + 64);
+    reg_fence<32>(v + 96);
+    nnan += nan_to_inf<32>(v + 96);
+    oem_sort<96, 32>(v);
+    oem_merge<64, 64, 1>(v);
     oem_merge<0, 128, 1>(v);
   } else {
     nnan = nan_to_inf<128>(v);

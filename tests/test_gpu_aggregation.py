@@ -270,9 +270,9 @@ def test_order_stats_nan_like_torch(cuda, K):
     X[1 % K, 100:200] = nan               # two NaN in these columns
     X[2 % K, 200:300] = float("inf")      # NaN / +inf ties
     X[3 % K, 300:400] = -nan              # negative-signed NaN sorts last too
-    # K = 256 / 512 screen each lane's two 64-client halves separately: NaN in
-    # a second half (clients 64..127 of a lane) and in the last lane
-    for r in (100, 200, 400, K - 1):
+    # K = 256 / 512 screen each lane's four 32-client quarters separately: NaN
+    # in every quarter of some lane (client % 128 = 40, 100, 72, 44, 16, 127)
+    for r in (40, 100, 200, 300, 400, K - 1):
         if r < K and r > 3:
             X[r, 500 + r % 97: 600 + r % 97] = nan
             X[r, 650:660] = nan
