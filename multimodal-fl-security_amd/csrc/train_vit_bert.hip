@@ -228,6 +228,11 @@ class Net {
     for (float*& p : bd_) p = alloc<float>(KC * Rb * Db_);
     bdq_ = alloc<float>(KC * Rb * 3 * Db_);
     bdp_ = alloc<float>(KC * Rb * Fb_);
+    // the weight-gradient stream's second copies of what a BERT layer's side work reads
+    bdq2_ = alloc<float>(KC * Rb * 3 * Db_);
+    bdp2_ = alloc<float>(KC * Rb * Fb_);
+    bdy2b_ = alloc<float>(KC * Rb * Db_);
+    bd1b_ = alloc<float>(KC * Rb * Db_);
     // ---- kernel scratch, sized by a dry pass over the schedule ----
     dry_ = true;
     kc_ = KC_;
@@ -376,23 +381,46 @@ class Net {
       FLR_TRY(flr_copy_rows(dxp_, Db, Db, bdx, Tb_ * Db, kc * B_, st_));
     }
     // ---- BERT layers, last first; bdx = dL/d(layer output) ----
-    for (int i = (int)bl_.size() - 1; i >= 0; --i) {
+    // With the weight-gradient stream, layer i's weight / bias gradients run on it (as the
+    // ViT layers' below): what they read (d(f), dpre, d(attn), dqkv) alternates between two
+    // copies, rewritten two layers later after the caller's stream waited on that layer.
+    wev_ = 0;
+    side_ = wgs_ != nullptr && !dry_ && vl_.size() <= 64 && bl_.size() <= 64 &&
+            5 * (vl_.size() + bl_.size()) <= (size_t)WgradStream::NEV;
+    hipEvent_t bdone[64];
+    int bit = 0;
+    for (int i = (int)bl_.size() - 1; i >= 0; --i, ++bit) {
       const Layer& L = bl_[i];
       LayerAct& a = ba_[i];
       const float* xin = i > 0 ? ba_[i - 1].y2 : xe_;
-      FLR_TRY(ln_bwd(bdx, a.s2, L.ln2w, L.ln2b, a.mean2, a.rstd2, nullptr, bdy2, Rb, Db));  // d(y1) and d(f)
-      FLR_TRY(mlp_bwd(bdy2, Rb, Db, Fb_, L, a.y1, a.pre, a.hm, bdp_, bdm));
-      FLR_TRY(launch(add_kernel, kc * Rb * Db, bdy2, bdm, bdsum, kc * Rb * Db));  // y1 feeds LN2 and the MLP
-      FLR_TRY(ln_bwd(bdsum, a.s1, L.ln1w, L.ln1b, a.mean1, a.rstd1, nullptr, bd1, Rb, Db));  // d(x) and d(attn)
-      FLR_TRY(dinput(bd1, Rb, L.projw, Db, bdc));
-      FLR_TRY(dweight(bd1, Rb * Db, Db, Rb, a.ctx, Rb * Db, Db, G(L.projw), Db, Db));
-      FLR_TRY(rowsum(bd1, Rb * Db, Db, Rb, Db, G(L.projb)));
-      if (!dry_) FLR_TRY(flr_attention_bwd(a.qkv, a.ctx, bdc, a.lse, kc * B_, Tb_, s.bert_heads, 64, bdq_, st_));
-      FLR_TRY(dinput(bdq_, Rb, L.qkvw, Db, bdm));
-      FLR_TRY(dweight(bdq_, Rb * 3 * Db, 3 * Db, Rb, xin, Rb * Db, Db, G(L.qkvw), Db, Db));
-      FLR_TRY(rowsum(bdq_, Rb * 3 * Db, 3 * Db, Rb, 3 * Db, G(L.qkvb)));
-      FLR_TRY(launch(add_kernel, kc * Rb * Db, bd1, bdm, bdx, kc * Rb * Db));  // x feeds LN1 and qkv
+      if (use_side() && bit >= 2 && hipStreamWaitEvent(st_, bdone[(bit - 2) & 63], 0) != hipSuccess)
+        return launch_status("train_vit_bert: weight-gradient join");
+      const bool odd = use_side() && (bit & 1);
+      float* by2 = odd ? bdy2b_ : bdy2;
+      float* bp = odd ? bdp2_ : bdp_;
+      float* b1 = odd ? bd1b_ : bd1;
+      float* bq = odd ? bdq2_ : bdq_;
+      FLR_TRY(ln_bwd(bdx, a.s2, L.ln2w, L.ln2b, a.mean2, a.rstd2, nullptr, by2, Rb, Db));  // d(y1) and d(f)
+      FLR_TRY(mlp_bwd(by2, Rb, Db, Fb_, L, a.y1, a.pre, a.hm, bp, bdm));
+      FLR_TRY(launch(add_kernel, kc * Rb * Db, by2, bdm, bdsum, kc * Rb * Db));  // y1 feeds LN2 and the MLP
+      FLR_TRY(ln_bwd(bdsum, a.s1, L.ln1w, L.ln1b, a.mean1, a.rstd1, nullptr, b1, Rb, Db));  // d(x) and d(attn)
+      if (use_side()) FLR_TRY(link(st_, wgs_->s));
+      FLR_TRY(dinput(b1, Rb, L.projw, Db, bdc));
+      FLR_TRY(dweight(b1, Rb * Db, Db, Rb, a.ctx, Rb * Db, Db, G(L.projw), Db, Db));
+      FLR_TRY(rowsum(b1, Rb * Db, Db, Rb, Db, G(L.projb)));
+      if (!dry_) FLR_TRY(flr_attention_bwd(a.qkv, a.ctx, bdc, a.lse, kc * B_, Tb_, s.bert_heads, 64, bq, st_));
+      if (use_side()) FLR_TRY(link(st_, wgs_->s));
+      FLR_TRY(dinput(bq, Rb, L.qkvw, Db, bdm));
+      FLR_TRY(dweight(bq, Rb * 3 * Db, 3 * Db, Rb, xin, Rb * Db, Db, G(L.qkvw), Db, Db));
+      FLR_TRY(rowsum(bq, Rb * 3 * Db, 3 * Db, Rb, 3 * Db, G(L.qkvb)));
+      if (use_side()) FLR_TRY(mark(&bdone[bit & 63]));
+      FLR_TRY(launch(add_kernel, kc * Rb * Db, b1, bdm, bdx, kc * Rb * Db));  // x feeds LN1 and qkv
     }
+    if (use_side())
+      for (int j = std::max(0, bit - 2); j < bit; ++j)
+        if (hipStreamWaitEvent(st_, bdone[j & 63], 0) != hipSuccess)
+          return launch_status("train_vit_bert: weight-gradient join");
+    side_ = false;
     FLR_TRY(ln_bwd(bdx, e_, p_ew_, p_eb_, meane_, rstde_, nullptr, bdm, Rb, Db));
     if (!dry_) {
       // one flr_embedding_bwd per table (ClientEmbeddingSum.backward): word, type, position
@@ -416,8 +444,9 @@ class Net {
     // the data-gradient chain of layers i and i-1: the scratch they read (dL/dr in a ring
     // of three, d(attn), dqkv, the MLP's dpre in two copies) is rewritten only two layers
     // later, after the caller's stream waited on that layer's side events.
-    wev_ = 0;
-    side_ = wgs_ != nullptr && !dry_ && vl_.size() <= 64 && 5 * vl_.size() <= (size_t)WgradStream::NEV;
+    // (wev_ continues from the BERT layers: one event set per pass)
+    side_ = wgs_ != nullptr && !dry_ && vl_.size() <= 64 && bl_.size() <= 64 &&
+            5 * (vl_.size() + bl_.size()) <= (size_t)WgradStream::NEV;
     float* ring[3] = {vdA, vdB, vdr3_};
     hipEvent_t done[64];
     int it = 0;
@@ -649,6 +678,7 @@ class Net {
   int wev_ = 0;                 // events used this pass
   float* bd_[6] = {};
   float *bdq_ = nullptr, *bdp_ = nullptr;
+  float *bdq2_ = nullptr, *bdp2_ = nullptr, *bdy2b_ = nullptr, *bd1b_ = nullptr;
 };
 
 inline int64_t auto_chunk(int64_t K, int64_t chunk) { return chunk > 0 ? std::min(chunk, K) : std::min<int64_t>(K, 32); }
