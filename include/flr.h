@@ -756,10 +756,11 @@ int64_t flr_resnet_gru_live_params(const flr_resnet_gru_spec* spec, float weight
  * labels [steps][K][B], dropout_masks NULL or [steps][K][B][fusion]).  The
  * family has no training-layout change: X's rows are in parameters() order
  * with or without FLR_TC_TRAIN_ORDER, written by the last optimizer step.  The
- * ViT layers' weight and bias gradients run on the per-device weight-gradient
- * stream of flr_train_clients (created by flr_train_vit_bert_workspace; forked
- * and joined by events inside the call, graph-capturable): one training call
- * per device at a time; FLR_WGRAD_STREAM=0 keeps them on `stream`, same bits. */
+ * ViT and BERT layers' weight and bias gradients run on the per-device
+ * weight-gradient stream of flr_train_clients (created by
+ * flr_train_vit_bert_workspace; forked and joined by events inside the call,
+ * graph-capturable): one training call per device at a time;
+ * FLR_WGRAD_STREAM=0 keeps them on `stream`, same bits. */
 typedef struct flr_vit_bert_spec {
   int64_t num_classes, image_size, in_channels, patch;
   int64_t vit_dim, vit_depth, vit_heads, vit_mlp;
