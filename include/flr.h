@@ -47,8 +47,9 @@ const char* flr_last_error(void);
  * from the medoid pivot, e.g. a cluster of sign-flipped updates) are flagged
  * from the pivot sample and recomputed from exact fp32 differences (up to 128
  * such rows per call: every row at K <= 128).  More flagged rows than that
- * (K > 128 only) makes every off-diagonal D entry NaN: a loud failure, never a
- * silently inaccurate distance.
+ * (K > 128 only) makes EVERY D entry NaN, the diagonal included — the marker
+ * callers test (D[0][0] is NaN only then; NaN client rows leave the diagonal
+ * 0): a loud failure, never a silently inaccurate distance.
  */
 size_t flr_pairwise_l2_workspace(int64_t K, int64_t P);
 int flr_pairwise_l2(const float* X, int64_t K, int64_t P, int64_t ldx,
@@ -98,19 +99,28 @@ int flr_pairwise_tail(const float* X, int64_t K, int64_t ldx, int64_t p0, int64_
 int flr_pairwise_finish(const double* gsum, const double* tail, int64_t K, double* D,
                         void* stream);
 
-/* Reference-exact variant (opt-in parity mode, pairwise_method="reference"):
+/* Reference-exact variant (pairwise_method="reference"):
  * D[i][j] bit-identical to the reference's fp32 torch.norm(flat_i - flat_j)
- * .item() (krum.py:89-97) — per pair, 8 fp32 lanes of sequential
- * fma(d, d, lane) over every 8th coordinate d = fl(x_i - x_j), the lanes
+ * .item() (krum.py:89-97) — per pair, 8 fp32 chains of sequential
+ * fma(d, d, chain) over every 8th coordinate d = fl(x_i - x_j), the chains
  * summed 0..7 in order, the P mod 8 tail added in order (a first group of 4
  * as separate multiply + add, the last 0..3 as fma), correctly rounded
  * sqrt_f32 (tail probed in tools/diag_norm_host.py;
- * oracle/norm_ref.c).  X in the
- * reference's coordinate order (parameters() order); rows 16-B aligned and
- * ldx % 4 == 0 (else FLR_ERR_ARG).  No workspace.  VALU / LDS bound: each
- * pair's 8 chains run the whole vector sequentially. */
+ * oracle/norm_ref.c).  X in the reference's coordinate order (parameters()
+ * order); rows 16-B aligned and ldx % 4 == 0 (else FLR_ERR_ARG).
+ * Workspace (256-B aligned): flr_pairwise_l2_reference_workspace(K, P) bytes
+ * — the chains' running sums plus one chain-major copy of a coordinate segment
+ * (at most 8 GiB; a smaller workspace runs more, shorter segments, the same
+ * result).  part / nparts: this call computes the pairs of tile range
+ * [part * T / nparts, (part + 1) * T / nparts), T =
+ * flr_pairwise_l2_reference_tiles(K), and writes 0 for every other pair: the
+ * nparts results summed (exact: one non-zero term per pair) are the whole D.
+ * VALU-issue bound: each pair's 8 chains run the whole vector sequentially. */
+size_t flr_pairwise_l2_reference_workspace(int64_t K, int64_t P);
+int flr_pairwise_l2_reference_tiles(int64_t K);
 int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx,
-                              double* D, void* stream);
+                              double* D, void* ws, size_t ws_bytes, int64_t part,
+                              int64_t nparts, void* stream);
 
 /* Direct-difference VALU variant (same contract, exact fp32 differences);
  * a slower second implementation used to cross-check the MFMA path. */
@@ -124,6 +134,8 @@ int flr_pairwise_l2_direct(const float* X, int64_t K, int64_t P, int64_t ldx,
  * (src/defenses/krum.py:101-131, 149-176):
  *   m = K - f - 2; scores[i] = numpy-pairwise-sum(sort(D[i])[1 : m+1]);
  *   order = argsort(scores) (ties broken by lower client index).
+ * NaN in numpy's order: after every value in the row sort and in the argsort
+ * (a client whose update is NaN gets a NaN score and the last ranks).
  * D: device fp64 K×K (row-major, ld = K). scores: device fp64 [K];
  * order: device int32 [K].  Returns FLR_ERR_KRUM_N if K < 2f+3.
  */

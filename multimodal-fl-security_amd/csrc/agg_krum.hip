@@ -9,12 +9,19 @@
 // exactly here, so scores are bit-identical to numpy given the same D.
 // np.argsort's default quicksort is not stable; exact score ties are broken
 // here by the lower client index (documented divergence, tests flag ties).
+// NaN as numpy orders it: np.sort and np.argsort put NaN after +inf, so a
+// NaN distance lands in a row's last ranks and a NaN score (a client that sent
+// NaN) is ranked last — rejected, not selected.  Every order slot is written.
 #include "flr_common.h"
 
 namespace flr {
 namespace krum {
 
 constexpr int MAXK = 1024;
+
+// a sorts after b in numpy's order (NaN after everything, NaNs equal)
+__device__ __forceinline__ bool np_after(double a, double b) { return a > b || (a != a && b == b); }
+__device__ __forceinline__ bool np_equal(double a, double b) { return a == b || (a != a && b != b); }
 
 // numpy pairwise_sum_DOUBLE (numpy/_core/src/umath/loops_utils.h.src), exact.
 template <int DEPTH>
@@ -54,7 +61,7 @@ __global__ __launch_bounds__(256) void score_kernel(const double* __restrict__ D
   int np2 = 1;
   while (np2 < K) np2 <<= 1;
   for (int j = threadIdx.x; j < np2; j += blockDim.x)
-    s[j] = j < K ? D[(int64_t)i * K + j] : __builtin_huge_val();
+    s[j] = j < K ? D[(int64_t)i * K + j] : __builtin_nan("");  // pads sort with the NaNs, after every value
   __syncthreads();
   for (int k = 2; k <= np2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
@@ -63,7 +70,7 @@ __global__ __launch_bounds__(256) void score_kernel(const double* __restrict__ D
         if (ixj > idx) {
           const double a = s[idx], b = s[ixj];
           const bool up = (idx & k) == 0;
-          if ((a > b) == up) {
+          if ((up && np_after(a, b)) || (!up && np_after(b, a))) {
             s[idx] = b;
             s[ixj] = a;
           }
@@ -86,7 +93,7 @@ __global__ __launch_bounds__(1024) void order_kernel(const double* __restrict__ 
     int rank = 0;
     for (int j = 0; j < K; ++j) {
       const double sj = s[j];
-      rank += (sj < si) || (sj == si && j < i);
+      rank += np_after(si, sj) || (np_equal(sj, si) && j < i);
     }
     order[rank] = i;
   }

@@ -744,6 +744,15 @@ __global__ void assemble_kernel(const double* __restrict__ gsum, int ngroups, in
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)K * K) return;
   int i = (int)(idx / K), j = (int)(idx % K);
+  // more flagged rows than the refine list holds (K > RMAX only): every entry
+  // NaN, the diagonal included — the marker KrumDefense checks (a NaN client
+  // update never makes the diagonal NaN); loud, not inaccurate
+  const double* hdr = gsum + (int64_t)ngroups * REC;  // slice 0's header (every slice holds the same)
+  const int c = (int)hdr[0];
+  if ((int)hdr[1 + RMAX] > c) {
+    D[idx] = __builtin_nan("");
+    return;
+  }
   if (i == j) {
     D[idx] = 0.0;
     return;
@@ -779,12 +788,6 @@ __global__ void assemble_kernel(const double* __restrict__ gsum, int ngroups, in
     }
   }
   // a refined pair (both rows in the refine list): the exact-difference sums
-  const double* hdr = gsum + (int64_t)ngroups * REC;  // slice 0's header (every slice holds the same)
-  const int c = (int)hdr[0];
-  if ((int)hdr[1 + RMAX] > c) {  // more flagged rows than the refine list holds: loud, not inaccurate
-    D[idx] = __builtin_nan("");
-    return;
-  }
   int pi = -1, pj = -1;
   for (int u = 0; u < c; ++u) {
     const int row = (int)hdr[1 + u];

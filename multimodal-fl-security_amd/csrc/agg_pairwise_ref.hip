@@ -5,156 +5,300 @@
 // probed on this image's torch; oracle/norm_ref.c restates it and
 // tests/test_oracle.py pins it against torch.norm):
 //   d = fl(x_i - x_j) elementwise;
-//   8 fp32 lanes, lane c = fma(d[8r+c], d[8r+c], lane c) sequentially over r;
-//   s = lane 0 + lane 1 + ... + lane 7 (in that order);
-//   the tail t >= 8*floor(P/8): while 4 or more remain, the next 4 as
+//   8 fp32 lanes ("chains"), chain c = fma(d[8r+c], d[8r+c], chain c)
+//   sequentially over the steps r = 0 .. R-1, R = P / 8;
+//   s = chain 0 + chain 1 + ... + chain 7 (in that order);
+//   the tail t >= 8R: while 4 or more remain, the next 4 as
 //   s = s + fl(d[t] * d[t]) (separate multiply and add), then the last
 //   0..3 as s = fma(d[t], d[t], s);
 //   sqrt_f32(s) (correctly rounded), widened to fp64 by .item().
 // Every fp32 operation here is that operation, in that order, so D is the
 // reference's D bit for bit — no tolerance, no margin argument.
 //
-// The cost of exactness: each of the 8 lanes of a pair is ONE sequential
-// chain over P/8 coordinates (no split over coordinates, no reassociation),
-// so the parallelism is 8 chains per pair (65,024 at K = 128).  A thread owns
-// the chain pair (2cp, 2cp+1) of one client pair and advances both with one
-// v_pk_add_f32 + one v_pk_fma_f32 per 8 coordinates (the packed ops are two
-// IEEE fp32 ops each, rounding unchanged).  A 128-thread workgroup owns a
-// tile of 4 rows (I) x 8 rows (J) = 32 pairs; per 32-step chunk (256
-// coordinates) the 12 rows are staged into LDS by LDS-DMA (one 1-KB
-// global_load_lds_dwordx4 per row) into a ring of NSTAGE buffers, NSTAGE - 1
-// chunks in flight (a chunk's compute is ~0.3 us, an L2 / HBM round trip
-// 1-2 us: with two buffers the kernel waited on every chunk, 54 ms at C3),
-// counted vmcnt waits and a raw s_barrier, with a 1056-B row stride
-// (8 dwords of padding: the 8 rows x 4 chain pairs of a ds_read_b64 lane
-// group land on 64 distinct banks).  Per chain step a thread reads one float2
-// of each row (2 ds_read_b64): 16 B of LDS and 2 VALU instructions per two
-// chain steps.  Bound: VALU issue / LDS, not HBM (each tile re-reads its 12
-// rows from L2 / MALL).
+// Round 5 design.  The parallelism is fixed by the reference: K(K-1)/2 pairs x
+// 8 chains, each chain a sequential fma over R steps (65,024 chains of 1.475 M
+// steps at C3) — about one chain per lane of one wave per SIMD.  So the time is
+// R x (instructions per step of one wave) x 4 cycles (a wave alone issues one
+// vector instruction per 4 cycles; two waves per SIMD share the 2-cycle pipe at
+// no loss), and the design minimises the per-step instruction stream:
+//  * one chain per lane: lane j of wave (i, c) runs chain c of pair (i, j);
+//  * the subtraction of two steps is one v_pk_add_f32 (steps are independent;
+//    only the fma accumulation is a chain), the fma is one v_fma_f32 per step:
+//    1.5 vector instructions per step;
+//  * operands arrive 4 steps per instruction: x_j by one ds_read_b128 of the
+//    lane's row, x_i by one uniform-address 16-B load (the same for every lane
+//    of the wave, 8 chunks' worth prefetched in registers).
+// That needs each chain's steps contiguous, so a segment of X is first
+// rewritten chain-major (chain_transpose_kernel, Xc[k][c][s] = X[k][8(r0+s)+c],
+// one read and one write of the segment at HBM rate).  Tiles: 64 J rows (one
+// per lane) x TI I rows (one per wave) x one chain; chain c = the XCD
+// (blockIdx % 8), so an XCD's L2 holds only its own chain's streams and the
+// WGs of one XCD share them.  Per chunk of 32 steps the WG stages its 64 J
+// rows' 128-B chain pieces by LDS-DMA (one global_load_lds_dwordx4 of 8 rows
+// per wave, XOR-swizzled 16-B slots so the ds_read_b128 lane groups hit 64
+// distinct banks) into a ring of 4 stages, one raw barrier per chunk.  Chains
+// longer than the segment carry their partial sums in A between segments.
+#include <type_traits>
+#include <utility>
+
 #include "flr_common.h"
 
 namespace flr {
 namespace pwref {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int TI = 4;                 // rows of a tile's I block
-constexpr int TJ = 8;                 // rows of a tile's J block
-constexpr int THREADS = TI * TJ * 4;  // 4 chain pairs per client pair: 128
-constexpr int CS = 32;                // chain steps per staged chunk
-constexpr int CW = 8 * CS;            // coordinates per chunk (1 KB per row)
-constexpr int RSTR = CW + 8;          // LDS row stride in floats (== 8 mod 64 dwords)
-constexpr int NROWS = TI + TJ;
-constexpr int BUF = NROWS * RSTR;     // floats per staging buffer
-constexpr int NSTAGE = 4;             // ring of staging buffers (NSTAGE - 1 chunks in flight)
-constexpr int DMA_PER_WAVE = NROWS / 2;  // one DMA per staged row, two waves
+constexpr int NJ = 64;             // J rows per tile: one per lane
+constexpr int TI = 8;              // I rows per tile: one per wave
+constexpr int THREADS = 64 * TI;   // 512
+#ifndef FLR_REF_CS
+#define FLR_REF_CS 32
+#endif
+#ifndef FLR_REF_NSTAGE
+#define FLR_REF_NSTAGE 4
+#endif
+constexpr int CS = FLR_REF_CS;     // chain steps per staged chunk (4 CS bytes of one chain stream)
+constexpr int NSTAGE = FLR_REF_NSTAGE;  // LDS ring and x_i register sets (NSTAGE - 1 chunks in flight)
+constexpr int STAGE = NJ * CS;     // floats per stage
+constexpr int NQ = CS / 4;         // 16-B pieces per chunk row
+constexpr int XW = CS / 16;        // x_i floats per lane per chunk (16 lanes of a row cover the chunk)
+constexpr int RPD = 256 / CS;      // chunk rows per 1-KB DMA instruction
+constexpr int DPW = 8 / RPD;       // DMA instructions per wave per chunk (wave w stages rows 8w .. 8w+7)
+constexpr int VMC = (NSTAGE - 2) * (DPW + 1);  // the steady state's counted wait (see ref_chain_kernel)
+constexpr int64_t XC_CAP = int64_t(8) << 30;  // bytes of one chain-major segment
+static_assert(CS == 32 || CS == 64, "chunk of 32 or 64 steps");
+static_assert(NSTAGE >= 3 && VMC < 64, "vmcnt counts to 63");
+typedef typename std::conditional<XW == 4, f32x4, f32x2>::type xvec;
 
-// Tiles: J block jb (rows 8jb..8jb+7) with I blocks ib = 0 .. min(nI, 2jb+2)-1
-// (4 ib < 8 jb + 7: some i < some j).  Tiles are numbered jb-major.
-__host__ __device__ inline int64_t tiles_upto(int jb, int nI) {
-  // sum_{b < jb} min(nI, 2b + 2)
-  int64_t n = 0;
-  for (int b = 0; b < jb; ++b) n += (2 * b + 2 < nI ? 2 * b + 2 : nI);
+// the XOR swizzle of a row's 16-B slots: the ds_read_b128 lane groups
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31} and +32) then hit 64 distinct banks
+__host__ __device__ constexpr int slot_swz(int row) { return CS == 32 ? ((row >> 1) & 7) : (row & 15); }
+
+// rows i that pair with some j > i of J block jb (j < K): i < jmax(jb)
+__host__ __device__ inline int igroups(int jb, int K) {
+  const int jmax = (NJ * jb + NJ - 1 < K - 1) ? NJ * jb + NJ - 1 : K - 1;
+  return jmax <= 0 ? 0 : (jmax + TI - 1) / TI;
+}
+__host__ __device__ inline int tiles_before(int jb, int K) {
+  int n = 0;
+  for (int b = 0; b < jb; ++b) n += igroups(b, K);
   return n;
 }
 
-__global__ __launch_bounds__(THREADS) void ref_norm_kernel(const float* __restrict__ X, int K, int64_t P,
-                                                           int64_t ldx, int ntiles, double* __restrict__ D) {
+// Xc[k][c][s] = X[k][8 (r0 + s) + c] for s < steps; stream stride ldc (x 8 per row).
+// Each wave moves 256 steps (8 KB) on its own: 8 lane-contiguous 16-B loads
+// (1 KB per instruction), the floats scattered into a chain-major LDS image
+// (rows of 256 + 4 floats: the b32 writes of a 32-lane group hit 32 banks),
+// then per chain one 16-B read of 4 steps per lane and a lane-contiguous 1-KB
+// store.  (Per-lane 128-B rows read at 3 TB/s: 64 cache lines per load.)
+constexpr int TW = 256;        // steps per wave
+constexpr int TROW = TW + 4;   // LDS floats per chain row
+__global__ __launch_bounds__(256) void chain_transpose_kernel(const float* __restrict__ X, int64_t ldx, int64_t r0,
+                                                              int64_t steps, int64_t ldc, float* __restrict__ Xc) {
+  __shared__ __attribute__((aligned(16))) float t[4 * 8 * TROW];
+  const int k = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * TW;
+  if (s0 >= steps) return;  // the whole wave (no workgroup barrier below)
+  const int nv = (int)(steps - s0 < TW ? steps - s0 : TW);
+  const float* src = X + (int64_t)k * ldx + 8 * (r0 + s0);
+  float* tw = t + wave * 8 * TROW;
+  const int h = lane & 1, sl = lane >> 1;
+  f32x4 v[8];
+  if (nv == TW) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src) + 64 * q + lane);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      v[q] = 32 * q + sl < nv ? reinterpret_cast<const f32x4*>(src)[64 * q + lane] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tw[(4 * h + e) * TROW + 32 * q + sl] = v[q][e];
+  // same wave: its LDS ops complete in order; the clobber keeps the compiler
+  // from moving the reads above the writes
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float* dst = Xc + (int64_t)k * 8 * ldc + s0 + 4 * lane;
+  if (nv == TW) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      *reinterpret_cast<f32x4*>(dst + (int64_t)c * ldc) = *reinterpret_cast<const f32x4*>(tw + c * TROW + 4 * lane);
+  } else {
+    for (int c = 0; c < 8; ++c)
+      for (int e = 0; e < 4 && 4 * lane + e < nv; ++e) dst[(int64_t)c * ldc + e] = tw[c * TROW + 4 * lane + e];
+  }
+}
+
+// x_i broadcast: lane L of every 16-lane row holds steps XW (L & 15) ..
+// XW (L & 15) + XW - 1 of the chunk (one 4 XW-byte load per lane, the four
+// rows alike); step S reaches every lane by a DPP row_newbcast of lane S / XW,
+// which the compiler folds into the subtraction (v_sub_f32_dpp: fl(x_i - x_j),
+// the reference's operand order), so the wave-uniform operand costs no extra
+// instruction, no LDS cycle and one TA request per chunk.
+template <int S>
+__device__ __forceinline__ float bcast(xvec xv) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xv[S % XW]), 0x150 + S / XW, 0xf, 0xf, false));
+}
+// the differences first (independent registers: one temporary reused for
+// every step made the hazard recognizer put an s_nop before each DPP write),
+// then the fma chain in step order
+template <int... S>
+__device__ __forceinline__ float chain_chunk(xvec xv, const f32x4 (&v)[NQ], float acc,
+                                             std::integer_sequence<int, S...>) {
+  float d[sizeof...(S)];
+  ((d[S] = bcast<S>(xv) - v[S >> 2][S & 3]), ...);
+  ((acc = __builtin_fmaf(d[S], d[S], acc)), ...);
+  return acc;
+}
+
+// One segment of steps for the tiles [t0, t0 + gridDim.x / 8): chain c of the
+// pairs (i, j), i = TI * ig + wave, j = NJ * jb + lane, i < j < K; the running
+// chain sums in A[c][i][j] (first: start from 0).
+__global__ __launch_bounds__(THREADS) void ref_chain_kernel(const float* __restrict__ Xc, int64_t ldc, int K,
+                                                            int64_t steps, int t0, int first,
+                                                            float* __restrict__ A) {
   // ONE __shared__ array (a second __shared__ object makes hipcc wait vmcnt(0)
-  // before the LDS reads, draining the DMA ring): the staging ring, then the
-  // lane partials of the final sum
-  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * BUF + 2 * THREADS];
-  f32x2* red = reinterpret_cast<f32x2*>(lds + NSTAGE * BUF);
-  const int nI = cdiv(K, TI), nJ = cdiv(K, TJ);
-  // XCD-aware: consecutive workgroup ids go to different XCDs, so XCD x takes
-  // the contiguous tile range [x * per, (x + 1) * per) of the jb-major order
-  // (tiles sharing J rows share one L2)
-  const int per = cdiv(ntiles, 8);
-  const int tile = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-  if (tile >= ntiles) return;  // uniform: the whole workgroup leaves
+  // before the LDS reads, draining the DMA ring)
+  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * STAGE];
+  const int c = (int)(blockIdx.x & 7);
+  const int tile = t0 + (int)(blockIdx.x >> 3);
   int jb = 0, base = 0;
-  for (; jb < nJ; ++jb) {
-    const int n = 2 * jb + 2 < nI ? 2 * jb + 2 : nI;
+  for (;; ++jb) {
+    const int n = igroups(jb, K);
     if (tile < base + n) break;
     base += n;
   }
-  const int ib = tile - base;
+  const int ig = tile - base;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int pi = tid >> 5, pj = (tid >> 2) & 7, cp = tid & 3;
-  const int i = TI * ib + pi, j = TJ * jb + pj;
+  const int i = TI * ig + wave;  // uniform
+  const int j = NJ * jb + lane;
+  const int jmax = (NJ * jb + NJ - 1 < K - 1) ? NJ * jb + NJ - 1 : K - 1;
+  const bool active = i < jmax;  // uniform: some lane of this wave holds a pair
+  const bool valid = i < j && j < K;
+  const int64_t rs = 8 * ldc;
 
-  // staging: wave w DMAs rows w, w + 2, ... of the 12 (I rows 0..3, J rows 4..11)
-  const int64_t R = P / 8;  // full chain steps
-  const int64_t nch = (R + CS - 1) / CS;
-  const float* src[NROWS / 2];
+  // staging: wave w moves J rows 8w .. 8w+7 of the block, RPD rows per DMA
+  // instruction; lane -> row 8w + RPD u + lane / NQ, LDS slot lane % NQ holding
+  // the chunk's piece slot ^ slot_swz(row)
+  const float* ssrc[DPW];
 #pragma unroll
-  for (int q = 0; q < NROWS / 2; ++q) {
-    const int row = wave + 2 * q;
-    int g = row < TI ? TI * ib + row : TJ * jb + (row - TI);
-    g = g < K ? g : K - 1;
-    src[q] = X + (int64_t)g * ldx;
+  for (int u = 0; u < DPW; ++u) {
+    const int srow = 8 * wave + RPD * u + lane / NQ;
+    int gj = NJ * jb + srow;
+    gj = gj < K ? gj : K - 1;
+    ssrc[u] = Xc + (int64_t)gj * rs + (int64_t)c * ldc + 4 * ((lane % NQ) ^ slot_swz(srow));
   }
-  auto stage = [&](int64_t ch, float* buf) {
-    const int64_t off = ch * CW + 4 * lane;  // this lane's 4 floats of the row's chunk
-    const bool ok = off + 4 <= R * 8;        // past the last full step: any valid address (unused)
+  float* sdst = lds + 8 * wave * CS;
+  // DMA of chunk ch's pieces into the stage of (virtual) chunk slot
+  auto stage = [&](int64_t ch, int64_t slot) {
 #pragma unroll
-    for (int q = 0; q < NROWS / 2; ++q) {
-      const int row = wave + 2 * q;
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src[q] + (ok ? off : 0)),
-          (__attribute__((address_space(3))) void*)(buf + row * RSTR), 16, 0, 0);
-    }
+    for (int u = 0; u < DPW; ++u)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc[u] + ch * CS),
+                                       (__attribute__((address_space(3))) void*)(sdst + (int)(slot % NSTAGE) * STAGE +
+                                                                                 256 * u),
+                                       16, 0, 0);
   };
+  const int gi = active ? i : 0;
+  const float* xi = Xc + (int64_t)gi * rs + (int64_t)c * ldc;
+  const float* xl = xi + XW * (lane & 15);
+  // x_i of chunk ch (see bcast), issued by asm so the compiler's waitcnt pass
+  // leaves it to the body's counted wait (its conservative merge across the
+  // rotated registers drained vmcnt(0) every chunk)
+  auto xload = [&](int64_t ch, xvec& x) {
+    if constexpr (XW == 4)
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(xl + ch * CS));
+    else
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x) : "v"(xl + ch * CS));
+  };
+  const int rsw = slot_swz(lane);
+  const float* rrow = lds + lane * CS;
 
-  f32x2 acc = {0.f, 0.f};
-  const float* arow = lds + pi * RSTR + 2 * cp;
-  const float* brow = lds + (TI + pj) * RSTR + 2 * cp;
-  for (int64_t c = 0; c < NSTAGE - 1 && c < nch; ++c) stage(c, lds + c * BUF);
-  for (int64_t ch = 0; ch < nch; ++ch) {
-    // chunk ch landed: this wave's DMAs of the chunks after it may stay in flight
-    if (ch + NSTAGE - 2 < nch) {
-      static_assert(DMA_PER_WAVE * (NSTAGE - 2) == 12, "vmcnt immediate below");
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    // every wave's DMA of chunk ch landed and every wave's reads of chunk ch-1
-    // are done (their buffer is restaged below): raw barrier, no vmcnt(0) drain
+  float acc = 0.f;
+  if (!first && valid) acc = A[((int64_t)c * K + i) * K + j];
+  const int64_t nch = (steps + CS - 1) / CS, nfull = steps / CS;
+
+  // Every body issues the same vector-memory ops in the same order — the DPW
+  // DMAs of chunk ch + NSTAGE - 1, then its x_i load, both clamped to the last
+  // chunk — so at the top of body ch exactly VMC = (NSTAGE - 2) (DPW + 1) ops
+  // are younger than chunk ch's: one counted wait covers this wave's DMA and
+  // x_i of chunk ch, and NSTAGE - 1 chunks of compute hide their latency.
+  auto issue = [&](int64_t ch, xvec& xn) {
+    const int64_t cl = ch < nch ? ch : nch - 1;
+    stage(cl, ch);
+    xload(cl, xn);
+  };
+  auto body = [&](int64_t ch, xvec& xc, xvec& xn) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
+    // every wave's DMA of chunk ch landed and every wave finished chunk ch-1,
+    // whose stage (and x_i register) is refilled below: raw barrier, no vmcnt(0) drain
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const int cur = (int)(ch % NSTAGE);
-    if (ch + NSTAGE - 1 < nch) stage(ch + NSTAGE - 1, lds + ((ch + NSTAGE - 1) % NSTAGE) * BUF);
-    const float* a = arow + cur * BUF;
-    const float* b = brow + cur * BUF;
-    const int64_t left = R - ch * CS;
-    if (left >= CS) {
+    issue(ch + NSTAGE - 1, xn);
+    if (active && ch < nfull) {
+      const float* rd = rrow + (int)(ch % NSTAGE) * STAGE;
+      f32x4 v[NQ];
 #pragma unroll
-      for (int s = 0; s < CS; ++s) {
-        const f32x2 d = *reinterpret_cast<const f32x2*>(a + 8 * s) - *reinterpret_cast<const f32x2*>(b + 8 * s);
-        acc = __builtin_elementwise_fma(d, d, acc);
-      }
-    } else {
-      for (int s = 0; s < (int)left; ++s) {
-        const f32x2 d = *reinterpret_cast<const f32x2*>(a + 8 * s) - *reinterpret_cast<const f32x2*>(b + 8 * s);
-        acc = __builtin_elementwise_fma(d, d, acc);
+      for (int q = 0; q < NQ; ++q) v[q] = *reinterpret_cast<const f32x4*>(rd + 4 * (q ^ rsw));
+      // (xc came from an asm load: keep the compiler from reading it before the wait above)
+      asm volatile("" : "+v"(xc));
+      acc = chain_chunk(xc, v, acc, std::make_integer_sequence<int, CS>{});
+    }
+  };
+
+  // the registers rotate with the chunk: xs[ch % NSTAGE] holds chunk ch's x_i;
+  // body ch refills xs[(ch - 1) % NSTAGE], the one body ch-1 consumed
+  xvec xs[NSTAGE];
+#pragma unroll
+  for (int u = 0; u < NSTAGE - 1; ++u) issue(u, xs[u]);
+  const int64_t nloop = (nfull + NSTAGE - 1) / NSTAGE * NSTAGE;  // whole unrolled groups: the last bodies wait, barrier, skip the compute
+  for (int64_t ch = 0; ch < nloop; ch += NSTAGE) {
+#pragma unroll
+    for (int u = 0; u < NSTAGE; ++u) body(ch + u, xs[u], xs[(u + NSTAGE - 1) % NSTAGE]);
+  }
+  if (nfull < nch) {
+    // the last, partial chunk (< CS steps): staged as chunk nfull (the loop's
+    // clamped DMAs rewrote its stage with the same bytes), x_i from global
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (active) {
+      const float* rd = rrow + (int)(nfull % NSTAGE) * STAGE;
+      for (int s = 0; s < (int)(steps - nfull * CS); ++s) {
+        const float d = xi[nfull * CS + s] - rd[4 * ((s >> 2) ^ rsw) + (s & 3)];
+        acc = __builtin_fmaf(d, d, acc);
       }
     }
   }
-  // lane sum 0..7 in order, then the tail, correctly rounded sqrt
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  red[tid] = acc;
-  __syncthreads();
-  if (cp == 0 && i < j && j < K) {
-    const f32x2 l01 = red[tid], l23 = red[tid + 1], l45 = red[tid + 2], l67 = red[tid + 3];
-    float s = l01[0];
-    s = add_rn(s, l01[1]);
-    s = add_rn(s, l23[0]);
-    s = add_rn(s, l23[1]);
-    s = add_rn(s, l45[0]);
-    s = add_rn(s, l45[1]);
-    s = add_rn(s, l67[0]);
-    s = add_rn(s, l67[1]);
+  if (valid) A[((int64_t)c * K + i) * K + j] = acc;
+}
+
+// D[i][j] = D[j][i] for the pairs of tiles [t0, t1): chains summed 0..7 in
+// order, the tail, correctly rounded sqrt; the other pairs 0 (the ranks' parts
+// are then summed: exactly one rank holds each pair), the diagonal 0.
+__global__ void ref_finish_kernel(const float* __restrict__ A, const float* __restrict__ X, int K, int64_t P,
+                                  int64_t ldx, int64_t R, int t0, int t1, double* __restrict__ D) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)K * K) return;
+  const int i = (int)(idx / K), j = (int)(idx % K);
+  if (i == j) {
+    D[idx] = 0.0;
+    return;
+  }
+  if (i > j) return;
+  const int tile = tiles_before(j / NJ, K) + i / TI;
+  double v = 0.0;
+  if (tile >= t0 && tile < t1) {
+    float s = 0.f;
+    if (R > 0) {
+      const int64_t kk = (int64_t)K * K, p = (int64_t)i * K + j;
+      s = A[p];
+#pragma unroll
+      for (int c = 1; c < 8; ++c) s = add_rn(s, A[c * kk + p]);
+    }
     const float* xi = X + (int64_t)i * ldx;
     const float* xj = X + (int64_t)j * ldx;
     int64_t t = R * 8;
@@ -167,16 +311,14 @@ __global__ __launch_bounds__(THREADS) void ref_norm_kernel(const float* __restri
       const float d = xi[t] - xj[t];
       s = __builtin_fmaf(d, d, s);
     }
-    const double v = (double)sqrt_rn(s);
-    D[(int64_t)i * K + j] = v;
-    D[(int64_t)j * K + i] = v;
+    v = (double)sqrt_rn(s);
   }
+  D[(int64_t)i * K + j] = v;
+  D[(int64_t)j * K + i] = v;
 }
 
-__global__ void diag_zero_kernel(int K, double* __restrict__ D) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < K) D[(int64_t)i * K + i] = 0.0;
-}
+// workspace layout: A [8][K][K] fp32 (256-B aligned), then the chain-major segment
+inline size_t a_bytes(int64_t K) { return align_up((size_t)(8 * K * K) * 4, 256); }
 
 }  // namespace pwref
 }  // namespace flr
@@ -184,19 +326,60 @@ __global__ void diag_zero_kernel(int K, double* __restrict__ D) {
 using namespace flr;
 using namespace flr::pwref;
 
-extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx, double* D,
-                                         void* stream) {
-  if (K < 1 || P < 0 || ldx < P || !D || (K > 1 && P > 0 && !X)) return FLR_ERR_ARG;
+extern "C" size_t flr_pairwise_l2_reference_workspace(int64_t K, int64_t P) {
+  if (K < 1 || P < 0) return 0;
+  const int64_t R = P / 8;
+  size_t n = a_bytes(K);
+  if (K < 2 || R == 0) return n;
+  const int64_t Rc = (R + CS - 1) / CS * CS;
+  const int64_t per_step = K * 8 * 4;
+  const int64_t nseg = (per_step * Rc + XC_CAP - 1) / XC_CAP;
+  const int64_t Rs = ((R + nseg - 1) / nseg + CS - 1) / CS * CS;
+  return n + (size_t)(per_step * Rs);
+}
+
+extern "C" int flr_pairwise_l2_reference_tiles(int64_t K) {
+  if (K < 2 || K > (1 << 15)) return 0;
+  return tiles_before(cdiv((int)K, NJ), (int)K);
+}
+
+extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx, double* D, void* ws,
+                                         size_t ws_bytes, int64_t part, int64_t nparts, void* stream) {
+  if (K < 1 || P < 0 || ldx < P || !D || (K > 1 && P > 0 && !X) || nparts < 1 || part < 0 || part >= nparts)
+    return FLR_ERR_ARG;
   if (K > (1 << 15)) return FLR_ERR_UNSUPPORTED;
-  // LDS-DMA reads 16-B pieces: rows must start 16-B aligned
+  // 16-B loads of the rows
   if (K > 1 && P >= 8 && (((reinterpret_cast<uintptr_t>(X) & 15) != 0) || (ldx % 4) != 0)) return FLR_ERR_ARG;
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(diag_zero_kernel, dim3(cdiv((int)K, 256)), dim3(256), 0, st, (int)K, D);
-  int rc = launch_status("diag_zero_kernel");
-  if (rc != FLR_OK || K == 1) return rc;
-  const int nI = cdiv((int)K, TI), nJ = cdiv((int)K, TJ);
-  const int64_t ntiles = tiles_upto(nJ, nI);
-  const int per = (int)((ntiles + 7) / 8);
-  hipLaunchKernelGGL(ref_norm_kernel, dim3(8 * per), dim3(THREADS), 0, st, X, (int)K, P, ldx, (int)ntiles, D);
-  return launch_status("ref_norm_kernel");
+  const int64_t R = P / 8;
+  const size_t na = a_bytes(K);
+  if (K > 1 && R > 0 && (!ws || (reinterpret_cast<uintptr_t>(ws) & 255) != 0)) return FLR_ERR_WORKSPACE;
+  const int ntiles = K > 1 ? tiles_before(cdiv((int)K, NJ), (int)K) : 0;
+  const int t0 = (int)(part * ntiles / nparts), t1 = (int)((part + 1) * ntiles / nparts);
+  float* A = reinterpret_cast<float*>(ws);
+  if (K > 1 && R > 0 && t1 > t0) {
+    if (ws_bytes < na) return FLR_ERR_WORKSPACE;
+    const int64_t per_step = K * 8 * 4;
+    const int64_t ldc = (int64_t)((ws_bytes - na) / (size_t)per_step) / CS * CS;
+    if (ldc < CS) return FLR_ERR_WORKSPACE;
+    const int64_t nseg = (R + ldc - 1) / ldc;
+    const int64_t Rs = ((R + nseg - 1) / nseg + CS - 1) / CS * CS;  // <= ldc
+    float* Xc = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + na);
+    for (int64_t seg = 0; seg < nseg; ++seg) {
+      const int64_t r0 = seg * Rs, steps = (R - r0 < Rs) ? R - r0 : Rs;
+      if (steps <= 0) break;
+      hipLaunchKernelGGL(chain_transpose_kernel, dim3((unsigned)((steps + 4 * TW - 1) / (4 * TW)), (unsigned)K), dim3(256), 0,
+                         st, X, ldx, r0, steps, ldc, Xc);
+      int rc = launch_status("chain_transpose_kernel");
+      if (rc != FLR_OK) return rc;
+      hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(THREADS), 0, st, Xc, ldc, (int)K, steps, t0,
+                         seg == 0 ? 1 : 0, A);
+      rc = launch_status("ref_chain_kernel");
+      if (rc != FLR_OK) return rc;
+    }
+  }
+  const int64_t kk = K * K;
+  hipLaunchKernelGGL(ref_finish_kernel, dim3((unsigned)((kk + 255) / 256)), dim3(256), 0, st, A, X, (int)K, P, ldx,
+                     R, t0, t1, D);
+  return launch_status("ref_finish_kernel");
 }

@@ -24,6 +24,9 @@ class KrumDefense(BaseDefense):
         self.num_malicious = defense_config.get("num_malicious", 1)
         self.multi_k = defense_config.get("multi_k", 1)
         self.pairwise_method = defense_config.get("pairwise_method", "gram")
+        # flr.shard.Comm of a multi-GPU round (set by RoundEngine): the
+        # reference-exact distances then split their pair tiles over the ranks
+        self.comm = None
         self.selected_clients: List[int] = []
         self.rejected_clients: List[int] = []
         self.client_scores: List[float] = []
@@ -38,9 +41,21 @@ class KrumDefense(BaseDefense):
         if n < 2 * f + 3:  # krum.py:153-157
             raise ValueError(
                 f"Krum requires n >= 2f + 3. Got n={n}, f={f}. Need at least {2 * f + 3} clients.")
-        self.distances = ops.pairwise_l2(cm.X, self.pairwise_method)
+        self.distances = ops.pairwise_l2(cm.X, self.pairwise_method, comm=self.comm)
+        self._check_refine_capacity(n)
         self.scores_device, self.order_device = ops.krum_select(self.distances, f)
         return self.order_device
+
+    def _check_refine_capacity(self, K: int) -> None:
+        """The Gram path's refine list holds 128 rows: every row at K <= 128.
+        Past that, more far-cluster rows than it holds turn the whole D NaN,
+        diagonal included (include/flr.h) — raised here, on the device path of
+        every round, before any row is selected (one 8-byte read, K > 128 and
+        the Gram path only)."""
+        if self.pairwise_method == "gram" and K > ops.REFINE_ROWS and bool(torch.isnan(self.distances[0, 0])):
+            from .._capi import FlrError
+            raise FlrError("KrumDefense", -3, "more far-cluster rows than the Gram path refines (128): use "
+                                              "pairwise_method='direct' or 'reference'")
 
     def aggregate_flat(self, cm: ClientMatrix, num_examples: List[int], publish: bool = True) -> torch.Tensor:
         """Device pipeline; with publish=False the host copies of the scores
@@ -73,6 +88,7 @@ class KrumDefense(BaseDefense):
             raise ValueError(
                 f"Krum requires n >= 2f + 3. Got n={n}, f={f}. Need at least {2 * f + 3} clients.")
         self.distances = ops.pairwise_l2_sharded(cs, events=events)
+        self._check_refine_capacity(n)
         self.scores_device, self.order_device = ops.krum_select(self.distances, f)
         if publish:
             self.publish()
@@ -81,17 +97,11 @@ class KrumDefense(BaseDefense):
         return ops.rows_mean(cs.X, self.order_device[: min(self.multi_k, n)], divisor=self.multi_k)
 
     def publish(self) -> None:
-        """Host copies of scores / selected / rejected (krum.py:171-176).
-        NaN scores from finite distances cannot arise; a NaN distance matrix is
-        the Gram path's loud refine-capacity overflow (include/flr.h) or NaN
-        client updates — raised here rather than published as a selection."""
+        """Host copies of scores / selected / rejected (krum.py:171-176).  A
+        client that sent NaN has a NaN score and is ranked last, as numpy's
+        sort / argsort order NaN (the reference rejects it)."""
         order_host = self.order_device.cpu().tolist()
         self.client_scores = self.scores_device.cpu().tolist()
-        if any(s != s for s in self.client_scores):
-            from .._capi import FlrError
-            raise FlrError("KrumDefense", -3, "NaN Krum scores: NaN client updates, or more far-cluster rows "
-                                              "than the Gram path refines (use pairwise_method='direct' or "
-                                              "'reference')")
         self.selected_clients = order_host[: self.multi_k]
         self.rejected_clients = order_host[self.multi_k:]
 
@@ -170,6 +180,7 @@ class KrumTrimmedMeanDefense(KrumDefense):
             raise ValueError(
                 f"Krum requires n >= 2f + 3. Got n={n}, f={f}. Need at least {2 * f + 3} clients.")
         self.distances = ops.pairwise_l2_sharded(cs, events=events)
+        self._check_refine_capacity(n)
         self.scores_device, self.order_device = ops.krum_select(self.distances, f)
         if publish:
             self.publish()

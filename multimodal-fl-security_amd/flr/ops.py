@@ -15,6 +15,7 @@ from . import _capi
 
 CHUNK = 64  # coordinates per pairwise chunk; client matrices pad ldx to this
 PW_SLICES = 8  # FLR_PW_SLICES: canonical coordinate slices of the pairwise kernels
+REFINE_ROWS = 128  # far-cluster rows the Gram path refines per call (include/flr.h, a9)
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -34,23 +35,32 @@ def _check_matrix(X: torch.Tensor, name: str = "X") -> Tuple[int, int, int]:
     return X.shape[0], X.shape[1], X.stride(0)
 
 
-def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None) -> torch.Tensor:
+def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None, comm=None) -> torch.Tensor:
     """K×K float64 distances, D[i][j] = fp32 ||X_i - X_j|| (krum.py:73-99).
 
-    method: "gram" (centred Gram on MFMA, the production path), "direct"
-    (exact fp32 differences, fp32/fp64 partial sums) or "reference" (the
-    reference's own torch.norm accumulation, bit-identical D; X must then be
-    in the reference's coordinate order).
+    method: "gram" (centred Gram on MFMA), "direct" (exact fp32 differences,
+    fp32/fp64 partial sums) or "reference" (the reference's own torch.norm
+    accumulation, bit-identical D; X must then be in the reference's
+    coordinate order).
     events: optional (begin, end) raw hipEvent_t handles recorded around the
-    main MFMA kernel (flr.timing.HipEventPair)."""
+    main MFMA kernel (flr.timing.HipEventPair).
+    comm: optional flr.shard.Comm for the reference mode: every rank holds the
+    whole X, computes 1/world of the pair tiles and one all-reduce (sum, exact:
+    one non-zero term per pair) of the 8·K² bytes of D gives every rank D."""
     K, P, ldx = _check_matrix(X)
     D = torch.empty((K, K), dtype=torch.float64, device=X.device)
     if method == "reference":
-        if X.data_ptr() % 16 or ldx % 4:  # the kernel stages 16-B pieces of 16-B aligned rows
+        if X.data_ptr() % 16 or ldx % 4:  # the kernels load 16-B pieces of 16-B aligned rows
             Xa = torch.zeros((K, (P + 63) // 64 * 64), dtype=torch.float32, device=X.device)
             Xa[:, :P].copy_(X)
             X, ldx = Xa, Xa.stride(0)
-        _capi.call("flr_pairwise_l2_reference", X.data_ptr(), K, P, ldx, D.data_ptr(), _stream(X))
+        part, nparts = (0, 1) if comm is None else (comm.rank, comm.world)
+        nbytes = int(_capi.lib().flr_pairwise_l2_reference_workspace(K, P))
+        ws, wp = _ws(nbytes, X.device)
+        _capi.call("flr_pairwise_l2_reference", X.data_ptr(), K, P, ldx, D.data_ptr(), wp, nbytes, part, nparts,
+                   _stream(X))
+        if nparts > 1:
+            comm.all_reduce_sum(D)
         return D
     if method == "gram":
         ws_fn, fn = "flr_pairwise_l2_workspace", "flr_pairwise_l2"

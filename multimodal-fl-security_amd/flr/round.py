@@ -49,9 +49,12 @@ class RoundConfig:
     graph: bool = True                   # replay the training phase as one captured HIP graph (FLR_GRAPH=0: eager)
     fallback_fedavg: bool = False        # defense raises -> FedAvg of the round (robust_server.py:120-122)
     # with fallback_fedavg: also fall back on library / device errors (FlrError,
-    # out of memory), as the reference's `except Exception` does (True, the
-    # default); False re-raises them and falls back on defense-logic errors only
-    fallback_device_errors: bool = True
+    # out of memory), as the reference's `except Exception` does.  Off by
+    # default: a device error is loud (a sticky HIP error would fail the
+    # fallback's own kernels too), and at world > 1 it is never swallowed — one
+    # rank falling back while the others wait in the defense's next collective
+    # would hang the round instead of failing it
+    fallback_device_errors: bool = False
 
 
 def initial_global(spec: ModelSpec, seed: int, device) -> torch.Tensor:
@@ -101,6 +104,10 @@ class RoundEngine:
             self.xchg = CoordExchange(K, self.hi - self.lo, self.trainer.P, self.device, Comm())
         else:
             self.full = self.trainer.X if world == 1 else ClientMatrix.empty(K, shapes, self.device)
+            if world > 1 and hasattr(self.defense, "comm"):
+                # whole rows on every rank: the reference-exact Krum distances
+                # split their pair tiles over the ranks (one 8·K² all-reduce)
+                self.defense.comm = Comm()
         self.global_flat = initial_global(spec, rcfg.seed, self.device)
         steps = tcfg.local_steps
         self.batches = synthetic_batches(spec, steps, range(self.lo, self.hi), rcfg.batch, self.device)
@@ -206,7 +213,8 @@ class RoundEngine:
         RCCL errors, out of memory) loud instead."""
         from ._capi import FlrError
         device_error = isinstance(err, (FlrError, torch.cuda.OutOfMemoryError))
-        if not self.rcfg.fallback_fedavg or (device_error and not self.rcfg.fallback_device_errors):
+        if not self.rcfg.fallback_fedavg or (device_error and (not self.rcfg.fallback_device_errors
+                                                               or self.world > 1)):
             raise err
         logging.getLogger(__name__).error("Defense aggregation failed: %s, falling back to FedAvg", err)
         self.fell_back = True

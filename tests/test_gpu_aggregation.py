@@ -134,20 +134,44 @@ def test_pairwise_far_cluster_refined(cuda, K, P, f):
 
 def test_pairwise_far_cluster_overflow_is_loud(cuda):
     """More far-cluster rows than the refine list holds (140 > 128, only
-    possible at K > 128): every off-diagonal distance is NaN and Krum's
-    publish raises — never a silently inaccurate selection."""
+    possible at K > 128): every distance is NaN, the diagonal included (the
+    marker), and Krum raises on the device path itself — with publish=False
+    (the round engine's call) too — never a silently inaccurate selection."""
     from flr._capi import FlrError
     K, P, f = 300, 64 * 200, 140
     X = _far_cluster_matrix(K, P, f, seed=3, device=cuda)
     D = ops.pairwise_l2(X[:, :P], "gram")
-    off = ~torch.eye(K, dtype=torch.bool, device=cuda)
-    assert torch.isnan(D[off]).all() and (D.diagonal() == 0).all()
-    d = KrumDefense({"num_malicious": f, "multi_k": K // 2})
-    with pytest.raises(FlrError):
-        d.aggregate_flat(ClientMatrix(X, P, [(P,)]), [1] * K)
+    assert torch.isnan(D).all()
+    for publish in (True, False):
+        d = KrumDefense({"num_malicious": f, "multi_k": K // 2})
+        with pytest.raises(FlrError):
+            d.aggregate_flat(ClientMatrix(X, P, [(P,)]), [1] * K, publish=publish)
     # the exact paths have no such limit
     Dd = ops.pairwise_l2(X[:, :P], "direct")
     assert not torch.isnan(Dd).any()
+
+
+def test_krum_nan_client_is_rejected(cuda):
+    """A client that sends NaN (krum.py:89-131 on numpy): its distances are
+    NaN, np.sort puts them last in every row, its own score is NaN and
+    np.argsort ranks it last — rejected, every order slot written, the other
+    clients' scores and order those of the oracle."""
+    K, P, f = 12, 3000, 2
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(K, P, generator=g) * 0.1
+    X[5, 17] = float("nan")
+    data = torch.zeros((K, 3008), dtype=torch.float32)
+    data[:, :P] = X
+    d = KrumDefense({"num_malicious": f, "multi_k": 4, "pairwise_method": "direct"})
+    d.aggregate_flat(ClientMatrix(data.to(cuda), P, [(P,)]), [1] * K)
+    assert sorted(d.selected_clients + d.rejected_clients) == list(range(K))
+    assert d.rejected_clients[-1] == 5 and d.client_scores[5] != d.client_scores[5]
+    Dh = d.distances.cpu().numpy()
+    scores = np.asarray(orc.krum_scores(Dh, K - f - 2))
+    order = np.argsort(scores, kind="stable")
+    assert d.selected_clients + d.rejected_clients == order.tolist()
+    fin = [i for i in range(K) if i != 5]
+    assert np.array_equal(np.asarray(d.client_scores)[fin], scores[fin])
 
 
 def test_pairwise_large_offset_centering(cuda):

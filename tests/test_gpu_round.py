@@ -47,8 +47,8 @@ def test_fedavg_fallback_when_defense_raises(cuda):
     strict = RoundEngine(TINY, RoundConfig(defense="krum", **kw), TrainConfig(local_steps=1), cuda)
     with pytest.raises(ValueError):
         strict.run_round()
-    # a device / library failure: the reference's `except Exception` falls back
-    # (the default); fallback_device_errors=False keeps it loud
+    # a device / library failure: loud by default (fallback_device_errors=False);
+    # fallback_device_errors=True falls back as the reference's `except Exception`
     from flr._capi import FlrError
 
     def _fail(*a, **k):
@@ -64,6 +64,19 @@ def test_fedavg_fallback_when_defense_raises(cuda):
                 boom.run_round()
         else:
             assert torch.equal(boom.run_round(), ref) and boom.fallback_error == "FlrError"
+
+
+def test_round_refine_overflow_raises(cuda):
+    """K = 300 with 140 sign-flipped clients — more far-cluster rows
+    than the Gram path refines.  The round raises on its own device path
+    (run_round never calls publish), instead of ranking a NaN matrix; with the
+    FedAvg fallback on, device errors stay loud by default."""
+    from flr._capi import FlrError
+    kw = dict(num_clients=300, batch=4, defense="krum", attack="sign_flip", num_attackers=140, graph=False)
+    for fb in (False, True):
+        eng = RoundEngine(TINY, RoundConfig(fallback_fedavg=fb, **kw), TrainConfig(local_steps=1), cuda)
+        with pytest.raises(FlrError):
+            eng.run_round()
 
 
 def test_fltrust_round(cuda):

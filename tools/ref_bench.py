@@ -1,0 +1,75 @@
+"""Time the reference-exact Krum distances (flr_pairwise_l2_reference) at a
+BASELINE shape and check D against the C restatement of torch.norm.
+
+    python tools/ref_bench.py [--K 128] [--P 11800394] [--reps 5] [--check 64]
+
+--check N: compare N pairs (a fixed spread over the matrix) with
+oracle.normref (test infrastructure, host CPU) — bit equality required.
+Prints one JSON line (ms per distance matrix: min / median over reps)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-fl-security_amd"))
+sys.path.insert(0, ROOT)
+
+from flr import ops  # noqa: E402
+from flr.matrix import padded_ld  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=128)
+    ap.add_argument("--P", type=int, default=11_800_394)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--check", type=int, default=64)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    K, P = a.K, a.P
+    g = torch.Generator(device=dev).manual_seed(1234)
+    data = torch.zeros((K, padded_ld(P)), dtype=torch.float32, device=dev)
+    data[:, :P] = torch.randn((K, P), generator=g, device=dev) * 0.01
+    data[: K // 5, :P] *= -1.0
+    X = data[:, :P]
+    D = ops.pairwise_l2(X, "reference")  # warm-up (workspace, code objects)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(a.reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        D = ops.pairwise_l2(X, "reference")
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1))
+    out = {"K": K, "P": P, "ms_min": min(times), "ms_median": float(np.median(times)), "reps": times}
+    if a.check:
+        from oracle import normref
+        Dh = D.cpu().numpy()
+        pairs = []
+        n = 0
+        for t in range(a.check):
+            i = (t * 37) % K
+            j = (t * 91 + 1 + i) % K
+            if i == j:
+                continue
+            pairs.append((i, j))
+        t0 = time.time()
+        bad = 0
+        for i, j in pairs:
+            want = normref.norm_diff(X[i].cpu().numpy(), X[j].cpu().numpy())
+            if Dh[i, j] != want or Dh[j, i] != want:
+                bad += 1
+            n += 1
+        out.update({"checked_pairs": n, "mismatches": bad, "check_s": round(time.time() - t0, 1),
+                    "symmetric": bool(np.array_equal(Dh, Dh.T)), "diag_zero": bool((np.diag(Dh) == 0).all())})
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
