@@ -34,6 +34,14 @@ extern "C" {
 #define FLR_ERR_KRUM_N (-5)       /* n < 2f+3 (krum.py:153-157)             */
 
 const char* flr_version(void);
+/* "gfx950", or "gfx950 ablation" for the tools build (make ABLATION=1) that
+ * adds the measured-slower and timing-only kernel forms. */
+const char* flr_build_info(void);
+/* The A/B switches (FLR_* names): the process environment's FLR_*
+ * variables are read once, when the library loads; this sets (value NULL:
+ * unsets) one afterwards, for an in-process A/B.  FLR_ERR_ARG unless the name
+ * starts with FLR_. */
+int flr_set_knob(const char* name, const char* value);
 const char* flr_status_string(int status);
 /* Last HIP error string recorded by a failing call on this thread. */
 const char* flr_last_error(void);

@@ -960,7 +960,7 @@ inline Layout layout(int64_t K, int64_t P, int nsl = FLR_PW_SLICES) {
 inline int gram_ablate() {
 #ifdef FLR_ABLATION
   static const int a = [] {
-    const char* e = getenv("FLR_GRAM_ABLATE");
+    const char* e = flr::knob("FLR_GRAM_ABLATE");
     return e ? atoi(e) : 0;
   }();
   return a;
@@ -975,7 +975,7 @@ inline int gram_ablate() {
 // at 2/3 of the kernel time.  FLR_GRAM_TERMS=2|3 overrides.  P is the WHOLE
 // vector's length (the same choice on every GPU of a sharded call).
 inline int gram_terms(int64_t P) {
-  const char* e = getenv("FLR_GRAM_TERMS");
+  const char* e = flr::knob("FLR_GRAM_TERMS");
   if (e && (e[0] == '2' || e[0] == '3')) return e[0] - '0';
   return P < (int64_t(1) << 20) ? 3 : 2;
 }
@@ -1020,7 +1020,7 @@ int launch_gram(const GramArgs& a, const Plan& p, int group_base, int ngroups, h
   // profiles/r3_gram_nt.txt).  FLR_GRAM_NT=0: default policy everywhere, 2:
   // non-temporal everywhere (A/B)
   {
-    const char* e = getenv("FLR_GRAM_NT");
+    const char* e = flr::knob("FLR_GRAM_NT");
     const int mode = e ? atoi(e) : 1;
     if (mode == 2 || (mode == 1 && !CROSS && a.K <= 32 * NL)) {
       FLR_GRAM_LAUNCH(2, 0, true);

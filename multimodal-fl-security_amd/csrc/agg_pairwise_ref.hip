@@ -55,6 +55,9 @@ constexpr int THREADS = 64 * TI;   // 512
 #ifndef FLR_REF_CS
 #define FLR_REF_CS 32
 #endif
+#ifndef FLR_REF_XI
+#define FLR_REF_XI 1
+#endif
 #ifndef FLR_REF_NSTAGE
 #define FLR_REF_NSTAGE 4
 #endif
@@ -276,6 +279,155 @@ __global__ __launch_bounds__(THREADS) void ref_chain_kernel(const float* __restr
   if (valid) A[((int64_t)c * K + i) * K + j] = acc;
 }
 
+// ---- x_i from scalar registers (FLR_REF_XI=1) ---------------------------------
+// The wave-uniform operand x_i reaches the VALU as a scalar operand: one
+// s_load_dwordx16 moves 16 steps of row i's chain c into SGPRs, and one
+// v_pk_add_f32 subtracts two steps (x_j from VGPRs, x_i from an SGPR pair; a
+// VOP3P instruction may read one SGPR pair), so a step costs 1.5 plain VALU
+// instructions — no DPP (which measured ~4x the issue cost of a plain VALU op on
+// gfx950, tools/hip/valu_lat.hip), no LDS cycle, no TA request.  Every LDS / SMEM
+// access of the chunk loop is inline asm with explicit waits: the chunk ch+1
+// operands (8 ds_read_b128 of x_j, 2 s_load_dwordx16 of x_i) are issued in body
+// ch and waited at the top of body ch+1 by one lgkmcnt(0) (SMEM returns out of
+// order, so only a full wait is exact), so their latency hides under chunk ch's
+// chain.  NSTAGE_S LDS stages: DMA(ch + NSTAGE_S - 1) issued in body ch, DMA(ch+1)
+// waited at the top of body ch (vmcnt counts the DMAs only).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr int NSTAGE_S = 6;          // LDS stages = the loop's unroll (static stage offsets)
+constexpr int CS_S = 32;
+constexpr int STAGE_S = NJ * CS_S;
+constexpr int VMC_S = NSTAGE_S - 3;  // DMAs younger than DMA(ch+1) at the top of body ch (one per body per wave)
+
+__device__ __forceinline__ f32x2 pk_sub_s(f32x2 v, f32x2 x) {
+  f32x2 r;
+  asm volatile("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(v), "s"(x));
+  return r;
+}
+template <int... S>
+__device__ __forceinline__ float chain_chunk_s(const f32x16& xa, const f32x16& xb, const f32x4 (&v)[8], float acc,
+                                               std::integer_sequence<int, S...>) {
+  // S = 0 .. 15: the step pair (2S, 2S + 1)
+  f32x2 d[16];
+  ((d[S] = pk_sub_s(__builtin_shufflevector(v[S >> 1], v[S >> 1], 2 * (S & 1), 2 * (S & 1) + 1),
+                    S < 8 ? __builtin_shufflevector(xa, xa, (2 * S) & 15, (2 * S + 1) & 15)
+                          : __builtin_shufflevector(xb, xb, (2 * S) & 15, (2 * S + 1) & 15))),
+   ...);
+  ((acc = __builtin_fmaf(d[S][1], d[S][1], __builtin_fmaf(d[S][0], d[S][0], acc))), ...);
+  return acc;
+}
+
+__global__ __launch_bounds__(THREADS) void ref_chain_s_kernel(const float* __restrict__ Xc, int64_t ldc, int K,
+                                                              int64_t steps, int t0, int first,
+                                                              float* __restrict__ A) {
+  __shared__ __attribute__((aligned(16))) float lds[NSTAGE_S * STAGE_S];
+  const int c = (int)(blockIdx.x & 7);
+  const int tile = t0 + (int)(blockIdx.x >> 3);
+  int jb = 0, base = 0;
+  for (;; ++jb) {
+    const int n = igroups(jb, K);
+    if (tile < base + n) break;
+    base += n;
+  }
+  const int ig = tile - base;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = TI * ig + wave;  // uniform
+  const int j = NJ * jb + lane;
+  const int jmax = (NJ * jb + NJ - 1 < K - 1) ? NJ * jb + NJ - 1 : K - 1;
+  const bool active = i < jmax;
+  const bool valid = i < j && j < K;
+  const int64_t rs = 8 * ldc;
+  // the running sum of the previous segments (asm load + full wait: nothing of
+  // the compiler's own vmcnt bookkeeping reaches into the DMA loop)
+  float acc = 0.f;
+  if (!first) {
+    const float* ap = A + ((int64_t)c * K + (i < K ? i : K - 1)) * K + (j < K ? j : K - 1);
+    asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(acc) : "v"(ap) : "memory");
+    acc = valid ? acc : 0.f;
+  }
+  // staging as ref_chain_kernel at CS = 32: wave w, lane -> row 8w + (lane >> 3), slot lane & 7
+  const int srow = 8 * wave + (lane >> 3);
+  int gj = NJ * jb + srow;
+  gj = gj < K ? gj : K - 1;
+  const float* ssrc = Xc + (int64_t)gj * rs + (int64_t)c * ldc + 4 * ((lane & 7) ^ ((srow >> 1) & 7));
+  float* sdst = lds + 8 * wave * CS_S;
+  auto stage = [&](int ch, int slot) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc + (int64_t)ch * CS_S),
+                                     (__attribute__((address_space(3))) void*)(sdst + slot * STAGE_S), 16, 0, 0);
+  };
+  const float* xi = Xc + (int64_t)(active ? i : 0) * rs + (int64_t)c * ldc;  // uniform
+  // buffer resource over row i's chain-c stream (raw, 4 * ldc bytes; dword
+  // format): the x_i scalar loads then take a 32-bit offset, one SGPR
+  const uint64_t xb64 = (uint64_t)(uintptr_t)xi;
+  const i32x4 xrsrc = {(int)(uint32_t)xb64, (int)(uint32_t)(xb64 >> 32) & 0xffff, (int)(4 * ldc), 0x00020000};
+  const int rsw = (lane >> 1) & 7;
+  // per-lane LDS byte addresses of the 8 swizzled 16-B pieces of this lane's row in stage 0
+  uint32_t ra[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) ra[q] = (uint32_t)(uintptr_t)(lds + lane * CS_S + 4 * (q ^ rsw));
+  // chunk ch's operands (stage `st` static): x_j 8 x 16 B from LDS, x_i 32 steps into SGPRs
+  auto fetch = [&ra](auto st, int ch, f32x4(&v)[8], f32x16& xa, f32x16& xb, i32x4 rsrc) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[q]) : "v"(ra[q]), "n"(decltype(st)::value * STAGE_S * 4)
+                   : "memory");
+    const int off = ch * CS_S * 4;  // byte offset into row i's chain-c stream
+    asm volatile("s_buffer_load_dwordx16 %0, %1, %2" : "=s"(xa) : "s"(rsrc), "s"(off) : "memory");
+    asm volatile("s_buffer_load_dwordx16 %0, %1, %2 offset:0x40" : "=s"(xb) : "s"(rsrc), "s"(off) : "memory");
+  };
+  // chunk indices in 32 bits (steps < 2^31 * 32 per segment): scalar min, no 64-bit compares
+  const int nch = (int)((steps + CS_S - 1) / CS_S), nfull = (int)(steps / CS_S), lastc = nch - 1;
+  auto clampc = [&](int ch) { return ch < lastc ? ch : lastc; };
+  f32x4 va[8], vb[8];
+  f32x16 xa0, xa1, xb0, xb1;
+  // body ch (stage ch % 6 = U): chunk ch's operands arrived (fetched in body
+  // ch - 1); DMA(ch + 5) into stage (U + 5) % 6 = the stage of chunk ch - 1, whose
+  // reads every wave finished before this barrier; fetch chunk ch + 1
+  auto body = [&](auto U, int ch, f32x4(&vc)[8], f32x16& xc0, f32x16& xc1, f32x4(&vn)[8], f32x16& xn0,
+                  f32x16& xn1) {
+    constexpr int u = decltype(U)::value;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC_S) : "memory");  // this wave's DMA(ch + 1) landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");             // chunk ch's x_j and x_i in registers
+    __builtin_amdgcn_s_barrier();  // every wave's DMA(ch + 1) landed; every wave read stage ch - 1
+    asm volatile("" ::: "memory");
+    stage(clampc(ch + NSTAGE_S - 1), (u + NSTAGE_S - 1) % NSTAGE_S);
+    fetch(std::integral_constant<int, (u + 1) % NSTAGE_S>{}, clampc(ch + 1), vn, xn0, xn1, xrsrc);
+    if (active && ch < nfull) acc = chain_chunk_s(xc0, xc1, vc, acc, std::make_integer_sequence<int, 16>{});
+  };
+  // prologue: DMA chunks 0 .. 4, wait for DMA(0), chunk 0's operands
+#pragma unroll
+  for (int u = 0; u < NSTAGE_S - 1; ++u) stage(clampc(u), u);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTAGE_S - 2) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  fetch(std::integral_constant<int, 0>{}, 0, va, xa0, xa1, xrsrc);
+  const int nloop = (nfull + NSTAGE_S - 1) / NSTAGE_S * NSTAGE_S;
+  for (int ch = 0; ch < nloop; ch += NSTAGE_S) {
+    body(std::integral_constant<int, 0>{}, ch, va, xa0, xa1, vb, xb0, xb1);
+    body(std::integral_constant<int, 1>{}, ch + 1, vb, xb0, xb1, va, xa0, xa1);
+    body(std::integral_constant<int, 2>{}, ch + 2, va, xa0, xa1, vb, xb0, xb1);
+    body(std::integral_constant<int, 3>{}, ch + 3, vb, xb0, xb1, va, xa0, xa1);
+    body(std::integral_constant<int, 4>{}, ch + 4, va, xa0, xa1, vb, xb0, xb1);
+    body(std::integral_constant<int, 5>{}, ch + 5, vb, xb0, xb1, va, xa0, xa1);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (nfull < nch) {
+    // the last, partial chunk: staged as chunk nfull in stage nfull % 6 (the
+    // clamped DMAs after it rewrote that stage with the same bytes)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (active) {
+      const float* rd = lds + lane * CS_S + (nfull % NSTAGE_S) * STAGE_S;
+      for (int s2 = 0; s2 < (int)(steps - (int64_t)nfull * CS_S); ++s2) {
+        const float d = xi[(int64_t)nfull * CS_S + s2] - rd[4 * ((s2 >> 2) ^ rsw) + (s2 & 3)];
+        acc = __builtin_fmaf(d, d, acc);
+      }
+    }
+  }
+  if (valid) A[((int64_t)c * K + i) * K + j] = acc;
+}
+
 // D[i][j] = D[j][i] for the pairs of tiles [t0, t1): chains summed 0..7 in
 // order, the tail, correctly rounded sqrt; the other pairs 0 (the ranks' parts
 // are then summed: exactly one rank holds each pair), the diagonal 0.
@@ -372,8 +524,13 @@ extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, i
                          st, X, ldx, r0, steps, ldc, Xc);
       int rc = launch_status("chain_transpose_kernel");
       if (rc != FLR_OK) return rc;
+#if FLR_REF_XI == 1
+      hipLaunchKernelGGL(ref_chain_s_kernel, dim3(8 * (t1 - t0)), dim3(THREADS), 0, st, Xc, ldc, (int)K, steps, t0,
+                         seg == 0 ? 1 : 0, A);
+#else
       hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(THREADS), 0, st, Xc, ldc, (int)K, steps, t0,
                          seg == 0 ? 1 : 0, A);
+#endif
       rc = launch_status("ref_chain_kernel");
       if (rc != FLR_OK) return rc;
     }

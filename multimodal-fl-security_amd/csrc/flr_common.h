@@ -12,6 +12,10 @@ namespace flr {
 // Records the last HIP error text for flr_last_error().
 void set_last_error(const char* where, hipError_t e);
 
+// An A/B switch's value (the FLR_* environment read once at library load, or
+// flr_set_knob since), nullptr when unset (capi.cpp).
+const char* knob(const char* name);
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // Checks the launch that was just enqueued.

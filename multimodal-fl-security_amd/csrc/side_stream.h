@@ -39,9 +39,15 @@ struct SideStream {
   hipEvent_t ev[NEV] = {};
 };
 
-inline bool side_overlap_enabled() {  // read per call: a test flips it within one process
-  const char* e = getenv("FLR_SGD_OVERLAP");
+// The optimizer update on a side stream under the next step's forward
+// (FLR_SGD_OVERLAP=1) measured no faster: tools build only.
+inline bool side_overlap_enabled() {
+#ifdef FLR_ABLATION
+  const char* e = flr::knob("FLR_SGD_OVERLAP");
   return e && e[0] == '1';
+#else
+  return false;
+#endif
 }
 
 // The current device's side stream; created on first use when create is set
@@ -82,7 +88,7 @@ struct TextStream {
 };
 
 inline bool text_stream_enabled() {
-  const char* e = getenv("FLR_TEXT_STREAM");
+  const char* e = flr::knob("FLR_TEXT_STREAM");
   return !(e && e[0] == '0');
 }
 
@@ -121,7 +127,7 @@ struct WgradStream {
 };
 
 inline bool wgrad_stream_enabled() {
-  const char* e = getenv("FLR_WGRAD_STREAM");
+  const char* e = flr::knob("FLR_WGRAD_STREAM");
   return !(e && e[0] == '0');
 }
 

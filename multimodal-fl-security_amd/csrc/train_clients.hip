@@ -171,7 +171,7 @@ class Net {
     Hp_ = (Hs_ + 2 - 3) / 2 + 1;  // the 3x3/2/1 max pool
     // the fused stem BN + ReLU + pool kernels' shapes (FLR_STEM_FUSED=0: the three-kernel form)
     {
-      const char* e = getenv("FLR_STEM_FUSED");
+      const char* e = flr::knob("FLR_STEM_FUSED");
       stem_fused_ = !(e && e[0] == '0') && Hs_ == 16 && (B_ == 16 || B_ == 32);
     }
     int64_t cin = w0, Hc = Hp_;
@@ -1031,12 +1031,12 @@ extern "C" int flr_train_clients_ex(const flr_resnet_gru_spec* spec, const float
   float* step_loss = reinterpret_cast<float*>(base + align_up(net.bytes(), 256));
   net.norms_ = norms_out;
   static const bool fuse_res = [] {
-    const char* e = getenv("FLR_FUSED_RES");
+    const char* e = flr::knob("FLR_FUSED_RES");
     return !(e && e[0] == '0');
   }();
   net.fuse_res_ = fuse_res;
   static const bool shared_first = [] {
-    const char* e = getenv("FLR_SHARED_FIRST");
+    const char* e = flr::knob("FLR_SHARED_FIRST");
     return !(e && e[0] == '0');
   }();
   net.shared_first_ = shared_first;

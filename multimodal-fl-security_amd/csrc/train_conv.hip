@@ -424,9 +424,9 @@ using namespace flr;
 using namespace flr::conv;
 
 // FLR_CONV_GENERIC=1 forces the generic gathers (A/B timing and cross-checks).
-static int getenv_generic() {
+static int generic_conv_forced() {
   static const int v = [] {
-    const char* e = getenv("FLR_CONV_GENERIC");
+    const char* e = flr::knob("FLR_CONV_GENERIC");
     return (e && e[0] == '1') ? 1 : 0;
   }();
   return v;
@@ -449,9 +449,9 @@ extern "C" int flr_conv2d_fwd(const float* x, const float* w, float* y, int64_t 
                               void* ws, size_t ws_bytes, void* stream) {
   if (!x || !w || !y || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
   const Geom g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
-  if (getenv_generic() == 0 && convt::im2col_eligible(g) && ws && ws_bytes >= convt::im2col_workspace(g))
+  if (generic_conv_forced() == 0 && convt::im2col_eligible(g) && ws && ws_bytes >= convt::im2col_workspace(g))
     return convt::fwd_im2col(g, x, w, y, ws, ws_bytes, as_stream(stream));
-  if (Cin % BK == 0 && getenv_generic() == 0) {
+  if (Cin % BK == 0 && generic_conv_forced() == 0) {
     FwdF pb;
     pb.g = g; pb.x = x; pb.w = w; pb.y = y;
     return launch(pb, ws, ws_bytes, as_stream(stream), "conv fwd");
@@ -466,7 +466,7 @@ extern "C" int flr_conv2d_bwd_data(const float* dy, const float* w, float* dx, i
                                    int64_t pad, void* ws, size_t ws_bytes, void* stream) {
   if (!dy || !w || !dx || !geom_ok(K, B, Cin, H, W, Cout, KH, KW, stride, pad)) return FLR_ERR_ARG;
   const Geom g = make_geom(K, B, Cin, H, W, Cout, KH, KW, stride, pad);
-  if (Cout % BK == 0 && getenv_generic() == 0) {
+  if (Cout % BK == 0 && generic_conv_forced() == 0) {
     DgradF pb;
     pb.g = g; pb.dy = dy; pb.w = w; pb.dx = dx;
     return launch(pb, ws, ws_bytes, as_stream(stream), "conv bwd data");
@@ -492,9 +492,9 @@ static int bwd_weight(const float* x, const float* dy, float* dw, int64_t K, int
     const int rc = launch_status("conv bwd weight: zero dead taps");
     if (rc != FLR_OK) return rc;
   }
-  if (getenv_generic() == 0 && convt::im2col_eligible(g) && ws && ws_bytes >= convt::im2col_workspace(g))
+  if (generic_conv_forced() == 0 && convt::im2col_eligible(g) && ws && ws_bytes >= convt::im2col_workspace(g))
     return convt::wgrad_im2col(g, x, dy, dw, ws, ws_bytes, st, have_col);
-  if (Cin % BN == 0 && getenv_generic() == 0) {
+  if (Cin % BN == 0 && generic_conv_forced() == 0) {
     WgtF pb;
     pb.g = g; pb.x = x; pb.dy = dy; pb.dw = dw;
     return launch(pb, ws, ws_bytes, st, "conv bwd weight");

@@ -192,28 +192,29 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& hi, bf16x8& 
 // launch so one process can compare both forms.
 // FLR_XCD=0 turns the XCD-aware tile order off (A/B timing).
 inline int xcd_remap() {
-  const char* e = getenv("FLR_XCD");
+  const char* e = flr::knob("FLR_XCD");
   return (e && e[0] == '0') ? 0 : 1;
 }
 
 // Wave priority raised around each MFMA cluster (FLR_PRIO=0: off, for A/B).
 inline int mfma_prio() {  // measured +0-5 % on the encoder GEMMs and the 3x3 convs (FLR_PRIO=0 turns it off)
-  const char* e = getenv("FLR_PRIO");
+  const char* e = flr::knob("FLR_PRIO");
   return (e && e[0] == '0') ? 0 : 1;
 }
 
-// 0: exact f32 MFMA; 1: bf16x6, accumulator-chain order (each output tile's six
-// products back to back); 2: bf16x6, product-major, software-pipelined; 4: the
-// same unpipelined; 5 (default): split at stash time where the plan supports
-// it (fwd / dgrad / batched GEMM), else 2.  FLR_GEMM=f32 | chain | pipe | old | stash.
+// 0: exact f32 MFMA; 2: bf16x6, product-major, software-pipelined; 5 (default):
+// split at stash time where the plan supports it (fwd / dgrad / batched GEMM),
+// else 2.  FLR_GEMM=f32 | pipe | stash.  The tools build (make ABLATION=1) adds
+// the measured-slower forms 1 (accumulator-chain order, FLR_GEMM=chain) and 4
+// (the unpipelined loop, =old), and the wrong-result timing ablation 3 (=A).
 inline int gemm_form() {
-  const char* e = getenv("FLR_GEMM");
+  const char* e = flr::knob("FLR_GEMM");
   if (e && e[0] == 'f') return 0;
-  if (e && e[0] == 'c') return 1;
 #ifdef FLR_ABLATION
+  if (e && e[0] == 'c') return 1;
   if (e && e[0] == 'A') return 3;  // ablation (timing only, wrong results): one bf16 term, no split; tools build only
-#endif
   if (e && e[0] == 'o') return 4;  // the unpipelined product-major loop (A/B timing)
+#endif
   if (e && e[0] == 'p') return 2;  // the pipelined loop for every plan
   return 5;  // split at stash (bf16 LDS images) where the plan has k8 loads, else pipelined
 }
@@ -2056,7 +2057,7 @@ __global__ __launch_bounds__(THREADS, 2) void dsgemm_kernel(const Plan pl, int S
 // profiles/r4_bgemm_dma_ab.txt): the per-wave split doubles the VALU split work
 // of the stash form, which costs more than the ds_write pass it removes.
 inline bool bgemm_dma() {
-  const char* e = getenv("FLR_BGEMM_DMA");
+  const char* e = flr::knob("FLR_BGEMM_DMA");
   return e && e[0] == '1';
 }
 // ---- the pre-split form (batched GEMMs with 128 x 128 tiles, FLR_BGEMM_PRESPLIT=1; measured slower) --
@@ -2229,7 +2230,7 @@ __global__ __launch_bounds__(THREADS, 2) void psgemm_kernel(const Plan pl, int S
 // 1.5x the bytes (2.8 GB per vit.qkv GEMM at 32 clients), and the split pass
 // itself transposes the row-contiguous (KR) operands of the weight gradients.
 inline bool bgemm_presplit() {
-  const char* e = getenv("FLR_BGEMM_PRESPLIT");
+  const char* e = flr::knob("FLR_BGEMM_PRESPLIT");
   return e && e[0] == '1';
 }
 
@@ -2551,7 +2552,7 @@ inline int choose_splits(int M, int N, int R, int /*K*/, int sub = 1, int min_kt
 
 inline int bgemm_min_kt() {
   static const int v = [] {
-    const char* e = getenv("FLR_BGEMM_MINKT");
+    const char* e = flr::knob("FLR_BGEMM_MINKT");
     const int x = e ? atoi(e) : 0;
     return x >= 1 && x <= 64 ? x : 32;
   }();
@@ -2564,7 +2565,7 @@ inline int bgemm_min_kt() {
 // most.  FLR_CONV_MINKT overrides (A/B timing).
 inline int conv_min_kt() {
   static const int v = [] {
-    const char* e = getenv("FLR_CONV_MINKT");
+    const char* e = flr::knob("FLR_CONV_MINKT");
     const int x = e ? atoi(e) : 0;
     return x >= 1 && x <= 256 ? x : 32;
   }();
@@ -2575,7 +2576,7 @@ inline int conv_min_kt() {
 // forward's split rule unless FLR_DGRAD_MINKT1 overrides it (A/B timing).
 inline int dgrad_min_kt1() {
   static const int v = [] {
-    const char* e = getenv("FLR_DGRAD_MINKT1");
+    const char* e = flr::knob("FLR_DGRAD_MINKT1");
     const int x = e ? atoi(e) : 0;
     return x >= 1 && x <= 256 ? x : 0;
   }();
@@ -2585,7 +2586,7 @@ inline int dgrad_min_kt1() {
 // Strided dgrad classes (FLR_DGRAD_MINKT2 overrides 8 for A/B timing).
 inline int dgrad_min_kt2() {
   static const int v = [] {
-    const char* e = getenv("FLR_DGRAD_MINKT2");
+    const char* e = flr::knob("FLR_DGRAD_MINKT2");
     const int x = e ? atoi(e) : 0;
     return x >= 1 && x <= 256 ? x : 8;
   }();
@@ -2616,7 +2617,7 @@ size_t splits_bytes(const Plan& pl) {  // enough for any sub-tile count (1, 2, 3
 // 128 x 512 outputs per client; 64 x 64 everywhere else.
 // FLR_CONV_TILE=11|21|12|22 forces a shape (read per launch, for A/B runs).
 inline int tile_choice(int M, int N, int R) {
-  const char* e = getenv("FLR_CONV_TILE");
+  const char* e = flr::knob("FLR_CONV_TILE");
   const int forced = e ? atoi(e) : 0;
   if (forced == 11) return 11;
   if (forced == 21 && M % 128 == 0) return 21;
@@ -2638,7 +2639,7 @@ template <int A, int B> struct is_bgemm_t<BGemm<A, B>> : std::true_type {
 // quad-lane stash's 2-way bank conflicts save — vit.qkv 493 vs 426 us at K=32,
 // profiles/r3_bgemm_timg.txt)
 inline bool bgemm_timg() {
-  const char* e = getenv("FLR_BGEMM_TIMG");
+  const char* e = flr::knob("FLR_BGEMM_TIMG");
   return e && e[0] == '1';
 }
 
@@ -2662,13 +2663,16 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
     // batched GEMMs with a k-contiguous operand: that operand on a transposed
     // image (coalesced 128-B row reads, conflict-free stashes; the row-major
     // image of a quad-lane load stashes 2-way bank-conflicted)
+#ifdef FLR_ABLATION
     if (form == 5 && bgemm_timg()) {
       hipLaunchKernelGGL((wsgemm_kernel<Plan, MS, NS, 2, is_bgemm_t<Plan>::ta, is_bgemm_t<Plan>::tb>), grid,
                          dim3(THREADS), 0, st, pl, S, static_cast<float*>(ws), xcd_remap());
       form = -1;
     }
+#endif
   }
   float* partp = static_cast<float*>(ws);  // split-K partials (after the planes in the pre-split form)
+#ifdef FLR_ABLATION  // the measured-slower batched-GEMM forms: tools build only
   if constexpr (std::is_base_of<BGemmArgs, Plan>::value && MS == 2 && NS == 2) {
     if (form == 5 && bgemm_presplit()) {
       const size_t pa_b = (ps_plane_bytes(K, M, R) + 255) / 256 * 256;
@@ -2698,10 +2702,11 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
       form = -1;
     }
   }
+#endif
   if constexpr (has_k8<Plan>::value) {
 #ifdef FLR_ABLATION
     if constexpr (MS == 2 && NS == 2) {
-      const char* ae = getenv("FLR_SG_ABL");  // timing ablations of the main loop (tools build only)
+      const char* ae = flr::knob("FLR_SG_ABL");  // timing ablations of the main loop (tools build only)
       const int abl = ae ? atoi(ae) : 0;
 #define FLR_SG_ABL_CASE(A)                                                                                  \
   if (form == 5 && abl == A) {                                                                               \
@@ -2735,20 +2740,20 @@ int launch_tiles(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, cons
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 0>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());
       break;
+#ifdef FLR_ABLATION
     case 1:
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 1>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());
       break;
-#ifdef FLR_ABLATION
     case 3:
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 3>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());
       break;
-#endif
     case 4:
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 4>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());
       break;
+#endif
     default:
       hipLaunchKernelGGL((tgemm_kernel<Plan, MS, NS, 2>), grid, dim3(THREADS), 0, st, pl, S,
                          static_cast<float*>(ws), xcd_remap(), mfma_prio());
@@ -2775,7 +2780,7 @@ constexpr bool wide_tiles() {
 template <class Plan>
 inline int plan_tile(const Plan& pl) {
   const int M = pl.M(), N = pl.N(), R = pl.R();
-  const char* e = getenv("FLR_CONV_TILE");
+  const char* e = flr::knob("FLR_CONV_TILE");
   const int forced = e ? atoi(e) : 0;
   if (forced) {  // A/B timing: any shape that leaves no sub-tile empty
     const int ms = forced / 10, ns = forced % 10;
@@ -2807,7 +2812,7 @@ int sq_slots(const Plan& pl) {
 // at most 32 columns (the l4 layers at 32 x 32 inputs: B * 1 * 1); FLR_CONV_NARROW=0:
 // the 64-wide tiles (A/B, read per launch).
 inline bool conv_narrow() {
-  const char* e = getenv("FLR_CONV_NARROW");
+  const char* e = flr::knob("FLR_CONV_NARROW");
   return !(e && e[0] == '0');
 }
 template <class Plan>
@@ -2837,7 +2842,7 @@ int launch_narrow(const Plan& pl, void* ws, size_t ws_bytes, hipStream_t st, con
 // FLR_CONV_FILL=0: off (A/B, read per launch).
 constexpr int FILL_WG = 512;  // two 128 x 128 workgroups per CU on 256 CUs
 inline bool conv_fill() {
-  const char* e = getenv("FLR_CONV_FILL");
+  const char* e = flr::knob("FLR_CONV_FILL");
   return !(e && e[0] == '0');
 }
 template <class Plan>
@@ -2926,13 +2931,13 @@ static int run_im2col(const Geom& g, const float* x, float* col, hipStream_t st)
 // im2col operand gathered on the fly (A/B timing); default: the direct stem
 // kernels (train_stem.hip) where eligible, else the gathered GEMM.
 inline bool stem_col() {
-  const char* e = getenv("FLR_STEM");
+  const char* e = flr::knob("FLR_STEM");
   return e && e[0] == 'c';
 }
 #endif
 #if FLR_CT_P0
 inline bool stem_direct(const Geom& g) {
-  const char* e = getenv("FLR_STEM");
+  const char* e = flr::knob("FLR_STEM");
   return !(e && (e[0] == 'c' || e[0] == 'g')) && stem_eligible(g);
 }
 #endif
@@ -3188,7 +3193,7 @@ int bgemm_mode(const float* p, int64_t s_k, int64_t s_row, int64_t s_r, int64_t 
 // ones (the GRU recurrence and the head, M = batch = 32).  Partial edge tiles
 // are bounds-checked in the loads and stores.  FLR_BGEMM_TILE=11|22 forces it.
 inline int bgemm_tile(int M, int N, int R) {
-  const char* e = getenv("FLR_BGEMM_TILE");
+  const char* e = flr::knob("FLR_BGEMM_TILE");
   const int forced = e ? atoi(e) : 0;
   if (forced == 11 || forced == 22) return forced;
   return (M >= 128 && N >= 128 && (R >= 256 || (int64_t)M * N >= 128 * 512)) ? 22 : 11;
@@ -3217,9 +3222,11 @@ extern "C" size_t flr_bgemm_workspace(int64_t batch, int64_t M, int64_t N, int64
   const int S = std::max(convt::choose_splits((int)M, (int)N, (int)R, (int)batch, 1, convt::bgemm_min_kt()),
                          convt::choose_splits((int)M, (int)N, (int)R, (int)batch, 4, convt::bgemm_min_kt()));
   size_t n = S > 1 ? (size_t)S * batch * M * N * sizeof(float) : 0;
+#ifdef FLR_ABLATION
   // the pre-split form's bf16 planes of both operands (128 x 128 tiles), before the partials
   if (convt::bgemm_presplit() && bgemm_tile((int)M, (int)N, (int)R) == 22)
     n += (convt::ps_plane_bytes(batch, M, R) + 255) / 256 * 256 + (convt::ps_plane_bytes(batch, N, R) + 255) / 256 * 256;
+#endif
   return n;
 }
 

@@ -499,7 +499,7 @@ namespace gru {
 // (tools/gru_bench.py); default 8 waves x 2 k-steps for both (C3: fwd 29 us, bwd 27 us per step)
 inline int cfg_index(const char* env, int dflt) {
   static const char* names[] = {"4,4", "8,2", "2,8", "8,2s", "8,6", "4,12", "16,3", "", "8,2s"};
-  const char* v = getenv(env);
+  const char* v = flr::knob(env);
   if (v)
     for (int i = 0; i < 9; ++i)
         if (names[i][0] && !strcmp(v, names[i])) return i;

@@ -566,7 +566,7 @@ extern "C" int flr_clip_sgd_step_phase(float* const* x_blocks, const float* cons
   }
   if (!(phase & FLR_SGD_PHASE_UPDATE)) return FLR_OK;
   static const int unroll = [] {
-    const char* e = getenv("FLR_SGD_U");
+    const char* e = flr::knob("FLR_SGD_U");
     const int u = e ? atoi(e) : 0;
     return (u == 2 || u == 4 || u == 8) ? u : 8;
   }();

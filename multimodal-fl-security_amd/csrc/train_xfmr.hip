@@ -820,7 +820,7 @@ namespace {
 // 492 -> 678 at KB = 1024, H = 6), so T <= 80 stays on 256.  FLR_ATT_THREADS=256 / 512
 // forces a form (A/B, read per launch; tools/att_bench.py).
 inline int att_threads(int NT) {
-  const char* e = getenv("FLR_ATT_THREADS");
+  const char* e = flr::knob("FLR_ATT_THREADS");
   if (e && atoi(e) == 256) return 256;
   if (e && atoi(e) == 512) return 512;
   return NT >= 6 ? 512 : 256;

@@ -29,6 +29,8 @@ _int = ctypes.c_int
 # name -> (restype, argtypes); must list every function include/flr.h declares.
 SIGNATURES = {
     "flr_version": (ctypes.c_char_p, []),
+    "flr_build_info": (ctypes.c_char_p, []),
+    "flr_set_knob": (_int, [ctypes.c_char_p, ctypes.c_char_p]),
     "flr_status_string": (ctypes.c_char_p, [_int]),
     "flr_last_error": (ctypes.c_char_p, []),
     "flr_pairwise_l2_workspace": (_size_t, [_i64, _i64]),
@@ -214,6 +216,17 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = args
         _lib = handle
         return _lib
+
+
+def set_knob(name: str, value) -> None:
+    """Set (value None: unset) one of the library's A/B switches (FLR_*; the
+    process environment is read once, when the library loads)."""
+    check("flr_set_knob", lib().flr_set_knob(name.encode(), None if value is None else str(value).encode()))
+
+
+def build_info() -> str:
+    """'gfx950', or 'gfx950 ablation' for the tools build (make ABLATION=1)."""
+    return lib().flr_build_info().decode()
 
 
 def status_string(status: int) -> str:

@@ -37,3 +37,27 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip("no GPU visible")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def knob():
+    """Set one of the library's A/B switches for this test (flr_set_knob: the
+    library reads the FLR_* environment once, at load); restored afterwards."""
+    from flr import _capi
+    names = []
+
+    def set_(name, value):
+        names.append(name)
+        _capi.set_knob(name, value)
+    yield set_
+    for n in names:
+        _capi.set_knob(n, os.environ.get(n))
+
+
+@pytest.fixture
+def ablation_build():
+    """Tests of the measured-slower / timing-only kernel forms: they exist only
+    in the tools build (make ABLATION=1; run with FLR_LIB pointing at it)."""
+    from flr import _capi
+    if "ablation" not in _capi.build_info():
+        pytest.skip("tools-build kernel form (make ABLATION=1)")

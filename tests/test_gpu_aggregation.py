@@ -67,12 +67,12 @@ def test_pairwise_gram_vs_direct_and_fp64(cuda, K, P):
 
 
 @pytest.mark.parametrize("K", [129, 300, 512])
-def test_pairwise_two_term_gram_wide(cuda, monkeypatch, K):
+def test_pairwise_two_term_gram_wide(cuda, knob, K):
     """The 2-term split that every BASELINE-size call runs (P >= 2^20), forced
     at a small P for K > 128 (the diagonal 128-row groups and the cross
     groups).  Against fp64 distances: 1e-4 for every pair, 2e-5 for the benign
     rows (measured 3.9e-6 / 1.3e-7)."""
-    monkeypatch.setenv("FLR_GRAM_TERMS", "2")
+    knob("FLR_GRAM_TERMS", "2")
     P = 65536 + 17
     f = K // 5
     X = update_matrix(K, P, f=f, seed=K, device=cuda)[:, :P]

@@ -1,6 +1,6 @@
 """GPU: the LDS-DMA form of the batched GEMM (dsgemm_kernel, 128 x 128 tiles with
 RK / KR operands) is bit-identical to the split-at-stash form (FLR_BGEMM_DMA=0,
-read per launch) — same bf16 products in the same order per accumulator — on the
+an A/B switch; tools build only) — same bf16 products in the same order per accumulator — on the
 encoder shapes, ragged edges (rows, columns and a partial last K-tile), split-K
 and the bias / addend epilogues; and within 2e-6 of fp64."""
 import pytest
@@ -8,7 +8,8 @@ import torch
 
 from flr.nn import bgemm
 
-pytestmark = pytest.mark.gpu
+# the LDS-DMA and pre-split forms measured slower: tools build only (make ABLATION=1)
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("ablation_build")]
 
 
 def _ops(K, M, N, R, ta, tb, seed):
@@ -21,13 +22,13 @@ def _ops(K, M, N, R, ta, tb, seed):
 @pytest.mark.parametrize("K,M,N,R", [(2, 2080, 1152, 384), (3, 130, 200, 260), (2, 257, 132, 1000),
                                      (1, 128, 128, 8192), (4, 512, 1024, 256), (2, 192, 384, 2080)])
 @pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
-def test_bgemm_dma_equals_stash(cuda, monkeypatch, K, M, N, R, ta, tb):
+def test_bgemm_dma_equals_stash(cuda, knob, K, M, N, R, ta, tb):
     A, B = _ops(K, M, N, R, ta, tb, K * 7 + M + N + R)
     A, B = A.to(cuda), B.to(cuda)
-    monkeypatch.setenv("FLR_BGEMM_PRESPLIT", "0")
-    monkeypatch.setenv("FLR_BGEMM_DMA", "0")
+    knob("FLR_BGEMM_PRESPLIT", "0")
+    knob("FLR_BGEMM_DMA", "0")
     C0 = bgemm(A, B)
-    monkeypatch.setenv("FLR_BGEMM_DMA", "1")
+    knob("FLR_BGEMM_DMA", "1")
     C1 = bgemm(A, B)
     torch.cuda.synchronize()
     assert torch.equal(C0, C1), (C0 - C1).abs().max().item()
@@ -36,15 +37,15 @@ def test_bgemm_dma_equals_stash(cuda, monkeypatch, K, M, N, R, ta, tb):
     assert err <= 2e-6 * max(ref.abs().max().item(), 1.0), err
 
 
-def test_bgemm_dma_epilogues_equal_stash(cuda, monkeypatch):
+def test_bgemm_dma_epilogues_equal_stash(cuda, knob):
     A, B = _ops(3, 260, 300, 512, False, False, 11)
     g = torch.Generator().manual_seed(12)
     bias, add = torch.randn(3, 300, generator=g).to(cuda), torch.randn(3, 260, 300, generator=g).to(cuda)
     A, B = A.to(cuda), B.to(cuda)
-    monkeypatch.setenv("FLR_BGEMM_PRESPLIT", "0")
+    knob("FLR_BGEMM_PRESPLIT", "0")
     outs = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("FLR_BGEMM_DMA", flag)
+        knob("FLR_BGEMM_DMA", flag)
         outs.append((bgemm(A, B, bias=bias), bgemm(A, B, add=add)))
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
@@ -53,7 +54,7 @@ def test_bgemm_dma_epilogues_equal_stash(cuda, monkeypatch):
 @pytest.mark.parametrize("K,M,N,R", [(2, 2080, 1152, 384), (3, 130, 200, 260), (2, 257, 132, 1000),
                                      (1, 128, 128, 8192), (4, 512, 1024, 256), (2, 192, 384, 2080)])
 @pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
-def test_bgemm_presplit_equals_stash(cuda, monkeypatch, K, M, N, R, ta, tb):
+def test_bgemm_presplit_equals_stash(cuda, knob, K, M, N, R, ta, tb):
     """The pre-split form (FLR_BGEMM_PRESPLIT=1, opt-in: measured slower; bf16 planes
     split once per GEMM, a six-product bf16 loop staged by LDS-DMA) against the
     default split-at-stash form: bit-identical, incl. ragged edges and split-K; and a
@@ -62,7 +63,7 @@ def test_bgemm_presplit_equals_stash(cuda, monkeypatch, K, M, N, R, ta, tb):
     A, B = A.to(cuda), B.to(cuda)
     outs = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("FLR_BGEMM_PRESPLIT", flag)
+        knob("FLR_BGEMM_PRESPLIT", flag)
         outs.append(bgemm(A, B).clone())
         outs.append(bgemm(A[:, :, ::2][:, :, :R // 2], B[:, :, ::2][:, :, :R // 2]).clone())  # gather mode
     torch.cuda.synchronize()
@@ -70,14 +71,14 @@ def test_bgemm_presplit_equals_stash(cuda, monkeypatch, K, M, N, R, ta, tb):
     assert torch.equal(outs[1], outs[3])
 
 
-def test_bgemm_presplit_epilogues_equal_stash(cuda, monkeypatch):
+def test_bgemm_presplit_epilogues_equal_stash(cuda, knob):
     A, B = _ops(3, 260, 300, 512, False, False, 13)
     g = torch.Generator().manual_seed(14)
     bias, add = torch.randn(3, 300, generator=g).to(cuda), torch.randn(3, 260, 300, generator=g).to(cuda)
     A, B = A.to(cuda), B.to(cuda)
     outs = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("FLR_BGEMM_PRESPLIT", flag)
+        knob("FLR_BGEMM_PRESPLIT", flag)
         outs.append((bgemm(A, B, bias=bias), bgemm(A, B, add=add)))
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

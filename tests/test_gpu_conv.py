@@ -122,40 +122,45 @@ def _run_tap_major(cuda, shape, seed):
 
 @pytest.mark.parametrize("form", ["pipe", "old"])
 @pytest.mark.parametrize("shape", TAP_SHAPES, ids=[str(s) for s in TAP_SHAPES])
-def test_gemm_forms_bit_identical(cuda, shape, form, monkeypatch):
+def test_gemm_forms_bit_identical(cuda, shape, form, knob):
     """Every bf16x6 form (FLR_GEMM: the default split at stash time (bf16 LDS
     images; the weight gradient's transposed images) where the plan supports
     it, "pipe", "old"; the split-at-stash kernels' prefetch depth) feeds each
     accumulator the same products in the same order: bit-identical results."""
+    from flr import _capi
+    if form == "old" and "ablation" not in _capi.build_info():
+        pytest.skip("the unpipelined loop is a tools-build form (make ABLATION=1)")
     ref = _run_tap_major(cuda, shape, 7)
-    if "=" in form:
-        monkeypatch.setenv(*form.split("="))
-    else:
-        monkeypatch.setenv("FLR_GEMM", form)
+    knob("FLR_GEMM", form)
     got = _run_tap_major(cuda, shape, 7)
     for a, b in zip(ref, got):
         assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("dims", [(3, 32, 768, 256), (2, 200, 130, 96), (4, 64, 64, 48)])
-def test_bgemm_forms_bit_identical(cuda, dims, monkeypatch):
+def test_bgemm_forms_bit_identical(cuda, dims, knob):
     from flr.nn import bgemm
     K, M, N, R = dims
     g = torch.Generator(device="cpu").manual_seed(M + N)
     A = torch.randn(K, M, R, generator=g).to(cuda)
     Bm = torch.randn(K, N, R, generator=g).to(cuda)
+    from flr import _capi
     outs = []
-    # default (row-major images), k-contiguous operands on transposed images, the per-wave split
-    for form in (None, "FLR_BGEMM_TIMG=1", "pipe"):
+    # default (row-major images), the per-wave split; the tools build adds
+    # k-contiguous operands on transposed images (measured slower)
+    forms = [None, "pipe"] + (["FLR_BGEMM_TIMG=1"] if "ablation" in _capi.build_info() else [])
+    for form in forms:
         if form and "=" in form:
-            monkeypatch.setenv(*form.split("="))
+            knob("FLR_GEMM", None)
+            knob(*form.split("="))
         elif form:
-            monkeypatch.setenv("FLR_GEMM", form)
-        outs += [bgemm(A, Bm).clone(), bgemm(A.transpose(1, 2).contiguous().transpose(1, 2), Bm).clone(),
-                 bgemm(A, Bm.transpose(1, 2).contiguous().transpose(1, 2)).clone()]
+            knob("FLR_GEMM", form)
+        outs.append([bgemm(A, Bm).clone(), bgemm(A.transpose(1, 2).contiguous().transpose(1, 2), Bm).clone(),
+                     bgemm(A, Bm.transpose(1, 2).contiguous().transpose(1, 2)).clone()])
     torch.cuda.synchronize()
-    for i in range(3):
-        assert torch.equal(outs[i], outs[3 + i]) and torch.equal(outs[i], outs[6 + i]), i
+    for f in range(1, len(outs)):
+        for i in range(3):
+            assert torch.equal(outs[0][i], outs[f][i]), (forms[f], i)
 
 
 NORM_SHAPES = [  # ResNet-18 layers at the C3 shapes (B = 32): split-K wgrad (l1), one tile pass, dead taps (l4)
@@ -208,7 +213,7 @@ def test_wgrad_norm_partials(cuda, shape):
 
 @pytest.mark.parametrize("form", [None, "pipe"])
 @pytest.mark.parametrize("shape", TAP_SHAPES, ids=[str(s) for s in TAP_SHAPES])
-def test_dgrad_addend_bit_identical(cuda, shape, form, monkeypatch):
+def test_dgrad_addend_bit_identical(cuda, shape, form, knob):
     """flr_conv2d_bwd_data_t_add: dx = dgrad + add in the epilogue (linear
     stride-1 stores, the parity-class stores, the split-K reduce, classes with
     no tap) equals flr_conv2d_bwd_data_t followed by one fp32 add — the sum
@@ -216,7 +221,7 @@ def test_dgrad_addend_bit_identical(cuda, shape, form, monkeypatch):
     from flr import _capi
     from flr.nn import _stream, _workspace_t
     if form:
-        monkeypatch.setenv("FLR_GEMM", form)
+        knob("FLR_GEMM", form)
     K, B, Cin, H, W, Cout, KS, stride, pad = shape
     g = torch.Generator(device="cpu").manual_seed(sum(shape) + 3)
     Ho, Wo = (H + 2 * pad - KS) // stride + 1, (W + 2 * pad - KS) // stride + 1
@@ -246,7 +251,7 @@ def test_dgrad_addend_bit_identical(cuda, shape, form, monkeypatch):
 @pytest.mark.parametrize("shape", [(32, 32, 512, 1, 1, 512, 3, 1, 1), (8, 8, 256, 2, 2, 512, 3, 2, 1),
                                    (5, 24, 256, 1, 1, 256, 1, 1, 0), (3, 32, 256, 2, 2, 512, 1, 2, 0)],
                          ids=["l4b", "l4a", "1x1-n24", "l4ds"])
-def test_narrow_tiles_bit_identical(cuda, shape, monkeypatch):
+def test_narrow_tiles_bit_identical(cuda, shape, knob):
     """The l4 convolutions' narrow-N tiles (N = B*Ho*Wo <= 32: four waves stacked
     along M) give the 64 x 64-tile kernels' bits: forward, data gradient (incl.
     the strided classes and the in-place addend) and split-K."""
@@ -264,7 +269,7 @@ def test_narrow_tiles_bit_identical(cuda, shape, monkeypatch):
     wsp = None if ws is None else ws.data_ptr()
     outs = []
     for narrow in ("1", "0"):
-        monkeypatch.setenv("FLR_CONV_NARROW", narrow)
+        knob("FLR_CONV_NARROW", narrow)
         y = torch.full((K * Cout, B, Ho, Wo), float("nan"), device=cuda)
         _capi.call("flr_conv2d_fwd_t", x.data_ptr(), wt.data_ptr(), y.data_ptr(), *geom, wsp, nb, _stream(x))
         dx = torch.full_like(x, float("nan"))
@@ -284,7 +289,7 @@ def test_narrow_tiles_bit_identical(cuda, shape, monkeypatch):
                                    (4, 32, 64, 8, 8, 64, 3, 1, 1), (16, 32, 128, 4, 4, 256, 1, 2, 0),
                                    (16, 32, 512, 1, 1, 512, 3, 1, 1), (16, 32, 256, 2, 2, 512, 3, 2, 1)],
                          ids=["l2b", "l3b", "l3a", "l2a", "l1-k4", "l3ds", "l4b-narrow", "l4a-narrow"])
-def test_fill_tiles_bit_identical(cuda, shape, monkeypatch):
+def test_fill_tiles_bit_identical(cuda, shape, knob):
     """Small client counts (K/G per GPU) run the forward and data-gradient
     launches whose default grid is under one wave of the chip on 64 x 64 tiles
     with the default tile's split-K count (FLR_CONV_FILL): the same bits as
@@ -304,7 +309,7 @@ def test_fill_tiles_bit_identical(cuda, shape, monkeypatch):
     wsp = None if ws is None else ws.data_ptr()
     outs = []
     for fill in ("1", "0"):
-        monkeypatch.setenv("FLR_CONV_FILL", fill)
+        knob("FLR_CONV_FILL", fill)
         y = torch.full((K * Cout, B, Ho, Wo), float("nan"), device=cuda)
         _capi.call("flr_conv2d_fwd_t", x.data_ptr(), wt.data_ptr(), y.data_ptr(), *geom, wsp, nb, _stream(x))
         dx = torch.full_like(x, float("nan"))

@@ -51,9 +51,9 @@ def _rel_offdiag(D, ref):
 
 @pytest.mark.parametrize("terms", ["auto", "2", "3"])
 @pytest.mark.parametrize("path", golden_files("c3krum"), ids=lambda p: p.split("/")[-1])
-def test_c3_krum_fixture_bitexact_selection(cuda, path, terms, monkeypatch):
+def test_c3_krum_fixture_bitexact_selection(cuda, path, terms, knob):
     if terms != "auto":
-        monkeypatch.setenv("FLR_GRAM_TERMS", terms)
+        knob("FLR_GRAM_TERMS", terms)
     fx = load_golden(path)
     K, P, f, mk = (int(fx[k]) for k in ("K", "P", "f", "multi_k"))
     X = update_matrix(K, P, f=f, seed=int(fx["seed"]), device="cpu")[:, :P]

@@ -24,11 +24,14 @@ pytestmark = pytest.mark.gpu
 # c3_b32: batch 32 takes the fused stem BN + ReLU + max-pool kernels (flr_batchnorm_relu_maxpool_fwd / _bwd)
 @pytest.mark.parametrize("spec_name,B,nneg", [("tiny", 4, 1), ("c3", 8, 1), ("c3_b32", 32, 1), ("c3_b40", 40, 0),
                                               ("c3_b128", 128, 0), ("c3_overlap", 8, 1)])
-def test_native_trainer_bit_identical_to_python_trainer(cuda, spec_name, B, nneg, monkeypatch):
+def test_native_trainer_bit_identical_to_python_trainer(cuda, spec_name, B, nneg, knob):
     spec = TINY if spec_name == "tiny" else ModelSpec()
     K, steps = 3, 2
     if spec_name == "c3_overlap":
-        monkeypatch.setenv("FLR_SGD_OVERLAP", "1")
+        from flr import _capi
+        if "ablation" not in _capi.build_info():
+            pytest.skip("the side-stream optimizer is a tools-build form (make ABLATION=1)")
+        knob("FLR_SGD_OVERLAP", "1")
         steps = 3
     cfg = TrainConfig(local_steps=steps)
     glob = initial_global(spec, 42, cuda)

@@ -122,8 +122,10 @@ def _round_worker(rank, world, port, defense, q, exchange="alltoall"):
     from flr.models.multimodal import TINY
     from flr.round import RoundConfig, RoundEngine
     from flr.train import TrainConfig
-    rc = RoundConfig(num_clients=8, batch=4, defense=defense, num_attackers=1, exchange=exchange,
-                     defense_cfg={"trim_ratio": 0.2} if defense == "trimmed_mean" else {})
+    cfg = {"trim_ratio": 0.2} if defense == "trimmed_mean" else {}
+    if defense == "krum_ref":  # the reference-exact distances: pair tiles split over the ranks
+        defense, cfg = "krum", {"pairwise_method": "reference"}
+    rc = RoundConfig(num_clients=8, batch=4, defense=defense, num_attackers=1, exchange=exchange, defense_cfg=cfg)
     eng = RoundEngine(TINY, rc, TrainConfig(local_steps=2), torch.device("cuda:0"), rank, world)
     for _ in range(2):
         g = eng.run_round()
@@ -131,7 +133,7 @@ def _round_worker(rank, world, port, defense, q, exchange="alltoall"):
     sel = None
     if defense == "krum":
         eng.defense.publish()
-        sel = eng.defense.selected_clients
+        sel = (eng.defense.selected_clients, eng.defense.distances.cpu().numpy().tobytes())
     q.put((rank, g.cpu().numpy(), sel))
     if world > 1:
         dist.barrier()
@@ -175,3 +177,27 @@ def test_sharded_round_four_ranks_equals_one(cuda, defense, exchange):
     for r in range(4):
         assert np.array_equal(one[0][1], four[r][1]), r
         assert one[0][2] == four[r][2]
+
+
+@pytest.mark.parametrize("defense,exchange", [("krum", "alltoall"), ("krum", "allgather"), ("median", "alltoall"),
+                                              ("krum_ref", "allgather")])
+def test_sharded_round_eight_ranks_equals_one(cuda, defense, exchange):
+    """World 8, the node's GPU count (one client per rank at K = 8): every
+    rank's global model, Krum selection and distance matrix equal the one-rank
+    round bit for bit, for both exchanges and for the reference-exact distances
+    whose pair tiles split over the ranks (one exact all-reduce of D)."""
+    one = _run(1, defense, exchange)
+    eight = _run(8, defense, exchange)
+    for r in range(8):
+        assert np.array_equal(one[0][1], eight[r][1]), r
+        assert one[0][2] == eight[r][2], r
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_reference_distances_split_over_ranks(cuda, world):
+    """The reference-exact Krum distances with their pair tiles split over 2 / 4
+    ranks (allgather exchange): bit-identical to one rank."""
+    one = _run(1, "krum_ref", "allgather")
+    many = _run(world, "krum_ref", "allgather")
+    for r in range(world):
+        assert np.array_equal(one[0][1], many[r][1]) and one[0][2] == many[r][2], r

@@ -107,7 +107,7 @@ def test_attention_fwd_bwd(cuda, T, H):
 
 
 @pytest.mark.parametrize("T", [65, 96])
-def test_attention_thread_forms_bit_identical(cuda, T, monkeypatch):
+def test_attention_thread_forms_bit_identical(cuda, T, knob):
     """The 256- and 512-thread attention forms (FLR_ATT_THREADS) compute every
     score and output in the same order: bit-identical outputs and gradients."""
     K, B, H, dh = 2, 3, 2, 64
@@ -116,7 +116,7 @@ def test_attention_thread_forms_bit_identical(cuda, T, monkeypatch):
     dctx = torch.randn(K, B, T, H * dh, generator=g).to(cuda)
     outs = []
     for thr in ("256", "512"):
-        monkeypatch.setenv("FLR_ATT_THREADS", thr)
+        knob("FLR_ATT_THREADS", thr)
         q_ = qkv.clone().requires_grad_(True)
         ctx = fnn.client_attention(q_, H)
         (dq,) = torch.autograd.grad(ctx, q_, dctx)

@@ -8,10 +8,7 @@ from flr import _capi
 
 
 def bench(KB, T, H, reps=20, threads=None):
-    if threads:
-        os.environ["FLR_ATT_THREADS"] = str(threads)
-    else:
-        os.environ.pop("FLR_ATT_THREADS", None)
+    _capi.set_knob("FLR_ATT_THREADS", str(threads) if threads else None)
     torch.manual_seed(0)
     D = H * 64
     qkv = torch.randn(KB * T, 3 * D, device="cuda")

@@ -3,6 +3,8 @@
 # then one PMC pass on the default library
 set -o pipefail
 mkdir -p gpurun_out/r5ab
+timeout -k 10 60 ./tools/hip/valu_lat > gpurun_out/r5ab/valu_lat.txt 2>&1 || { echo "valu_lat failed"; cat gpurun_out/r5ab/valu_lat.txt; exit 1; }
+cat gpurun_out/r5ab/valu_lat.txt
 for v in default ref_cs64_ns4 ref_cs32_ns8 ref_cs64_ns6 ref_cs64_ns8; do
   if [ $v = default ]; then L=multimodal-fl-security_amd/lib/libflr.so; else L=abl/$v/libflr.so; fi
   FLR_LIB=$L timeout -k 10 120 python -u tools/ref_bench.py --reps 5 --check 16 > gpurun_out/r5ab/$v.json 2> gpurun_out/r5ab/$v.err || { echo "$v failed"; tail -5 gpurun_out/r5ab/$v.err; exit 1; }
