@@ -17,27 +17,29 @@
 //
 // Round 5 design.  The parallelism is fixed by the reference: K(K-1)/2 pairs x
 // 8 chains, each chain a sequential fma over R steps (65,024 chains of 1.475 M
-// steps at C3) — about one chain per lane of one wave per SIMD.  So the time is
-// R x (instructions per step of one wave) x 4 cycles (a wave alone issues one
-// vector instruction per 4 cycles; two waves per SIMD share the 2-cycle pipe at
-// no loss), and the design minimises the per-step instruction stream:
-//  * one chain per lane: lane j of wave (i, c) runs chain c of pair (i, j);
-//  * the subtraction of two steps is one v_pk_add_f32 (steps are independent;
-//    only the fma accumulation is a chain), the fma is one v_fma_f32 per step:
-//    1.5 vector instructions per step;
-//  * operands arrive 4 steps per instruction: x_j by one ds_read_b128 of the
-//    lane's row, x_i by one uniform-address 16-B load (the same for every lane
-//    of the wave, 8 chunks' worth prefetched in registers).
-// That needs each chain's steps contiguous, so a segment of X is first
-// rewritten chain-major (chain_transpose_kernel, Xc[k][c][s] = X[k][8(r0+s)+c],
-// one read and one write of the segment at HBM rate).  Tiles: 64 J rows (one
-// per lane) x TI I rows (one per wave) x one chain; chain c = the XCD
-// (blockIdx % 8), so an XCD's L2 holds only its own chain's streams and the
-// WGs of one XCD share them.  Per chunk of 32 steps the WG stages its 64 J
-// rows' 128-B chain pieces by LDS-DMA (one global_load_lds_dwordx4 of 8 rows
-// per wave, XOR-swizzled 16-B slots so the ds_read_b128 lane groups hit 64
-// distinct banks) into a ring of 4 stages, one raw barrier per chunk.  Chains
-// longer than the segment carry their partial sums in A between segments.
+// steps at C3): about one chain per lane of one to two waves per SIMD, so
+// every step of a wave must be cheap.
+//  * One chain per lane: each lane runs chain c of one pair (i, j) (tiles below:
+//    diagonal blocks as circulants, so no lane idles on the triangle).
+//  * Chain-major operands: a segment of X is first rewritten chain-major
+//    (chain_transpose_kernel, Xc[k][c][s] = X[k][8(r0+s)+c], one read and one
+//    write of the segment at HBM rate) so each chain's steps are contiguous.
+//  * x_j per lane from LDS: per chunk of CS = 64 steps the workgroup stages its
+//    64 J rows' 256-B chain pieces by LDS-DMA (four global_load_lds_dwordx4 of 4
+//    rows per wave, XOR-swizzled 16-B slots so the ds_read_b128 lane groups hit
+//    64 distinct banks) into a ring of NSTAGE stages; each lane reads its row's
+//    16 pieces with ds_read_b128 ONE CHUNK AHEAD (two register buffers), so the
+//    LDS latency hides under the previous chunk's chain.
+//  * x_i (wave-uniform) by DPP: lane L of each 16-lane row holds 4 steps of the
+//    chunk (one 16-B load per lane per chunk, NSTAGE - 1 chunks ahead); step S
+//    reaches every lane by a row_newbcast of lane S / 4 folded into the
+//    subtraction (v_sub_f32_dpp).  Measured alternatives (tools/hip/valu_lat*.hip,
+//    same-box A/B): x_i through LDS broadcast reads (LDS-bound),
+//    v_readlane into SGPRs, scalar loads into SGPRs (the scalar cache streams
+//    poorly), uniform-address vector loads (TA-bound), v_pk_add_f32 pairs.
+//  * chain c = the XCD (blockIdx % 8): an XCD's L2 holds only its own chain's
+//    streams, and the 8 / 16 workgroups of one J block re-read them from L2.
+// Chains longer than the segment carry their partial sums in A between segments.
 #include <type_traits>
 #include <utility>
 
@@ -50,43 +52,68 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NJ = 64;             // J rows per tile: one per lane
-constexpr int TI = 8;              // I rows per tile: one per wave
-constexpr int THREADS = 64 * TI;   // 512
-#ifndef FLR_REF_CS
-#define FLR_REF_CS 32
-#endif
-#ifndef FLR_REF_XI
-#define FLR_REF_XI 1
-#endif
-#ifndef FLR_REF_NSTAGE
-#define FLR_REF_NSTAGE 4
-#endif
-constexpr int CS = FLR_REF_CS;     // chain steps per staged chunk (4 CS bytes of one chain stream)
-constexpr int NSTAGE = FLR_REF_NSTAGE;  // LDS ring and x_i register sets (NSTAGE - 1 chunks in flight)
-constexpr int STAGE = NJ * CS;     // floats per stage
+constexpr int TI = 4;              // waves per workgroup (one per SIMD)
+constexpr int THREADS = 64 * TI;   // 256
+constexpr int OFF_WG = 64 / TI;    // workgroups of an off-diagonal block pair (one I row per wave)
+constexpr int DIAG_WG = 32 / TI;   // workgroups of a diagonal block (two I rows per wave)
+constexpr int CS = 64;             // chain steps per staged chunk (256 B of one chain stream)
+constexpr int NSTAGE = 4;          // LDS ring = the loop's unroll (static stage offsets: ds_read's 16-bit offset)
+constexpr int STAGE = NJ * CS;     // floats per stage (16 KB)
 constexpr int NQ = CS / 4;         // 16-B pieces per chunk row
-constexpr int XW = CS / 16;        // x_i floats per lane per chunk (16 lanes of a row cover the chunk)
-constexpr int RPD = 256 / CS;      // chunk rows per 1-KB DMA instruction
-constexpr int DPW = 8 / RPD;       // DMA instructions per wave per chunk (wave w stages rows 8w .. 8w+7)
-constexpr int VMC = (NSTAGE - 2) * (DPW + 1);  // the steady state's counted wait (see ref_chain_kernel)
+constexpr int RPD = 256 / CS;      // chunk rows per 1-KB DMA instruction (4)
+constexpr int RPW = NJ / TI;       // J rows each wave stages (16)
+constexpr int DPW = RPW / RPD;     // DMA instructions per wave per chunk (4)
+constexpr int OPB = DPW + 1;       // vector-memory ops per body: the DMAs, then the x_i load
 constexpr int64_t XC_CAP = int64_t(8) << 30;  // bytes of one chain-major segment
-static_assert(CS == 32 || CS == 64, "chunk of 32 or 64 steps");
-static_assert(NSTAGE >= 3 && VMC < 64, "vmcnt counts to 63");
-typedef typename std::conditional<XW == 4, f32x4, f32x2>::type xvec;
+static_assert(CS == 64 && NQ == 16, "x_i layout: 16 lanes x 4 steps per chunk");
+static_assert((NSTAGE - 2) * OPB + 1 < 64, "vmcnt counts to 63");
+static_assert((NSTAGE - 1) * STAGE * 4 < 65536, "ds_read_b128's 16-bit offset reaches every stage");
 
 // the XOR swizzle of a row's 16-B slots: the ds_read_b128 lane groups
-// ({0-3,12-15,20-27}, {4-11,16-19,28-31} and +32) then hit 64 distinct banks
-__host__ __device__ constexpr int slot_swz(int row) { return CS == 32 ? ((row >> 1) & 7) : (row & 15); }
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31} and +32) hit 64 distinct banks
+__host__ __device__ constexpr int slot_swz(int row) { return row & 15; }
 
-// rows i that pair with some j > i of J block jb (j < K): i < jmax(jb)
-__host__ __device__ inline int igroups(int jb, int K) {
-  const int jmax = (NJ * jb + NJ - 1 < K - 1) ? NJ * jb + NJ - 1 : K - 1;
-  return jmax <= 0 ? 0 : (jmax + TI - 1) / TI;
+// Tiles (per chain).  The K rows form blocks of 64; block pair (bi, bj), bi <= bj:
+//  * bi < bj: 64 x 64 pairs, OFF_WG workgroups; wave -> one I row of block bi,
+//    lane -> one J row of block bj;
+//  * bi == bj: the block's 64 * 63 / 2 pairs as a circulant: I row a takes
+//    J rows a + 1 .. a + 32 (mod 64), the antipodal pair (a, a + 32) once (from
+//    a < 32); DIAG_WG workgroups, a wave holds rows (w, w + 32) of the block in
+//    its lane halves (every DPP row_newbcast stays inside one 16-lane row, so a
+//    half-wave's operand is uniform to it) — every lane a distinct pair, none
+//    idle (the triangle of a plain diagonal tile wasted a third of the lanes).
+// Tiles are numbered bj-major: bj's tiles start at (32 / TI) * bj^2; within bj
+// the off-diagonal pairs bi = 0 .. bj-1, then the diagonal block.
+__host__ __device__ inline int tiles_before(int bj) { return DIAG_WG * bj * bj; }
+__host__ __device__ inline int ntiles_of(int K) { return tiles_before((K + NJ - 1) / NJ); }
+struct Tile {
+  int bi, bj, g;
+  bool diag;
+};
+__host__ __device__ inline Tile tile_of(int t) {
+  int bj = 0;
+  while (tiles_before(bj + 1) <= t) ++bj;  // at most ~K / 64 steps
+  const int local = t - tiles_before(bj);
+  Tile r;
+  r.bj = bj;
+  if (local < bj * OFF_WG) {
+    r.bi = local / OFF_WG;
+    r.g = local % OFF_WG;
+    r.diag = false;
+  } else {
+    r.bi = bj;
+    r.g = local - bj * OFF_WG;
+    r.diag = true;
+  }
+  return r;
 }
-__host__ __device__ inline int tiles_before(int jb, int K) {
-  int n = 0;
-  for (int b = 0; b < jb; ++b) n += igroups(b, K);
-  return n;
+// the tile that computes pair (i, j), i < j
+__host__ __device__ inline int tile_of_pair(int i, int j) {
+  const int bi = i / NJ, bj = j / NJ;
+  if (bi < bj) return tiles_before(bj) + bi * OFF_WG + (i % NJ) / TI;
+  const int a = i % NJ, b = j % NJ, o = b - a;  // 1 .. 63
+  const int ii = o <= 32 ? a : b;               // the row whose circulant half holds the pair
+  return tiles_before(bj) + bj * OFF_WG + (ii & 31) / TI;
 }
 
 // Xc[k][c][s] = X[k][8 (r0 + s) + c] for s < steps; stream stride ldc (x 8 per row).
@@ -134,21 +161,17 @@ __global__ __launch_bounds__(256) void chain_transpose_kernel(const float* __res
   }
 }
 
-// x_i broadcast: lane L of every 16-lane row holds steps XW (L & 15) ..
-// XW (L & 15) + XW - 1 of the chunk (one 4 XW-byte load per lane, the four
-// rows alike); step S reaches every lane by a DPP row_newbcast of lane S / XW,
-// which the compiler folds into the subtraction (v_sub_f32_dpp: fl(x_i - x_j),
-// the reference's operand order), so the wave-uniform operand costs no extra
-// instruction, no LDS cycle and one TA request per chunk.
+// step S of the chunk for every lane: lane S / 4 of each 16-lane row holds it
+// (component S % 4); DPP row_newbcast, folded into the subtraction
 template <int S>
-__device__ __forceinline__ float bcast(xvec xv) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xv[S % XW]), 0x150 + S / XW, 0xf, 0xf, false));
+__device__ __forceinline__ float bcast(f32x4 xv) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xv[S & 3]), 0x150 + (S >> 2), 0xf, 0xf, false));
 }
 // the differences first (independent registers: one temporary reused for
 // every step made the hazard recognizer put an s_nop before each DPP write),
 // then the fma chain in step order
 template <int... S>
-__device__ __forceinline__ float chain_chunk(xvec xv, const f32x4 (&v)[NQ], float acc,
+__device__ __forceinline__ float chain_chunk(f32x4 xv, const f32x4 (&v)[NQ], float acc,
                                              std::integer_sequence<int, S...>) {
   float d[sizeof...(S)];
   ((d[S] = bcast<S>(xv) - v[S >> 2][S & 3]), ...);
@@ -156,9 +179,22 @@ __device__ __forceinline__ float chain_chunk(xvec xv, const f32x4 (&v)[NQ], floa
   return acc;
 }
 
-// One segment of steps for the tiles [t0, t0 + gridDim.x / 8): chain c of the
-// pairs (i, j), i = TI * ig + wave, j = NJ * jb + lane, i < j < K; the running
-// chain sums in A[c][i][j] (first: start from 0).
+// One segment of steps for the tiles [t0, t0 + gridDim.x / 8) (tile_of): chain
+// c of each lane's pair; the running chain sums in A[c][min(i,j)][max(i,j)]
+// (first: start from 0).
+//
+// Body ch (stage u = ch % NSTAGE, static in the unrolled loop):
+//   wait  this wave's DMA(ch + 1) and x_i(ch) landed (counted vmcnt), this
+//         wave's ds_reads of chunk ch landed (lgkmcnt(0)), then one barrier:
+//         every wave's DMA(ch + 1) is in LDS and every wave finished reading
+//         stage (ch - 1) % NSTAGE
+//   issue DMA(ch + NSTAGE - 1) into that stage and x_i(ch + NSTAGE - 1);
+//         ds_read_b128 x 16 of chunk ch + 1 into the other register buffer
+//   chain chunk ch (registers read in body ch - 1)
+// Every body issues the same vector-memory ops (clamped to the last chunk), so
+// the counts are static; the LDS reads and the register loads are inline asm
+// with explicit waits (the compiler's waitcnt pass, merging across the
+// rotated registers, drained vmcnt(0) every chunk).
 __global__ __launch_bounds__(THREADS) void ref_chain_kernel(const float* __restrict__ Xc, int64_t ldc, int K,
                                                             int64_t steps, int t0, int first,
                                                             float* __restrict__ A) {
@@ -166,266 +202,128 @@ __global__ __launch_bounds__(THREADS) void ref_chain_kernel(const float* __restr
   // before the LDS reads, draining the DMA ring)
   __shared__ __attribute__((aligned(16))) float lds[NSTAGE * STAGE];
   const int c = (int)(blockIdx.x & 7);
-  const int tile = t0 + (int)(blockIdx.x >> 3);
-  int jb = 0, base = 0;
-  for (;; ++jb) {
-    const int n = igroups(jb, K);
-    if (tile < base + n) break;
-    base += n;
+  const Tile T = tile_of(t0 + (int)(blockIdx.x >> 3));
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // this lane's pair (i, j): rows of blocks bi / bj; jj = J row within the staged block
+  int ii, jj;
+  bool keep = true;
+  if (T.diag) {
+    const int w = TI * T.g + wave;  // 0 .. 31
+    ii = lane < 32 ? w : w + 32;
+    const int o = (lane & 31) + 1;  // 1 .. 32
+    jj = (ii + o) & 63;
+    keep = o < 32 || ii < 32;  // the antipodal pair once
+  } else {
+    ii = TI * T.g + wave;
+    jj = lane;
   }
-  const int ig = tile - base;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int i = TI * ig + wave;  // uniform
-  const int j = NJ * jb + lane;
-  const int jmax = (NJ * jb + NJ - 1 < K - 1) ? NJ * jb + NJ - 1 : K - 1;
-  const bool active = i < jmax;  // uniform: some lane of this wave holds a pair
-  const bool valid = i < j && j < K;
+  const int i = NJ * T.bi + ii, j = NJ * T.bj + jj;
+  const bool valid = keep && i < K && j < K;
+  const int lo = i < j ? i : j, hi = i < j ? j : i;  // A holds the pair at [lo][hi]
+  const int jb = T.bj;
+  // uniform per wave: some lane holds a pair (off-diagonal: the I row exists)
+  const bool active = T.diag ? NJ * T.bi + TI * T.g + wave < K : i < K;
   const int64_t rs = 8 * ldc;
 
-  // staging: wave w moves J rows 8w .. 8w+7 of the block, RPD rows per DMA
-  // instruction; lane -> row 8w + RPD u + lane / NQ, LDS slot lane % NQ holding
-  // the chunk's piece slot ^ slot_swz(row)
+  // the running sum of the previous segments: an asm load and a full wait
+  // before any DMA, so no compiler-tracked load reaches into the loop
+  float acc = 0.f;
+  if (!first) {
+    const float* ap = A + ((int64_t)c * K + (lo < K ? lo : K - 1)) * K + (hi < K ? hi : K - 1);
+    asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(acc) : "v"(ap) : "memory");
+    acc = valid ? acc : 0.f;
+  }
+
+  // staging: wave w moves J rows RPW w .. RPW w + RPW - 1, RPD rows per DMA
+  // instruction; lane -> row RPW w + RPD u + lane / NQ, LDS slot lane % NQ
+  // holding the chunk's piece slot ^ slot_swz(row)
   const float* ssrc[DPW];
 #pragma unroll
   for (int u = 0; u < DPW; ++u) {
-    const int srow = 8 * wave + RPD * u + lane / NQ;
+    const int srow = RPW * wave + RPD * u + lane / NQ;
     int gj = NJ * jb + srow;
     gj = gj < K ? gj : K - 1;
     ssrc[u] = Xc + (int64_t)gj * rs + (int64_t)c * ldc + 4 * ((lane % NQ) ^ slot_swz(srow));
   }
-  float* sdst = lds + 8 * wave * CS;
-  // DMA of chunk ch's pieces into the stage of (virtual) chunk slot
-  auto stage = [&](int64_t ch, int64_t slot) {
+  float* sdst = lds + RPW * wave * CS;
+  // x_i: lane L of each 16-lane row loads steps 4 (L & 15) .. of its half-wave's I row
+  const float* xl = Xc + (int64_t)(i < K ? i : K - 1) * rs + (int64_t)c * ldc + 4 * (lane & 15);
+  const int nch = (int)((steps + CS - 1) / CS), nfull = (int)(steps / CS), lastc = nch - 1;
+  auto clampc = [&](int ch) { return ch < lastc ? ch : lastc; };
+  // DMA(ch) into stage `slot`, then x_i(ch) into register set x
+  auto issue = [&](int ch, int slot, f32x4& x) {
+    const int cl = clampc(ch);
 #pragma unroll
     for (int u = 0; u < DPW; ++u)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc[u] + ch * CS),
-                                       (__attribute__((address_space(3))) void*)(sdst + (int)(slot % NSTAGE) * STAGE +
-                                                                                 256 * u),
-                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc[u] + (int64_t)cl * CS),
+                                       (__attribute__((address_space(3))) void*)(sdst + slot * STAGE + 256 * u), 16,
+                                       0, 0);
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(xl + (int64_t)cl * CS) : "memory");
   };
-  const int gi = active ? i : 0;
-  const float* xi = Xc + (int64_t)gi * rs + (int64_t)c * ldc;
-  const float* xl = xi + XW * (lane & 15);
-  // x_i of chunk ch (see bcast), issued by asm so the compiler's waitcnt pass
-  // leaves it to the body's counted wait (its conservative merge across the
-  // rotated registers drained vmcnt(0) every chunk)
-  auto xload = [&](int64_t ch, xvec& x) {
-    if constexpr (XW == 4)
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(xl + ch * CS));
-    else
-      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x) : "v"(xl + ch * CS));
-  };
-  const int rsw = slot_swz(lane);
-  const float* rrow = lds + lane * CS;
-
-  float acc = 0.f;
-  if (!first && valid) acc = A[((int64_t)c * K + i) * K + j];
-  const int64_t nch = (steps + CS - 1) / CS, nfull = steps / CS;
-
-  // Every body issues the same vector-memory ops in the same order — the DPW
-  // DMAs of chunk ch + NSTAGE - 1, then its x_i load, both clamped to the last
-  // chunk — so at the top of body ch exactly VMC = (NSTAGE - 2) (DPW + 1) ops
-  // are younger than chunk ch's: one counted wait covers this wave's DMA and
-  // x_i of chunk ch, and NSTAGE - 1 chunks of compute hide their latency.
-  auto issue = [&](int64_t ch, xvec& xn) {
-    const int64_t cl = ch < nch ? ch : nch - 1;
-    stage(cl, ch);
-    xload(cl, xn);
-  };
-  auto body = [&](int64_t ch, xvec& xc, xvec& xn) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
-    // every wave's DMA of chunk ch landed and every wave finished chunk ch-1,
-    // whose stage (and x_i register) is refilled below: raw barrier, no vmcnt(0) drain
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    issue(ch + NSTAGE - 1, xn);
-    if (active && ch < nfull) {
-      const float* rd = rrow + (int)(ch % NSTAGE) * STAGE;
-      f32x4 v[NQ];
+  // per-lane LDS byte addresses of row jj's 16 swizzled pieces in stage 0
+  const int rsw = slot_swz(jj);
+  uint32_t ra[NQ];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) v[q] = *reinterpret_cast<const f32x4*>(rd + 4 * (q ^ rsw));
-      // (xc came from an asm load: keep the compiler from reading it before the wait above)
-      asm volatile("" : "+v"(xc));
-      acc = chain_chunk(xc, v, acc, std::make_integer_sequence<int, CS>{});
-    }
-  };
-
-  // the registers rotate with the chunk: xs[ch % NSTAGE] holds chunk ch's x_i;
-  // body ch refills xs[(ch - 1) % NSTAGE], the one body ch-1 consumed
-  xvec xs[NSTAGE];
+  for (int q = 0; q < NQ; ++q) ra[q] = (uint32_t)(uintptr_t)(lds + jj * CS + 4 * (q ^ rsw));
+  auto rows = [](auto st, f32x4(&v)[NQ], const uint32_t(&a)[NQ]) {
 #pragma unroll
-  for (int u = 0; u < NSTAGE - 1; ++u) issue(u, xs[u]);
-  const int64_t nloop = (nfull + NSTAGE - 1) / NSTAGE * NSTAGE;  // whole unrolled groups: the last bodies wait, barrier, skip the compute
-  for (int64_t ch = 0; ch < nloop; ch += NSTAGE) {
-#pragma unroll
-    for (int u = 0; u < NSTAGE; ++u) body(ch + u, xs[u], xs[(u + NSTAGE - 1) % NSTAGE]);
-  }
-  if (nfull < nch) {
-    // the last, partial chunk (< CS steps): staged as chunk nfull (the loop's
-    // clamped DMAs rewrote its stage with the same bytes), x_i from global
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (active) {
-      const float* rd = rrow + (int)(nfull % NSTAGE) * STAGE;
-      for (int s = 0; s < (int)(steps - nfull * CS); ++s) {
-        const float d = xi[nfull * CS + s] - rd[4 * ((s >> 2) ^ rsw) + (s & 3)];
-        acc = __builtin_fmaf(d, d, acc);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (valid) A[((int64_t)c * K + i) * K + j] = acc;
-}
-
-// ---- x_i from scalar registers (FLR_REF_XI=1) ---------------------------------
-// The wave-uniform operand x_i reaches the VALU as a scalar operand: one
-// s_load_dwordx16 moves 16 steps of row i's chain c into SGPRs, and one
-// v_pk_add_f32 subtracts two steps (x_j from VGPRs, x_i from an SGPR pair; a
-// VOP3P instruction may read one SGPR pair), so a step costs 1.5 plain VALU
-// instructions — no DPP (which measured ~4x the issue cost of a plain VALU op on
-// gfx950, tools/hip/valu_lat.hip), no LDS cycle, no TA request.  Every LDS / SMEM
-// access of the chunk loop is inline asm with explicit waits: the chunk ch+1
-// operands (8 ds_read_b128 of x_j, 2 s_load_dwordx16 of x_i) are issued in body
-// ch and waited at the top of body ch+1 by one lgkmcnt(0) (SMEM returns out of
-// order, so only a full wait is exact), so their latency hides under chunk ch's
-// chain.  NSTAGE_S LDS stages: DMA(ch + NSTAGE_S - 1) issued in body ch, DMA(ch+1)
-// waited at the top of body ch (vmcnt counts the DMAs only).
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-constexpr int NSTAGE_S = 6;          // LDS stages = the loop's unroll (static stage offsets)
-constexpr int CS_S = 32;
-constexpr int STAGE_S = NJ * CS_S;
-constexpr int VMC_S = NSTAGE_S - 3;  // DMAs younger than DMA(ch+1) at the top of body ch (one per body per wave)
-
-__device__ __forceinline__ f32x2 pk_sub_s(f32x2 v, f32x2 x) {
-  f32x2 r;
-  asm volatile("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(v), "s"(x));
-  return r;
-}
-template <int... S>
-__device__ __forceinline__ float chain_chunk_s(const f32x16& xa, const f32x16& xb, const f32x4 (&v)[8], float acc,
-                                               std::integer_sequence<int, S...>) {
-  // S = 0 .. 15: the step pair (2S, 2S + 1)
-  f32x2 d[16];
-  ((d[S] = pk_sub_s(__builtin_shufflevector(v[S >> 1], v[S >> 1], 2 * (S & 1), 2 * (S & 1) + 1),
-                    S < 8 ? __builtin_shufflevector(xa, xa, (2 * S) & 15, (2 * S + 1) & 15)
-                          : __builtin_shufflevector(xb, xb, (2 * S) & 15, (2 * S + 1) & 15))),
-   ...);
-  ((acc = __builtin_fmaf(d[S][1], d[S][1], __builtin_fmaf(d[S][0], d[S][0], acc))), ...);
-  return acc;
-}
-
-__global__ __launch_bounds__(THREADS) void ref_chain_s_kernel(const float* __restrict__ Xc, int64_t ldc, int K,
-                                                              int64_t steps, int t0, int first,
-                                                              float* __restrict__ A) {
-  __shared__ __attribute__((aligned(16))) float lds[NSTAGE_S * STAGE_S];
-  const int c = (int)(blockIdx.x & 7);
-  const int tile = t0 + (int)(blockIdx.x >> 3);
-  int jb = 0, base = 0;
-  for (;; ++jb) {
-    const int n = igroups(jb, K);
-    if (tile < base + n) break;
-    base += n;
-  }
-  const int ig = tile - base;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int i = TI * ig + wave;  // uniform
-  const int j = NJ * jb + lane;
-  const int jmax = (NJ * jb + NJ - 1 < K - 1) ? NJ * jb + NJ - 1 : K - 1;
-  const bool active = i < jmax;
-  const bool valid = i < j && j < K;
-  const int64_t rs = 8 * ldc;
-  // the running sum of the previous segments (asm load + full wait: nothing of
-  // the compiler's own vmcnt bookkeeping reaches into the DMA loop)
-  float acc = 0.f;
-  if (!first) {
-    const float* ap = A + ((int64_t)c * K + (i < K ? i : K - 1)) * K + (j < K ? j : K - 1);
-    asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(acc) : "v"(ap) : "memory");
-    acc = valid ? acc : 0.f;
-  }
-  // staging as ref_chain_kernel at CS = 32: wave w, lane -> row 8w + (lane >> 3), slot lane & 7
-  const int srow = 8 * wave + (lane >> 3);
-  int gj = NJ * jb + srow;
-  gj = gj < K ? gj : K - 1;
-  const float* ssrc = Xc + (int64_t)gj * rs + (int64_t)c * ldc + 4 * ((lane & 7) ^ ((srow >> 1) & 7));
-  float* sdst = lds + 8 * wave * CS_S;
-  auto stage = [&](int ch, int slot) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc + (int64_t)ch * CS_S),
-                                     (__attribute__((address_space(3))) void*)(sdst + slot * STAGE_S), 16, 0, 0);
-  };
-  const float* xi = Xc + (int64_t)(active ? i : 0) * rs + (int64_t)c * ldc;  // uniform
-  // buffer resource over row i's chain-c stream (raw, 4 * ldc bytes; dword
-  // format): the x_i scalar loads then take a 32-bit offset, one SGPR
-  const uint64_t xb64 = (uint64_t)(uintptr_t)xi;
-  const i32x4 xrsrc = {(int)(uint32_t)xb64, (int)(uint32_t)(xb64 >> 32) & 0xffff, (int)(4 * ldc), 0x00020000};
-  const int rsw = (lane >> 1) & 7;
-  // per-lane LDS byte addresses of the 8 swizzled 16-B pieces of this lane's row in stage 0
-  uint32_t ra[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) ra[q] = (uint32_t)(uintptr_t)(lds + lane * CS_S + 4 * (q ^ rsw));
-  // chunk ch's operands (stage `st` static): x_j 8 x 16 B from LDS, x_i 32 steps into SGPRs
-  auto fetch = [&ra](auto st, int ch, f32x4(&v)[8], f32x16& xa, f32x16& xb, i32x4 rsrc) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[q]) : "v"(ra[q]), "n"(decltype(st)::value * STAGE_S * 4)
+    for (int q = 0; q < NQ; ++q)
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[q]) : "v"(a[q]), "n"(decltype(st)::value * STAGE * 4)
                    : "memory");
-    const int off = ch * CS_S * 4;  // byte offset into row i's chain-c stream
-    asm volatile("s_buffer_load_dwordx16 %0, %1, %2" : "=s"(xa) : "s"(rsrc), "s"(off) : "memory");
-    asm volatile("s_buffer_load_dwordx16 %0, %1, %2 offset:0x40" : "=s"(xb) : "s"(rsrc), "s"(off) : "memory");
   };
-  // chunk indices in 32 bits (steps < 2^31 * 32 per segment): scalar min, no 64-bit compares
-  const int nch = (int)((steps + CS_S - 1) / CS_S), nfull = (int)(steps / CS_S), lastc = nch - 1;
-  auto clampc = [&](int ch) { return ch < lastc ? ch : lastc; };
-  f32x4 va[8], vb[8];
-  f32x16 xa0, xa1, xb0, xb1;
-  // body ch (stage ch % 6 = U): chunk ch's operands arrived (fetched in body
-  // ch - 1); DMA(ch + 5) into stage (U + 5) % 6 = the stage of chunk ch - 1, whose
-  // reads every wave finished before this barrier; fetch chunk ch + 1
-  auto body = [&](auto U, int ch, f32x4(&vc)[8], f32x16& xc0, f32x16& xc1, f32x4(&vn)[8], f32x16& xn0,
-                  f32x16& xn1) {
+
+  f32x4 va[NQ], vb[NQ];
+  f32x4 xs[NSTAGE];
+  auto body = [&](auto U, int ch, f32x4(&vc)[NQ], f32x4(&vn)[NQ]) {
     constexpr int u = decltype(U)::value;
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC_S) : "memory");  // this wave's DMA(ch + 1) landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");             // chunk ch's x_j and x_i in registers
-    __builtin_amdgcn_s_barrier();  // every wave's DMA(ch + 1) landed; every wave read stage ch - 1
+    // DMA(ch + 1) was issued in body ch + 2 - NSTAGE; younger than it: its
+    // x_i load and the NSTAGE - 3 bodies since (x_i(ch) is older: covered)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 3) * OPB + 1) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                              // chunk ch's x_j
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    stage(clampc(ch + NSTAGE_S - 1), (u + NSTAGE_S - 1) % NSTAGE_S);
-    fetch(std::integral_constant<int, (u + 1) % NSTAGE_S>{}, clampc(ch + 1), vn, xn0, xn1, xrsrc);
-    if (active && ch < nfull) acc = chain_chunk_s(xc0, xc1, vc, acc, std::make_integer_sequence<int, 16>{});
+    issue(ch + NSTAGE - 1, (u + NSTAGE - 1) % NSTAGE, xs[(u + NSTAGE - 1) % NSTAGE]);
+    rows(std::integral_constant<int, (u + 1) % NSTAGE>{}, vn, ra);
+    if (active && ch < nfull) {
+      // chunk ch's operands arrived before the waits above: tie them to here
+      asm volatile("" : "+v"(vc[0]), "+v"(vc[1]), "+v"(vc[2]), "+v"(vc[3]), "+v"(vc[4]), "+v"(vc[5]), "+v"(vc[6]),
+                   "+v"(vc[7]), "+v"(vc[8]), "+v"(vc[9]), "+v"(vc[10]), "+v"(vc[11]), "+v"(vc[12]), "+v"(vc[13]),
+                   "+v"(vc[14]), "+v"(vc[15]), "+v"(xs[u]));
+      acc = chain_chunk(xs[u], vc, acc, std::make_integer_sequence<int, CS>{});
+    }
   };
-  // prologue: DMA chunks 0 .. 4, wait for DMA(0), chunk 0's operands
+  // prologue = the issues of bodies -(NSTAGE-1) .. -1, then chunk 0's rows
 #pragma unroll
-  for (int u = 0; u < NSTAGE_S - 1; ++u) stage(clampc(u), u);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTAGE_S - 2) : "memory");
+  for (int u = 0; u < NSTAGE - 1; ++u) issue(u, u, xs[u]);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * OPB + 1) : "memory");  // DMA(0): x_i(0) + NSTAGE - 2 issues younger
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  fetch(std::integral_constant<int, 0>{}, 0, va, xa0, xa1, xrsrc);
-  const int nloop = (nfull + NSTAGE_S - 1) / NSTAGE_S * NSTAGE_S;
-  for (int ch = 0; ch < nloop; ch += NSTAGE_S) {
-    body(std::integral_constant<int, 0>{}, ch, va, xa0, xa1, vb, xb0, xb1);
-    body(std::integral_constant<int, 1>{}, ch + 1, vb, xb0, xb1, va, xa0, xa1);
-    body(std::integral_constant<int, 2>{}, ch + 2, va, xa0, xa1, vb, xb0, xb1);
-    body(std::integral_constant<int, 3>{}, ch + 3, vb, xb0, xb1, va, xa0, xa1);
-    body(std::integral_constant<int, 4>{}, ch + 4, va, xa0, xa1, vb, xb0, xb1);
-    body(std::integral_constant<int, 5>{}, ch + 5, vb, xb0, xb1, va, xa0, xa1);
+  rows(std::integral_constant<int, 0>{}, va, ra);
+  const int nloop = (nfull + NSTAGE - 1) / NSTAGE * NSTAGE;
+  static_assert(NSTAGE == 4, "the unrolled loop below");
+  for (int ch = 0; ch < nloop; ch += NSTAGE) {
+    body(std::integral_constant<int, 0>{}, ch, va, vb);
+    body(std::integral_constant<int, 1>{}, ch + 1, vb, va);
+    body(std::integral_constant<int, 2>{}, ch + 2, va, vb);
+    body(std::integral_constant<int, 3>{}, ch + 3, vb, va);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (nfull < nch) {
-    // the last, partial chunk: staged as chunk nfull in stage nfull % 6 (the
-    // clamped DMAs after it rewrote that stage with the same bytes)
+    // the last, partial chunk: staged as chunk nfull in stage nfull % NSTAGE
+    // (the clamped DMAs after it rewrote that stage with the same bytes)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (active) {
-      const float* rd = lds + lane * CS_S + (nfull % NSTAGE_S) * STAGE_S;
-      for (int s2 = 0; s2 < (int)(steps - (int64_t)nfull * CS_S); ++s2) {
-        const float d = xi[(int64_t)nfull * CS_S + s2] - rd[4 * ((s2 >> 2) ^ rsw) + (s2 & 3)];
+      const float* rd = lds + jj * CS + (nfull % NSTAGE) * STAGE;
+      const float* xi = Xc + (int64_t)(i < K ? i : K - 1) * rs + (int64_t)c * ldc + (int64_t)nfull * CS;
+      for (int s2 = 0; s2 < (int)(steps - (int64_t)nfull * CS); ++s2) {
+        const float d = xi[s2] - rd[4 * ((s2 >> 2) ^ rsw) + (s2 & 3)];
         acc = __builtin_fmaf(d, d, acc);
       }
     }
   }
-  if (valid) A[((int64_t)c * K + i) * K + j] = acc;
+  if (valid) A[((int64_t)c * K + lo) * K + hi] = acc;
 }
 
 // D[i][j] = D[j][i] for the pairs of tiles [t0, t1): chains summed 0..7 in
@@ -441,7 +339,7 @@ __global__ void ref_finish_kernel(const float* __restrict__ A, const float* __re
     return;
   }
   if (i > j) return;
-  const int tile = tiles_before(j / NJ, K) + i / TI;
+  const int tile = tile_of_pair(i, j);
   double v = 0.0;
   if (tile >= t0 && tile < t1) {
     float s = 0.f;
@@ -492,7 +390,7 @@ extern "C" size_t flr_pairwise_l2_reference_workspace(int64_t K, int64_t P) {
 
 extern "C" int flr_pairwise_l2_reference_tiles(int64_t K) {
   if (K < 2 || K > (1 << 15)) return 0;
-  return tiles_before(cdiv((int)K, NJ), (int)K);
+  return ntiles_of((int)K);
 }
 
 extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx, double* D, void* ws,
@@ -506,7 +404,7 @@ extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, i
   const int64_t R = P / 8;
   const size_t na = a_bytes(K);
   if (K > 1 && R > 0 && (!ws || (reinterpret_cast<uintptr_t>(ws) & 255) != 0)) return FLR_ERR_WORKSPACE;
-  const int ntiles = K > 1 ? tiles_before(cdiv((int)K, NJ), (int)K) : 0;
+  const int ntiles = K > 1 ? ntiles_of((int)K) : 0;
   const int t0 = (int)(part * ntiles / nparts), t1 = (int)((part + 1) * ntiles / nparts);
   float* A = reinterpret_cast<float*>(ws);
   if (K > 1 && R > 0 && t1 > t0) {
@@ -524,13 +422,8 @@ extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, i
                          st, X, ldx, r0, steps, ldc, Xc);
       int rc = launch_status("chain_transpose_kernel");
       if (rc != FLR_OK) return rc;
-#if FLR_REF_XI == 1
-      hipLaunchKernelGGL(ref_chain_s_kernel, dim3(8 * (t1 - t0)), dim3(THREADS), 0, st, Xc, ldc, (int)K, steps, t0,
-                         seg == 0 ? 1 : 0, A);
-#else
       hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(THREADS), 0, st, Xc, ldc, (int)K, steps, t0,
                          seg == 0 ? 1 : 0, A);
-#endif
       rc = launch_status("ref_chain_kernel");
       if (rc != FLR_OK) return rc;
     }

@@ -40,26 +40,42 @@ def _mask_dropouts(model: nn.Module) -> List[_MaskDropout]:
 
 def local_update(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, lr: float = 0.01,
                  momentum: float = 0.9, weight_decay: float = 0.0, max_norm: float = 1.0,
-                 masks: Optional[Sequence[torch.Tensor]] = None, threads: Optional[int] = None
-                 ) -> Tuple[List[torch.Tensor], float]:
-    """One client's local update.  Returns (params after training, mean loss)."""
+                 masks: Optional[Sequence[torch.Tensor]] = None, threads: Optional[int] = None,
+                 dtype: torch.dtype = torch.float32, start_params: Optional[torch.Tensor] = None,
+                 start_momentum: Optional[Sequence[torch.Tensor]] = None, return_momentum: bool = False):
+    """One client's local update.  Returns (params after training, mean loss).
+    dtype=torch.float64 runs the same loop in double precision: not the
+    reference (which trains in fp32), but the yardstick of how far the
+    reference's own fp32 result is from exact (tests/parity.py
+    check_conditioned).  start_params / start_momentum: continue a local
+    update from another trainer's state (flat parameters, per-parameter
+    momentum buffers) instead of the global model — one step of the reference
+    from the GPU's own state; return_momentum: also return the buffers."""
     if threads:
         torch.set_num_threads(threads)
-    model = model_cls(spec)
+    model = model_cls(spec).to(dtype)
     off = 0
     with torch.no_grad():
         for p in model.parameters():  # load_state_dict(global) for parameters() (:203)
             n = p.numel()
-            p.copy_(global_flat[off:off + n].view(p.shape))
+            src = global_flat if start_params is None else start_params
+            p.copy_(src[off:off + n].view(p.shape).to(dtype))
             off += n
     drops = _mask_dropouts(model)
     optimizer = torch.optim.SGD(model.parameters(), lr=lr, momentum=momentum, weight_decay=weight_decay)  # :206-211
+    if start_momentum is not None:
+        for p, buf in zip(model.parameters(), start_momentum):
+            optimizer.state[p]["momentum_buffer"] = buf.detach().clone().to(dtype)
     criterion = nn.CrossEntropyLoss()
     model.train()
     losses = []
     for s, (images, tokens, labels) in enumerate(batches):
         for d in drops:
             d.mask = None if masks is None else masks[s]
+        if dtype != torch.float32:
+            images = images.to(dtype)
+            for d in drops:
+                d.mask = None if d.mask is None else d.mask.to(dtype)
         optimizer.zero_grad()
         outputs = model(images, tokens)
         loss = criterion(outputs, labels)
@@ -68,6 +84,9 @@ def local_update(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, 
         optimizer.step()
         losses.append(loss.item())
     update = [p.data.clone() for p in model.parameters()]  # :238
+    if return_momentum:
+        return update, sum(losses) / len(losses), [optimizer.state[p]["momentum_buffer"].clone()
+                                                   for p in model.parameters()]
     return update, sum(losses) / len(losses)
 
 

@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from oracle import training as otrain
-from parity import check_delta, delta_report, record
+from parity import check_conditioned, check_delta, conditioned_report, delta_report, record
 from flr import native_trainer as nt
 from flr.models.multimodal import TINY, ModelSpec, MultimodalNet, param_layout
 from flr.round import initial_global
@@ -62,14 +62,20 @@ def test_native_trainer_matches_reference_loop(cuda):
     summation orders (tools/diag_layer_grads.py locates it: every gradient down to
     the block output within 3e-6 of fp64, the first one past the flipped gate off;
     profiles/r4_records/native_resnet_gru_update_parity.json records both steps'
-    per-tensor figures).  The momentum path is checked per tensor by the C2 round
-    (5 steps, tests/test_gpu_train.py)."""
+    per-tensor figures).  Step 2 is asserted per tensor as a STEP, from the
+    GPU's own step-1 state: the GPU's second step against the reference's
+    second step from that state, within 4x the reference's own distance from
+    the same step in fp64 plus 1e-5 of the update (tests/parity.py
+    check_conditioned); the record also holds how far the reference's own step
+    2 moves when its step-1 state is replaced by the GPU's.  The momentum path is checked per
+    tensor by the C2 round (tests/test_gpu_train.py)."""
     spec = ModelSpec()
     K, B, steps = 2, 32, 2
     glob = initial_global(spec, 42, cuda)
     batches = synthetic_batches(spec, steps, range(K), B, cuda)
     masks = make_dropout_masks(spec, steps, K, B, cuda, seed=3)
     payload = {"config": "flr_train_clients, ResNet-18 + GRU, K=2, B=32, dropout masks"}
+    w1, step2, step2c, cond = {}, {}, {}, {}
     for nst in (1, 2):
         X, loss, _ = nt.train_clients(spec, glob, batches[:nst], TrainConfig(local_steps=nst), masks[:nst])
         reps = {}
@@ -82,10 +88,36 @@ def test_native_trainer_matches_reference_loop(cuda):
             assert err < 1e-5, (nst, k, err)
             assert abs(loss[k].item() - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
             reps[f"client{k}"] = delta_report(X[k], ref, glob, param_layout(spec))
+            if nst == 1:
+                w1[k] = X[k].clone()
+            else:
+                # step 2 of the reference FROM THE GPU'S OWN STEP-1 STATE (its
+                # weights; the reference's step-1 momentum, equal to the GPU's
+                # clipped gradient within fp32 noise): the step itself per tensor
+                # at the bar; and the conditioning, recorded: how far the fp32
+                # reference's own step 2 moves when its step-1 state is replaced
+                # by the GPU's (the step-1 states agree to fp32 noise)
+                _, _, buf1 = otrain.local_update(MultimodalNet, spec, glob.cpu(), cb[:1], masks=[masks[0][k].cpu()],
+                                                 return_momentum=True)
+                upd_h, _ = otrain.local_update(MultimodalNet, spec, glob.cpu(), cb[1:], masks=[masks[1][k].cpu()],
+                                               start_params=w1[k].cpu(), start_momentum=buf1)
+                ref_h = torch.cat([u.reshape(-1) for u in upd_h])
+                upd_h64, _ = otrain.local_update(MultimodalNet, spec, glob.cpu(), cb[1:], masks=[masks[1][k].cpu()],
+                                                 start_params=w1[k].cpu(), start_momentum=buf1, dtype=torch.float64)
+                ref_h64 = torch.cat([u.reshape(-1) for u in upd_h64])
+                step2[f"client{k}"] = delta_report(X[k], ref_h, w1[k], param_layout(spec))
+                step2c[f"client{k}"] = conditioned_report(X[k], ref_h, ref_h64, w1[k], param_layout(spec))
+                cond[f"client{k}"] = delta_report(ref_h, ref, w1[k], param_layout(spec))
         payload[f"steps{nst}"] = reps
         if nst == 1:
             check_delta(reps)
+    payload["step2_from_gpu_state"] = step2
+    payload["step2_from_gpu_state_conditioned"] = step2c
+    payload["step2_reference_conditioning"] = cond
     record("native_resnet_gru_update_parity.json", payload)
+    # step 2 from the same state: the GPU within 4x the fp32 reference's own
+    # distance from the fp64 step (plus 1e-5 of the update) per tensor
+    check_conditioned(step2c)
 
 
 def _vit_python(spec, glob, batches, masks, K, steps, chunk, nneg, cuda):
