@@ -15,30 +15,29 @@
 // Every fp32 operation here is that operation, in that order, so D is the
 // reference's D bit for bit — no tolerance, no margin argument.
 //
-// Round 5 design.  The parallelism is fixed by the reference: K(K-1)/2 pairs x
-// 8 chains, each chain a sequential fma over R steps (65,024 chains of 1.475 M
-// steps at C3): about one chain per lane of one to two waves per SIMD, so
-// every step of a wave must be cheap.
-//  * One chain per lane: each lane runs chain c of one pair (i, j) (tiles below:
-//    diagonal blocks as circulants, so no lane idles on the triangle).
+// Design.  The parallelism is fixed by the reference: K(K-1)/2 pairs x 8
+// chains, each chain a sequential fma over R steps (65,024 chains of 1.475 M
+// steps at C3): about one chain per lane of one wave per SIMD, so every step of
+// a wave must be cheap and no wave may wait for another.
 //  * Chain-major operands: a segment of X is first rewritten chain-major
 //    (chain_transpose_kernel, Xc[k][c][s] = X[k][8(r0+s)+c], one read and one
 //    write of the segment at HBM rate) so each chain's steps are contiguous.
-//  * x_j per lane from LDS: per chunk of CS = 64 steps the workgroup stages its
-//    64 J rows' 256-B chain pieces by LDS-DMA (four global_load_lds_dwordx4 of 4
-//    rows per wave, XOR-swizzled 16-B slots so the ds_read_b128 lane groups hit
-//    64 distinct banks) into a ring of NSTAGE stages; each lane reads its row's
-//    16 pieces with ds_read_b128 ONE CHUNK AHEAD (two register buffers), so the
-//    LDS latency hides under the previous chunk's chain.
-//  * x_i (wave-uniform) by DPP: lane L of each 16-lane row holds 4 steps of the
-//    chunk (one 16-B load per lane per chunk, NSTAGE - 1 chunks ahead); step S
-//    reaches every lane by a row_newbcast of lane S / 4 folded into the
-//    subtraction (v_sub_f32_dpp).  Measured alternatives (tools/hip/valu_lat*.hip,
-//    same-box A/B): x_i through LDS broadcast reads (LDS-bound),
-//    v_readlane into SGPRs, scalar loads into SGPRs (the scalar cache streams
-//    poorly), uniform-address vector loads (TA-bound), v_pk_add_f32 pairs.
+//  * One wave per workgroup, one chain per lane: a wave holds 4 I rows (its
+//    16-lane DPP rows) x 16 J rows (the lanes of a row) — 64 pairs — and
+//    stages only the J rows it reads, so no wave waits at a barrier for
+//    another (a shared 64-row J block behind a workgroup barrier cost 2.1 of
+//    10.3 ms at C3: tools/gpu_r5_l.sh, profiles/r5_ref/).
+//  * x_j per lane from LDS: per chunk of CS = 64 steps the wave stages its 16
+//    (diagonal tiles: 20) J rows' 256-B chain pieces by LDS-DMA (one
+//    global_load_lds_dwordx4 per 4 rows, XOR-swizzled 16-B slots so the
+//    ds_read_b128 lane groups hit distinct banks) into a ring of NSTAGE stages
+//    (DMA NSTAGE - 1 chunks ahead); each lane reads its row's 16 pieces with
+//    ds_read_b128 one chunk ahead (two register buffers).
+//  * x_i by DPP: lane L of each 16-lane row holds 4 steps of the chunk (one
+//    16-B load per lane per chunk); step S reaches every lane of the row by a
+//    row_newbcast of lane S / 4 folded into the subtraction (v_sub_f32_dpp).
 //  * chain c = the XCD (blockIdx % 8): an XCD's L2 holds only its own chain's
-//    streams, and the 8 / 16 workgroups of one J block re-read them from L2.
+//    streams.  40 KB of LDS per workgroup: four per CU, one wave per SIMD.
 // Chains longer than the segment carry their partial sums in A between segments.
 #include <type_traits>
 #include <utility>
@@ -48,72 +47,82 @@
 namespace flr {
 namespace pwref {
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int NJ = 64;             // J rows per tile: one per lane
-constexpr int TI = 4;              // waves per workgroup (one per SIMD)
-constexpr int THREADS = 64 * TI;   // 256
-constexpr int OFF_WG = 64 / TI;    // workgroups of an off-diagonal block pair (one I row per wave)
-constexpr int DIAG_WG = 32 / TI;   // workgroups of a diagonal block (two I rows per wave)
+constexpr int IW = 4;              // I rows per wave: its 16-lane DPP rows
+constexpr int JW = 16;             // J rows per wave: the lanes of a DPP row
+constexpr int SB = 32;             // rows per super-block (tiles below)
+constexpr int OFF_W = (SB / IW) * (SB / JW);  // waves of an off-diagonal super-block pair (16)
+constexpr int DIAG_W = SB / IW;               // waves of a diagonal super-block (8)
 constexpr int CS = 64;             // chain steps per staged chunk (256 B of one chain stream)
-constexpr int NSTAGE = 4;          // LDS ring = the loop's unroll (static stage offsets: ds_read's 16-bit offset)
-constexpr int STAGE = NJ * CS;     // floats per stage (16 KB)
 constexpr int NQ = CS / 4;         // 16-B pieces per chunk row
 constexpr int RPD = 256 / CS;      // chunk rows per 1-KB DMA instruction (4)
-constexpr int RPW = NJ / TI;       // J rows each wave stages (16)
-constexpr int DPW = RPW / RPD;     // DMA instructions per wave per chunk (4)
-constexpr int OPB = DPW + 1;       // vector-memory ops per body: the DMAs, then the x_i load
+constexpr int SROWS = 20;          // staged rows per stage (diagonal tiles read 19)
+#ifndef FLR_REF_NSTAGE
+#define FLR_REF_NSTAGE 8
+#endif
+constexpr int NSTAGE = FLR_REF_NSTAGE;    // LDS ring = the loop's unroll (DMA NSTAGE - 1 chunks ahead)
+constexpr int STAGE = SROWS * CS;         // floats per stage (5 KB)
 constexpr int64_t XC_CAP = int64_t(8) << 30;  // bytes of one chain-major segment
 static_assert(CS == 64 && NQ == 16, "x_i layout: 16 lanes x 4 steps per chunk");
-static_assert((NSTAGE - 2) * OPB + 1 < 64, "vmcnt counts to 63");
+static_assert(NSTAGE % 2 == 0 && NSTAGE >= 4, "two register buffers");
 static_assert((NSTAGE - 1) * STAGE * 4 < 65536, "ds_read_b128's 16-bit offset reaches every stage");
+static_assert(NSTAGE * STAGE * 4 > 163840 / 5, "LDS caps the CU at four workgroups: one wave per SIMD");
+template <bool DIAG>
+struct Staging {
+  static constexpr int DPW = (DIAG ? SROWS : JW) / RPD;  // DMA instructions per chunk (5 | 4)
+  static constexpr int OPB = DPW + 1;                   // vector-memory ops per body: the DMAs, then x_i
+  static_assert((NSTAGE - 2) * OPB + 1 < 64, "vmcnt counts to 63");
+};
 
-// the XOR swizzle of a row's 16-B slots: the ds_read_b128 lane groups
-// ({0-3,12-15,20-27}, {4-11,16-19,28-31} and +32) hit 64 distinct banks
+// the XOR swizzle of a staged row's 16-B slots: the rows one ds_read_b128 lane
+// group ({0-3,12-15,20-27}, {4-11,16-19,28-31} and +32) reads are distinct
+// modulo 16, or the same row (a broadcast), on both tile kinds
 __host__ __device__ constexpr int slot_swz(int row) { return row & 15; }
 
-// Tiles (per chain).  The K rows form blocks of 64; block pair (bi, bj), bi <= bj:
-//  * bi < bj: 64 x 64 pairs, OFF_WG workgroups; wave -> one I row of block bi,
-//    lane -> one J row of block bj;
-//  * bi == bj: the block's 64 * 63 / 2 pairs as a circulant: I row a takes
-//    J rows a + 1 .. a + 32 (mod 64), the antipodal pair (a, a + 32) once (from
-//    a < 32); DIAG_WG workgroups, a wave holds rows (w, w + 32) of the block in
-//    its lane halves (every DPP row_newbcast stays inside one 16-lane row, so a
-//    half-wave's operand is uniform to it) — every lane a distinct pair, none
-//    idle (the triangle of a plain diagonal tile wasted a third of the lanes).
-// Tiles are numbered bj-major: bj's tiles start at (32 / TI) * bj^2; within bj
-// the off-diagonal pairs bi = 0 .. bj-1, then the diagonal block.
-__host__ __device__ inline int tiles_before(int bj) { return DIAG_WG * bj * bj; }
-__host__ __device__ inline int ntiles_of(int K) { return tiles_before((K + NJ - 1) / NJ); }
+// Tiles (per chain): one wave each.  The K rows form super-blocks of 32;
+// super-block pair (X, Y), X <= Y:
+//  * X < Y: 32 x 32 pairs in OFF_W waves (g, h): I rows 32X + 4g + r (DPP row
+//    r), J rows 32Y + 16h + lane % 16;
+//  * X == Y: the super-block's 32 * 31 / 2 pairs as a circulant: I row a takes
+//    J rows a + 1 .. a + 16 (mod 32), the antipodal pair (a, a + 16) once
+//    (from a < 16); wave g holds a = 4g + r, so its J rows are 4g + 1 ..
+//    4g + 19 (mod 32): 20 staged rows, lane (r, o - 1) reading row r + o - 1.
+//    496 of 512 lanes hold a pair.
+// Tiles are numbered Y-major: Y's tiles start at 8 Y^2; within Y the
+// off-diagonal pairs X = 0 .. Y-1 (16 waves each, w = 2g + h), then the diagonal.
+__host__ __device__ inline int tiles_before(int Y) { return DIAG_W * Y * Y; }
+__host__ __device__ inline int ntiles_of(int K) { return tiles_before((K + SB - 1) / SB); }
 struct Tile {
-  int bi, bj, g;
+  int X, Y, g, h;
   bool diag;
 };
 __host__ __device__ inline Tile tile_of(int t) {
-  int bj = 0;
-  while (tiles_before(bj + 1) <= t) ++bj;  // at most ~K / 64 steps
-  const int local = t - tiles_before(bj);
+  int Y = 0;
+  while (tiles_before(Y + 1) <= t) ++Y;  // at most ~K / 32 steps
+  const int local = t - tiles_before(Y);
   Tile r;
-  r.bj = bj;
-  if (local < bj * OFF_WG) {
-    r.bi = local / OFF_WG;
-    r.g = local % OFF_WG;
+  r.Y = Y;
+  if (local < Y * OFF_W) {
+    r.X = local / OFF_W;
+    r.g = (local % OFF_W) >> 1;
+    r.h = local & 1;
     r.diag = false;
   } else {
-    r.bi = bj;
-    r.g = local - bj * OFF_WG;
+    r.X = Y;
+    r.g = local - Y * OFF_W;
+    r.h = 0;
     r.diag = true;
   }
   return r;
 }
 // the tile that computes pair (i, j), i < j
 __host__ __device__ inline int tile_of_pair(int i, int j) {
-  const int bi = i / NJ, bj = j / NJ;
-  if (bi < bj) return tiles_before(bj) + bi * OFF_WG + (i % NJ) / TI;
-  const int a = i % NJ, b = j % NJ, o = b - a;  // 1 .. 63
-  const int ii = o <= 32 ? a : b;               // the row whose circulant half holds the pair
-  return tiles_before(bj) + bj * OFF_WG + (ii & 31) / TI;
+  const int X = i / SB, Y = j / SB;
+  if (X < Y) return tiles_before(Y) + X * OFF_W + 2 * ((i % SB) / IW) + (j % SB) / JW;
+  const int a = i % SB, b = j % SB, o = b - a;  // 1 .. 31
+  const int ii = o <= SB / 2 ? a : b;           // the row whose circulant half holds the pair
+  return tiles_before(Y) + Y * OFF_W + ii / IW;
 }
 
 // Xc[k][c][s] = X[k][8 (r0 + s) + c] for s < steps; stream stride ldc (x 8 per row).
@@ -161,69 +170,150 @@ __global__ __launch_bounds__(256) void chain_transpose_kernel(const float* __res
   }
 }
 
-// step S of the chunk for every lane: lane S / 4 of each 16-lane row holds it
-// (component S % 4); DPP row_newbcast, folded into the subtraction
-template <int S>
-__device__ __forceinline__ float bcast(f32x4 xv) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xv[S & 3]), 0x150 + (S >> 2), 0xf, 0xf, false));
-}
-// the differences first (independent registers: one temporary reused for
-// every step made the hazard recognizer put an s_nop before each DPP write),
-// then the fma chain in step order
-template <int... S>
-__device__ __forceinline__ float chain_chunk(f32x4 xv, const f32x4 (&v)[NQ], float acc,
-                                             std::integer_sequence<int, S...>) {
-  float d[sizeof...(S)];
-  ((d[S] = bcast<S>(xv) - v[S >> 2][S & 3]), ...);
-  ((acc = __builtin_fmaf(d[S], d[S], acc)), ...);
+// One chunk (CS = 64 steps) of a lane's chain: step S subtracts its x_j from
+// x_i's step S, which lane S / 4 of each 16-lane row holds (component S % 4) and
+// a DPP row_newbcast hands to every lane, folded into the subtraction
+// (v_sub_f32_dpp), then acc = fma(d, d, acc).  Inline asm fixes the order
+// (the subtraction of step S + 2 in the gap before the dependent fma of step
+// S; blocks of 16 steps, three rotating temporaries).  The s_nop before the
+// first block covers the DPP read-after-VALU-write hazard on x_i (the compiler
+// cannot see a DPP inside asm; the later blocks follow asm that writes only the
+// temporaries and acc).
+// FLR_REF_ABL (tools build, timing only, wrong results): 1 plain v_sub instead
+// of the DPP broadcast, 2 no LDS reads, 3 no DMA / x_i loads, 4 no barrier,
+// 5 no chain arithmetic
+#ifndef FLR_REF_ABL
+#define FLR_REF_ABL 0
+#endif
+#if FLR_REF_ABL == 1
+#define FLR_CHAIN16(A, B, C, D, NOP) \
+  NOP \
+  "v_sub_f32 %[t0], %[x0], %[j0]\n\t" \
+  "v_sub_f32 %[t1], %[x1], %[j1]\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t" \
+  "v_sub_f32 %[t2], %[x2], %[j2]\n\t" \
+  "v_fmac_f32 %[acc], %[t1], %[t1]\n\t" \
+  "v_sub_f32 %[t0], %[x3], %[j3]\n\t" \
+  "v_fmac_f32 %[acc], %[t2], %[t2]\n\t" \
+  "v_sub_f32 %[t1], %[x0], %[j4]\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t" \
+  "v_sub_f32 %[t2], %[x1], %[j5]\n\t" \
+  "v_fmac_f32 %[acc], %[t1], %[t1]\n\t" \
+  "v_sub_f32 %[t0], %[x2], %[j6]\n\t" \
+  "v_fmac_f32 %[acc], %[t2], %[t2]\n\t" \
+  "v_sub_f32 %[t1], %[x3], %[j7]\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t" \
+  "v_sub_f32 %[t2], %[x0], %[j8]\n\t" \
+  "v_fmac_f32 %[acc], %[t1], %[t1]\n\t" \
+  "v_sub_f32 %[t0], %[x1], %[j9]\n\t" \
+  "v_fmac_f32 %[acc], %[t2], %[t2]\n\t" \
+  "v_sub_f32 %[t1], %[x2], %[j10]\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t" \
+  "v_sub_f32 %[t2], %[x3], %[j11]\n\t" \
+  "v_fmac_f32 %[acc], %[t1], %[t1]\n\t" \
+  "v_sub_f32 %[t0], %[x0], %[j12]\n\t" \
+  "v_fmac_f32 %[acc], %[t2], %[t2]\n\t" \
+  "v_sub_f32 %[t1], %[x1], %[j13]\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t" \
+  "v_sub_f32 %[t2], %[x2], %[j14]\n\t" \
+  "v_fmac_f32 %[acc], %[t1], %[t1]\n\t" \
+  "v_sub_f32 %[t0], %[x3], %[j15]\n\t" \
+  "v_fmac_f32 %[acc], %[t2], %[t2]\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t"
+#else
+#define FLR_CHAIN16(A, B, C, D, NOP) \
+  NOP \
+  "v_sub_f32_dpp %[t0], %[x0], %[j0] row_newbcast:" #A " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_sub_f32_dpp %[t1], %[x1], %[j1] row_newbcast:" #A " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t" \
+  "v_sub_f32_dpp %[t2], %[x2], %[j2] row_newbcast:" #A " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t1], %[t1]\n\t" \
+  "v_sub_f32_dpp %[t0], %[x3], %[j3] row_newbcast:" #A " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t2], %[t2]\n\t" \
+  "v_sub_f32_dpp %[t1], %[x0], %[j4] row_newbcast:" #B " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t" \
+  "v_sub_f32_dpp %[t2], %[x1], %[j5] row_newbcast:" #B " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t1], %[t1]\n\t" \
+  "v_sub_f32_dpp %[t0], %[x2], %[j6] row_newbcast:" #B " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t2], %[t2]\n\t" \
+  "v_sub_f32_dpp %[t1], %[x3], %[j7] row_newbcast:" #B " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t" \
+  "v_sub_f32_dpp %[t2], %[x0], %[j8] row_newbcast:" #C " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t1], %[t1]\n\t" \
+  "v_sub_f32_dpp %[t0], %[x1], %[j9] row_newbcast:" #C " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t2], %[t2]\n\t" \
+  "v_sub_f32_dpp %[t1], %[x2], %[j10] row_newbcast:" #C " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t" \
+  "v_sub_f32_dpp %[t2], %[x3], %[j11] row_newbcast:" #C " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t1], %[t1]\n\t" \
+  "v_sub_f32_dpp %[t0], %[x0], %[j12] row_newbcast:" #D " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t2], %[t2]\n\t" \
+  "v_sub_f32_dpp %[t1], %[x1], %[j13] row_newbcast:" #D " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t" \
+  "v_sub_f32_dpp %[t2], %[x2], %[j14] row_newbcast:" #D " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t1], %[t1]\n\t" \
+  "v_sub_f32_dpp %[t0], %[x3], %[j15] row_newbcast:" #D " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[t2], %[t2]\n\t" \
+  "v_fmac_f32 %[acc], %[t0], %[t0]\n\t"
+#endif
+#define FLR_CHAIN_BLOCK(b, A, B, C, D, NOP)                                                                 \
+  asm volatile(FLR_CHAIN16(A, B, C, D, NOP)                                                                \
+               : [acc] "+v"(acc), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)                        \
+               : [x0] "v"(xv[0]), [x1] "v"(xv[1]), [x2] "v"(xv[2]), [x3] "v"(xv[3]), [j0] "v"(v[4 * (b) + 0][0]), [j1] "v"(v[4 * (b) + 0][1]), [j2] "v"(v[4 * (b) + 0][2]), [j3] "v"(v[4 * (b) + 0][3]), [j4] "v"(v[4 * (b) + 1][0]), [j5] "v"(v[4 * (b) + 1][1]), [j6] "v"(v[4 * (b) + 1][2]), [j7] "v"(v[4 * (b) + 1][3]), [j8] "v"(v[4 * (b) + 2][0]), [j9] "v"(v[4 * (b) + 2][1]), [j10] "v"(v[4 * (b) + 2][2]), [j11] "v"(v[4 * (b) + 2][3]), [j12] "v"(v[4 * (b) + 3][0]), [j13] "v"(v[4 * (b) + 3][1]), [j14] "v"(v[4 * (b) + 3][2]), [j15] "v"(v[4 * (b) + 3][3]))
+__device__ __forceinline__ float chain_chunk(f32x4 xv, const f32x4 (&v)[NQ], float acc) {
+  static_assert(NQ == 16, "four blocks of 16 steps");
+  float t0, t1, t2;
+  FLR_CHAIN_BLOCK(0, 0, 1, 2, 3, "s_nop 1\n\t");
+  FLR_CHAIN_BLOCK(1, 4, 5, 6, 7, "");
+  FLR_CHAIN_BLOCK(2, 8, 9, 10, 11, "");
+  FLR_CHAIN_BLOCK(3, 12, 13, 14, 15, "");
   return acc;
 }
+#undef FLR_CHAIN_BLOCK
+#undef FLR_CHAIN16
 
-// One segment of steps for the tiles [t0, t0 + gridDim.x / 8) (tile_of): chain
-// c of each lane's pair; the running chain sums in A[c][min(i,j)][max(i,j)]
-// (first: start from 0).
+template <class F, int... U>
+__device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, U...>) {
+  (f(std::integral_constant<int, U>{}), ...);
+}
+
+// One segment of steps of one tile (one wave): chain c of each lane's pair; the
+// running chain sums in A[c][min(i,j)][max(i,j)] (first: start from 0).
 //
 // Body ch (stage u = ch % NSTAGE, static in the unrolled loop):
-//   wait  this wave's DMA(ch + 1) and x_i(ch) landed (counted vmcnt), this
-//         wave's ds_reads of chunk ch landed (lgkmcnt(0)), then one barrier:
-//         every wave's DMA(ch + 1) is in LDS and every wave finished reading
-//         stage (ch - 1) % NSTAGE
+//   wait  DMA(ch + 1) and x_i(ch) landed (counted vmcnt: the DMA's LDS writes
+//         are then visible to this wave), the ds_reads of chunk ch landed
+//         (lgkmcnt(0): stage (ch - 1) % NSTAGE is free)
 //   issue DMA(ch + NSTAGE - 1) into that stage and x_i(ch + NSTAGE - 1);
 //         ds_read_b128 x 16 of chunk ch + 1 into the other register buffer
 //   chain chunk ch (registers read in body ch - 1)
 // Every body issues the same vector-memory ops (clamped to the last chunk), so
 // the counts are static; the LDS reads and the register loads are inline asm
 // with explicit waits (the compiler's waitcnt pass, merging across the
-// rotated registers, drained vmcnt(0) every chunk).
-__global__ __launch_bounds__(THREADS) void ref_chain_kernel(const float* __restrict__ Xc, int64_t ldc, int K,
-                                                            int64_t steps, int t0, int first,
-                                                            float* __restrict__ A) {
-  // ONE __shared__ array (a second __shared__ object makes hipcc wait vmcnt(0)
-  // before the LDS reads, draining the DMA ring)
-  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * STAGE];
-  const int c = (int)(blockIdx.x & 7);
-  const Tile T = tile_of(t0 + (int)(blockIdx.x >> 3));
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // this lane's pair (i, j): rows of blocks bi / bj; jj = J row within the staged block
-  int ii, jj;
+// rotated registers, drained vmcnt(0) every chunk).  No workgroup barrier:
+// the wave is the workgroup and reads only what it staged.
+template <bool DIAG>
+__device__ __forceinline__ void ref_chain_tile(float* lds, const Tile T, const int c, const float* __restrict__ Xc,
+                                               int64_t ldc, int K, int64_t steps, int first,
+                                               float* __restrict__ A) {
+  using S = Staging<DIAG>;
+  const int lane = threadIdx.x & 63, r = lane >> 4, jl = lane & 15;
+  // this lane's pair (i, j) and the staged row it reads
+  int i, j, srow;
   bool keep = true;
-  if (T.diag) {
-    const int w = TI * T.g + wave;  // 0 .. 31
-    ii = lane < 32 ? w : w + 32;
-    const int o = (lane & 31) + 1;  // 1 .. 32
-    jj = (ii + o) & 63;
-    keep = o < 32 || ii < 32;  // the antipodal pair once
+  if (DIAG) {
+    const int a = IW * T.g + r, o = jl + 1;
+    i = SB * T.X + a;
+    j = SB * T.X + ((a + o) & (SB - 1));
+    srow = r + jl;
+    keep = o < SB / 2 || a < SB / 2;  // the antipodal pair once
   } else {
-    ii = TI * T.g + wave;
-    jj = lane;
+    i = SB * T.X + IW * T.g + r;
+    j = SB * T.Y + JW * T.h + jl;
+    srow = jl;
   }
-  const int i = NJ * T.bi + ii, j = NJ * T.bj + jj;
   const bool valid = keep && i < K && j < K;
   const int lo = i < j ? i : j, hi = i < j ? j : i;  // A holds the pair at [lo][hi]
-  const int jb = T.bj;
-  // uniform per wave: some lane holds a pair (off-diagonal: the I row exists)
-  const bool active = T.diag ? NJ * T.bi + TI * T.g + wave < K : i < K;
   const int64_t rs = 8 * ldc;
 
   // the running sum of the previous segments: an asm load and a full wait
@@ -235,42 +325,68 @@ __global__ __launch_bounds__(THREADS) void ref_chain_kernel(const float* __restr
     acc = valid ? acc : 0.f;
   }
 
-  // staging: wave w moves J rows RPW w .. RPW w + RPW - 1, RPD rows per DMA
-  // instruction; lane -> row RPW w + RPD u + lane / NQ, LDS slot lane % NQ
-  // holding the chunk's piece slot ^ slot_swz(row)
-  const float* ssrc[DPW];
+  // staging: DMA instruction u moves staged rows RPD u .. RPD u + 3, lane ->
+  // row RPD u + lane / NQ, LDS slot lane % NQ holding the piece slot ^ slot_swz(row).
+  // Global addresses as a uniform base (SGPRs, advanced per chunk) + a 32-bit
+  // per-lane offset (the saddr form: no 64-bit address arithmetic per DMA);
+  // the DMAs of a chunk share one M0 (the stage + 2 KB) and differ in the
+  // instruction offset (u - 2) KB, which applies to the global and the LDS
+  // address alike (13-bit signed: -2 .. +2 KB), so the lane offsets carry
+  // 2 KB - (u - 2) KB of slack and the base sits 2 KB low.
+  const int jrow0 = DIAG ? SB * T.X : min(SB * T.Y + JW * T.h, K - 1);  // lowest staged row (clamped)
+  const char* sbj = reinterpret_cast<const char*>(Xc + (int64_t)jrow0 * rs + (int64_t)c * ldc) - 2048;
+  uint32_t voj[S::DPW];
 #pragma unroll
-  for (int u = 0; u < DPW; ++u) {
-    const int srow = RPW * wave + RPD * u + lane / NQ;
-    int gj = NJ * jb + srow;
+  for (int u = 0; u < S::DPW; ++u) {
+    const int s = RPD * u + lane / NQ;
+    int gj = DIAG ? SB * T.X + ((IW * T.g + 1 + s) & (SB - 1)) : SB * T.Y + JW * T.h + s;
     gj = gj < K ? gj : K - 1;
-    ssrc[u] = Xc + (int64_t)gj * rs + (int64_t)c * ldc + 4 * ((lane % NQ) ^ slot_swz(srow));
+    voj[u] = (uint32_t)((int64_t)(gj - jrow0) * rs * 4 + 16 * ((lane % NQ) ^ slot_swz(s)) - 1024 * (u - 2) + 2048);
   }
-  float* sdst = lds + RPW * wave * CS;
-  // x_i: lane L of each 16-lane row loads steps 4 (L & 15) .. of its half-wave's I row
-  const float* xl = Xc + (int64_t)(i < K ? i : K - 1) * rs + (int64_t)c * ldc + 4 * (lane & 15);
+  // x_i: lane jl of DPP row r loads steps 4 jl .. 4 jl + 3 of the row's I row
+  const int irow0 = min(SB * T.X + IW * T.g, K - 1);
+  const char* sbi = reinterpret_cast<const char*>(Xc + (int64_t)irow0 * rs + (int64_t)c * ldc);
+  const uint32_t voi = (uint32_t)((int64_t)((i < K ? i : K - 1) - irow0) * rs * 4 + 16 * jl);
   const int nch = (int)((steps + CS - 1) / CS), nfull = (int)(steps / CS), lastc = nch - 1;
   auto clampc = [&](int ch) { return ch < lastc ? ch : lastc; };
-  // DMA(ch) into stage `slot`, then x_i(ch) into register set x
+  // DMA(ch) into stage `slot`, then x_i(ch) into register set x (inline asm:
+  // hipcc built 64-bit addresses per DMA instead of the saddr form)
   auto issue = [&](int ch, int slot, f32x4& x) {
-    const int cl = clampc(ch);
-#pragma unroll
-    for (int u = 0; u < DPW; ++u)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc[u] + (int64_t)cl * CS),
-                                       (__attribute__((address_space(3))) void*)(sdst + slot * STAGE + 256 * u), 16,
-                                       0, 0);
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(xl + (int64_t)cl * CS) : "memory");
+    const int64_t co = (int64_t)clampc(ch) * CS * 4;  // the chunk's byte offset in a stream
+    if (FLR_REF_ABL == 3) return;
+    const char* sb = sbj + co;
+    const uint32_t m = (uint32_t)(uintptr_t)lds + 4 * slot * STAGE + 2048;
+    uint32_t keep;
+    // M0 is written in the statement that reads it and restored (compiler-reserved)
+#define FLR_DMA(n, off) "global_load_lds_dwordx4 %[v" #n "], %[sb] offset:" #off "\n\t"
+    if constexpr (S::DPW == 5)
+      asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[m]\n\ts_nop 0\n\t" FLR_DMA(0, -2048) FLR_DMA(1, -1024)
+                       FLR_DMA(2, 0) FLR_DMA(3, 1024) FLR_DMA(4, 2048) "s_mov_b32 m0, %[keep]"
+                   : [keep] "=&s"(keep)
+                   : [m] "s"(m), [sb] "s"(sb), [v0] "v"(voj[0]), [v1] "v"(voj[1]), [v2] "v"(voj[2]), [v3] "v"(voj[3]),
+                     [v4] "v"(voj[S::DPW - 1])
+                   : "memory");
+    else
+      asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[m]\n\ts_nop 0\n\t" FLR_DMA(0, -2048) FLR_DMA(1, -1024)
+                       FLR_DMA(2, 0) FLR_DMA(3, 1024) "s_mov_b32 m0, %[keep]"
+                   : [keep] "=&s"(keep)
+                   : [m] "s"(m), [sb] "s"(sb), [v0] "v"(voj[0]), [v1] "v"(voj[1]), [v2] "v"(voj[2]), [v3] "v"(voj[3])
+                   : "memory");
+#undef FLR_DMA
+    static_assert(S::DPW == 4 || S::DPW == 5, "the DMA statements above");
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x) : "v"(voi), "s"(sbi + co) : "memory");
   };
-  // per-lane LDS byte addresses of row jj's 16 swizzled pieces in stage 0
-  const int rsw = slot_swz(jj);
+  // per-lane LDS byte addresses of staged row srow's 16 swizzled pieces in stage 0
+  const int rsw = slot_swz(srow);
   uint32_t ra[NQ];
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) ra[q] = (uint32_t)(uintptr_t)(lds + jj * CS + 4 * (q ^ rsw));
+  for (int q = 0; q < NQ; ++q) ra[q] = (uint32_t)(uintptr_t)(lds + srow * CS + 4 * (q ^ rsw));
   auto rows = [](auto st, f32x4(&v)[NQ], const uint32_t(&a)[NQ]) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[q]) : "v"(a[q]), "n"(decltype(st)::value * STAGE * 4)
-                   : "memory");
+      if (FLR_REF_ABL != 2)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[q]) : "v"(a[q]), "n"(decltype(st)::value * STAGE * 4)
+                     : "memory");
   };
 
   f32x4 va[NQ], vb[NQ];
@@ -279,51 +395,61 @@ __global__ __launch_bounds__(THREADS) void ref_chain_kernel(const float* __restr
     constexpr int u = decltype(U)::value;
     // DMA(ch + 1) was issued in body ch + 2 - NSTAGE; younger than it: its
     // x_i load and the NSTAGE - 3 bodies since (x_i(ch) is older: covered)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 3) * OPB + 1) : "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                              // chunk ch's x_j
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 3) * S::OPB + 1) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // chunk ch's x_j
     issue(ch + NSTAGE - 1, (u + NSTAGE - 1) % NSTAGE, xs[(u + NSTAGE - 1) % NSTAGE]);
     rows(std::integral_constant<int, (u + 1) % NSTAGE>{}, vn, ra);
-    if (active && ch < nfull) {
+    if (ch < nfull) {
       // chunk ch's operands arrived before the waits above: tie them to here
       asm volatile("" : "+v"(vc[0]), "+v"(vc[1]), "+v"(vc[2]), "+v"(vc[3]), "+v"(vc[4]), "+v"(vc[5]), "+v"(vc[6]),
                    "+v"(vc[7]), "+v"(vc[8]), "+v"(vc[9]), "+v"(vc[10]), "+v"(vc[11]), "+v"(vc[12]), "+v"(vc[13]),
                    "+v"(vc[14]), "+v"(vc[15]), "+v"(xs[u]));
-      acc = chain_chunk(xs[u], vc, acc, std::make_integer_sequence<int, CS>{});
+      if (FLR_REF_ABL != 5) acc = chain_chunk(xs[u], vc, acc);
     }
   };
   // prologue = the issues of bodies -(NSTAGE-1) .. -1, then chunk 0's rows
 #pragma unroll
   for (int u = 0; u < NSTAGE - 1; ++u) issue(u, u, xs[u]);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * OPB + 1) : "memory");  // DMA(0): x_i(0) + NSTAGE - 2 issues younger
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * S::OPB + 1) : "memory");  // DMA(0)
   rows(std::integral_constant<int, 0>{}, va, ra);
   const int nloop = (nfull + NSTAGE - 1) / NSTAGE * NSTAGE;
-  static_assert(NSTAGE == 4, "the unrolled loop below");
-  for (int ch = 0; ch < nloop; ch += NSTAGE) {
-    body(std::integral_constant<int, 0>{}, ch, va, vb);
-    body(std::integral_constant<int, 1>{}, ch + 1, vb, va);
-    body(std::integral_constant<int, 2>{}, ch + 2, va, vb);
-    body(std::integral_constant<int, 3>{}, ch + 3, vb, va);
-  }
+  for (int ch = 0; ch < nloop; ch += NSTAGE)
+    static_for(
+        [&](auto U) {
+          constexpr int u = decltype(U)::value;
+          if constexpr (u % 2 == 0)
+            body(U, ch + u, va, vb);
+          else
+            body(U, ch + u, vb, va);
+        },
+        std::make_integer_sequence<int, NSTAGE>{});
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (nfull < nch) {
     // the last, partial chunk: staged as chunk nfull in stage nfull % NSTAGE
     // (the clamped DMAs after it rewrote that stage with the same bytes)
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (active) {
-      const float* rd = lds + jj * CS + (nfull % NSTAGE) * STAGE;
-      const float* xi = Xc + (int64_t)(i < K ? i : K - 1) * rs + (int64_t)c * ldc + (int64_t)nfull * CS;
-      for (int s2 = 0; s2 < (int)(steps - (int64_t)nfull * CS); ++s2) {
-        const float d = xi[s2] - rd[4 * ((s2 >> 2) ^ rsw) + (s2 & 3)];
-        acc = __builtin_fmaf(d, d, acc);
-      }
+    const float* rd = lds + srow * CS + (nfull % NSTAGE) * STAGE;
+    const float* xi = Xc + (int64_t)(i < K ? i : K - 1) * rs + (int64_t)c * ldc + (int64_t)nfull * CS;
+    for (int s2 = 0; s2 < (int)(steps - (int64_t)nfull * CS); ++s2) {
+      const float d = xi[s2] - rd[4 * ((s2 >> 2) ^ rsw) + (s2 & 3)];
+      acc = __builtin_fmaf(d, d, acc);
     }
   }
   if (valid) A[((int64_t)c * K + lo) * K + hi] = acc;
+}
+
+// grid 8 x (t1 - t0) one-wave workgroups: chain c = blockIdx % 8 (the XCD),
+// tile t0 + blockIdx / 8
+__global__ __launch_bounds__(64) void ref_chain_kernel(const float* __restrict__ Xc, int64_t ldc, int K,
+                                                       int64_t steps, int t0, int first, float* __restrict__ A) {
+  // ONE __shared__ array (a second __shared__ object makes hipcc wait vmcnt(0)
+  // before the LDS reads, draining the DMA ring)
+  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * STAGE];
+  const int c = (int)(blockIdx.x & 7);
+  const Tile T = tile_of(t0 + (int)(blockIdx.x >> 3));
+  if (T.diag)
+    ref_chain_tile<true>(lds, T, c, Xc, ldc, K, steps, first, A);
+  else
+    ref_chain_tile<false>(lds, T, c, Xc, ldc, K, steps, first, A);
 }
 
 // D[i][j] = D[j][i] for the pairs of tiles [t0, t1): chains summed 0..7 in
@@ -418,11 +544,11 @@ extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, i
     for (int64_t seg = 0; seg < nseg; ++seg) {
       const int64_t r0 = seg * Rs, steps = (R - r0 < Rs) ? R - r0 : Rs;
       if (steps <= 0) break;
-      hipLaunchKernelGGL(chain_transpose_kernel, dim3((unsigned)((steps + 4 * TW - 1) / (4 * TW)), (unsigned)K), dim3(256), 0,
-                         st, X, ldx, r0, steps, ldc, Xc);
+      hipLaunchKernelGGL(chain_transpose_kernel, dim3((unsigned)((steps + 4 * TW - 1) / (4 * TW)), (unsigned)K),
+                         dim3(256), 0, st, X, ldx, r0, steps, ldc, Xc);
       int rc = launch_status("chain_transpose_kernel");
       if (rc != FLR_OK) return rc;
-      hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(THREADS), 0, st, Xc, ldc, (int)K, steps, t0,
+      hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(64), 0, st, Xc, ldc, (int)K, steps, t0,
                          seg == 0 ? 1 : 0, A);
       rc = launch_status("ref_chain_kernel");
       if (rc != FLR_OK) return rc;
