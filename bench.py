@@ -49,7 +49,7 @@ REFERENCE_SHA = {}
 _SHA_FILE = os.path.join(ROOT, "profiles", "reference_sha.json")
 if os.path.exists(_SHA_FILE):
     REFERENCE_SHA = {tuple(k.split("|")[:2]) + (int(k.split("|")[2]),): v
-                     for k, v in json.load(open(_SHA_FILE)).items()}
+                     for k, v in json.load(open(_SHA_FILE)).items() if not k.startswith("_")}
 
 
 def gram_traffic(K: int, P: int):
@@ -418,9 +418,11 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "allgather"])
-    ap.add_argument("--pairwise", default="gram", choices=["gram", "reference"],
-                    help="Krum distances: the centred Gram on MFMA, or the reference-exact fp32 torch.norm "
-                         "accumulation (D bit-identical to krum.py:89-97; whole rows: the all-gather exchange)")
+    ap.add_argument("--pairwise", default="reference", choices=["gram", "reference"],
+                    help="Krum distances: the reference-exact fp32 torch.norm accumulation (default: D "
+                         "bit-identical to krum.py:89-97, so the selection is the reference's by construction; "
+                         "whole rows: the all-gather exchange), or the centred Gram on MFMA (HBM-bound, "
+                         "coordinate-sharded, selection equal only where the scores are well conditioned)")
     ap.add_argument("--defense", default=None, help="override the preset's defense (fedavg, krum, trimmed_mean, median)")
     ap.add_argument("--model", default=None, choices=["resnet_gru", "cub", "vit_bert"])
     ap.add_argument("--client-chunk", type=int, default=0, help="clients per forward/backward pass (0: automatic)")
@@ -467,7 +469,7 @@ def main() -> None:
     spec = {"cub": CUB, "vit_bert": VIT_BERT}.get(model, ModelSpec())
     P = num_params(spec)
     krum = defense in ("krum", "multi_krum", "krum_trimmed_mean")
-    if krum and args.pairwise != "gram":
+    if krum:
         dcfg = dict(dcfg, pairwise_method=args.pairwise)
     f = int(afrac * K)
     rcfg = RoundConfig(num_clients=K, defense=defense, defense_cfg=dict(dcfg), num_attackers=f,
@@ -510,9 +512,17 @@ def main() -> None:
     from flr.defenses import get_defense
     aggregate_ms_all = {}
     for name in ("fedavg", "krum", "trimmed_mean", "median"):
-        cfg = ({"num_malicious": f if krum else int(0.2 * K), "multi_k": max(1, K // 2)} if name == "krum" else
+        cfg = ({"num_malicious": f if krum else int(0.2 * K), "multi_k": max(1, K // 2),
+                "pairwise_method": args.pairwise} if name == "krum" else
                {"trim_ratio": dcfg.get("trim_ratio", 0.1)} if name == "trimmed_mean" else {})
         d = get_defense(name, cfg)
+        if name == "krum":  # the round's matrix order (a training-order round: the coordinate map)
+            d.comm = getattr(eng.defense, "comm", None)
+            d.tap_blocks = (eng.defense.tap_blocks if hasattr(eng.defense, "tap_blocks") else
+                            eng._tap_blocks()[1] if eng.train_order else None)
+        if name == "krum" and args.pairwise == "reference" and sharded:
+            aggregate_ms_all[name] = None  # whole rows only (this round is coordinate-sharded)
+            continue
         kwd = {"publish": False} if hasattr(d, "publish") else {}
         run = ((lambda: eng.slice.gather_vector(d.aggregate_sharded(eng.slice, eng.num_examples, **kwd),
                                                 torch.empty_like(eng.global_flat))) if sharded else
@@ -524,7 +534,7 @@ def main() -> None:
         ev1.record()
         torch.cuda.synchronize()
         aggregate_ms_all[name] = ev0.elapsed_time(ev1) / reps
-    # the dominant aggregation kernel of the headline config: centred-Gram pairwise
+    # the Gram path's kernel: centred-Gram pairwise
     # (HIP events around its launch, on the stream it runs on); sharded: this
     # GPU's coordinates.  Timed for every config (the Krum roofline line).
     kms = []
@@ -548,7 +558,8 @@ def main() -> None:
             if sharded:
                 ops.pairwise_l2_sharded(eng.slice)
             else:
-                ops.pairwise_l2(eng.full.X, method, comm=getattr(eng.defense, "comm", None))
+                ops.pairwise_l2(eng.full.X, method, comm=getattr(eng.defense, "comm", None),
+                                tap_blocks=getattr(eng.defense, "tap_blocks", None) if method == "reference" else None)
             ev1.record()
             torch.cuda.synchronize()
             pms.append(ev0.elapsed_time(ev1))
@@ -571,6 +582,32 @@ def main() -> None:
     pair_bytes = 4.0 * K * n_coords + 8.0 * K * K
     achieved = pair_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = gram_traffic(K, n_coords)
+    gram_roofline = {
+        "kernel": "gram_partials_kernel (Krum pairwise, centred Gram on MFMA)" + (
+            " — the --pairwise gram path, timed here beside the round" if phase and phase["method"] == "reference"
+            else ""),
+        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+        "kernel_ms": kernel_ms, "algorithmic_bytes": pair_bytes, "coords_per_gpu": n_coords,
+    }
+    # the reference-exact distances (the default Krum path): VALU-issue bound —
+    # every pair's 8 chains run the whole vector sequentially, one chain per
+    # lane, one wave per SIMD; the phase (transposes + chains + finish) timed
+    # live with HIP events; its chain kernel alone in profiles/ (rocprofv3)
+    ref_roofline = None
+    if phase is not None and phase["method"] == "reference":
+        ref_roofline = {
+            "kernel": "reference-exact distance phase (chain_transpose_kernel + tap_chain_kernel + ref_chain_kernel "
+                      "+ ref_finish_kernel)",
+            "bound": "valu", "unit": "Gop/s", "achieved": phase["valu_lane_ops"] / (phase["ms"] * 1e-3) / 1e9,
+            "peak": VALU_PEAK_OPS / 1e9, "frac": phase["valu_frac"], "traffic": None,
+            "kernel_ms": phase["ms"], "lane_ops": phase["valu_lane_ops"],
+            "one_wave_issue_frac": phase["valu_frac"] * 2.0,
+            "note": "lane-ops = 2 (v_sub + v_fma) x 8 chains x K(K-1)/2 pairs x P/8 steps; peak = fp32 VALU at "
+                    "2 cycles per wave64 instruction per SIMD; one wave per SIMD issues at most every 4 cycles "
+                    "(MI355X_MICROARCH.md), so one_wave_issue_frac = 2 x frac is this layout's ceiling "
+                    "(the chains fill ~1 wave per SIMD at C3)",
+        }
     # training-phase time (one round's local updates, this rank's clients)
     ev0.record()
     if eng._graph is not None:
@@ -638,12 +675,8 @@ def main() -> None:
         if model == "vit_bert" else None,
         "collectives": round_collectives(eng, defense, K, P, world),
         "distance_phase": phase,
-        "roofline": {
-            "kernel": "gram_partials_kernel (Krum pairwise, centred Gram on MFMA)",
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel_ms": kernel_ms, "algorithmic_bytes": pair_bytes, "coords_per_gpu": n_coords,
-        },
+        "roofline": ref_roofline if ref_roofline is not None else gram_roofline,
+        "roofline_gram": gram_roofline if ref_roofline is not None else None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(spec, P, K, defense, f, multi_k, args.local_steps, rcfg.batch,

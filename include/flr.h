@@ -129,6 +129,16 @@ int flr_pairwise_l2_reference_tiles(int64_t K);
 int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx,
                               double* D, void* ws, size_t ws_bytes, int64_t part,
                               int64_t nparts, void* stream);
+/* The same over a training-order client matrix: the ntaps blocks taps[4b ..
+ * 4b+3] = {off, Cout, Cin, KK} (ascending, disjoint, inside [0, P)) hold a
+ * convolution weight stored tap-major, column off + (t * Cin + ci) * Cout + co
+ * for reference coordinate off + (co * Cin + ci) * KK + t (torch's
+ * [Cout][Cin][kh][kw]); every other column is its own coordinate.  The
+ * trainers' layout (flr_resnet_gru_reorder), so a round's matrix goes in as
+ * written, no torch-order copy; ntaps = 0 is flr_pairwise_l2_reference. */
+int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t P, int64_t ldx,
+                                  const int64_t* taps, int64_t ntaps, double* D, void* ws,
+                                  size_t ws_bytes, int64_t part, int64_t nparts, void* stream);
 
 /* Direct-difference VALU variant (same contract, exact fp32 differences);
  * a slower second implementation used to cross-check the MFMA path. */

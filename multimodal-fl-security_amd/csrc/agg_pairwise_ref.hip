@@ -39,6 +39,7 @@
 //  * chain c = the XCD (blockIdx % 8): an XCD's L2 holds only its own chain's
 //    streams.  40 KB of LDS per workgroup: four per CU, one wave per SIMD.
 // Chains longer than the segment carry their partial sums in A between segments.
+#include <cstdint>
 #include <type_traits>
 #include <utility>
 
@@ -133,12 +134,25 @@ __host__ __device__ inline int tile_of_pair(int i, int j) {
 // store.  (Per-lane 128-B rows read at 3 TB/s: 64 cache lines per load.)
 constexpr int TW = 256;        // steps per wave
 constexpr int TROW = TW + 4;   // LDS floats per chain row
+// Coordinate ranges another kernel writes (tap_chain_kernel): a wave whose
+// 2048 coordinates lie inside one of them skips its loads and stores.
+struct SkipRanges {
+  static constexpr int MAX = 32;
+  int n;
+  int64_t lo[MAX], hi[MAX];
+};
 __global__ __launch_bounds__(256) void chain_transpose_kernel(const float* __restrict__ X, int64_t ldx, int64_t r0,
-                                                              int64_t steps, int64_t ldc, float* __restrict__ Xc) {
+                                                              int64_t steps, int64_t ldc, float* __restrict__ Xc,
+                                                              const SkipRanges skip) {
   __shared__ __attribute__((aligned(16))) float t[4 * 8 * TROW];
   const int k = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * TW;
   if (s0 >= steps) return;  // the whole wave (no workgroup barrier below)
+  {
+    const int64_t u0 = 8 * (r0 + s0), u1 = u0 + 8 * TW;
+    for (int b = 0; b < skip.n; ++b)
+      if (u0 >= skip.lo[b] && u1 <= skip.hi[b]) return;
+  }
   const int nv = (int)(steps - s0 < TW ? steps - s0 : TW);
   const float* src = X + (int64_t)k * ldx + 8 * (r0 + s0);
   float* tw = t + wave * 8 * TROW;
@@ -167,6 +181,82 @@ __global__ __launch_bounds__(256) void chain_transpose_kernel(const float* __res
   } else {
     for (int c = 0; c < 8; ++c)
       for (int e = 0; e < 4 && 4 * lane + e < nv; ++e) dst[(int64_t)c * ldc + e] = tw[c * TROW + 4 * lane + e];
+  }
+}
+
+// The tap-major blocks of a training-order client matrix (a convolution
+// weight stored [KK][Cin][Cout], KK = kh * kw, whose reference order is
+// torch's [Cout][Cin][KK]): chain_transpose_kernel skips them, this kernel
+// writes their coordinates chain-major.  A workgroup takes a tile of 32 output
+// channels x CI input channels x every tap of one row: coalesced 128-B reads of
+// the training layout (32 channels of one (tap, input channel)) into LDS, then,
+// per output channel, its run of CI * KK consecutive torch coordinates written
+// chain-major (chain c = u % 8, step u / 8 - r0: CI * KK / 8 consecutive floats
+// per chain).  The next CI of the same channels continues those runs: tiles
+// are numbered channel-group-major and dealt to the XCDs in contiguous ranges
+// (blockIdx % 8 is the XCD), so the workgroups that fill one stretch of a chain
+// stream share an L2 and run together.  Grid (tiles, K).
+constexpr int TAP_CO = 32;
+constexpr int TAP_ROWS = 288;  // LDS tile rows (tap, input channel): CI = TAP_ROWS / KK
+template <int KKT, bool VEC>  // KKT: 9, 1, or 0 = KK at run time; VEC: 16-B aligned tile rows
+__global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict__ X, int64_t ldx, int64_t off,
+                                                        int Cout, int Cin, int KKr, int64_t r0, int64_t steps,
+                                                        int64_t ldc, float* __restrict__ Xc) {
+  __shared__ float tile[TAP_ROWS][TAP_CO + 1];
+  const int KK = KKT > 0 ? KKT : KKr;
+  const int CI = TAP_ROWS / KK;
+  const int nci_t = (Cin + CI - 1) / CI, ntiles = (int)gridDim.x;
+  // XCD-contiguous tile numbering: XCD x = blockIdx % 8 takes tiles
+  // [x * ntiles / 8, (x + 1) * ntiles / 8)
+  const int x = (int)(blockIdx.x & 7), j = (int)(blockIdx.x >> 3);
+  const int tl = x * (ntiles / 8) + min(x, ntiles % 8) + j;
+  const int co0 = (tl / nci_t) * TAP_CO, ci0 = (tl % nci_t) * CI;
+  const int nci = min(CI, Cin - ci0), nco_v = min(TAP_CO, Cout - co0);
+  const int k = blockIdx.y;
+  const float* row = X + (int64_t)k * ldx + off;
+  const int nrows = KK * CI;
+  // load: tile row r = t * CI + ci, column = output channel; every load of a
+  // thread issued before its LDS stores
+  if constexpr (VEC) {  // nco_v == 32: a row is 8 x 16 B
+    const int sub = threadIdx.x & 7, rr = threadIdx.x >> 3;
+    constexpr int IT = (TAP_ROWS + 31) / 32;
+    f32x4 v[IT];
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+      const int r = rr + 32 * q, t = r / CI, ci = r - t * CI;
+      v[q] = (r < nrows && ci < nci)
+                 ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(
+                       row + ((int64_t)t * Cin + ci0 + ci) * Cout + co0 + 4 * sub))
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+      const int r = rr + 32 * q;
+      if (r < nrows)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tile[r][4 * sub + e] = v[q][e];
+    }
+  } else {
+    for (int e = threadIdx.x; e < nrows * TAP_CO; e += 256) {
+      const int co = e % TAP_CO, r = e / TAP_CO, t = r / CI, ci = r % CI;
+      if (ci < nci && co < nco_v) tile[r][co] = row[((int64_t)t * Cin + ci0 + ci) * Cout + co0 + co];
+    }
+  }
+  __syncthreads();
+  // write: output channel co's run [u0, u0 + nci * KK) (at most 288
+  // coordinates: 38 steps per chain), clipped to the segment
+  // [8 r0, 8 (r0 + steps)); item i -> (co = i / 512, chain = i / 64 % 8,
+  // step = i % 64): a wave writes consecutive steps of one chain stream
+  const int64_t L = (int64_t)nci * KK;
+  const int64_t ulo = 8 * r0, uhi = 8 * (r0 + steps);
+  float* out = Xc + (int64_t)k * 8 * ldc;
+  for (int i = threadIdx.x; i < nco_v * 512; i += 256) {
+    const int ns = i & 63, c = (i >> 6) & 7, co = i >> 9;
+    const int64_t u0 = off + ((int64_t)(co0 + co) * Cin + ci0) * KK;
+    const int64_t u = 8 * ((u0 >> 3) + ns) + c;
+    if (u < u0 || u >= u0 + L || u < ulo || u >= uhi) continue;
+    const int rel = (int)(u - u0), ci = rel / KK, t = rel - ci * KK;
+    out[(int64_t)c * ldc + ((u >> 3) - r0)] = tile[t * CI + ci][co];
   }
 }
 
@@ -455,8 +545,12 @@ __global__ __launch_bounds__(64) void ref_chain_kernel(const float* __restrict__
 // D[i][j] = D[j][i] for the pairs of tiles [t0, t1): chains summed 0..7 in
 // order, the tail, correctly rounded sqrt; the other pairs 0 (the ranks' parts
 // are then summed: exactly one rank holds each pair), the diagonal 0.
-__global__ void ref_finish_kernel(const float* __restrict__ A, const float* __restrict__ X, int K, int64_t P,
-                                  int64_t ldx, int64_t R, int t0, int t1, double* __restrict__ D) {
+// the columns of the tail coordinates 8R .. P-1 (at most 7)
+struct TailCols {
+  int64_t c[8];
+};
+__global__ void ref_finish_kernel(const float* __restrict__ A, const float* __restrict__ X, const TailCols tc, int K,
+                                  int64_t P, int64_t ldx, int64_t R, int t0, int t1, double* __restrict__ D) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)K * K) return;
   const int i = (int)(idx / K), j = (int)(idx % K);
@@ -478,13 +572,14 @@ __global__ void ref_finish_kernel(const float* __restrict__ A, const float* __re
     const float* xi = X + (int64_t)i * ldx;
     const float* xj = X + (int64_t)j * ldx;
     int64_t t = R * 8;
+    auto col = [&](int64_t c) { return tc.c[c - R * 8]; };
     if (t + 4 <= P)
       for (const int64_t e = t + 4; t < e; ++t) {
-        const float d = xi[t] - xj[t];
+        const float d = xi[col(t)] - xj[col(t)];
         s = add_rn(s, mul_rn(d, d));
       }
     for (; t < P; ++t) {
-      const float d = xi[t] - xj[t];
+      const float d = xi[col(t)] - xj[col(t)];
       s = __builtin_fmaf(d, d, s);
     }
     v = (double)sqrt_rn(s);
@@ -519,11 +614,21 @@ extern "C" int flr_pairwise_l2_reference_tiles(int64_t K) {
   return ntiles_of((int)K);
 }
 
-extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx, double* D, void* ws,
-                                         size_t ws_bytes, int64_t part, int64_t nparts, void* stream) {
+extern "C" int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t P, int64_t ldx,
+                                             const int64_t* taps, int64_t ntaps, double* D, void* ws, size_t ws_bytes,
+                                             int64_t part, int64_t nparts, void* stream) {
   if (K < 1 || P < 0 || ldx < P || !D || (K > 1 && P > 0 && !X) || nparts < 1 || part < 0 || part >= nparts)
     return FLR_ERR_ARG;
   if (K > (1 << 15)) return FLR_ERR_UNSUPPORTED;
+  if (ntaps < 0 || (ntaps > 0 && !taps)) return FLR_ERR_ARG;
+  // tap-major blocks: {off, Cout, Cin, KK}, inside [0, P), ascending, disjoint
+  for (int64_t b = 0, end = 0; b < ntaps; ++b) {
+    const int64_t off = taps[4 * b], co = taps[4 * b + 1], ci = taps[4 * b + 2], kk = taps[4 * b + 3];
+    if (off < end || co < 1 || ci < 1 || kk < 1 || kk > TAP_ROWS || co > INT32_MAX || ci > INT32_MAX ||
+        off + co * ci * kk > P)
+      return FLR_ERR_ARG;
+    end = off + co * ci * kk;
+  }
   // 16-B loads of the rows
   if (K > 1 && P >= 8 && (((reinterpret_cast<uintptr_t>(X) & 15) != 0) || (ldx % 4) != 0)) return FLR_ERR_ARG;
   hipStream_t st = as_stream(stream);
@@ -541,21 +646,56 @@ extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, i
     const int64_t nseg = (R + ldc - 1) / ldc;
     const int64_t Rs = ((R + nseg - 1) / nseg + CS - 1) / CS * CS;  // <= ldc
     float* Xc = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + na);
+    SkipRanges skip;
+    skip.n = 0;
+    for (int64_t b = 0; b < ntaps && skip.n < SkipRanges::MAX; ++b) {
+      skip.lo[skip.n] = taps[4 * b];
+      skip.hi[skip.n++] = taps[4 * b] + taps[4 * b + 1] * taps[4 * b + 2] * taps[4 * b + 3];
+    }
     for (int64_t seg = 0; seg < nseg; ++seg) {
       const int64_t r0 = seg * Rs, steps = (R - r0 < Rs) ? R - r0 : Rs;
       if (steps <= 0) break;
       hipLaunchKernelGGL(chain_transpose_kernel, dim3((unsigned)((steps + 4 * TW - 1) / (4 * TW)), (unsigned)K),
-                         dim3(256), 0, st, X, ldx, r0, steps, ldc, Xc);
+                         dim3(256), 0, st, X, ldx, r0, steps, ldc, Xc, skip);
       int rc = launch_status("chain_transpose_kernel");
       if (rc != FLR_OK) return rc;
+      for (int64_t b = 0; b < ntaps; ++b) {  // the tap-major blocks of this segment, rewritten
+        const int64_t off = taps[4 * b], co = taps[4 * b + 1], ci = taps[4 * b + 2], kk = taps[4 * b + 3];
+        if (off + co * ci * kk <= 8 * r0 || off >= 8 * (r0 + steps)) continue;
+        const int64_t tiles = (co + TAP_CO - 1) / TAP_CO * ((ci + TAP_ROWS / kk - 1) / (TAP_ROWS / kk));
+        const bool vec = off % 4 == 0 && co % TAP_CO == 0;  // 16-B aligned rows, full 32-channel tiles
+        auto kern = kk == 9 ? (vec ? tap_chain_kernel<9, true> : tap_chain_kernel<9, false>)
+                  : kk == 1 ? (vec ? tap_chain_kernel<1, true> : tap_chain_kernel<1, false>)
+                            : (vec ? tap_chain_kernel<0, true> : tap_chain_kernel<0, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)tiles, (unsigned)K), dim3(256), 0, st, X, ldx, off, (int)co, (int)ci,
+                           (int)kk, r0, steps, ldc, Xc);
+        if ((rc = launch_status("tap_chain_kernel")) != FLR_OK) return rc;
+      }
       hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(64), 0, st, Xc, ldc, (int)K, steps, t0,
                          seg == 0 ? 1 : 0, A);
       rc = launch_status("ref_chain_kernel");
       if (rc != FLR_OK) return rc;
     }
   }
+  // the tail coordinates' columns (identity outside the tap-major blocks)
+  TailCols tc;
+  for (int64_t u = 8 * R; u < 8 * R + 8; ++u) {
+    int64_t c = u;
+    for (int64_t b = 0; b < ntaps && u < P; ++b) {
+      const int64_t off = taps[4 * b], co = taps[4 * b + 1], ci = taps[4 * b + 2], kk = taps[4 * b + 3];
+      if (u < off || u >= off + co * ci * kk) continue;
+      const int64_t rel = u - off, o = rel / (ci * kk), i = (rel / kk) % ci, t = rel % kk;
+      c = off + (t * ci + i) * co + o;
+    }
+    tc.c[u - 8 * R] = c;
+  }
   const int64_t kk = K * K;
-  hipLaunchKernelGGL(ref_finish_kernel, dim3((unsigned)((kk + 255) / 256)), dim3(256), 0, st, A, X, (int)K, P, ldx,
-                     R, t0, t1, D);
+  hipLaunchKernelGGL(ref_finish_kernel, dim3((unsigned)((kk + 255) / 256)), dim3(256), 0, st, A, X, tc, (int)K, P,
+                     ldx, R, t0, t1, D);
   return launch_status("ref_finish_kernel");
+}
+
+extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx, double* D, void* ws,
+                                         size_t ws_bytes, int64_t part, int64_t nparts, void* stream) {
+  return flr_pairwise_l2_reference_tap(X, K, P, ldx, nullptr, 0, D, ws, ws_bytes, part, nparts, stream);
 }

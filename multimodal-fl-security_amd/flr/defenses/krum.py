@@ -27,6 +27,9 @@ class KrumDefense(BaseDefense):
         # flr.shard.Comm of a multi-GPU round (set by RoundEngine): the
         # reference-exact distances then split their pair tiles over the ranks
         self.comm = None
+        # reference mode over a training-order client matrix: its tap-major
+        # convolution blocks [(off, Cout, Cin, KK), ...] (set by RoundEngine)
+        self.tap_blocks = None
         self.selected_clients: List[int] = []
         self.rejected_clients: List[int] = []
         self.client_scores: List[float] = []
@@ -41,7 +44,8 @@ class KrumDefense(BaseDefense):
         if n < 2 * f + 3:  # krum.py:153-157
             raise ValueError(
                 f"Krum requires n >= 2f + 3. Got n={n}, f={f}. Need at least {2 * f + 3} clients.")
-        self.distances = ops.pairwise_l2(cm.X, self.pairwise_method, comm=self.comm)
+        self.distances = ops.pairwise_l2(cm.X, self.pairwise_method, comm=self.comm,
+                                         tap_blocks=self.tap_blocks if self.pairwise_method == "reference" else None)
         self._check_refine_capacity(n)
         self.scores_device, self.order_device = ops.krum_select(self.distances, f)
         return self.order_device
@@ -69,15 +73,20 @@ class KrumDefense(BaseDefense):
 
     # pairwise_method="reference" reproduces the reference's torch.norm
     # accumulation, which runs over the whole vector in parameters() order:
-    # it needs whole rows (all-gather exchange) in torch order (no
-    # training-order rounds)
+    # it needs whole rows (all-gather exchange), in torch order or with
+    # tap_blocks naming the tap-major convolution weights (training-order rounds)
     @property
     def supports_sharded(self) -> bool:
         return self.pairwise_method != "reference"
 
     @property
     def order_free(self) -> bool:
-        return self.pairwise_method != "reference"
+        return True
+
+    @property
+    def needs_tap_blocks(self) -> bool:
+        """A training-order client matrix needs tap_blocks set (reference mode)."""
+        return self.pairwise_method == "reference"
 
     def aggregate_sharded(self, cs, num_examples: List[int], publish: bool = True, events=None) -> torch.Tensor:
         """Coordinate-sharded Krum (flr.shard): distances from the per-slice

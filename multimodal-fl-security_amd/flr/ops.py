@@ -7,7 +7,8 @@ wrong dtype or a missing library raises.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+import ctypes
+from typing import Optional, Sequence, Tuple
 
 import torch
 
@@ -35,13 +36,16 @@ def _check_matrix(X: torch.Tensor, name: str = "X") -> Tuple[int, int, int]:
     return X.shape[0], X.shape[1], X.stride(0)
 
 
-def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None, comm=None) -> torch.Tensor:
+def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None, comm=None,
+                tap_blocks: Optional[Sequence[Tuple[int, int, int, int]]] = None) -> torch.Tensor:
     """K×K float64 distances, D[i][j] = fp32 ||X_i - X_j|| (krum.py:73-99).
 
     method: "gram" (centred Gram on MFMA), "direct" (exact fp32 differences,
     fp32/fp64 partial sums) or "reference" (the reference's own torch.norm
-    accumulation, bit-identical D; X must then be in the reference's
-    coordinate order).
+    accumulation, bit-identical D over the reference's coordinate order:
+    X's columns in that order, or tap_blocks [(off, Cout, Cin, KK), ...]
+    naming the convolution weights X holds tap-major — a training-order
+    matrix, no reordered copy; include/flr.h flr_pairwise_l2_reference_tap).
     events: optional (begin, end) raw hipEvent_t handles recorded around the
     main MFMA kernel (flr.timing.HipEventPair).
     comm: optional flr.shard.Comm for the reference mode: every rank holds the
@@ -57,8 +61,10 @@ def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None, comm=None) -
         part, nparts = (0, 1) if comm is None else (comm.rank, comm.world)
         nbytes = int(_capi.lib().flr_pairwise_l2_reference_workspace(K, P))
         ws, wp = _ws(nbytes, X.device)
-        _capi.call("flr_pairwise_l2_reference", X.data_ptr(), K, P, ldx, D.data_ptr(), wp, nbytes, part, nparts,
-                   _stream(X))
+        taps = [int(v) for blk in (tap_blocks or ()) for v in blk]
+        tarr = (ctypes.c_int64 * max(1, len(taps)))(*taps)
+        _capi.call("flr_pairwise_l2_reference_tap", X.data_ptr(), K, P, ldx, ctypes.addressof(tarr), len(taps) // 4,
+                   D.data_ptr(), wp, nbytes, part, nparts, _stream(X))
         if nparts > 1:
             comm.all_reduce_sum(D)
         return D

@@ -127,10 +127,44 @@ class RoundEngine:
         # gtrain is the global model in that order (FLR_ORDER=torch: off)
         self.train_order = (getattr(self.defense, "order_free", False) and not self._wants_global
                             and os.environ.get("FLR_ORDER", "train") != "torch")
+        if self.train_order and getattr(self.defense, "needs_tap_blocks", False):
+            # the reference-exact distances read the training-order matrix,
+            # told which blocks are tap-major (no torch-order copy)
+            ok, taps = self._tap_blocks()
+            self.train_order = ok
+            self.defense.tap_blocks = taps if ok else None
         self.gtrain = self.trainer.to_train_order(self.global_flat) if self.train_order else None
         self.round_index = 0
         self.fell_back = False
         self.fallback_error: Optional[str] = None   # exception type of the last FedAvg fallback
+
+    def _tap_blocks(self):
+        """(ok, blocks): the training-order matrix's tap-major convolution
+        weights [(off, Cout, Cin, KK), ...] (flr_pairwise_l2_reference_tap),
+        checked once against the trainer's own reorder of a column-index
+        vector (float32: exact below 2^24 coordinates; past that, or on any
+        mismatch, ok=False: a torch-order round)."""
+        from .models.multimodal import param_layout, tap_major_names
+        P = self.trainer.P
+        if P >= 1 << 24:
+            return False, None
+        tapn = tap_major_names(self.spec) if self.spec.family != "vit_bert" else frozenset()
+        blocks, off = [], 0
+        for name, shape in param_layout(self.spec):
+            n = 1
+            for d in shape:
+                n *= int(d)
+            if name in tapn:
+                blocks.append((off, int(shape[0]), int(shape[1]), int(shape[2]) * int(shape[3])))
+            off += n
+        want = torch.arange(P, dtype=torch.int64, device=self.device)
+        for o, co, ci, kk in blocks:
+            u = torch.arange(co * ci * kk, dtype=torch.int64, device=self.device)
+            want[o:o + co * ci * kk] = o + ((u % kk) * ci + (u // kk) % ci) * co + u // (ci * kk)
+        got = self.trainer.to_torch_order(torch.arange(P, dtype=torch.float32, device=self.device))
+        if not torch.equal(got.to(torch.int64), want):
+            return False, None
+        return True, blocks
 
     def _num_flipped(self) -> int:
         """Local rows of sign-flip attackers (clients 0..f-1): they submit

@@ -83,9 +83,10 @@ def test_reference_mode_c3_fixtures(cuda, path):
 
 def test_reference_mode_round_engine(cuda):
     """A round with Krum in the reference mode: the engine hands the defense
-    whole rows in the reference's coordinate order (all-gather exchange, no
-    training-order rows), and D / selection / rejection equal the oracle's
-    torch.norm loop on those rows."""
+    whole rows (all-gather exchange) in the trainer's coordinate order with
+    the map of each reference coordinate's column, and D / selection /
+    rejection equal the oracle's torch.norm loop on the rows in the
+    reference's order."""
     from flr.models.multimodal import TINY
     from flr.round import RoundConfig, RoundEngine
     from flr.train import TrainConfig
@@ -93,12 +94,49 @@ def test_reference_mode_round_engine(cuda):
     rc = RoundConfig(num_clients=K, batch=4, defense="krum", num_attackers=f,
                      defense_cfg={"pairwise_method": "reference"})
     eng = RoundEngine(TINY, rc, TrainConfig(local_steps=2), cuda)
-    assert eng.exchange == "allgather" and not eng.train_order
+    assert eng.exchange == "allgather" and eng.train_order
     eng.run_round()
     eng.defense.publish()
     P = eng.trainer.P
-    rows = [eng.trainer.X.data[k, :P].cpu() for k in range(K)]
+    rows = [eng.trainer.to_torch_order(eng.trainer.X.data[k, :P]).cpu() for k in range(K)]
     _, scores, sel, rej, dist = orc.krum([[r] for r in rows], f, K // 2)
     assert np.array_equal(eng.defense.distances.cpu().numpy(), dist)
     assert eng.defense.client_scores == [float(s) for s in scores]
     assert eng.defense.selected_clients == sel and eng.defense.rejected_clients == rej
+
+
+@pytest.mark.parametrize("K,blocks", [
+    (16, [(5, 64, 64, 9), (36_869 + 7, 64, 3, 9), (36_869 + 7 + 1728 + 3, 128, 64, 1)]),
+    (33, [(0, 128, 64, 9), (73_728 + 1, 40, 24, 9)]),
+    (128, [(100, 512, 256, 9), (100 + 1_179_648 + 13, 64, 64, 1)])])
+def test_reference_mode_tap_major_blocks(cuda, K, blocks):
+    """A training-order matrix (convolution weights stored tap-major, column
+    off + (t * Cin + ci) * Cout + co for reference coordinate
+    off + (co * Cin + ci) * KK + t) read through flr_pairwise_l2_reference_tap:
+    D bit-identical to the reference-order matrix's.  Blocks at odd offsets
+    (chain steps shared with the plain columns beside them), partial 32-channel
+    tiles, KK 9 and 1, a block reaching the tail."""
+    P = max(o + co * ci * kk for o, co, ci, kk in blocks) + 5
+    X, data = _matrix(K, P, 13 + K, cuda)
+    train = data.clone()
+    for o, co, ci, kk in blocks:
+        w = data[:, o:o + co * ci * kk].reshape(K, co, ci, kk)
+        train[:, o:o + co * ci * kk] = w.permute(0, 3, 2, 1).reshape(K, -1)
+    D = ops.pairwise_l2(train[:, :P], "reference", tap_blocks=blocks).cpu().numpy()
+    want = ops.pairwise_l2(data[:, :P], "reference").cpu().numpy()
+    assert np.array_equal(D, want)
+    if K <= 33:
+        assert np.array_equal(D, normref.distance_matrix(X.numpy()))
+
+
+def test_reference_mode_tap_blocks_reach_the_tail(cuda):
+    """A tap-major block ending at P with P % 8 != 0: the tail coordinates'
+    columns come from the block."""
+    K, blocks = 9, [(3, 64, 8, 9)]
+    P = 3 + 64 * 8 * 9
+    X, data = _matrix(K, P, 99, cuda)
+    train = data.clone()
+    w = data[:, 3:P].reshape(K, 64, 8, 9)
+    train[:, 3:P] = w.permute(0, 3, 2, 1).reshape(K, -1)
+    D = ops.pairwise_l2(train[:, :P], "reference", tap_blocks=blocks).cpu().numpy()
+    assert np.array_equal(D, normref.distance_matrix(X.numpy()))
