@@ -23,7 +23,10 @@ class KrumDefense(BaseDefense):
         super().__init__(defense_config)
         self.num_malicious = defense_config.get("num_malicious", 1)
         self.multi_k = defense_config.get("multi_k", 1)
-        self.pairwise_method = defense_config.get("pairwise_method", "gram")
+        # "reference" (default): D bit-identical to the reference's torch.norm,
+        # so the selection is the reference's by construction; "gram": the
+        # centred Gram on MFMA (HBM-bound, coordinate-sharded: the scaling path)
+        self.pairwise_method = defense_config.get("pairwise_method", "reference")
         # flr.shard.Comm of a multi-GPU round (set by RoundEngine): the
         # reference-exact distances then split their pair tiles over the ranks
         self.comm = None

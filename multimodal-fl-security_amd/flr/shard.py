@@ -178,7 +178,10 @@ def _stream(t: torch.Tensor) -> int:
 
 def pack_for_exchange(local: torch.Tensor, P: int, plan: CoordPlan, send: torch.Tensor) -> None:
     """send [world, K_local, ld] <- local [K_local, >=P] cut at the ranks'
-    coordinate ranges (block r = columns plan.coords(r))."""
+    coordinate ranges (block r = columns plan.coords(r)).  Only the gloo
+    rehearsal of CUDA tensors uses it (the staged all-to-all needs one
+    contiguous send buffer); RCCL and CPU ranks exchange the row pieces as
+    they lie (CoordExchange.exchange)."""
     K_l = local.shape[0]
     for r in range(plan.world):
         b, e = plan.coords(r)
@@ -190,8 +193,17 @@ def pack_for_exchange(local: torch.Tensor, P: int, plan: CoordPlan, send: torch.
 
 
 class CoordExchange:
-    """The all-to-all of a round: client-sharded rows in, coordinate slice out.
-    Buffers are allocated once and reused every round."""
+    """The exchange of a round: client-sharded rows in, coordinate slice out.
+    Buffers are allocated once and reused every round.
+
+    The transpose of the client sharding is a set of row pieces: rank s's
+    client k sends its columns plan.coords(r) to rank r, where they land as
+    row k of block s (recv[s][k][:n_r]).  Each piece is a contiguous run of
+    the trainer's own row, so RCCL sends it in place (one batch of p2p
+    sends / receives, K_local per peer): no pack copy of the local matrix
+    (round 4's all_to_all_single needed one contiguous send buffer: a read
+    and a write of the whole local matrix per round).  Only this rank's own
+    block is copied, local -> recv."""
 
     def __init__(self, K: int, K_local: int, P: int, device, comm: Optional[Comm] = None):
         self.comm = comm or Comm()
@@ -201,12 +213,37 @@ class CoordExchange:
         world = self.comm.world
         self.send = self.recv = None
         if world > 1:
-            self.send = torch.zeros(world, K_local, ld, dtype=torch.float32, device=device)
             self.recv = torch.zeros(world, K_local, ld, dtype=torch.float32, device=device)
+            if self.comm.staged and torch.device(device).type == "cuda":
+                self.send = torch.zeros(world, K_local, ld, dtype=torch.float32, device=device)
 
     def exchange(self, local: torch.Tensor) -> CoordSlice:
         if self.comm.world == 1:  # one GPU holds every coordinate: no copy
             return CoordSlice(local, self.plan, 0, self.comm)
-        pack_for_exchange(local, self.plan.P, self.plan, self.send)
-        self.comm.all_to_all(self.recv, self.send)  # recv block s = rank s's clients
+        if self.send is not None:  # gloo staging CUDA tensors through the host: one all-to-all
+            pack_for_exchange(local, self.plan.P, self.plan, self.send)
+            self.comm.all_to_all(self.recv, self.send)  # recv block s = rank s's clients
+        else:
+            self._exchange_pieces(local)
         return CoordSlice(self.recv.view(self.K, self.plan.ld), self.plan, self.comm.rank, self.comm)
+
+    def _exchange_pieces(self, local: torch.Tensor) -> None:
+        plan, me, world = self.plan, self.comm.rank, self.comm.world
+        K_l = local.shape[0]
+        b, e = plan.coords(me)
+        n = e - b
+        if local.is_cuda:  # this rank's own block
+            _capi.call("flr_copy_rows", local.data_ptr() + 4 * b, local.stride(0), n, self.recv[me].data_ptr(),
+                       plan.ld, K_l, _stream(local))
+        else:
+            self.recv[me, :, :n].copy_(local[:, b:e])
+        ops = []
+        for step in range(1, world):  # peers in ring order from this rank: every pair's sends interleave
+            dst, src = (me + step) % world, (me - step) % world
+            bd, ed = plan.coords(dst)
+            for k in range(K_l):
+                ops.append(dist.P2POp(dist.isend, local[k, bd:ed], dst, group=self.comm.group))
+            for k in range(K_l):
+                ops.append(dist.P2POp(dist.irecv, self.recv[src, k, :n], src, group=self.comm.group))
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()

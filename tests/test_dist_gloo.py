@@ -94,8 +94,10 @@ def _shard_worker(rank, world, port, K, P, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_gloo_coordinate_exchange(world):
+    """The exchange's row pieces (batched p2p, no pack copy) over gloo on CPU
+    ranks: every rank's slice is all K clients' columns of its range."""
     K, P = 8, 64 * 8 * 5 + 29
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -143,12 +143,15 @@ def test_pairwise_far_cluster_overflow_is_loud(cuda):
     D = ops.pairwise_l2(X[:, :P], "gram")
     assert torch.isnan(D).all()
     for publish in (True, False):
-        d = KrumDefense({"num_malicious": f, "multi_k": K // 2})
+        d = KrumDefense({"num_malicious": f, "multi_k": K // 2, "pairwise_method": "gram"})
         with pytest.raises(FlrError):
             d.aggregate_flat(ClientMatrix(X, P, [(P,)]), [1] * K, publish=publish)
-    # the exact paths have no such limit
+    # the exact paths have no such limit (the reference mode: the default)
     Dd = ops.pairwise_l2(X[:, :P], "direct")
     assert not torch.isnan(Dd).any()
+    d = KrumDefense({"num_malicious": f, "multi_k": K // 2})
+    d.aggregate_flat(ClientMatrix(X, P, [(P,)]), [1] * K)
+    assert not torch.isnan(d.distances).any()
 
 
 def test_krum_nan_client_is_rejected(cuda):

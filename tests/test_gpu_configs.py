@@ -119,9 +119,12 @@ def _order_report(scores_a, scores_b, scores64, multi_k):
 @pytest.mark.timeout(900)
 def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
     """C3 exactly as bench.py runs it (K = 128, B = 32, 5 local steps, full
-    P): the engine's Multi-Krum selection equals the reference's — fp32
-    torch.norm distances of the trained (sign-flipped) rows in torch order,
-    numpy scores, np.argsort (krum.py:89-97, 126-129, 174)."""
+    P; the default reference-exact distances over the training-order matrix):
+    the engine's D is the reference's bit for bit — fp32 torch.norm distances
+    of the trained (sign-flipped) rows in torch order — so its scores, selected
+    and rejected lists are the reference's (krum.py:89-97, 126-129, 174).  The
+    Gram path's D on the same rows is recorded beside it (selection equal where
+    the scores are well conditioned)."""
     spec = ModelSpec()
     K, f, B, steps, mk = 128, 25, 32, 5, 64
     rc = RoundConfig(num_clients=K, batch=B, defense="krum", attack="sign_flip", num_attackers=f)
@@ -141,13 +144,16 @@ def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
         Xt[k, :P].copy_(r)
         rows.append(r.cpu())
     t_copy = time.perf_counter() - t0
-    # the reference-exact mode (pairwise_method="reference") on the same rows
+    # the reference-exact mode on the torch-order copy (the engine read the
+    # training-order matrix through its tap-major blocks), and the Gram path
+    assert eng.defense.pairwise_method == "reference" and eng.train_order
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()  # the op's kernels run on torch's current stream
     D_mode = ops.pairwise_l2(Xt[:, :P], "reference")
     ev1.record()
     torch.cuda.synchronize()
     mode_ms = ev0.elapsed_time(ev1)
+    D_gram = ops.pairwise_l2(Xt[:, :P], "gram").cpu().numpy()
     _, order_mode = ops.krum_select(D_mode, f)
     order_mode = order_mode.cpu().tolist()
     D_mode = D_mode.cpu().numpy()
@@ -185,15 +191,20 @@ def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
         "reference_mode_rejected_identical": order_mode[mk:] == rej_ref,
         "reference_mode_kernel_ms": mode_ms,
         "selected_reference": sel_ref, "selected_gpu": eng.defense.selected_clients,
+        "engine_D_bit_identical": bool(np.array_equal(D_gpu.cpu().numpy(), D_ref)),
+        "gram_distance_rel_err_vs_fp64": float(np.max(np.abs(D_gram - D64h)[off] / D64h[off])),
+        "gram_selected_identical": np.argsort(np.asarray(orc.krum_scores(D_gram, m)))[:mk].tolist() == sel_ref,
     }
     _record("c3_krum_trained_round.json", payload)
     # the reference-exact mode: the reference's D bit for bit, so its whole order
     assert np.array_equal(D_mode, D_ref)
     assert order_mode[:mk] == sel_ref and order_mode[mk:] == rej_ref
-    # the production (centred Gram) path: the selected clients, in order
-    assert eng.defense.selected_clients == sel_ref
+    # the engine (the default reference-exact distances): D, scores and the
+    # whole order are the reference's
+    assert np.array_equal(D_gpu.cpu().numpy(), D_ref)
+    assert eng.defense.client_scores == [float(v) for v in s_ref]
+    assert eng.defense.selected_clients == sel_ref and eng.defense.rejected_clients == rej_ref
     assert not set(eng.defense.selected_clients) & set(range(f))
-    assert rep["differences_within_error"], rep["positions_differing"]
 
 
 def _strided(P: int, n: int = 1_100_000) -> torch.Tensor:
@@ -294,7 +305,20 @@ def test_c5_round_backdoor_krum_trimmed_mean(cuda):
     D64 = fp64_distances(X, P)
     off = ~torch.eye(K, dtype=torch.bool, device=cuda)
     dist_err = ((D_gpu - D64).abs()[off] / D64[off]).max().item()
-    assert dist_err < 5e-5, dist_err
+    # the default reference-exact distances: sampled pairs bit-identical to the
+    # reference's fp32 torch.norm accumulation (oracle/norm_ref.c) of the
+    # torch-order rows; the whole D within the reference's own fp32 error of fp64
+    assert eng.defense.pairwise_method == "reference"
+    from oracle import normref
+    ks = [0, 1, 101, 102, 300, 511]
+    rows = {k: (eng.trainer.to_torch_order(X[k]) if eng.train_order else X[k]).cpu().numpy() for k in ks}
+    Dh = D_gpu.cpu().numpy()
+    for a in range(len(ks)):
+        for b in range(a + 1, len(ks)):
+            i, j = ks[a], ks[b]
+            assert Dh[i, j] == normref.norm_diff(rows[i], rows[j]), (i, j)
+    del rows
+    assert dist_err < 1e-2, dist_err
     m, mk = K - f - 2, K // 2
     s_gpu = orc.krum_scores(D_gpu.cpu().numpy(), m)
     s64 = orc.krum_scores(D64.cpu().numpy(), m)

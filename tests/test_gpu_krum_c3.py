@@ -62,7 +62,7 @@ def test_c3_krum_fixture_bitexact_selection(cuda, path, terms, knob):
     data = torch.zeros((K, padded_ld(P)), dtype=torch.float32, device=cuda)
     data[:, :P] = X.to(cuda)
     cm = ClientMatrix(data, P, [(P,)])
-    d = KrumDefense({"num_malicious": f, "multi_k": mk})
+    d = KrumDefense({"num_malicious": f, "multi_k": mk, "pairwise_method": "gram"})
     flat = d.aggregate_flat(cm, [1] * K)
     D = d.distances.cpu().numpy()
     assert np.all(np.diag(D) == 0) and np.array_equal(D, D.T)

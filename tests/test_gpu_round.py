@@ -72,7 +72,8 @@ def test_round_refine_overflow_raises(cuda):
     (run_round never calls publish), instead of ranking a NaN matrix; with the
     FedAvg fallback on, device errors stay loud by default."""
     from flr._capi import FlrError
-    kw = dict(num_clients=300, batch=4, defense="krum", attack="sign_flip", num_attackers=140, graph=False)
+    kw = dict(num_clients=300, batch=4, defense="krum", attack="sign_flip", num_attackers=140, graph=False,
+              defense_cfg={"pairwise_method": "gram"})
     for fb in (False, True):
         eng = RoundEngine(TINY, RoundConfig(fallback_fedavg=fb, **kw), TrainConfig(local_steps=1), cuda)
         with pytest.raises(FlrError):

@@ -83,8 +83,8 @@ def test_slice_chunks_match_library():
             assert (a.value, b.value) == slice_chunks(P, q)
 
 
-@pytest.mark.parametrize("name,cfg", [("krum", {"num_malicious": 3, "multi_k": 8}),
-                                      ("krum", {"num_malicious": 3, "multi_k": 1}),
+@pytest.mark.parametrize("name,cfg", [("krum", {"num_malicious": 3, "multi_k": 8, "pairwise_method": "gram"}),
+                                      ("krum", {"num_malicious": 3, "multi_k": 1, "pairwise_method": "gram"}),
                                       ("trimmed_mean", {"trim_ratio": 0.2}), ("median", {}), ("fedavg", {})])
 def test_sharded_defense_world1_equals_flat(cuda, name, cfg):
     """World 1: the sharded entry point on the whole matrix == aggregate_flat."""
@@ -122,7 +122,7 @@ def _round_worker(rank, world, port, defense, q, exchange="alltoall"):
     from flr.models.multimodal import TINY
     from flr.round import RoundConfig, RoundEngine
     from flr.train import TrainConfig
-    cfg = {"trim_ratio": 0.2} if defense == "trimmed_mean" else {}
+    cfg = {"trim_ratio": 0.2} if defense == "trimmed_mean" else {"pairwise_method": "gram"} if defense == "krum" else {}
     if defense == "krum_ref":  # the reference-exact distances: pair tiles split over the ranks
         defense, cfg = "krum", {"pairwise_method": "reference"}
     rc = RoundConfig(num_clients=8, batch=4, defense=defense, num_attackers=1, exchange=exchange, defense_cfg=cfg)
