@@ -520,9 +520,6 @@ def main() -> None:
             d.comm = getattr(eng.defense, "comm", None)
             d.tap_blocks = (eng.defense.tap_blocks if hasattr(eng.defense, "tap_blocks") else
                             eng._tap_blocks()[1] if eng.train_order else None)
-        if name == "krum" and args.pairwise == "reference" and sharded:
-            aggregate_ms_all[name] = None  # whole rows only (this round is coordinate-sharded)
-            continue
         kwd = {"publish": False} if hasattr(d, "publish") else {}
         run = ((lambda: eng.slice.gather_vector(d.aggregate_sharded(eng.slice, eng.num_examples, **kwd),
                                                 torch.empty_like(eng.global_flat))) if sharded else
@@ -556,7 +553,7 @@ def main() -> None:
         for _ in range(reps):
             ev0.record()
             if sharded:
-                ops.pairwise_l2_sharded(eng.slice)
+                eng.defense._sharded_distances(eng.slice)
             else:
                 ops.pairwise_l2(eng.full.X, method, comm=getattr(eng.defense, "comm", None),
                                 tap_blocks=getattr(eng.defense, "tap_blocks", None) if method == "reference" else None)

@@ -139,6 +139,20 @@ int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx,
 int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t P, int64_t ldx,
                                   const int64_t* taps, int64_t ntaps, double* D, void* ws,
                                   size_t ws_bytes, int64_t part, int64_t nparts, void* stream);
+/* The same split over coordinate ranges held by different ranks (the
+ * coordinate-sharded exchange): each range continues the chains where the
+ * previous range left them.  _partial: `steps` chain steps of X (coordinates
+ * 0 .. 8 steps - 1 of each row; a range starting at a multiple of 8 reference
+ * coordinates) added to the running chain sums held in ws's first 8 K^2 floats
+ * (first: start from 0; otherwise the previous range's ws sums, copied in);
+ * ws as for flr_pairwise_l2_reference_workspace(K, 8 steps).  _finish: D from
+ * the chain sums (chains = 0: none) and the last P mod 8 coordinates (Xtail,
+ * ntail <= 7).  Each step is the same fp32 operation in the same order as in
+ * the one-call form, so D is bit-identical to it. */
+int flr_pairwise_l2_reference_partial(const float* X, int64_t K, int64_t steps, int64_t ldx,
+                                      int first, void* ws, size_t ws_bytes, void* stream);
+int flr_pairwise_l2_reference_finish(const float* Xtail, int64_t K, int64_t ntail, int64_t ldx,
+                                     int chains, const void* ws, double* D, void* stream);
 
 /* Direct-difference VALU variant (same contract, exact fp32 differences);
  * a slower second implementation used to cross-check the MFMA path. */

@@ -549,8 +549,9 @@ __global__ __launch_bounds__(64) void ref_chain_kernel(const float* __restrict__
 struct TailCols {
   int64_t c[8];
 };
-__global__ void ref_finish_kernel(const float* __restrict__ A, const float* __restrict__ X, const TailCols tc, int K,
-                                  int64_t P, int64_t ldx, int64_t R, int t0, int t1, double* __restrict__ D) {
+__global__ void ref_finish_kernel(const float* __restrict__ A, int chains, const float* __restrict__ X,
+                                  const TailCols tc, int K, int64_t P, int64_t ldx, int64_t R, int t0, int t1,
+                                  double* __restrict__ D) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)K * K) return;
   const int i = (int)(idx / K), j = (int)(idx % K);
@@ -563,7 +564,7 @@ __global__ void ref_finish_kernel(const float* __restrict__ A, const float* __re
   double v = 0.0;
   if (tile >= t0 && tile < t1) {
     float s = 0.f;
-    if (R > 0) {
+    if (chains) {
       const int64_t kk = (int64_t)K * K, p = (int64_t)i * K + j;
       s = A[p];
 #pragma unroll
@@ -614,6 +615,60 @@ extern "C" int flr_pairwise_l2_reference_tiles(int64_t K) {
   return ntiles_of((int)K);
 }
 
+// The chains of tiles [t0, t1) over `steps` chain steps of X (coordinates
+// 0 .. 8 steps - 1 of each row), continuing the sums in A (first: from 0):
+// per segment the chain-major transpose (skipping the tap-major blocks), the
+// tap blocks' rewrite, the chain kernel.
+static int run_chains(const float* X, int64_t K, int64_t steps_total, int64_t ldx, const int64_t* taps, int64_t ntaps,
+                      int first, float* A, void* ws, size_t ws_bytes, int t0, int t1, hipStream_t st) {
+  const size_t na = a_bytes(K);
+  if (ws_bytes < na) return FLR_ERR_WORKSPACE;
+  const int64_t R = steps_total;
+  const int64_t per_step = K * 8 * 4;
+  const int64_t ldc = (int64_t)((ws_bytes - na) / (size_t)per_step) / CS * CS;
+  if (ldc < CS) return FLR_ERR_WORKSPACE;
+  const int64_t nseg = (R + ldc - 1) / ldc;
+  const int64_t Rs = ((R + nseg - 1) / nseg + CS - 1) / CS * CS;  // <= ldc
+  float* Xc = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + na);
+  SkipRanges skip;
+  skip.n = 0;
+  for (int64_t b = 0; b < ntaps && skip.n < SkipRanges::MAX; ++b) {
+    skip.lo[skip.n] = taps[4 * b];
+    skip.hi[skip.n++] = taps[4 * b] + taps[4 * b + 1] * taps[4 * b + 2] * taps[4 * b + 3];
+  }
+  for (int64_t seg = 0; seg < nseg; ++seg) {
+    const int64_t r0 = seg * Rs, steps = (R - r0 < Rs) ? R - r0 : Rs;
+    if (steps <= 0) break;
+    hipLaunchKernelGGL(chain_transpose_kernel, dim3((unsigned)((steps + 4 * TW - 1) / (4 * TW)), (unsigned)K),
+                       dim3(256), 0, st, X, ldx, r0, steps, ldc, Xc, skip);
+    int rc = launch_status("chain_transpose_kernel");
+    if (rc != FLR_OK) return rc;
+    for (int64_t b = 0; b < ntaps; ++b) {  // the tap-major blocks of this segment, rewritten
+      const int64_t off = taps[4 * b], co = taps[4 * b + 1], ci = taps[4 * b + 2], kk = taps[4 * b + 3];
+      if (off + co * ci * kk <= 8 * r0 || off >= 8 * (r0 + steps)) continue;
+      const int64_t tiles = (co + TAP_CO - 1) / TAP_CO * ((ci + TAP_ROWS / kk - 1) / (TAP_ROWS / kk));
+      const bool vec = off % 4 == 0 && co % TAP_CO == 0;  // 16-B aligned rows, full 32-channel tiles
+      auto kern = kk == 9 ? (vec ? tap_chain_kernel<9, true> : tap_chain_kernel<9, false>)
+                : kk == 1 ? (vec ? tap_chain_kernel<1, true> : tap_chain_kernel<1, false>)
+                          : (vec ? tap_chain_kernel<0, true> : tap_chain_kernel<0, false>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)tiles, (unsigned)K), dim3(256), 0, st, X, ldx, off, (int)co, (int)ci,
+                         (int)kk, r0, steps, ldc, Xc);
+      if ((rc = launch_status("tap_chain_kernel")) != FLR_OK) return rc;
+    }
+    hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(64), 0, st, Xc, ldc, (int)K, steps, t0,
+                       (first && seg == 0) ? 1 : 0, A);
+    rc = launch_status("ref_chain_kernel");
+    if (rc != FLR_OK) return rc;
+  }
+  return FLR_OK;
+}
+
+static int check_rows(const float* X, int64_t K, int64_t n, int64_t ldx) {
+  // 16-B loads of the rows
+  if (K > 1 && n >= 8 && (((reinterpret_cast<uintptr_t>(X) & 15) != 0) || (ldx % 4) != 0)) return FLR_ERR_ARG;
+  return FLR_OK;
+}
+
 extern "C" int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t P, int64_t ldx,
                                              const int64_t* taps, int64_t ntaps, double* D, void* ws, size_t ws_bytes,
                                              int64_t part, int64_t nparts, void* stream) {
@@ -629,54 +684,17 @@ extern "C" int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t 
       return FLR_ERR_ARG;
     end = off + co * ci * kk;
   }
-  // 16-B loads of the rows
-  if (K > 1 && P >= 8 && (((reinterpret_cast<uintptr_t>(X) & 15) != 0) || (ldx % 4) != 0)) return FLR_ERR_ARG;
+  int rc = check_rows(X, K, P, ldx);
+  if (rc != FLR_OK) return rc;
   hipStream_t st = as_stream(stream);
   const int64_t R = P / 8;
-  const size_t na = a_bytes(K);
   if (K > 1 && R > 0 && (!ws || (reinterpret_cast<uintptr_t>(ws) & 255) != 0)) return FLR_ERR_WORKSPACE;
   const int ntiles = K > 1 ? ntiles_of((int)K) : 0;
   const int t0 = (int)(part * ntiles / nparts), t1 = (int)((part + 1) * ntiles / nparts);
   float* A = reinterpret_cast<float*>(ws);
-  if (K > 1 && R > 0 && t1 > t0) {
-    if (ws_bytes < na) return FLR_ERR_WORKSPACE;
-    const int64_t per_step = K * 8 * 4;
-    const int64_t ldc = (int64_t)((ws_bytes - na) / (size_t)per_step) / CS * CS;
-    if (ldc < CS) return FLR_ERR_WORKSPACE;
-    const int64_t nseg = (R + ldc - 1) / ldc;
-    const int64_t Rs = ((R + nseg - 1) / nseg + CS - 1) / CS * CS;  // <= ldc
-    float* Xc = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + na);
-    SkipRanges skip;
-    skip.n = 0;
-    for (int64_t b = 0; b < ntaps && skip.n < SkipRanges::MAX; ++b) {
-      skip.lo[skip.n] = taps[4 * b];
-      skip.hi[skip.n++] = taps[4 * b] + taps[4 * b + 1] * taps[4 * b + 2] * taps[4 * b + 3];
-    }
-    for (int64_t seg = 0; seg < nseg; ++seg) {
-      const int64_t r0 = seg * Rs, steps = (R - r0 < Rs) ? R - r0 : Rs;
-      if (steps <= 0) break;
-      hipLaunchKernelGGL(chain_transpose_kernel, dim3((unsigned)((steps + 4 * TW - 1) / (4 * TW)), (unsigned)K),
-                         dim3(256), 0, st, X, ldx, r0, steps, ldc, Xc, skip);
-      int rc = launch_status("chain_transpose_kernel");
-      if (rc != FLR_OK) return rc;
-      for (int64_t b = 0; b < ntaps; ++b) {  // the tap-major blocks of this segment, rewritten
-        const int64_t off = taps[4 * b], co = taps[4 * b + 1], ci = taps[4 * b + 2], kk = taps[4 * b + 3];
-        if (off + co * ci * kk <= 8 * r0 || off >= 8 * (r0 + steps)) continue;
-        const int64_t tiles = (co + TAP_CO - 1) / TAP_CO * ((ci + TAP_ROWS / kk - 1) / (TAP_ROWS / kk));
-        const bool vec = off % 4 == 0 && co % TAP_CO == 0;  // 16-B aligned rows, full 32-channel tiles
-        auto kern = kk == 9 ? (vec ? tap_chain_kernel<9, true> : tap_chain_kernel<9, false>)
-                  : kk == 1 ? (vec ? tap_chain_kernel<1, true> : tap_chain_kernel<1, false>)
-                            : (vec ? tap_chain_kernel<0, true> : tap_chain_kernel<0, false>);
-        hipLaunchKernelGGL(kern, dim3((unsigned)tiles, (unsigned)K), dim3(256), 0, st, X, ldx, off, (int)co, (int)ci,
-                           (int)kk, r0, steps, ldc, Xc);
-        if ((rc = launch_status("tap_chain_kernel")) != FLR_OK) return rc;
-      }
-      hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(64), 0, st, Xc, ldc, (int)K, steps, t0,
-                         seg == 0 ? 1 : 0, A);
-      rc = launch_status("ref_chain_kernel");
-      if (rc != FLR_OK) return rc;
-    }
-  }
+  if (K > 1 && R > 0 && t1 > t0 &&
+      (rc = run_chains(X, K, R, ldx, taps, ntaps, 1, A, ws, ws_bytes, t0, t1, st)) != FLR_OK)
+    return rc;
   // the tail coordinates' columns (identity outside the tap-major blocks)
   TailCols tc;
   for (int64_t u = 8 * R; u < 8 * R + 8; ++u) {
@@ -690,12 +708,45 @@ extern "C" int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t 
     tc.c[u - 8 * R] = c;
   }
   const int64_t kk = K * K;
-  hipLaunchKernelGGL(ref_finish_kernel, dim3((unsigned)((kk + 255) / 256)), dim3(256), 0, st, A, X, tc, (int)K, P,
-                     ldx, R, t0, t1, D);
+  hipLaunchKernelGGL(ref_finish_kernel, dim3((unsigned)((kk + 255) / 256)), dim3(256), 0, st, A, R > 0 ? 1 : 0, X, tc,
+                     (int)K, P, ldx, R, t0, t1, D);
   return launch_status("ref_finish_kernel");
 }
 
 extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx, double* D, void* ws,
                                          size_t ws_bytes, int64_t part, int64_t nparts, void* stream) {
   return flr_pairwise_l2_reference_tap(X, K, P, ldx, nullptr, 0, D, ws, ws_bytes, part, nparts, stream);
+}
+
+extern "C" int flr_pairwise_l2_reference_partial(const float* X, int64_t K, int64_t steps, int64_t ldx, int first,
+                                                 void* ws, size_t ws_bytes, void* stream) {
+  if (K < 1 || steps < 0 || ldx < 8 * steps || (K > 1 && steps > 0 && !X)) return FLR_ERR_ARG;
+  if (K > (1 << 15)) return FLR_ERR_UNSUPPORTED;
+  int rc = check_rows(X, K, 8 * steps, ldx);
+  if (rc != FLR_OK) return rc;
+  if (!ws || (reinterpret_cast<uintptr_t>(ws) & 255) != 0 || ws_bytes < a_bytes(K)) return FLR_ERR_WORKSPACE;
+  hipStream_t st = as_stream(stream);
+  float* A = reinterpret_cast<float*>(ws);
+  if (K < 2) return FLR_OK;
+  if (steps == 0) {  // nothing to add; a first call still starts every chain at 0
+    if (first && hipMemsetAsync(A, 0, (size_t)8 * K * K * 4, st) != hipSuccess)
+      return launch_status("reference distances: zero the chains");
+    return FLR_OK;
+  }
+  return run_chains(X, K, steps, ldx, nullptr, 0, first, A, ws, ws_bytes, 0, ntiles_of((int)K), st);
+}
+
+extern "C" int flr_pairwise_l2_reference_finish(const float* Xtail, int64_t K, int64_t ntail, int64_t ldx,
+                                                int chains, const void* ws, double* D, void* stream) {
+  if (K < 1 || ntail < 0 || ntail > 7 || ldx < ntail || !D || (K > 1 && ntail > 0 && !Xtail) ||
+      (K > 1 && chains && !ws))
+    return FLR_ERR_ARG;
+  if (K > (1 << 15)) return FLR_ERR_UNSUPPORTED;
+  TailCols tc;
+  for (int u = 0; u < 8; ++u) tc.c[u] = u;
+  const int64_t kk = K * K;
+  hipLaunchKernelGGL(ref_finish_kernel, dim3((unsigned)((kk + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float*>(ws), chains ? 1 : 0, Xtail, tc, (int)K, ntail, ldx, (int64_t)0, 0,
+                     K > 1 ? ntiles_of((int)K) : 0, D);
+  return launch_status("ref_finish_kernel");
 }

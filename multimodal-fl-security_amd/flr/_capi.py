@@ -54,6 +54,8 @@ SIGNATURES = {
                                          _c_void_p]),
     "flr_pairwise_l2_reference_tap": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p, _c_void_p,
                                              _size_t, _i64, _i64, _c_void_p]),
+    "flr_pairwise_l2_reference_partial": (_int, [_c_void_p, _i64, _i64, _i64, _int, _c_void_p, _size_t, _c_void_p]),
+    "flr_pairwise_l2_reference_finish": (_int, [_c_void_p, _i64, _i64, _i64, _int, _c_void_p, _c_void_p, _c_void_p]),
     "flr_pairwise_l2_direct_workspace": (_size_t, [_i64, _i64]),
     "flr_pairwise_l2_direct": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "flr_krum_select": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),

@@ -76,11 +76,12 @@ class KrumDefense(BaseDefense):
 
     # pairwise_method="reference" reproduces the reference's torch.norm
     # accumulation, which runs over the whole vector in parameters() order:
-    # it needs whole rows (all-gather exchange), in torch order or with
-    # tap_blocks naming the tap-major convolution weights (training-order rounds)
+    # whole rows (all-gather exchange) in torch order or with tap_blocks naming
+    # the tap-major convolution weights (training-order rounds), or coordinate
+    # slices in torch order (the chains run through the ranks in order)
     @property
     def supports_sharded(self) -> bool:
-        return self.pairwise_method != "reference"
+        return True
 
     @property
     def order_free(self) -> bool:
@@ -99,7 +100,7 @@ class KrumDefense(BaseDefense):
         if n < 2 * f + 3:  # krum.py:153-157
             raise ValueError(
                 f"Krum requires n >= 2f + 3. Got n={n}, f={f}. Need at least {2 * f + 3} clients.")
-        self.distances = ops.pairwise_l2_sharded(cs, events=events)
+        self.distances = self._sharded_distances(cs, events)
         self._check_refine_capacity(n)
         self.scores_device, self.order_device = ops.krum_select(self.distances, f)
         if publish:
@@ -107,6 +108,17 @@ class KrumDefense(BaseDefense):
         if self.multi_k == 1:
             return cs.data[self.order_device[0].long(), : cs.n]
         return ops.rows_mean(cs.X, self.order_device[: min(self.multi_k, n)], divisor=self.multi_k)
+
+    def _sharded_distances(self, cs, events=None):
+        if self.pairwise_method == "reference":
+            if cs.comm.world == 1:  # the one slice is the whole matrix
+                return ops.pairwise_l2(cs.X, "reference", tap_blocks=self.tap_blocks)
+            if self.tap_blocks:
+                raise ValueError("reference-exact distances over coordinate slices need torch-order slices")
+            return ops.pairwise_l2_reference_sharded(cs)
+        if self.pairwise_method != "gram":
+            raise ValueError(f"pairwise_method {self.pairwise_method!r} has no coordinate-sharded form")
+        return ops.pairwise_l2_sharded(cs, events=events)
 
     def publish(self) -> None:
         """Host copies of scores / selected / rejected (krum.py:171-176).  A
@@ -191,7 +203,7 @@ class KrumTrimmedMeanDefense(KrumDefense):
         if n < 2 * f + 3:  # krum.py:153-157
             raise ValueError(
                 f"Krum requires n >= 2f + 3. Got n={n}, f={f}. Need at least {2 * f + 3} clients.")
-        self.distances = ops.pairwise_l2_sharded(cs, events=events)
+        self.distances = self._sharded_distances(cs, events)
         self._check_refine_capacity(n)
         self.scores_device, self.order_device = ops.krum_select(self.distances, f)
         if publish:

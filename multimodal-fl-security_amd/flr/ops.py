@@ -225,6 +225,48 @@ def _ws(nbytes: int, device) -> Tuple[torch.Tensor, int]:
     return ws, ws.data_ptr() + (-ws.data_ptr()) % 256
 
 
+def pairwise_l2_reference_sharded(cs) -> torch.Tensor:
+    """The reference-exact distances (pairwise_l2 "reference") from coordinate
+    slices (flr.shard.CoordSlice, the reference's coordinate order): the
+    chains run through the ranks in order — rank r continues every pair's 8
+    chains over its coordinate range from where rank r-1 left them (the
+    8·K² fp32 sums passed on), the last rank adds the P mod 8 tail and takes
+    the square roots, and D is broadcast.  Each chain step is the same fp32
+    operation in the same order as on one GPU, so D is bit-identical to
+    pairwise_l2(X, "reference") at every world size.  A chain cannot be split,
+    so the ranks run one after another: the phase costs about the one-GPU
+    chain time at any G, with only this rank's 1/G of the rows transposed."""
+    lib = _capi.lib()
+    K, P, dev = cs.K, cs.P, cs.data.device
+    X, ld = cs.data, cs.data.stride(0)
+    comm, rank, world = cs.comm, cs.comm.rank, cs.comm.world
+    R = P // 8
+    full_end = min(cs.end, 8 * R)
+    steps = max(0, full_end - cs.begin) // 8
+    if cs.begin % 8:
+        raise ValueError("coordinate slices must start at a multiple of 8 coordinates")
+    if X.data_ptr() % 16 or ld % 4:
+        raise ValueError("coordinate slice rows must be 16-B aligned")
+    nbytes = int(lib.flr_pairwise_l2_reference_workspace(K, 8 * steps))
+    ws, wp = _ws(nbytes, dev)
+    st = _stream(X)
+    A = torch.empty(0, dtype=torch.float32, device=dev)
+    if K > 1:
+        A = torch.as_strided(ws, (8 * K * K * 4,), (1,), (wp - ws.data_ptr())).view(torch.float32)
+        if rank > 0:
+            comm.recv(A, rank - 1)
+        _capi.call("flr_pairwise_l2_reference_partial", X.data_ptr(), K, steps, ld, int(rank == 0), wp, nbytes, st)
+        if rank < world - 1:
+            comm.send(A, rank + 1)
+    D = torch.empty((K, K), dtype=torch.float64, device=dev)
+    if rank == world - 1:
+        ntail = P - 8 * R
+        xt = X.data_ptr() + 4 * (8 * R - cs.begin)
+        _capi.call("flr_pairwise_l2_reference_finish", xt, K, ntail, ld, int(R > 0), wp, D.data_ptr(), st)
+    comm.broadcast(D, world - 1)
+    return D
+
+
 def pairwise_l2_sharded(cs, events=None) -> torch.Tensor:
     """K×K float64 distances from a coordinate slice (flr.shard.CoordSlice):
     every rank ends with the same D, bit-identical to pairwise_l2 on the

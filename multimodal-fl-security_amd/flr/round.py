@@ -127,6 +127,10 @@ class RoundEngine:
         # gtrain is the global model in that order (FLR_ORDER=torch: off)
         self.train_order = (getattr(self.defense, "order_free", False) and not self._wants_global
                             and os.environ.get("FLR_ORDER", "train") != "torch")
+        if (self.train_order and getattr(self.defense, "needs_tap_blocks", False) and self.exchange == "alltoall"
+                and world > 1):
+            # coordinate slices of the reference-exact chains: torch-order slices
+            self.train_order = False
         if self.train_order and getattr(self.defense, "needs_tap_blocks", False):
             # the reference-exact distances read the training-order matrix,
             # told which blocks are tap-major (no torch-order copy)

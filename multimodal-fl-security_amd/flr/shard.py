@@ -104,6 +104,23 @@ class Comm:
         if ho is not out:
             out.copy_(ho)
 
+    def send(self, t: torch.Tensor, dst: int) -> None:
+        dist.send(self._host(t.contiguous()), dst, group=self.group)
+
+    def recv(self, t: torch.Tensor, src: int) -> None:
+        h = self._host(t)
+        dist.recv(h, src, group=self.group)
+        if h is not t:
+            t.copy_(h)
+
+    def broadcast(self, t: torch.Tensor, src: int) -> None:
+        if self.world == 1:
+            return
+        h = self._host(t)
+        dist.broadcast(h, src, group=self.group)
+        if h is not t:
+            t.copy_(h)
+
     def all_to_all(self, out: torch.Tensor, t: torch.Tensor) -> None:
         """Equal splits along dim 0: block r of t goes to rank r; out block s came from rank s."""
         if self.world == 1:

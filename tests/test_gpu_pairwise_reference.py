@@ -83,7 +83,7 @@ def test_reference_mode_c3_fixtures(cuda, path):
 
 def test_reference_mode_round_engine(cuda):
     """A round with Krum in the reference mode: the engine hands the defense
-    whole rows (all-gather exchange) in the trainer's coordinate order with
+    whole rows in the trainer's coordinate order with
     the map of each reference coordinate's column, and D / selection /
     rejection equal the oracle's torch.norm loop on the rows in the
     reference's order."""
@@ -94,7 +94,7 @@ def test_reference_mode_round_engine(cuda):
     rc = RoundConfig(num_clients=K, batch=4, defense="krum", num_attackers=f,
                      defense_cfg={"pairwise_method": "reference"})
     eng = RoundEngine(TINY, rc, TrainConfig(local_steps=2), cuda)
-    assert eng.exchange == "allgather" and eng.train_order
+    assert eng.train_order  # one GPU: the one coordinate slice is the whole matrix
     eng.run_round()
     eng.defense.publish()
     P = eng.trainer.P

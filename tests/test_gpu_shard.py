@@ -180,12 +180,14 @@ def test_sharded_round_four_ranks_equals_one(cuda, defense, exchange):
 
 
 @pytest.mark.parametrize("defense,exchange", [("krum", "alltoall"), ("krum", "allgather"), ("median", "alltoall"),
-                                              ("krum_ref", "allgather")])
+                                              ("krum_ref", "allgather"), ("krum_ref", "alltoall")])
 def test_sharded_round_eight_ranks_equals_one(cuda, defense, exchange):
     """World 8, the node's GPU count (one client per rank at K = 8): every
     rank's global model, Krum selection and distance matrix equal the one-rank
     round bit for bit, for both exchanges and for the reference-exact distances
-    whose pair tiles split over the ranks (one exact all-reduce of D)."""
+    — whole rows with their pair tiles split over the ranks (one exact
+    all-reduce of D), or coordinate slices whose chains run through the ranks
+    in order (the default exchange of the benchmarked C3 path)."""
     one = _run(1, defense, exchange)
     eight = _run(8, defense, exchange)
     for r in range(8):
@@ -194,10 +196,12 @@ def test_sharded_round_eight_ranks_equals_one(cuda, defense, exchange):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_reference_distances_split_over_ranks(cuda, world):
-    """The reference-exact Krum distances with their pair tiles split over 2 / 4
-    ranks (allgather exchange): bit-identical to one rank."""
-    one = _run(1, "krum_ref", "allgather")
-    many = _run(world, "krum_ref", "allgather")
+@pytest.mark.parametrize("exchange", ["allgather", "alltoall"])
+def test_reference_distances_split_over_ranks(cuda, world, exchange):
+    """The reference-exact Krum distances over 2 / 4 ranks: pair tiles split
+    (allgather) or the chains handed from rank to rank over the coordinate
+    slices (alltoall): bit-identical to one rank."""
+    one = _run(1, "krum_ref", exchange)
+    many = _run(world, "krum_ref", exchange)
     for r in range(world):
         assert np.array_equal(one[0][1], many[r][1]) and one[0][2] == many[r][2], r
