@@ -114,7 +114,8 @@ int flr_pairwise_finish(const double* gsum, const double* tail, int64_t K, doubl
  * summed 0..7 in order, the P mod 8 tail added in order (a first group of 4
  * as separate multiply + add, the last 0..3 as fma), correctly rounded
  * sqrt_f32 (tail probed in tools/diag_norm_host.py;
- * oracle/norm_ref.c).  X in the reference's coordinate order (parameters()
+ * oracle/norm_ref.c; the same bits under torch's AVX2 and AVX512 dispatch,
+ * tests/test_oracle.py test_norm_ref_model_cpu_capability).  X in the reference's coordinate order (parameters()
  * order); rows 16-B aligned and ldx % 4 == 0 (else FLR_ERR_ARG).
  * Workspace (256-B aligned): flr_pairwise_l2_reference_workspace(K, P) bytes
  * — the chains' running sums plus one chain-major copy of a coordinate segment

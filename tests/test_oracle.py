@@ -204,3 +204,43 @@ def test_norm_ref_distance_matrix_equals_oracle():
     X[:3] = -X[:3]
     want = orc.distance_matrix([[X[k]] for k in range(9)])
     assert np.array_equal(normref.distance_matrix(X.numpy()), want)
+
+
+_CAP_SCRIPT = r"""
+import sys, json, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from oracle import normref
+g = np.random.default_rng(5)
+bad = 0
+for n in (7, 8, 15, 16, 17, 31, 33, 100, 1023, 4101, 100003, 1 << 20):
+    for t in range(4):
+        a = g.standard_normal(n).astype(np.float32) * np.float32(10.0 ** g.uniform(-3, 3))
+        b = g.standard_normal(n).astype(np.float32)
+        bad += torch.norm(torch.from_numpy(a) - torch.from_numpy(b)).item() != normref.norm_diff(a, b)
+print(json.dumps({"capability": torch.backends.cpu.get_cpu_capability(), "mismatches": int(bad)}))
+"""
+
+
+@pytest.mark.parametrize("cap", [None, "avx2", "avx512"])
+def test_norm_ref_model_cpu_capability(cap):
+    """the 8-lane accumulation is ATen's Vectorized<float> width on
+    the AVX2 path; pinned here under each SIMD dispatch this torch offers
+    (ATEN_CPU_CAPABILITY), the capability recorded: the same bits on AVX2 and
+    AVX512 (this container reports AVX512 by default, the GPU boxes' EPYC 9575F
+    too).  A capability whose torch.norm differed would fail here."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    if cap:
+        env["ATEN_CPU_CAPABILITY"] = cap
+    out = subprocess.run([sys.executable, "-c", _CAP_SCRIPT, root], env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    print(f"\n[torch.norm capability] requested {cap}: {rec}")
+    if cap:
+        assert rec["capability"].lower() == cap
+    assert rec["mismatches"] == 0, rec
