@@ -120,7 +120,9 @@ int flr_pairwise_finish(const double* gsum, const double* tail, int64_t K, doubl
  * Workspace (256-B aligned): flr_pairwise_l2_reference_workspace(K, P) bytes
  * — the chains' running sums plus one chain-major copy of a coordinate segment
  * (at most 8 GiB; a smaller workspace runs more, shorter segments, the same
- * result).  part / nparts: this call computes the pairs of tile range
+ * result; segments hold whole multiples of 512 chain steps, zero-filled past
+ * the last, plus 4 KB of prefetch slack: below K x 16 KiB + 4 KiB past the
+ * sums, FLR_ERR_WORKSPACE).  part / nparts: this call computes the pairs of tile range
  * [part * T / nparts, (part + 1) * T / nparts), T =
  * flr_pairwise_l2_reference_tiles(K), and writes 0 for every other pair: the
  * nparts results summed (exact: one non-zero term per pair) are the whole D.

@@ -65,8 +65,15 @@ constexpr int SROWS = 20;          // staged rows per stage (diagonal tiles read
 constexpr int NSTAGE = FLR_REF_NSTAGE;    // LDS ring = the loop's unroll (DMA NSTAGE - 1 chunks ahead)
 constexpr int STAGE = SROWS * CS;         // floats per stage (5 KB)
 constexpr int64_t XC_CAP = int64_t(8) << 30;  // bytes of one chain-major segment
+constexpr int64_t XC_SLACK = 4096;            // bytes past the last stream the chunk prefetch may read
+// A segment's streams are zero-filled from its last step up to a multiple of
+// XC_GROUP steps (one loop trip of the chain kernel): fma(0, 0, s) = s for the
+// non-negative sums, so the loop runs whole groups without a per-chunk check
+// and the last, partial chunk needs no separate path.
+constexpr int64_t XC_GROUP = (int64_t)NSTAGE * CS;
 static_assert(CS == 64 && NQ == 16, "x_i layout: 16 lanes x 4 steps per chunk");
 static_assert(NSTAGE % 2 == 0 && NSTAGE >= 4, "two register buffers");
+static_assert((NSTAGE - 1) * CS * 4 <= XC_SLACK, "the prefetch past a stream stays inside the slack");
 static_assert((NSTAGE - 1) * STAGE * 4 < 65536, "ds_read_b128's 16-bit offset reaches every stage");
 static_assert(NSTAGE * STAGE * 4 > 163840 / 5, "LDS caps the CU at four workgroups: one wave per SIMD");
 template <bool DIAG>
@@ -377,8 +384,10 @@ __device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, U..
 //   issue DMA(ch + NSTAGE - 1) into that stage and x_i(ch + NSTAGE - 1);
 //         ds_read_b128 x 16 of chunk ch + 1 into the other register buffer
 //   chain chunk ch (registers read in body ch - 1)
-// Every body issues the same vector-memory ops (clamped to the last chunk), so
-// the counts are static; the LDS reads and the register loads are inline asm
+// Every body issues the same vector-memory ops (past the last group they read
+// the next stream or the workspace slack: nothing consumes them), so the counts
+// are static; the loop runs whole groups of NSTAGE chunks over the zero-filled
+// streams (XC_GROUP), without a per-chunk check; the LDS reads and the register loads are inline asm
 // with explicit waits (the compiler's waitcnt pass, merging across the
 // rotated registers, drained vmcnt(0) every chunk).  No workgroup barrier:
 // the wave is the workgroup and reads only what it staged.
@@ -437,29 +446,32 @@ __device__ __forceinline__ void ref_chain_tile(float* lds, const Tile T, const i
   const int irow0 = min(SB * T.X + IW * T.g, K - 1);
   const char* sbi = reinterpret_cast<const char*>(Xc + (int64_t)irow0 * rs + (int64_t)c * ldc);
   const uint32_t voi = (uint32_t)((int64_t)((i < K ? i : K - 1) - irow0) * rs * 4 + 16 * jl);
-  const int nch = (int)((steps + CS - 1) / CS), nfull = (int)(steps / CS), lastc = nch - 1;
-  auto clampc = [&](int ch) { return ch < lastc ? ch : lastc; };
+  const int ngroup = (int)((steps + XC_GROUP - 1) / XC_GROUP);  // zero-filled past `steps`
   // DMA(ch) into stage `slot`, then x_i(ch) into register set x (inline asm:
   // hipcc built 64-bit addresses per DMA instead of the saddr form)
   auto issue = [&](int ch, int slot, f32x4& x) {
-    const int64_t co = (int64_t)clampc(ch) * CS * 4;  // the chunk's byte offset in a stream
+    // the chunk's byte offset in a stream: the prefetch runs up to NSTAGE - 1
+    // chunks past the last one (reads nothing consumes; the workspace carries
+    // XC_SLACK bytes past the last stream)
+    const int64_t co = (int64_t)ch * CS * 4;
     if (FLR_REF_ABL == 3) return;
     const char* sb = sbj + co;
     const uint32_t m = (uint32_t)(uintptr_t)lds + 4 * slot * STAGE + 2048;
-    uint32_t keep;
-    // M0 is written in the statement that reads it and restored (compiler-reserved)
+    // M0 written in the statement that reads it; no other instruction of this
+    // kernel reads M0 (the compiler emits none: checked in the ISA), so it is
+    // not restored
 #define FLR_DMA(n, off) "global_load_lds_dwordx4 %[v" #n "], %[sb] offset:" #off "\n\t"
     if constexpr (S::DPW == 5)
-      asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[m]\n\ts_nop 0\n\t" FLR_DMA(0, -2048) FLR_DMA(1, -1024)
-                       FLR_DMA(2, 0) FLR_DMA(3, 1024) FLR_DMA(4, 2048) "s_mov_b32 m0, %[keep]"
-                   : [keep] "=&s"(keep)
+      asm volatile("s_mov_b32 m0, %[m]\n\ts_nop 0\n\t" FLR_DMA(0, -2048) FLR_DMA(1, -1024) FLR_DMA(2, 0)
+                       FLR_DMA(3, 1024) FLR_DMA(4, 2048)
+                   :
                    : [m] "s"(m), [sb] "s"(sb), [v0] "v"(voj[0]), [v1] "v"(voj[1]), [v2] "v"(voj[2]), [v3] "v"(voj[3]),
                      [v4] "v"(voj[S::DPW - 1])
                    : "memory");
     else
-      asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[m]\n\ts_nop 0\n\t" FLR_DMA(0, -2048) FLR_DMA(1, -1024)
-                       FLR_DMA(2, 0) FLR_DMA(3, 1024) "s_mov_b32 m0, %[keep]"
-                   : [keep] "=&s"(keep)
+      asm volatile("s_mov_b32 m0, %[m]\n\ts_nop 0\n\t" FLR_DMA(0, -2048) FLR_DMA(1, -1024) FLR_DMA(2, 0)
+                       FLR_DMA(3, 1024)
+                   :
                    : [m] "s"(m), [sb] "s"(sb), [v0] "v"(voj[0]), [v1] "v"(voj[1]), [v2] "v"(voj[2]), [v3] "v"(voj[3])
                    : "memory");
 #undef FLR_DMA
@@ -487,23 +499,20 @@ __device__ __forceinline__ void ref_chain_tile(float* lds, const Tile T, const i
     // x_i load and the NSTAGE - 3 bodies since (x_i(ch) is older: covered)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 3) * S::OPB + 1) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // chunk ch's x_j
+    // chunk ch's operands arrived at the waits above: tie them to here
+    asm volatile("" : "+v"(vc[0]), "+v"(vc[1]), "+v"(vc[2]), "+v"(vc[3]), "+v"(vc[4]), "+v"(vc[5]), "+v"(vc[6]),
+                 "+v"(vc[7]), "+v"(vc[8]), "+v"(vc[9]), "+v"(vc[10]), "+v"(vc[11]), "+v"(vc[12]), "+v"(vc[13]),
+                 "+v"(vc[14]), "+v"(vc[15]), "+v"(xs[u]));
     issue(ch + NSTAGE - 1, (u + NSTAGE - 1) % NSTAGE, xs[(u + NSTAGE - 1) % NSTAGE]);
     rows(std::integral_constant<int, (u + 1) % NSTAGE>{}, vn, ra);
-    if (ch < nfull) {
-      // chunk ch's operands arrived before the waits above: tie them to here
-      asm volatile("" : "+v"(vc[0]), "+v"(vc[1]), "+v"(vc[2]), "+v"(vc[3]), "+v"(vc[4]), "+v"(vc[5]), "+v"(vc[6]),
-                   "+v"(vc[7]), "+v"(vc[8]), "+v"(vc[9]), "+v"(vc[10]), "+v"(vc[11]), "+v"(vc[12]), "+v"(vc[13]),
-                   "+v"(vc[14]), "+v"(vc[15]), "+v"(xs[u]));
-      if (FLR_REF_ABL != 5) acc = chain_chunk(xs[u], vc, acc);
-    }
+    if (FLR_REF_ABL != 5) acc = chain_chunk(xs[u], vc, acc);
   };
   // prologue = the issues of bodies -(NSTAGE-1) .. -1, then chunk 0's rows
 #pragma unroll
   for (int u = 0; u < NSTAGE - 1; ++u) issue(u, u, xs[u]);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * S::OPB + 1) : "memory");  // DMA(0)
   rows(std::integral_constant<int, 0>{}, va, ra);
-  const int nloop = (nfull + NSTAGE - 1) / NSTAGE * NSTAGE;
-  for (int ch = 0; ch < nloop; ch += NSTAGE)
+  for (int ch = 0; ch < ngroup * NSTAGE; ch += NSTAGE)
     static_for(
         [&](auto U) {
           constexpr int u = decltype(U)::value;
@@ -514,16 +523,6 @@ __device__ __forceinline__ void ref_chain_tile(float* lds, const Tile T, const i
         },
         std::make_integer_sequence<int, NSTAGE>{});
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  if (nfull < nch) {
-    // the last, partial chunk: staged as chunk nfull in stage nfull % NSTAGE
-    // (the clamped DMAs after it rewrote that stage with the same bytes)
-    const float* rd = lds + srow * CS + (nfull % NSTAGE) * STAGE;
-    const float* xi = Xc + (int64_t)(i < K ? i : K - 1) * rs + (int64_t)c * ldc + (int64_t)nfull * CS;
-    for (int s2 = 0; s2 < (int)(steps - (int64_t)nfull * CS); ++s2) {
-      const float d = xi[s2] - rd[4 * ((s2 >> 2) ^ rsw) + (s2 & 3)];
-      acc = __builtin_fmaf(d, d, acc);
-    }
-  }
   if (valid) A[((int64_t)c * K + lo) * K + hi] = acc;
 }
 
@@ -603,11 +602,11 @@ extern "C" size_t flr_pairwise_l2_reference_workspace(int64_t K, int64_t P) {
   const int64_t R = P / 8;
   size_t n = a_bytes(K);
   if (K < 2 || R == 0) return n;
-  const int64_t Rc = (R + CS - 1) / CS * CS;
+  const int64_t Rc = (R + XC_GROUP - 1) / XC_GROUP * XC_GROUP;
   const int64_t per_step = K * 8 * 4;
   const int64_t nseg = (per_step * Rc + XC_CAP - 1) / XC_CAP;
-  const int64_t Rs = ((R + nseg - 1) / nseg + CS - 1) / CS * CS;
-  return n + (size_t)(per_step * Rs);
+  const int64_t Rs = ((R + nseg - 1) / nseg + XC_GROUP - 1) / XC_GROUP * XC_GROUP;
+  return n + (size_t)(per_step * Rs + XC_SLACK);
 }
 
 extern "C" int flr_pairwise_l2_reference_tiles(int64_t K) {
@@ -625,10 +624,11 @@ static int run_chains(const float* X, int64_t K, int64_t steps_total, int64_t ld
   if (ws_bytes < na) return FLR_ERR_WORKSPACE;
   const int64_t R = steps_total;
   const int64_t per_step = K * 8 * 4;
-  const int64_t ldc = (int64_t)((ws_bytes - na) / (size_t)per_step) / CS * CS;
-  if (ldc < CS) return FLR_ERR_WORKSPACE;
+  if (ws_bytes < na + (size_t)XC_SLACK) return FLR_ERR_WORKSPACE;
+  const int64_t ldc = (int64_t)((ws_bytes - na - XC_SLACK) / (size_t)per_step) / XC_GROUP * XC_GROUP;
+  if (ldc < XC_GROUP) return FLR_ERR_WORKSPACE;
   const int64_t nseg = (R + ldc - 1) / ldc;
-  const int64_t Rs = ((R + nseg - 1) / nseg + CS - 1) / CS * CS;  // <= ldc
+  const int64_t Rs = ((R + nseg - 1) / nseg + XC_GROUP - 1) / XC_GROUP * XC_GROUP;  // <= ldc
   float* Xc = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + na);
   SkipRanges skip;
   skip.n = 0;
@@ -655,6 +655,10 @@ static int run_chains(const float* X, int64_t K, int64_t steps_total, int64_t ld
                          (int)kk, r0, steps, ldc, Xc);
       if ((rc = launch_status("tap_chain_kernel")) != FLR_OK) return rc;
     }
+    const int64_t padded = (steps + XC_GROUP - 1) / XC_GROUP * XC_GROUP;  // <= Rs <= ldc
+    if (padded > steps &&
+        hipMemset2DAsync(Xc + steps, (size_t)ldc * 4, 0, (size_t)(padded - steps) * 4, (size_t)(K * 8), st) != hipSuccess)
+      return FLR_ERR_HIP;
     hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(64), 0, st, Xc, ldc, (int)K, steps, t0,
                        (first && seg == 0) ? 1 : 0, A);
     rc = launch_status("ref_chain_kernel");
