@@ -205,32 +205,35 @@ __global__ __launch_bounds__(256) void chain_transpose_kernel(const float* __res
 // stream share an L2 and run together.  Grid (tiles, K).
 constexpr int TAP_CO = 32;
 constexpr int TAP_ROWS = 288;  // LDS tile rows (tap, input channel): CI = TAP_ROWS / KK
-template <int KKT, bool VEC>  // KKT: 9, 1, or 0 = KK at run time; VEC: 16-B aligned tile rows
+// WR: the write phase (0 one (co, chain) run per 64 items, 1 the same unrolled,
+// 2 dense items, falling back to 1's loop for a ragged tile); TCO x TROWS: the tile
+template <int KKT, bool VEC, int WR, int TCO = TAP_CO, int TROWS = TAP_ROWS>
 __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict__ X, int64_t ldx, int64_t off,
                                                         int Cout, int Cin, int KKr, int64_t r0, int64_t steps,
                                                         int64_t ldc, float* __restrict__ Xc) {
-  __shared__ float tile[TAP_ROWS][TAP_CO + 1];
+  __shared__ float tile[TROWS][TCO + 1];
   const int KK = KKT > 0 ? KKT : KKr;
-  const int CI = TAP_ROWS / KK;
+  const int CI = TROWS / KK;
   const int nci_t = (Cin + CI - 1) / CI, ntiles = (int)gridDim.x;
   // XCD-contiguous tile numbering: XCD x = blockIdx % 8 takes tiles
   // [x * ntiles / 8, (x + 1) * ntiles / 8)
   const int x = (int)(blockIdx.x & 7), j = (int)(blockIdx.x >> 3);
   const int tl = x * (ntiles / 8) + min(x, ntiles % 8) + j;
-  const int co0 = (tl / nci_t) * TAP_CO, ci0 = (tl % nci_t) * CI;
-  const int nci = min(CI, Cin - ci0), nco_v = min(TAP_CO, Cout - co0);
+  const int co0 = (tl / nci_t) * TCO, ci0 = (tl % nci_t) * CI;
+  const int nci = min(CI, Cin - ci0), nco_v = min(TCO, Cout - co0);
   const int k = blockIdx.y;
   const float* row = X + (int64_t)k * ldx + off;
   const int nrows = KK * CI;
   // load: tile row r = t * CI + ci, column = output channel; every load of a
   // thread issued before its LDS stores
-  if constexpr (VEC) {  // nco_v == 32: a row is 8 x 16 B
-    const int sub = threadIdx.x & 7, rr = threadIdx.x >> 3;
-    constexpr int IT = (TAP_ROWS + 31) / 32;
+  if constexpr (VEC) {  // nco_v == TCO: a row is TCO / 4 pieces of 16 B
+    constexpr int LPR = TCO / 4, RPP = 256 / LPR;  // lanes per row, rows per pass
+    const int sub = threadIdx.x % LPR, rr = threadIdx.x / LPR;
+    constexpr int IT = (TROWS + RPP - 1) / RPP;
     f32x4 v[IT];
 #pragma unroll
     for (int q = 0; q < IT; ++q) {
-      const int r = rr + 32 * q, t = r / CI, ci = r - t * CI;
+      const int r = rr + RPP * q, t = r / CI, ci = r - t * CI;
       v[q] = (r < nrows && ci < nci)
                  ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(
                        row + ((int64_t)t * Cin + ci0 + ci) * Cout + co0 + 4 * sub))
@@ -238,14 +241,14 @@ __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict_
     }
 #pragma unroll
     for (int q = 0; q < IT; ++q) {
-      const int r = rr + 32 * q;
+      const int r = rr + RPP * q;
       if (r < nrows)
 #pragma unroll
         for (int e = 0; e < 4; ++e) tile[r][4 * sub + e] = v[q][e];
     }
   } else {
-    for (int e = threadIdx.x; e < nrows * TAP_CO; e += 256) {
-      const int co = e % TAP_CO, r = e / TAP_CO, t = r / CI, ci = r % CI;
+    for (int e = threadIdx.x; e < nrows * TCO; e += 256) {
+      const int co = e % TCO, r = e / TCO, t = r / CI, ci = r % CI;
       if (ci < nci && co < nco_v) tile[r][co] = row[((int64_t)t * Cin + ci0 + ci) * Cout + co0 + co];
     }
   }
@@ -257,13 +260,42 @@ __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict_
   const int64_t L = (int64_t)nci * KK;
   const int64_t ulo = 8 * r0, uhi = 8 * (r0 + steps);
   float* out = Xc + (int64_t)k * 8 * ldc;
-  for (int i = threadIdx.x; i < nco_v * 512; i += 256) {
-    const int ns = i & 63, c = (i >> 6) & 7, co = i >> 9;
+  if constexpr (WR >= 2) {
+    // every co's run whole inside the segment, and the same chain split for
+    // every co (Cin KK and L multiples of 8: m steps per chain): the items
+    // enumerated densely, (co, chain, step) with step fastest
+    const int64_t CL = (int64_t)Cin * KK;
+    const int64_t ufirst = off + ((int64_t)co0 * Cin + ci0) * KK;
+    if (CL % 8 == 0 && L % 8 == 0 && ufirst >= ulo && ufirst + (nco_v - 1) * CL + L <= uhi) {
+      const int Li = (int)L, m = Li / 8, a0 = (int)(ufirst & 7);
+      const int64_t sb0 = (ufirst >> 3) - r0, CLs = CL / 8;
+      const float inv_L = 1.f / (float)Li, inv_m = 1.f / (float)m;
+      const int n = nco_v * Li;
+#pragma unroll 4
+      for (int i = threadIdx.x; i < n; i += 256) {
+        const int co = (int)(((float)i + 0.5f) * inv_L);  // exact: i < 2^14
+        const int q = i - co * Li;
+        const int c = (int)(((float)q + 0.5f) * inv_m);
+        const int jj = q - c * m;
+        const int dc = (c - a0) & 7;  // chain c's first coordinate in the run: u0 + dc
+        const int rel = dc + 8 * jj, ci = rel / KK, t = rel - ci * KK;
+        out[(int64_t)c * ldc + sb0 + co * CLs + ((a0 + dc) >> 3) + jj] = tile[t * CI + ci][co];
+      }
+      return;
+    }
+  }
+  constexpr int UNR = WR == 0 ? 1 : 4;
+  constexpr int NS = TROWS / 8 + 1 <= 64 ? 64 : 128;  // item slots per (co, chain) run
+  static_assert(TROWS / 8 + 1 <= NS, "a run's steps fit its slots");
+#pragma unroll UNR
+  for (int i = threadIdx.x; i < nco_v * 8 * NS; i += 256) {
+    const int ns = i % NS, c = (i / NS) % 8, co = i / (8 * NS);
     const int64_t u0 = off + ((int64_t)(co0 + co) * Cin + ci0) * KK;
     const int64_t u = 8 * ((u0 >> 3) + ns) + c;
-    if (u < u0 || u >= u0 + L || u < ulo || u >= uhi) continue;
-    const int rel = (int)(u - u0), ci = rel / KK, t = rel - ci * KK;
-    out[(int64_t)c * ldc + ((u >> 3) - r0)] = tile[t * CI + ci][co];
+    if (u >= u0 && u < u0 + L && u >= ulo && u < uhi) {
+      const int rel = (int)(u - u0), ci = rel / KK, t = rel - ci * KK;
+      out[(int64_t)c * ldc + ((u >> 3) - r0)] = tile[t * CI + ci][co];
+    }
   }
 }
 
@@ -614,6 +646,30 @@ extern "C" int flr_pairwise_l2_reference_tiles(int64_t K) {
   return ntiles_of((int)K);
 }
 
+template <int WR, int TCO, int TROWS>
+static auto tap_kernel_for_wr(int64_t kk, bool vec) {
+  return kk == 9 ? (vec ? tap_chain_kernel<9, true, WR, TCO, TROWS> : tap_chain_kernel<9, false, WR, TCO, TROWS>)
+       : kk == 1 ? (vec ? tap_chain_kernel<1, true, WR, TCO, TROWS> : tap_chain_kernel<1, false, WR, TCO, TROWS>)
+                 : (vec ? tap_chain_kernel<0, true, WR, TCO, TROWS> : tap_chain_kernel<0, false, WR, TCO, TROWS>);
+}
+struct TapForm {
+  void (*kern)(const float*, int64_t, int64_t, int, int, int, int64_t, int64_t, int64_t, float*);
+  int tco, trows;
+};
+static TapForm tap_form(int64_t kk, int64_t off, int64_t co) {
+  const char* e = flr::knob("FLR_TAP_WR");
+  const int wr = e ? atoi(e) : 0;
+  if (wr == 3) {
+    const bool vec = off % 4 == 0 && co % 16 == 0;  // 16-B aligned rows, full 16-channel tiles
+    return {tap_kernel_for_wr<3, 16, 576>(kk, vec), 16, 576};
+  }
+  const bool vec = off % 4 == 0 && co % TAP_CO == 0;  // 16-B aligned rows, full 32-channel tiles
+  return {wr == 2   ? tap_kernel_for_wr<2, TAP_CO, TAP_ROWS>(kk, vec)
+          : wr == 1 ? tap_kernel_for_wr<1, TAP_CO, TAP_ROWS>(kk, vec)
+                    : tap_kernel_for_wr<0, TAP_CO, TAP_ROWS>(kk, vec),
+          TAP_CO, TAP_ROWS};
+}
+
 // The chains of tiles [t0, t1) over `steps` chain steps of X (coordinates
 // 0 .. 8 steps - 1 of each row), continuing the sums in A (first: from 0):
 // per segment the chain-major transpose (skipping the tap-major blocks), the
@@ -646,11 +702,10 @@ static int run_chains(const float* X, int64_t K, int64_t steps_total, int64_t ld
     for (int64_t b = 0; b < ntaps; ++b) {  // the tap-major blocks of this segment, rewritten
       const int64_t off = taps[4 * b], co = taps[4 * b + 1], ci = taps[4 * b + 2], kk = taps[4 * b + 3];
       if (off + co * ci * kk <= 8 * r0 || off >= 8 * (r0 + steps)) continue;
-      const int64_t tiles = (co + TAP_CO - 1) / TAP_CO * ((ci + TAP_ROWS / kk - 1) / (TAP_ROWS / kk));
-      const bool vec = off % 4 == 0 && co % TAP_CO == 0;  // 16-B aligned rows, full 32-channel tiles
-      auto kern = kk == 9 ? (vec ? tap_chain_kernel<9, true> : tap_chain_kernel<9, false>)
-                : kk == 1 ? (vec ? tap_chain_kernel<1, true> : tap_chain_kernel<1, false>)
-                          : (vec ? tap_chain_kernel<0, true> : tap_chain_kernel<0, false>);
+      const TapForm tf = tap_form(kk, off, co);
+      const int64_t cit = tf.trows / kk;  // input channels per tile
+      const int64_t tiles = (co + tf.tco - 1) / tf.tco * ((ci + cit - 1) / cit);
+      auto kern = tf.kern;
       hipLaunchKernelGGL(kern, dim3((unsigned)tiles, (unsigned)K), dim3(256), 0, st, X, ldx, off, (int)co, (int)ci,
                          (int)kk, r0, steps, ldc, Xc);
       if ((rc = launch_status("tap_chain_kernel")) != FLR_OK) return rc;

@@ -1,7 +1,12 @@
 """Time the reference-exact Krum distances (flr_pairwise_l2_reference) at a
 BASELINE shape and check D against the C restatement of torch.norm.
 
-    python tools/ref_bench.py [--K 128] [--P 11800394] [--reps 5] [--check 64]
+    python tools/ref_bench.py [--K 128] [--P 11800394] [--reps 5] [--check 64] [--taps]
+
+--taps: X is a training-order matrix of the C3 model (ResNet-18 + GRU, P =
+11,800,394): its tap-major conv weights named to flr_pairwise_l2_reference_tap
+as the round engine does (the tap_chain_kernel path); the check maps rows back
+to torch order.
 
 --check N: compare N pairs (a fixed spread over the matrix) with
 oracle.normref (test infrastructure, host CPU) — bit equality required.
@@ -29,28 +34,50 @@ def main():
     ap.add_argument("--P", type=int, default=11_800_394)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--check", type=int, default=64)
+    ap.add_argument("--taps", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda")
     K, P = a.K, a.P
+    blocks = None
+    if a.taps:
+        from flr.models.multimodal import ModelSpec, param_layout, tap_major_names
+        spec = ModelSpec()
+        tapn = tap_major_names(spec)
+        blocks, off = [], 0
+        for name, shape in param_layout(spec):
+            if name in tapn:
+                blocks.append((off, int(shape[0]), int(shape[1]), int(shape[2]) * int(shape[3])))
+            off += int(shape.numel())
+        P = off
     g = torch.Generator(device=dev).manual_seed(1234)
     data = torch.zeros((K, padded_ld(P)), dtype=torch.float32, device=dev)
     data[:, :P] = torch.randn((K, P), generator=g, device=dev) * 0.01
     data[: K // 5, :P] *= -1.0
     X = data[:, :P]
-    D = ops.pairwise_l2(X, "reference")  # warm-up (workspace, code objects)
+    D = ops.pairwise_l2(X, "reference", tap_blocks=blocks)  # warm-up (workspace, code objects)
     torch.cuda.synchronize()
     times = []
     for _ in range(a.reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        D = ops.pairwise_l2(X, "reference")
+        D = ops.pairwise_l2(X, "reference", tap_blocks=blocks)
         e1.record()
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1))
-    out = {"K": K, "P": P, "ms_min": min(times), "ms_median": float(np.median(times)), "reps": times}
+    out = {"K": K, "P": P, "taps": len(blocks or ()), "ms_min": min(times), "ms_median": float(np.median(times)), "reps": times}
     if a.check:
         from oracle import normref
         Dh = D.cpu().numpy()
+        perm = None
+        if blocks:  # torch-order coordinate v of a tap block <- training-order column
+            perm = np.arange(P)
+            for o, co, ci, kk in blocks:
+                u = np.arange(co * ci * kk)
+                perm[o:o + co * ci * kk] = o + ((u % kk) * ci + (u // kk) % ci) * co + u // (ci * kk)
+
+        def row(i):
+            r = X[i].cpu().numpy()
+            return r if perm is None else r[perm]
         pairs = []
         n = 0
         for t in range(a.check):
@@ -62,7 +89,7 @@ def main():
         t0 = time.time()
         bad = 0
         for i, j in pairs:
-            want = normref.norm_diff(X[i].cpu().numpy(), X[j].cpu().numpy())
+            want = normref.norm_diff(row(i), row(j))
             if Dh[i, j] != want or Dh[j, i] != want:
                 bad += 1
             n += 1
