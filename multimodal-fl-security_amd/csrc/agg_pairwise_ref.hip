@@ -42,6 +42,7 @@
 #include <cstdint>
 #include <type_traits>
 #include <utility>
+#include <vector>
 
 #include "flr_common.h"
 
@@ -141,25 +142,25 @@ __host__ __device__ inline int tile_of_pair(int i, int j) {
 // store.  (Per-lane 128-B rows read at 3 TB/s: 64 cache lines per load.)
 constexpr int TW = 256;        // steps per wave
 constexpr int TROW = TW + 4;   // LDS floats per chain row
-// Coordinate ranges another kernel writes (tap_chain_kernel): a wave whose
-// 2048 coordinates lie inside one of them skips its loads and stores.
-struct SkipRanges {
-  static constexpr int MAX = 32;
+// The waves to run, as runs of consecutive wave indices (wave w: steps
+// w TW .. w TW + TW - 1): the host leaves out every wave whose 2048
+// coordinates lie inside one tap-major block (tap_chain_kernel writes those),
+// so no workgroup is launched only to find it has nothing to do.
+struct WaveRuns {
+  static constexpr int MAX = 48;
   int n;
-  int64_t lo[MAX], hi[MAX];
+  int64_t w0[MAX], pre[MAX + 1];  // run r: waves w0[r] .., launch ordinals pre[r] .. pre[r + 1] - 1
 };
 __global__ __launch_bounds__(256) void chain_transpose_kernel(const float* __restrict__ X, int64_t ldx, int64_t r0,
                                                               int64_t steps, int64_t ldc, float* __restrict__ Xc,
-                                                              const SkipRanges skip) {
+                                                              const WaveRuns runs) {
   __shared__ __attribute__((aligned(16))) float t[4 * 8 * TROW];
   const int k = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * TW;
-  if (s0 >= steps) return;  // the whole wave (no workgroup barrier below)
-  {
-    const int64_t u0 = 8 * (r0 + s0), u1 = u0 + 8 * TW;
-    for (int b = 0; b < skip.n; ++b)
-      if (u0 >= skip.lo[b] && u1 <= skip.hi[b]) return;
-  }
+  const int64_t q = (int64_t)blockIdx.x * 4 + wave;
+  if (q >= runs.pre[runs.n]) return;  // the whole wave (no workgroup barrier below)
+  int r = 0;
+  while (q >= runs.pre[r + 1]) ++r;
+  const int64_t s0 = (runs.w0[r] + q - runs.pre[r]) * TW;
   const int nv = (int)(steps - s0 < TW ? steps - s0 : TW);
   const float* src = X + (int64_t)k * ldx + 8 * (r0 + s0);
   float* tw = t + wave * 8 * TROW;
@@ -205,12 +206,11 @@ __global__ __launch_bounds__(256) void chain_transpose_kernel(const float* __res
 // stream share an L2 and run together.  Grid (tiles, K).
 constexpr int TAP_CO = 32;
 constexpr int TAP_ROWS = 288;  // LDS tile rows (tap, input channel): CI = TAP_ROWS / KK
-// WR: the write phase (0 one (co, chain) run per 64 items, 1 the same unrolled,
-// 2 dense items, falling back to 1's loop for a ragged tile); TCO x TROWS: the tile
-template <int KKT, bool VEC, int WR, int TCO = TAP_CO, int TROWS = TAP_ROWS>
+template <int KKT, bool VEC>  // KKT: 9, 1, or 0 = KK at run time; VEC: 16-B aligned tile rows
 __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict__ X, int64_t ldx, int64_t off,
                                                         int Cout, int Cin, int KKr, int64_t r0, int64_t steps,
                                                         int64_t ldc, float* __restrict__ Xc) {
+  constexpr int TCO = TAP_CO, TROWS = TAP_ROWS;
   __shared__ float tile[TROWS][TCO + 1];
   const int KK = KKT > 0 ? KKT : KKr;
   const int CI = TROWS / KK;
@@ -255,15 +255,16 @@ __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict_
   __syncthreads();
   // write: output channel co's run [u0, u0 + nci * KK) (at most 288
   // coordinates: 38 steps per chain), clipped to the segment
-  // [8 r0, 8 (r0 + steps)); item i -> (co = i / 512, chain = i / 64 % 8,
-  // step = i % 64): a wave writes consecutive steps of one chain stream
+  // [8 r0, 8 (r0 + steps)), chain-major: a wave writes consecutive steps of
+  // a chain stream
   const int64_t L = (int64_t)nci * KK;
   const int64_t ulo = 8 * r0, uhi = 8 * (r0 + steps);
   float* out = Xc + (int64_t)k * 8 * ldc;
-  if constexpr (WR >= 2) {
+  {
     // every co's run whole inside the segment, and the same chain split for
     // every co (Cin KK and L multiples of 8: m steps per chain): the items
-    // enumerated densely, (co, chain, step) with step fastest
+    // enumerated densely, (co, chain, step) with step fastest — every lane
+    // busy, against 36 or 37 of 64 in the general loop below (-13 % time)
     const int64_t CL = (int64_t)Cin * KK;
     const int64_t ufirst = off + ((int64_t)co0 * Cin + ci0) * KK;
     if (CL % 8 == 0 && L % 8 == 0 && ufirst >= ulo && ufirst + (nco_v - 1) * CL + L <= uhi) {
@@ -284,12 +285,12 @@ __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict_
       return;
     }
   }
-  constexpr int UNR = WR == 0 ? 1 : 4;
-  constexpr int NS = TROWS / 8 + 1 <= 64 ? 64 : 128;  // item slots per (co, chain) run
-  static_assert(TROWS / 8 + 1 <= NS, "a run's steps fit its slots");
-#pragma unroll UNR
-  for (int i = threadIdx.x; i < nco_v * 8 * NS; i += 256) {
-    const int ns = i % NS, c = (i / NS) % 8, co = i / (8 * NS);
+  // the general tile (ragged, or crossing a segment end): item i -> (co =
+  // i / 512, chain = i / 64 % 8, step slot i % 64)
+  static_assert(TROWS / 8 + 1 <= 64, "a run's steps fit its slots");
+#pragma unroll 4
+  for (int i = threadIdx.x; i < nco_v * 512; i += 256) {
+    const int ns = i & 63, c = (i >> 6) & 7, co = i >> 9;
     const int64_t u0 = off + ((int64_t)(co0 + co) * Cin + ci0) * KK;
     const int64_t u = 8 * ((u0 >> 3) + ns) + c;
     if (u >= u0 && u < u0 + L && u >= ulo && u < uhi) {
@@ -646,28 +647,40 @@ extern "C" int flr_pairwise_l2_reference_tiles(int64_t K) {
   return ntiles_of((int)K);
 }
 
-template <int WR, int TCO, int TROWS>
-static auto tap_kernel_for_wr(int64_t kk, bool vec) {
-  return kk == 9 ? (vec ? tap_chain_kernel<9, true, WR, TCO, TROWS> : tap_chain_kernel<9, false, WR, TCO, TROWS>)
-       : kk == 1 ? (vec ? tap_chain_kernel<1, true, WR, TCO, TROWS> : tap_chain_kernel<1, false, WR, TCO, TROWS>)
-                 : (vec ? tap_chain_kernel<0, true, WR, TCO, TROWS> : tap_chain_kernel<0, false, WR, TCO, TROWS>);
-}
-struct TapForm {
-  void (*kern)(const float*, int64_t, int64_t, int, int, int, int64_t, int64_t, int64_t, float*);
-  int tco, trows;
-};
-static TapForm tap_form(int64_t kk, int64_t off, int64_t co) {
-  const char* e = flr::knob("FLR_TAP_WR");
-  const int wr = e ? atoi(e) : 0;
-  if (wr == 3) {
-    const bool vec = off % 4 == 0 && co % 16 == 0;  // 16-B aligned rows, full 16-channel tiles
-    return {tap_kernel_for_wr<3, 16, 576>(kk, vec), 16, 576};
+// The transpose's waves for segment [r0, r0 + steps): every wave not inside
+// one tap block (the blocks ascending and disjoint, checked by the caller).
+// Past WaveRuns::MAX runs the shortest gaps are bridged (those waves then
+// also run; the tap kernel, launched after, rewrites their coordinates).
+static WaveRuns wave_runs(const int64_t* taps, int64_t ntaps, int64_t r0, int64_t steps) {
+  const int64_t nw = (steps + TW - 1) / TW;
+  std::vector<std::pair<int64_t, int64_t>> v;  // [first, last + 1) wave runs
+  int64_t b = 0;
+  for (int64_t w = 0; w < nw; ++w) {
+    const int64_t u0 = 8 * (r0 + w * TW), u1 = u0 + 8 * TW;
+    while (b < ntaps && taps[4 * b] + taps[4 * b + 1] * taps[4 * b + 2] * taps[4 * b + 3] <= u0) ++b;
+    const bool inside = b < ntaps && u0 >= taps[4 * b] &&
+                        u1 <= taps[4 * b] + taps[4 * b + 1] * taps[4 * b + 2] * taps[4 * b + 3];
+    if (inside) continue;
+    if (!v.empty() && v.back().second == w)
+      v.back().second = w + 1;
+    else
+      v.push_back({w, w + 1});
   }
-  const bool vec = off % 4 == 0 && co % TAP_CO == 0;  // 16-B aligned rows, full 32-channel tiles
-  return {wr == 2   ? tap_kernel_for_wr<2, TAP_CO, TAP_ROWS>(kk, vec)
-          : wr == 1 ? tap_kernel_for_wr<1, TAP_CO, TAP_ROWS>(kk, vec)
-                    : tap_kernel_for_wr<0, TAP_CO, TAP_ROWS>(kk, vec),
-          TAP_CO, TAP_ROWS};
+  while ((int)v.size() > WaveRuns::MAX) {  // bridge the shortest gap
+    size_t best = 1;
+    for (size_t i = 2; i < v.size(); ++i)
+      if (v[i].first - v[i - 1].second < v[best].first - v[best - 1].second) best = i;
+    v[best - 1].second = v[best].second;
+    v.erase(v.begin() + (int64_t)best);
+  }
+  WaveRuns wr;
+  wr.n = (int)v.size();
+  wr.pre[0] = 0;
+  for (int i = 0; i < wr.n; ++i) {
+    wr.w0[i] = v[i].first;
+    wr.pre[i + 1] = wr.pre[i] + (v[i].second - v[i].first);
+  }
+  return wr;
 }
 
 // The chains of tiles [t0, t1) over `steps` chain steps of X (coordinates
@@ -686,26 +699,24 @@ static int run_chains(const float* X, int64_t K, int64_t steps_total, int64_t ld
   const int64_t nseg = (R + ldc - 1) / ldc;
   const int64_t Rs = ((R + nseg - 1) / nseg + XC_GROUP - 1) / XC_GROUP * XC_GROUP;  // <= ldc
   float* Xc = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + na);
-  SkipRanges skip;
-  skip.n = 0;
-  for (int64_t b = 0; b < ntaps && skip.n < SkipRanges::MAX; ++b) {
-    skip.lo[skip.n] = taps[4 * b];
-    skip.hi[skip.n++] = taps[4 * b] + taps[4 * b + 1] * taps[4 * b + 2] * taps[4 * b + 3];
-  }
   for (int64_t seg = 0; seg < nseg; ++seg) {
     const int64_t r0 = seg * Rs, steps = (R - r0 < Rs) ? R - r0 : Rs;
     if (steps <= 0) break;
-    hipLaunchKernelGGL(chain_transpose_kernel, dim3((unsigned)((steps + 4 * TW - 1) / (4 * TW)), (unsigned)K),
-                       dim3(256), 0, st, X, ldx, r0, steps, ldc, Xc, skip);
-    int rc = launch_status("chain_transpose_kernel");
-    if (rc != FLR_OK) return rc;
+    const WaveRuns runs = wave_runs(taps, ntaps, r0, steps);
+    int rc = FLR_OK;
+    if (runs.pre[runs.n] > 0) {
+      hipLaunchKernelGGL(chain_transpose_kernel, dim3((unsigned)((runs.pre[runs.n] + 3) / 4), (unsigned)K), dim3(256),
+                         0, st, X, ldx, r0, steps, ldc, Xc, runs);
+      if ((rc = launch_status("chain_transpose_kernel")) != FLR_OK) return rc;
+    }
     for (int64_t b = 0; b < ntaps; ++b) {  // the tap-major blocks of this segment, rewritten
       const int64_t off = taps[4 * b], co = taps[4 * b + 1], ci = taps[4 * b + 2], kk = taps[4 * b + 3];
       if (off + co * ci * kk <= 8 * r0 || off >= 8 * (r0 + steps)) continue;
-      const TapForm tf = tap_form(kk, off, co);
-      const int64_t cit = tf.trows / kk;  // input channels per tile
-      const int64_t tiles = (co + tf.tco - 1) / tf.tco * ((ci + cit - 1) / cit);
-      auto kern = tf.kern;
+      const int64_t tiles = (co + TAP_CO - 1) / TAP_CO * ((ci + TAP_ROWS / kk - 1) / (TAP_ROWS / kk));
+      const bool vec = off % 4 == 0 && co % TAP_CO == 0;  // 16-B aligned rows, full 32-channel tiles
+      auto kern = kk == 9 ? (vec ? tap_chain_kernel<9, true> : tap_chain_kernel<9, false>)
+                : kk == 1 ? (vec ? tap_chain_kernel<1, true> : tap_chain_kernel<1, false>)
+                          : (vec ? tap_chain_kernel<0, true> : tap_chain_kernel<0, false>);
       hipLaunchKernelGGL(kern, dim3((unsigned)tiles, (unsigned)K), dim3(256), 0, st, X, ldx, off, (int)co, (int)ci,
                          (int)kk, r0, steps, ldc, Xc);
       if ((rc = launch_status("tap_chain_kernel")) != FLR_OK) return rc;

@@ -142,18 +142,18 @@ def test_reference_mode_tap_blocks_reach_the_tail(cuda):
     assert np.array_equal(D, normref.distance_matrix(X.numpy()))
 
 
-@pytest.mark.parametrize("wr", ["0", "1", "2", "3"])
-def test_reference_mode_tap_blocks_segmented(cuda, wr):
-    """A workspace for 2048 chain steps: three segments (2048, 2048 and a last
-    one of 1904 steps zero-filled to 2048), tap blocks crossing the segment
-    boundaries (the clipped runs), one with Cin * KK not a multiple of 8 and a
-    partial ci tile; each tap write form (FLR_TAP_WR): D bit-identical to the
-    reference-order matrix's through the whole workspace."""
+def test_reference_mode_tap_blocks_segmented(cuda):
+    """A workspace for 2048 chain steps: four segments (3 x 2048 and a last one
+    of 356 steps zero-filled to 512), tap blocks crossing the segment
+    boundaries (the clipped runs: the tap kernel's general write loop), one
+    with Cin * KK not a multiple of 8 and a partial ci tile (the dense write
+    form for its whole tiles): D bit-identical to the reference-order
+    matrix's through the whole workspace."""
     import ctypes
     from flr import _capi
     K = 16
     blocks = [(5, 64, 64, 9), (36_869 + 3, 64, 3, 9), (36_869 + 3 + 1728 + 1, 32, 40, 9)]
-    P = 8 * 6000 + 5
+    P = 8 * 6500 + 5
     assert max(o + co * ci * kk for o, co, ci, kk in blocks) <= P
     X, data = _matrix(K, P, 21, cuda)
     train = data.clone()
@@ -170,13 +170,9 @@ def test_reference_mode_tap_blocks_segmented(cuda, wr):
     tarr = (ctypes.c_int64 * len(taps))(*taps)
     D = torch.empty((K, K), dtype=torch.float64, device=cuda)
     st = torch.cuda.current_stream().cuda_stream
-    _capi.set_knob("FLR_TAP_WR", wr)
-    try:
-        _capi.call("flr_pairwise_l2_reference_tap", train.data_ptr(), K, P, train.stride(0), ctypes.addressof(tarr),
-                   len(blocks), D.data_ptr(), wp, nbytes, 0, 1, st)
-        torch.cuda.synchronize()
-    finally:
-        _capi.set_knob("FLR_TAP_WR", None)
+    _capi.call("flr_pairwise_l2_reference_tap", train.data_ptr(), K, P, train.stride(0), ctypes.addressof(tarr),
+               len(blocks), D.data_ptr(), wp, nbytes, 0, 1, st)
+    torch.cuda.synchronize()
     want = ops.pairwise_l2(data[:, :P], "reference").cpu().numpy()
     assert np.array_equal(D.cpu().numpy(), want)
     assert np.array_equal(want, normref.distance_matrix(X.numpy()))
