@@ -206,6 +206,9 @@ __global__ __launch_bounds__(256) void chain_transpose_kernel(const float* __res
 // stream share an L2 and run together.  Grid (tiles, K).
 constexpr int TAP_CO = 32;
 constexpr int TAP_ROWS = 288;  // LDS tile rows (tap, input channel): CI = TAP_ROWS / KK
+// the dense write enumeration divides item indices < TAP_CO * TAP_ROWS through
+// a float reciprocal: exact while they stay far below 2^24 / (the divisor)
+static_assert(TAP_CO * TAP_ROWS < (1 << 14), "dense write items exact in fp32");
 template <int KKT, bool VEC>  // KKT: 9, 1, or 0 = KK at run time; VEC: 16-B aligned tile rows
 __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict__ X, int64_t ldx, int64_t off,
                                                         int Cout, int Cin, int KKr, int64_t r0, int64_t steps,
