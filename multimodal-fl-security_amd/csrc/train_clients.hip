@@ -25,6 +25,8 @@
 #include <vector>
 
 namespace flr {
+int clip_sumsq_blocks(const float* const* g_blocks, const int64_t* numel, const int64_t* client_stride,
+                      int64_t nblocks, int64_t K, double* out, int64_t out_ld, int nslots, hipStream_t st);
 namespace tc {
 
 constexpr int THREADS = 256;
@@ -116,6 +118,7 @@ struct Param {
   bool tap = false;            // trained tap-major
   bool dead = false;           // has dead taps skipped by the optimizer (wd == 0)
   int sq_base = -1;            // fused clip-norm partial slots (tap-major convs)
+  bool sq_early = false;       // its clip-norm partials taken early on the text stream (text branch, head)
   float *w = nullptr, *m = nullptr, *g = nullptr, *tmp = nullptr;
 };
 
@@ -276,6 +279,16 @@ class Net {
         p.sq_base = (int)nsq_;
         nsq_ += n;
       }
+    // the text branch's and the head's partials: their gradients are final once
+    // the text backward ends, long before the trunk's, so their sum of squares
+    // runs on the text stream there (clip_sumsq_blocks) instead of in the
+    // optimizer's pass at the end of the backward; kEarlySlots slots after the convs'
+    sq_early_base_ = -1;
+    if (clip_ > 0) {
+      sq_early_base_ = nsq_;
+      nsq_ += kEarlySlots;
+      for (int j : {p_emb_, p_wih_, p_whh_, p_bih_, p_bhh_, p_w1_, p_b1_, p_w2_, p_b2_}) ps_[j].sq_early = true;
+    }
     sq_ = alloc<double>(K_ * std::max<int64_t>(1, nsq_));
     sgd_ws_n_ = flr_clip_sgd_workspace(K_);
     sgd_ws_ = alloc<char>(sgd_ws_n_);
@@ -651,6 +664,7 @@ class Net {
     FLR_TRY(gemm(dgi_, N * H3, 1, H3, emb_, N * E_, 1, E_, wih.g, H3 * E_, E_, 1, nullptr, 0, nullptr, H3, E_, N, ts));
     FLR_TRY(rowsum(dgi_, N * H3, H3, N, H3, bih.g, ts));
     FLR_TRY(flr_embedding_bwd(demb_, tokens, N, K_, N, s.vocab, E_, emb.g, s.vocab * E_, 1, ews_, ews_n_, ts));
+    if (sq_early_base_ >= 0) FLR_TRY(early_sumsq(ts));  // the head's gradients: on st before fork 2
     if (conc) FLR_TRY(fork(ts, st, 3));
     // trunk, last block first
     for (int bi = (int)blocks_.size() - 1; bi >= 0; --bi) {
@@ -715,7 +729,7 @@ class Net {
       mb.push_back(p.m + b.o);
       nb.push_back(b.n);
       cs.push_back(b.cs);
-      normed.push_back(p.sq_base >= 0 ? 1 : 0);
+      normed.push_back(p.sq_base >= 0 || p.sq_early ? 1 : 0);
     }
     const bool fuse = clip_ > 0 && nsq_ > 0;
     // first step in training order: the tap-major blocks read the shared global copy
@@ -778,6 +792,23 @@ class Net {
     if (!(e & 1) && hipStreamWaitEvent(to, text_->ev[e], 0) != hipSuccess)
       return launch_status("train_clients: text-stream fork");
     return FLR_OK;
+  }
+
+  // the clip-norm partials of the parameters marked sq_early (their optimizer
+  // blocks) into sq_[k][sq_early_base_ ..]
+  int early_sumsq(hipStream_t s) {
+    std::vector<const float*> g;
+    std::vector<int64_t> n, cs;
+    for (const auto& b : blocks_opt_) {
+      const Param& p = ps_[b.j];
+      if (!p.sq_early) continue;
+      g.push_back(p.g + b.o);
+      n.push_back(b.n);
+      cs.push_back(b.cs);
+    }
+    if (g.empty()) return FLR_ERR_ARG;
+    return clip_sumsq_blocks(g.data(), n.data(), cs.data(), (int64_t)g.size(), K_, sq_ + sq_early_base_, nsq_,
+                             kEarlySlots, s);
   }
 
   int wait_group(int g, hipStream_t st) {
@@ -962,6 +993,8 @@ class Net {
   std::vector<int> gthr_;  // optimizer group g: parameters [gthr_[g-1], gthr_[g]) (forward segments)
   std::vector<int> gorder_;  // the groups in forward order: text branch, stem, residual blocks, head
   int gtext_ = 0, ghead_ = 0;
+  static constexpr int kEarlySlots = 32;  // clip_sumsq_blocks' partials per client (train_step.hip NBLK)
+  int sq_early_base_ = -1;                // their first slot in sq_ (-1: none)
  public:
   SideStream* side_ = nullptr;  // the optimizer's side stream (nullptr: the update runs on the caller's stream)
   TextStream* text_ = nullptr;  // the text branch's stream (nullptr: the caller's stream)

@@ -177,7 +177,7 @@ __device__ __forceinline__ void visit_range(int64_t lo, int64_t hi, int64_t pre,
 }
 
 __global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable tb, int64_t P,
-                                                                double* __restrict__ partial) {
+                                                                double* __restrict__ partial, int64_t ld = NBLK) {
   __shared__ double red[THREADS / 64];
   const int k = blockIdx.y, b = blockIdx.x;
   const int64_t p0 = P * b / NBLK, p1 = P * (b + 1) / NBLK;
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(THREADS) void sumsq_blocked_kernel(const BlockTable
   if (threadIdx.x == 0) {
     double s = 0.0;
     for (int w = 0; w < THREADS / 64; ++w) s += red[w];
-    partial[(int64_t)k * NBLK + b] = s;
+    partial[(int64_t)k * ld + b] = s;
   }
 }
 
@@ -355,6 +355,37 @@ __global__ __launch_bounds__(THREADS) void sgd_blocked_kernel(const BlockTable t
 }  // namespace flr
 
 using namespace flr;
+
+namespace flr {
+// The clip norm's sum-of-squares partials of a set of gradient blocks (block j:
+// g_blocks[j] + k * client_stride[j], numel[j] values per client), NBLK per
+// client at out[k * out_ld + b] — the same pass and order as the optimizer's
+// own (sumsq_blocked_kernel), launched early on a side stream by a trainer
+// whose blocks' gradients are final before the backward ends; the optimizer
+// then takes them as extra partials (block_normed set for those blocks).
+int clip_sumsq_blocks(const float* const* g_blocks, const int64_t* numel, const int64_t* client_stride,
+                      int64_t nblocks, int64_t K, double* out, int64_t out_ld, int nslots, hipStream_t st) {
+  if (nslots != train::NBLK || nblocks < 1 || nblocks > train::MAXB || K < 1 || !out || out_ld < train::NBLK)
+    return FLR_ERR_ARG;
+  train::BlockTable tb;
+  tb.nb = (int)nblocks;
+  tb.pre[0] = 0;
+  for (int q = 0; q < tb.nb; ++q) {
+    const int64_t cs = client_stride[q];
+    if (!g_blocks[q] || numel[q] < 0 || cs < numel[q] || cs >= ((int64_t)1 << 31)) return FLR_ERR_ARG;
+    tb.x[q] = nullptr;
+    tb.g[q] = g_blocks[q];
+    tb.m[q] = nullptr;
+    tb.pre[q + 1] = tb.pre[q] + numel[q];
+    tb.cs[q] = (int32_t)cs;
+    tb.vec[q] = (numel[q] % 4 == 0 && cs % 4 == 0 && (reinterpret_cast<uintptr_t>(g_blocks[q]) & 15) == 0) ? 1 : 0;
+    tb.xo[q] = 0;
+  }
+  hipLaunchKernelGGL(train::sumsq_blocked_kernel, dim3(train::NBLK, (unsigned)K), dim3(train::THREADS), 0, st, tb,
+                     tb.pre[tb.nb], out, out_ld);
+  return launch_status("sumsq_blocked_kernel");
+}
+}  // namespace flr
 
 extern "C" size_t flr_clip_sgd_workspace(int64_t K) {
   return align_up((size_t)train::MAX_PARTS * K * train::NBLK * sizeof(double), 256) +
