@@ -1,0 +1,13 @@
+#!/bin/bash
+# the round's global load as one launch: trainer / round tests, alternating C3 timing + sha
+set -o pipefail
+D=gpurun_out/r5bcast; mkdir -p $D
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_native_trainer.py tests/test_gpu_round.py tests/test_gpu_configs.py -k "not c4 and not c5" > $D/tests.log 2>&1 || { echo "tests failed"; tail -30 $D/tests.log; exit 1; }
+tail -1 $D/tests.log
+for i in 1 2 3; do
+  for v in base new; do
+    lib=multimodal-fl-security_amd/lib/libflr.so; [ $v = base ] && lib=abl/base/libflr.so
+    FLR_LIB=$lib timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 --warmup 5 > $D/$v$i.json 2> $D/$v$i.err || { echo "bench $v failed"; tail -20 $D/$v$i.err; exit 1; }
+    python3 -c "import json; d=json.loads(open('$D/$v$i.json').read().strip().splitlines()[-1]); print('$v', round(d['value'],3), round(d['train_ms_per_round'],2), d['global_sha256'][:12])"
+  done
+done
