@@ -82,7 +82,9 @@ inline SideStream* side_stream(bool create, hipStream_t st = nullptr) {
 // call per device at a time.  FLR_TEXT_STREAM=0: everything on the caller's
 // stream (A/B, read per call).
 struct TextStream {
-  static constexpr int NEV = 4;  // forward fork / join, backward fork / join
+  // forward fork / join, backward fork / join; 4 .. NEV - 2: the trunk's last
+  // weight gradients forked onto it (idle by then), NEV - 1 their join
+  static constexpr int NEV = 8;
   hipStream_t s = nullptr;
   hipEvent_t ev[NEV] = {};
 };

@@ -382,6 +382,7 @@ class Net {
     ews_ = alloc<char>(ews_n_);
     cws_ = alloc<char>(cws_n_);  // the largest convolution workspace (conv_ws)
     cws2_ = alloc<char>(cws_n_);  // the weight-gradient stream's own (split-K partials)
+    cws3_ = alloc<char>(cws_n_);  // the text stream's, for the trunk's last weight gradients
     if (N > 4096) return FLR_ERR_UNSUPPORTED;
     return FLR_OK;
   }
@@ -666,9 +667,17 @@ class Net {
     FLR_TRY(flr_embedding_bwd(demb_, tokens, N, K_, N, s.vocab, E_, emb.g, s.vocab * E_, 1, ews_, ews_n_, ts));
     if (sq_early_base_ >= 0) FLR_TRY(early_sumsq(ts));  // the head's gradients: on st before fork 2
     if (conc) FLR_TRY(fork(ts, st, 3));
-    // trunk, last block first
+    // trunk, last block first.  The first blocks' weight gradients come last,
+    // behind the weight-gradient stream's backlog, when the text stream has long
+    // been idle: they run there instead (FLR_WG_TEXT blocks; 0: off)
+    const int wg_text = conc ? [] {
+      const char* e = flr::knob("FLR_WG_TEXT");
+      return e ? atoi(e) : 2;
+    }() : 0;
+    tev_ = 4;
     for (int bi = (int)blocks_.size() - 1; bi >= 0; --bi) {
       Block& bk = blocks_[bi];
+      wg_on_text_ = bi < wg_text;
       const float* d_out = bi + 1 < (int)blocks_.size() ? blocks_[bi + 1].d_in : d_x4_;
       FLR_TRY(bn_bwd(bk.b2, d_out, bk.y2, bk.out, true, bk.d_y2, bk.d_res, st));
       FLR_TRY(conv_bwd(bk.c2, bk.a1, bk.d_y2, bk.d_a1, st));
@@ -706,9 +715,15 @@ class Net {
       FLR_TRY(flr_maxpool2d_bwd(d_p0_, arg0_, d_a0_, K_ * s.widths[0] * B_, Hs_, Hs_, 3, 3, 2, 1, st));
       FLR_TRY(bn_bwd(stem_bn_, d_a0_, y0_, a0_, true, d_y0_, nullptr, st));
     }
+    wg_on_text_ = false;
     FLR_TRY(conv_bwd(stem_, ximg_, d_y0_, nullptr, st));
     if (conc && hipStreamWaitEvent(st, text_->ev[3], 0) != hipSuccess)
       return launch_status("train_clients: text-stream join");
+    if (conc && tev_ > 4) {  // the weight gradients run on the text stream
+      if (hipEventRecord(text_->ev[TextStream::NEV - 1], text_->s) != hipSuccess ||
+          hipStreamWaitEvent(st, text_->ev[TextStream::NEV - 1], 0) != hipSuccess)
+        return launch_status("train_clients: text-stream weight-gradient join");
+    }
     if (wgs_ && wev_ > 0) {  // every weight gradient (and its clip-norm partials) before the clip
       if (wev_ >= WgradStream::NEV) return FLR_ERR_UNSUPPORTED;
       if (hipEventRecord(wgs_->ev[wev_], wgs_->s) != hipSuccess || hipStreamWaitEvent(st, wgs_->ev[wev_], 0) != hipSuccess)
@@ -935,7 +950,13 @@ class Net {
       const float* w = tap_w(p, wst);
       hipStream_t ws = st;
       char* wsp = cws_;
-      if (wgs_ && wev_ + 1 < WgradStream::NEV) {  // one event kept for the join
+      if (wg_on_text_ && text_ && tev_ < TextStream::NEV - 1) {
+        if (hipEventRecord(text_->ev[tev_], st) != hipSuccess || hipStreamWaitEvent(text_->s, text_->ev[tev_], 0) != hipSuccess)
+          return launch_status("train_clients: text-stream weight-gradient fork");
+        ++tev_;
+        ws = text_->s;
+        wsp = cws3_;
+      } else if (wgs_ && wev_ + 1 < WgradStream::NEV) {  // one event kept for the join
         if (hipEventRecord(wgs_->ev[wev_], st) != hipSuccess || hipStreamWaitEvent(wgs_->s, wgs_->ev[wev_], 0) != hipSuccess)
           return launch_status("train_clients: weight-gradient fork");
         ++wev_;
@@ -1003,7 +1024,10 @@ class Net {
   bool stem_fused_ = false;     // bn1 + relu + maxpool fused (flr_batchnorm_relu_maxpool_fwd / _bwd)
  private:
   bool pending_ = false;        // a side-stream update the next forward must wait for
-  char *sgd_ws_ = nullptr, *gws_ = nullptr, *rws_ = nullptr, *ews_ = nullptr, *cws_ = nullptr, *cws2_ = nullptr;
+  char *sgd_ws_ = nullptr, *gws_ = nullptr, *rws_ = nullptr, *ews_ = nullptr, *cws_ = nullptr, *cws2_ = nullptr,
+       *cws3_ = nullptr;
+  bool wg_on_text_ = false;  // this conv's dW on the text stream (the first FLR_WG_TEXT residual blocks)
+  int tev_ = 4;              // text-stream fork events used by them this step
   size_t sgd_ws_n_ = 0, gws_n_ = 0, rws_n_ = 0, ews_n_ = 0, cws_n_ = 0;
   float *ximg_ = nullptr, *y0_ = nullptr, *a0_ = nullptr, *d_a0_ = nullptr, *d_y0_ = nullptr, *p0_ = nullptr,
         *d_p0_ = nullptr, *d_x4_ = nullptr;
