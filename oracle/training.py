@@ -10,10 +10,12 @@ instead of a shuffling DataLoader, and dropout applied through an explicit mask
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+import contextlib
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 
 class _MaskDropout(nn.Module):
@@ -38,11 +40,79 @@ def _mask_dropouts(model: nn.Module) -> List[_MaskDropout]:
     return out
 
 
+class _TiedRelu(torch.autograd.Function):
+    """F.relu with some gate decisions given instead of computed (m: the gate
+    mask, (x > 0) except at the tie positions).  Forward where(m, x, 0),
+    backward where(m, g, 0): torch's relu / threshold_backward wherever m is
+    (x > 0)."""
+
+    @staticmethod
+    def forward(ctx, x, m):
+        ctx.save_for_backward(m)
+        return torch.where(m, x, torch.zeros((), dtype=x.dtype))
+
+    @staticmethod
+    def backward(ctx, g):
+        (m,) = ctx.saved_tensors
+        return torch.where(m, g, torch.zeros((), dtype=g.dtype)), None
+
+
+@contextlib.contextmanager
+def _relu_hooks(override: Optional[Dict[int, Tuple[torch.Tensor, torch.Tensor]]] = None,
+                record: Optional[List[torch.Tensor]] = None):
+    """Within the block, the n-th F.relu call of a forward (counted from 0 per
+    forward: reset the counter list between forwards) takes the gate decisions
+    override[n] = (flat element indices, decisions) at those elements; record,
+    if given, collects every ReLU input."""
+    if not override and record is None:
+        yield [0]
+        return
+    orig = F.relu
+    count = [0]
+
+    def relu(x, *a, **kw):
+        n = count[0]
+        count[0] += 1
+        if record is not None:
+            record.append(x.detach().clone())
+        if override and n in override:
+            idx, on = override[n]
+            m = (x > 0).reshape(-1).clone()
+            m[idx] = on
+            return _TiedRelu.apply(x, m.view_as(x))
+        return orig(x, *a, **kw)
+
+    F.relu = relu
+    try:
+        yield count
+    finally:
+        F.relu = orig
+
+
+def relu_inputs(model_cls, spec, params_flat: torch.Tensor, images: torch.Tensor, tokens: torch.Tensor,
+                dtype: torch.dtype = torch.float32) -> List[torch.Tensor]:
+    """Every ReLU input of one train-mode forward of the reference model (the
+    fp32 reference, or fp64 as the yardstick) from the flat parameters, in call
+    order.  Test infrastructure: the gate-tie check of tests/parity.py."""
+    model = model_cls(spec).to(dtype)
+    off = 0
+    with torch.no_grad():
+        for p in model.parameters():
+            p.copy_(params_flat[off:off + p.numel()].view(p.shape).to(dtype))
+            off += p.numel()
+    model.train()
+    rec: List[torch.Tensor] = []
+    with torch.no_grad(), _relu_hooks(record=rec):
+        model(images.to(dtype), tokens)
+    return rec
+
+
 def local_update(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, lr: float = 0.01,
                  momentum: float = 0.9, weight_decay: float = 0.0, max_norm: float = 1.0,
                  masks: Optional[Sequence[torch.Tensor]] = None, threads: Optional[int] = None,
                  dtype: torch.dtype = torch.float32, start_params: Optional[torch.Tensor] = None,
-                 start_momentum: Optional[Sequence[torch.Tensor]] = None, return_momentum: bool = False):
+                 start_momentum: Optional[Sequence[torch.Tensor]] = None, return_momentum: bool = False,
+                 relu_ties: Optional[Dict[int, Tuple[torch.Tensor, torch.Tensor]]] = None):
     """One client's local update.  Returns (params after training, mean loss).
     dtype=torch.float64 runs the same loop in double precision: not the
     reference (which trains in fp32), but the yardstick of how far the
@@ -50,7 +120,13 @@ def local_update(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, 
     check_conditioned).  start_params / start_momentum: continue a local
     update from another trainer's state (flat parameters, per-parameter
     momentum buffers) instead of the global model — one step of the reference
-    from the GPU's own state; return_momentum: also return the buffers."""
+    from the GPU's own state; return_momentum: also return the buffers.
+    relu_ties: {ReLU call index: (flat element indices, decisions)} — gate
+    decisions given instead of computed at those elements of that ReLU's input
+    (one batch only): the gate ties of tests/parity.py gate_ties, where the
+    fp64 pre-activation lies inside the fp32 rounding band of zero and the
+    engine's fp32 sums decided the other way.  Every other element, and every
+    arithmetic operation, is the reference's."""
     if threads:
         torch.set_num_threads(threads)
     model = model_cls(spec).to(dtype)
@@ -69,6 +145,8 @@ def local_update(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, 
     criterion = nn.CrossEntropyLoss()
     model.train()
     losses = []
+    if relu_ties and len(batches) != 1:
+        raise ValueError("relu_ties describe one forward: give one batch")
     for s, (images, tokens, labels) in enumerate(batches):
         for d in drops:
             d.mask = None if masks is None else masks[s]
@@ -77,9 +155,10 @@ def local_update(model_cls, spec, global_flat: torch.Tensor, batches: Sequence, 
             for d in drops:
                 d.mask = None if d.mask is None else d.mask.to(dtype)
         optimizer.zero_grad()
-        outputs = model(images, tokens)
-        loss = criterion(outputs, labels)
-        loss.backward()
+        with _relu_hooks(relu_ties):
+            outputs = model(images, tokens)
+            loss = criterion(outputs, labels)
+            loss.backward()
         torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)  # :234
         optimizer.step()
         losses.append(loss.item())

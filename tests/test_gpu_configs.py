@@ -31,7 +31,7 @@ from oracle import training as otrain
 from flr import ops
 from flr.matrix import padded_ld
 from flr.models.multimodal import VIT_BERT, ModelSpec, model_class, param_layout
-from parity import check_delta, delta_report
+from parity import aggregate_report, check_delta, delta_report, tensor_sample
 from flr.round import RoundConfig, RoundEngine
 from flr.train import TrainConfig, make_dropout_masks, synthetic_batches
 
@@ -129,7 +129,8 @@ def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
     K, f, B, steps, mk = 128, 25, 32, 5, 64
     rc = RoundConfig(num_clients=K, batch=B, defense="krum", attack="sign_flip", num_attackers=f)
     eng = RoundEngine(spec, rc, TrainConfig(local_steps=steps), cuda)
-    eng.run_round()
+    glob = eng.global_flat.clone().cpu()
+    new = eng.run_round().clone().cpu()
     eng.defense.publish()
     torch.cuda.synchronize()
     P = eng.trainer.P
@@ -161,6 +162,11 @@ def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
     t0 = time.perf_counter()
     D_ref = reference_distances(rows)
     t_ref = time.perf_counter() - t0
+    # the Multi-Krum mean of the reference's selection (krum.py:182-192: Python
+    # sum of the selected rows in selection order, / multi_k), whole vector, per tensor
+    order_ref0 = np.argsort(orc.krum_scores(D_ref, K - f - 2)).tolist()
+    want = sum(rows[i] for i in order_ref0[:mk]) / mk
+    agg_rep = aggregate_report(new, want, glob, param_layout(spec))
     del rows
     D64h = D64.cpu().numpy()
     off = ~np.eye(K, dtype=bool)
@@ -194,8 +200,12 @@ def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
         "engine_D_bit_identical": bool(np.array_equal(D_gpu.cpu().numpy(), D_ref)),
         "gram_distance_rel_err_vs_fp64": float(np.max(np.abs(D_gram - D64h)[off] / D64h[off])),
         "gram_selected_identical": np.argsort(np.asarray(orc.krum_scores(D_gram, m)))[:mk].tolist() == sel_ref,
+        "aggregate_per_tensor": agg_rep, "aggregate_bit_identical": bool(torch.equal(new, want)),
     }
     _record("c3_krum_trained_round.json", payload)
+    # the aggregate: every tensor's Δ_agg against the oracle's mean of the same rows
+    check_delta({"aggregate": agg_rep})
+    assert torch.equal(new, want)
     # the reference-exact mode: the reference's D bit for bit, so its whole order
     assert np.array_equal(D_mode, D_ref)
     assert order_mode[:mk] == sel_ref and order_mode[mk:] == rej_ref
@@ -205,11 +215,6 @@ def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
     assert eng.defense.client_scores == [float(v) for v in s_ref]
     assert eng.defense.selected_clients == sel_ref and eng.defense.rejected_clients == rej_ref
     assert not set(eng.defense.selected_clients) & set(range(f))
-
-
-def _strided(P: int, n: int = 1_100_000) -> torch.Tensor:
-    step = max(1, P // n)
-    return torch.arange(0, P, step, dtype=torch.int64)
 
 
 def _sample_rows(eng, clients, idx: torch.Tensor) -> torch.Tensor:
@@ -264,15 +269,16 @@ def test_c4_round_trimmed_mean_vit_bert(cuda):
     _record("c4_update_parity_b8_1step.json", {"config": "C4 round, B=8, 1 step", **reps})
     check_delta(reps)
     P = eng.trainer.P
-    idx = _strided(P)
+    idx, lay = tensor_sample(param_layout(spec))
     sub = _sample_rows(eng, range(K), idx)
     want, t = orc.trimmed_mean([[sub[k]] for k in range(K)], 0.1)
     assert t == 25
     got = new[idx.to(cuda)].cpu()
-    err = _rel(got, want[0])
+    agg_rep = aggregate_report(got, want[0], glob[idx], lay)
     _record("c4_trimmed_round.json", {"config": "C4: K=256 trimmed mean (t=25), ViT-S/4 + BERT-mini, B=8, 1 step",
-                                      "P": P, "coords_checked": int(idx.numel()), "aggregate_rel_err": err})
-    assert err < 1e-5, err
+                                      "P": P, "coords_checked": int(idx.numel()),
+                                      "aggregate_rel_err": _rel(got, want[0]), "aggregate_per_tensor": agg_rep})
+    check_delta({"aggregate": agg_rep})
 
 
 @pytest.mark.timeout(900)
@@ -310,14 +316,27 @@ def test_c5_round_backdoor_krum_trimmed_mean(cuda):
     # torch-order rows; the whole D within the reference's own fp32 error of fp64
     assert eng.defense.pairwise_method == "reference"
     from oracle import normref
-    ks = [0, 1, 101, 102, 300, 511]
-    rows = {k: (eng.trainer.to_torch_order(X[k]) if eng.train_order else X[k]).cpu().numpy() for k in ks}
     Dh = D_gpu.cpu().numpy()
-    for a in range(len(ks)):
-        for b in range(a + 1, len(ks)):
-            i, j = ks[a], ks[b]
-            assert Dh[i, j] == normref.norm_diff(rows[i], rows[j]), (i, j)
-    del rows
+
+    def torch_row(k):
+        return (eng.trainer.to_torch_order(X[k]) if eng.train_order else X[k]).cpu().numpy()
+    # two whole rows of D (an attacker's and a benign client's: 2 x 511 pairs)
+    # against the reference's fp32 accumulation (oracle/norm_ref.c), bit for bit
+    t0 = time.perf_counter()
+    row_pairs = 0
+    for i in (0, 300):
+        ri = torch_row(i)
+        for c0 in range(0, K, 32):
+            js = [j for j in range(c0, min(K, c0 + 32)) if j != i]
+            rj = {j: torch_row(j) for j in js}
+            with ThreadPoolExecutor(16) as ex:
+                vals = list(ex.map(lambda j: normref.norm_diff(ri, rj[j]), js))
+            for j, v in zip(js, vals):
+                assert Dh[i, j] == v and Dh[j, i] == v, (i, j, Dh[i, j], v)
+            row_pairs += len(js)
+            del rj
+        print(f"[D row {i}] {K - 1} pairs bit-identical, {time.perf_counter() - t0:.1f} s", flush=True)
+    del ri
     assert dist_err < 1e-2, dist_err
     m, mk = K - f - 2, K // 2
     s_gpu = orc.krum_scores(D_gpu.cpu().numpy(), m)
@@ -327,18 +346,19 @@ def test_c5_round_backdoor_krum_trimmed_mean(cuda):
     rep = _order_report(s_gpu, s64, s64, mk)
     rep.pop("order_a"), rep.pop("order_b")
     sel = eng.defense.selected_clients
-    idx = _strided(P)
+    idx, lay = tensor_sample(param_layout(spec))
     sub = _sample_rows(eng, sel, idx)  # in selection (score) order, as the reference stacks them
     want, t = orc.trimmed_mean([[sub[i]] for i in range(len(sel))], 0.1)
     assert t == eng.defense.num_trimmed_per_end == 25
     got = new[idx.to(cuda)].cpu()
-    err = _rel(got, want[0])
+    agg_rep = aggregate_report(got, want[0], glob[idx], lay)
     _record("c5_backdoor_round.json", {
         "config": "C5: K=512, backdoor clients 0..101, Multi-Krum (multi_k=256) + trimmed mean (t=25), "
                   "ViT-S/4 + BERT-mini, B=32, 1 step",
-        "P": P, "distance_rel_err_gpu_vs_fp64": dist_err, "coords_checked": int(idx.numel()),
-        "aggregate_rel_err": err, "backdoor_clients_selected": sorted(set(sel) & set(range(f))), **rep})
-    assert err < 1e-5, err
+        "P": P, "distance_rel_err_gpu_vs_fp64": dist_err, "D_pairs_bit_identical_to_reference": row_pairs,
+        "coords_checked": int(idx.numel()), "aggregate_rel_err": _rel(got, want[0]),
+        "aggregate_per_tensor": agg_rep, "backdoor_clients_selected": sorted(set(sel) & set(range(f))), **rep})
+    check_delta({"aggregate": agg_rep})
 
 
 @pytest.mark.timeout(900)
@@ -357,13 +377,14 @@ def test_c4_round_bench_shape_update_parity(cuda):
     new = eng.run_round().clone()
     torch.cuda.synchronize()
     reps = _check_clients(eng, spec, glob, [3, 250], eng.batches, eng.masks, losses=True)
-    P = eng.trainer.P
-    idx = _strided(P, 400_000)
+    idx, lay = tensor_sample(param_layout(spec), 2048)
     sub = _sample_rows(eng, range(K), idx)
     want, t = orc.trimmed_mean([[sub[k]] for k in range(K)], 0.1)
-    err = _rel(new[idx.to(cuda)].cpu(), want[0])
+    got = new[idx.to(cuda)].cpu()
+    agg_rep = aggregate_report(got, want[0], glob[idx], lay)
     _record("c4_update_parity_bench_shape.json", {"config": "C4 round at the bench shape: K=256 trimmed mean, "
                                                             "ViT-S/4 + BERT-mini, B=32, 5 local steps",
-                                                  "aggregate_rel_err": err, **reps})
-    assert err < 1e-5, err
+                                                  "aggregate_rel_err": _rel(got, want[0]),
+                                                  "aggregate_per_tensor": agg_rep, **reps})
     check_delta(reps)
+    check_delta({"aggregate": agg_rep})

@@ -244,3 +244,27 @@ def test_norm_ref_model_cpu_capability(cap):
     if cap:
         assert rec["capability"].lower() == cap
     assert rec["mismatches"] == 0, rec
+
+
+def test_relu_ties_resolve_only_the_given_gates():
+    """oracle.training relu_ties (the gate-tie resolution of the step-2 parity
+    check): the reference's own decisions given back leave the step bit-identical;
+    one decision forced the other way changes it; relu_inputs reads the inputs."""
+    from oracle import training as otrain
+    from flr.models.multimodal import TINY, MultimodalNet, param_layout
+    torch.manual_seed(0)
+    P = sum(int(np.prod(s)) for _, s in param_layout(TINY))
+    glob = torch.randn(P) * 0.1
+    im = torch.randn(4, TINY.in_channels, 32, 32)
+    tk = torch.randint(0, TINY.vocab, (4, TINY.seq_len))
+    lb = torch.randint(0, TINY.num_classes, (4,))
+    cb = [(im, tk, lb)]
+    base, _ = otrain.local_update(MultimodalNet, TINY, glob, cb)
+    z = otrain.relu_inputs(MultimodalNet, TINY, glob, im, tk)
+    assert len(z) >= 2 and z[1].dim() == 4
+    idx = torch.arange(0, z[1].numel(), 7)
+    same, _ = otrain.local_update(MultimodalNet, TINY, glob, cb, relu_ties={1: (idx, z[1].reshape(-1)[idx] > 0)})
+    assert all(torch.equal(a, b) for a, b in zip(base, same))
+    j = int((z[1].reshape(-1) > 0).nonzero()[0])
+    off, _ = otrain.local_update(MultimodalNet, TINY, glob, cb, relu_ties={1: (torch.tensor([j]), torch.tensor([False]))})
+    assert not all(torch.equal(a, b) for a, b in zip(base, off))
