@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of library builds: conv_bench + C3 bench per FLR_LIB.
-# usage: tools/gpu_ab_libs.sh name1 name2 ...  (names under abl/, "main" = the in-tree lib)
+# usage: tools/archive/gpu_ab_libs.sh name1 name2 ...  (names under abl/, "main" = the in-tree lib)
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out

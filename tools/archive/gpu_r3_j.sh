@@ -9,4 +9,4 @@ FLR_SG_DB=2 timeout -k 10 600 python -u -m pytest tests/test_gpu_conv.py tests/t
   --timeout-method thread > gpurun_out/r3j_db_tests.log 2>&1 || exit 1
 timeout -k 10 300 python -u tools/conv_bench.py --variants "FLR_SG_DB=2;FLR_SG_DB=3" > gpurun_out/r3j_conv.txt 2>&1 || exit 1
 timeout -k 10 300 python -u tools/bgemm_bench.py --variants "FLR_SG_DB=2;FLR_SG_DB=3" > gpurun_out/r3j_bgemm.txt 2>&1 || exit 1
-bash tools/gpu_r3_i.sh
+bash tools/archive/gpu_r3_i.sh

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 closing check on the final library: full -m gpu suite + smoke, the C3 line (cpu_baseline), the
-# C4 / C5 lines come from tools/gpu_r4_bench.sh (CONFIGS="C4 C5") in a call of their own.
+# C4 / C5 lines come from tools/archive/gpu_r4_bench.sh (CONFIGS="C4 C5") in a call of their own.
 export TMPDIR=/tmp
 set -o pipefail
 cd "$(dirname "$0")/.."

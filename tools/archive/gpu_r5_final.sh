@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-5 final library: the whole -m gpu suite (two processes), smoke(), the default bench line
 set -o pipefail
-sed 's#r5full#r5final3#g' tools/gpu_r5_full.sh > /tmp/final.sh && bash /tmp/final.sh || exit $?
+sed 's#r5full#r5final3#g' tools/archive/gpu_r5_full.sh > /tmp/final.sh && bash /tmp/final.sh || exit $?
 D=gpurun_out/r5final3
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $D/smoke.log; exit 1; }
 tail -1 $D/smoke.log

@@ -1,7 +1,7 @@
 #!/bin/bash
 # the whole -m gpu suite on the zero-filled-stream chain kernel, then the default bench line and its kernel summary
 set -o pipefail
-sed 's#r5full#r5full2#g' tools/gpu_r5_full.sh > /tmp/full2.sh && bash /tmp/full2.sh || exit $?
+sed 's#r5full#r5full2#g' tools/archive/gpu_r5_full.sh > /tmp/full2.sh && bash /tmp/full2.sh || exit $?
 mkdir -p gpurun_out/r5z
 timeout -k 10 300 python -u bench.py > gpurun_out/r5z/c3_default.json 2> gpurun_out/r5z/c3_default.err || { echo "bench failed"; tail -20 gpurun_out/r5z/c3_default.err; exit 1; }
 cat gpurun_out/r5z/c3_default.json

@@ -1,4 +1,4 @@
-# PMC stall breakdown of the conv kernels: usage LAYERS="l1 l3b" bash tools/pmc_conv.sh
+# PMC stall breakdown of the conv kernels: usage LAYERS="l1 l3b" bash tools/archive/pmc_conv.sh
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for L in ${LAYERS:-l1 l3b}; do

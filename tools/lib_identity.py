@@ -1,7 +1,7 @@
 """Bit-identity of library builds: one seeded round of the ResNet+GRU model (C3
 shapes, K clients) and one of the ViT-S + BERT-mini model (C4 shapes, 2 clients
 of 1 step), printing the sha256 of the client matrix X and the new global vector.
-Run once per FLR_LIB and compare the lines (tools/gpu_r3_y.sh).
+Run once per FLR_LIB and compare the lines (tools/archive/gpu_r3_y.sh).
 usage: FLR_LIB=... python tools/lib_identity.py"""
 import hashlib
 import os
