@@ -162,8 +162,9 @@ __global__ __launch_bounds__(THREADS, 3) void orderstat_kernel(const float* __re
 // the in-lane sort's 32-register quarters screened and sorted in turn, so ≈ 1600 of
 // its ≈ 5250 compare-exchange instructions run while later quarters' loads are
 // still in flight (C5 trimmed mean 23.7 -> 23.3 ms, median 19.9 -> 19.2; C4 10.1 ->
-// 9.8 and 8.5 -> 8.0; halves gave 23.4 / 19.4 / 9.9 / 8.2).  Trimmed sums are per-lane sequential in rank
-// order, combined in lane order (deterministic; 1e-5 vs torch, not bit-exact).
+// 9.8 and 8.5 -> 8.0; halves gave 23.4 / 19.4 / 9.9 / 8.2).  Trimmed sums follow
+// torch's cascade in rank order across the group's lanes (below): bit-identical
+// to torch on the vectorised columns, as the single-lane kernel.
 template <int CTRL>
 __device__ __forceinline__ float dpp_swap(float x) {
   // all lanes valid (quad permutation, full masks): no "old" operand to initialise
@@ -302,23 +303,41 @@ __global__ __launch_bounds__(THREADS) void orderstat_multilane_kernel(const floa
     for (int i = 0; i < 128; ++i) r = (i == loc) ? v[i] : r;
     if (active && g == med / 128) out[p] = nnan > 0 ? __builtin_nanf("") : r;  // the lane that owns rank med
   } else {
-    const int lo = t, hi = K - t;
-    float acc = 0.f;
+    // torch's outer-reduction cascade (multi_row_sum, level step 16: the block
+    // sums folded into a1 every 16 ranks, a1 into a2 every 256) over the ranks
+    // [t, K - t) in rank order, which run through the group's lanes in lane
+    // order: pass s continues the cascade over lane s's registers from the state
+    // lane s - 1 left (broadcast in the group), so every add is torch's add in
+    // torch's order (bit-identical on the vectorised columns, like the
+    // single-lane kernel).  Every lane runs every pass (wave-uniform work: L x
+    // 128 conditional adds against the ~5000-instruction sort)
+    const int tu = __builtin_amdgcn_readfirstlane(t);
+    const int R = __builtin_amdgcn_readfirstlane(K - 2 * tu);
+    const int nfull = R & ~15;
+    static_assert(128 * L <= 4096, "the level-3 fold (4096 ranks) is not implemented");
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    const int gbase = (int)(threadIdx.x & 63) & ~(L - 1);
 #pragma unroll
-    for (int i = 0; i < 128; ++i) {
-      const int e = 128 * g + i;
-      acc = (e >= lo && e < hi) ? add_rn(acc, v[i]) : acc;
-    }
-    // combine lanes in order 0..L-1 (lane 0 ends with the total)
-    float tot = acc;
-    if constexpr (L >= 2) {
-      const float a1 = __shfl_down(acc, 1, 64);
-      tot = add_rn(acc, a1);  // lanes 0: acc0 + acc1 ; lane 2: acc2 + acc3
-      if constexpr (L == 4) {
-        const float t2 = __shfl_down(tot, 2, 64);
-        tot = add_rn(tot, t2);
+    for (int s = 0; s < L; ++s) {
+      float b0 = a0, b1 = a1, b2 = a2;
+#pragma unroll
+      for (int i = 0; i < 128; ++i) {
+        const int pos = 128 * g + i - tu;
+        const bool in = (unsigned)pos < (unsigned)R;
+        b0 = in ? add_rn(b0, v[i]) : b0;
+        const bool f1 = in && pos < nfull && ((pos + 1) & 15) == 0;
+        const bool f2 = f1 && ((pos + 1) & 0xF0) == 0;
+        b1 = f1 ? add_rn(b1, b0) : b1;
+        b0 = f1 ? 0.f : b0;
+        b2 = f2 ? add_rn(b2, b1) : b2;
+        b1 = f2 ? 0.f : b1;
       }
+      a0 = __shfl(b0, gbase + s, 64);
+      a1 = __shfl(b1, gbase + s, 64);
+      a2 = __shfl(b2, gbase + s, 64);
     }
+    float tot = add_rn(a0, a1);
+    tot = add_rn(tot, a2);
     if (active && g == 0) out[p] = nnan > t ? __builtin_nanf("") : div_rn(tot, (float)(K - 2 * t));
   }
 }

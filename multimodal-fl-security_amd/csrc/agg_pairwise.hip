@@ -839,10 +839,21 @@ __global__ __launch_bounds__(256) void pivot_kernel(const double* __restrict__ D
   __shared__ int bi[256];
   double v = __builtin_huge_val();
   int ix = 0x7fffffff;
+  // rows with a non-finite sample distance to at most half the others: a
+  // client that sent NaN / inf (its whole row non-finite) is never the pivot,
+  // and the others' sums skip its column (a NaN pivot made every
+  // off-diagonal distance NaN, so Krum's order fell back to the identity)
   for (int i = threadIdx.x; i < K; i += 256) {
     double r = 0.0;
-    for (int j = 0; j < K; ++j) r += Ds[(int64_t)i * K + j];
-    if (r < v) { v = r; ix = i; }
+    int bad = 0;
+    for (int j = 0; j < K; ++j) {
+      const double d = Ds[(int64_t)i * K + j];
+      if (__builtin_isfinite(d))
+        r += d;
+      else
+        ++bad;
+    }
+    if (2 * bad <= K - 1 && r < v) { v = r; ix = i; }
   }
   bv[threadIdx.x] = v;
   bi[threadIdx.x] = ix;

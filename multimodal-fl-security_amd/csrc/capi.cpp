@@ -38,11 +38,23 @@ __attribute__((constructor)) void knobs_from_environment() {
 }
 }  // namespace
 
+// The value is copied under the lock into this thread's own table (ADVICE r5:
+// a pointer into the shared table dangled when another thread's
+// flr_set_knob replaced the entry).  The returned pointer stays valid until
+// this thread asks for the same name again.
 const char* knob(const char* name) {
-  std::lock_guard<std::mutex> lock(g_knob_mu);
-  auto& t = knob_table();
-  auto it = t.find(name);
-  return it == t.end() ? nullptr : it->second.c_str();
+  thread_local std::unordered_map<std::string, std::string> copies;
+  std::string v;
+  {
+    std::lock_guard<std::mutex> lock(g_knob_mu);
+    auto& t = knob_table();
+    auto it = t.find(name);
+    if (it == t.end()) return nullptr;
+    v = it->second;
+  }
+  std::string& c = copies[name];
+  c = std::move(v);
+  return c.c_str();
 }
 }  // namespace flr
 

@@ -8,7 +8,8 @@ wrong dtype or a missing library raises.
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Sequence, Tuple
+import os
+from typing import Dict, Optional, Sequence, Tuple
 
 import torch
 
@@ -59,8 +60,7 @@ def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None, comm=None,
             Xa[:, :P].copy_(X)
             X, ldx = Xa, Xa.stride(0)
         part, nparts = (0, 1) if comm is None else (comm.rank, comm.world)
-        nbytes = int(_capi.lib().flr_pairwise_l2_reference_workspace(K, P))
-        ws, wp = _ws(nbytes, X.device)
+        wp, nbytes = _ref_workspace(K, P, X.device, _stream(X))
         taps = [int(v) for blk in (tap_blocks or ()) for v in blk]
         tarr = (ctypes.c_int64 * max(1, len(taps)))(*taps)
         _capi.call("flr_pairwise_l2_reference_tap", X.data_ptr(), K, P, ldx, ctypes.addressof(tarr), len(taps) // 4,
@@ -219,6 +219,33 @@ def weighted_rows(X: torch.Tensor, weights, divisor: float, rows=None, scales=No
 
 
 # ---- coordinate-sharded Krum distances (flr_pairwise_* phases, include/flr.h) ----
+
+# The reference-exact distances' workspace (the chain sums and the chain-major
+# copy of X, up to 8 GiB per segment: ~6 GB at C3) is kept per (device,
+# stream) and reused by every later call that fits in it, instead of being
+# allocated per call.  FLR_REF_WS_CAP (bytes) bounds it: the
+# library then runs the chains over more, shorter segments (the same D).
+REF_WS_CAP = int(os.environ.get("FLR_REF_WS_CAP", "0")) or None
+_REF_WS: Dict[Tuple[int, int], torch.Tensor] = {}
+
+
+def _ref_workspace(K: int, P: int, device, stream: int) -> Tuple[int, int]:
+    nbytes = int(_capi.lib().flr_pairwise_l2_reference_workspace(K, P))
+    if REF_WS_CAP is not None:
+        nbytes = min(nbytes, REF_WS_CAP)
+    key = (torch.device(device).index or 0, stream)
+    ws = _REF_WS.get(key)
+    if ws is None or ws.numel() < nbytes + 256:
+        _REF_WS.pop(key, None)
+        ws = torch.empty(max(nbytes, 256) + 256, dtype=torch.uint8, device=device)
+        _REF_WS[key] = ws
+    return ws.data_ptr() + (-ws.data_ptr()) % 256, nbytes
+
+
+def release_workspaces() -> None:
+    """Drop the cached reference-exact workspaces (their HBM returns to torch's allocator)."""
+    _REF_WS.clear()
+
 
 def _ws(nbytes: int, device) -> Tuple[torch.Tensor, int]:
     ws = torch.empty(max(nbytes, 256) + 256, dtype=torch.uint8, device=device)

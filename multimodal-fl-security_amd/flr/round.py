@@ -49,12 +49,12 @@ class RoundConfig:
     graph: bool = True                   # replay the training phase as one captured HIP graph (FLR_GRAPH=0: eager)
     fallback_fedavg: bool = False        # defense raises -> FedAvg of the round (robust_server.py:120-122)
     # with fallback_fedavg: also fall back on library / device errors (FlrError,
-    # out of memory), as the reference's `except Exception` does.  Off by
-    # default: a device error is loud (a sticky HIP error would fail the
-    # fallback's own kernels too), and at world > 1 it is never swallowed — one
-    # rank falling back while the others wait in the defense's next collective
-    # would hang the round instead of failing it
-    fallback_device_errors: bool = False
+    # out of memory), as the reference's `except Exception` does (the default:
+    # ADVICE r5, parity with robust_server.py:120-122).  At world > 1 a device
+    # error is never swallowed — one rank falling back while the others wait in
+    # the defense's next collective would hang the round instead of failing it;
+    # False keeps device errors loud at world 1 too
+    fallback_device_errors: bool = True
 
 
 def initial_global(spec: ModelSpec, seed: int, device) -> torch.Tensor:

@@ -217,6 +217,42 @@ def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
     assert not set(eng.defense.selected_clients) & set(range(f))
 
 
+def _trimmed_cascade(sub: torch.Tensor, trim_ratio: float = 0.1):
+    """trimmed_mean.py:63-90 on the sampled [n_rows, n] host matrix: torch.sort
+    along the clients, rows [t, n_rows - t), summed in torch's vectorised
+    outer-reduction order (oracle.aggregation.torch_outer_sum: every column of
+    a real parameter but the last numel % 16, i.e. all but fc2.bias's 10 in
+    both models) / R.  Returns (mean, t)."""
+    n = sub.shape[0]
+    t = max(1, int(n * trim_ratio))
+    srt = torch.sort(sub, dim=0)[0][t:n - t]
+    return orc.torch_outer_sum(srt) / (n - 2 * t), t
+
+
+def _tail_param_report(eng, spec, new, rows, glob, name="fc2.bias"):
+    """The scalar-tail parameter (numel % 16 columns torch reduces with its
+    4-way row_sum instead of the vectorised cascade): the reference's own
+    per-parameter trimmed mean (torch on the [n_rows, numel] stack) against
+    the engine's, and against the vectorised order the engine restates."""
+    off = 0
+    for nm, shp in param_layout(spec):
+        k = int(np.prod(shp))
+        if nm == name:
+            break
+        off += k
+    idx = torch.arange(off, off + k, dtype=torch.int64)
+    sub = _sample_rows(eng, rows, idx)
+    t = max(1, int(len(rows) * 0.1))
+    ref_torch = torch.sort(sub, dim=0)[0][t:len(rows) - t].mean(dim=0)  # trimmed_mean.py:85-88, this parameter
+    vec, _ = _trimmed_cascade(sub)
+    got = new[idx.to(new.device)].cpu()
+    d_gpu = (got - ref_torch).abs()
+    d_vec = (vec - ref_torch).abs()
+    return {"param": name, "coords": k, "engine_equals_vectorised_order": bool(torch.equal(got, vec)),
+            "max_abs_engine_vs_torch": float(d_gpu.max()), "max_abs_vectorised_vs_torch": float(d_vec.max()),
+            "max_delta_ref": float((ref_torch - glob[idx]).abs().max()), "ok": bool((d_gpu <= d_vec).all())}
+
+
 def _sample_rows(eng, clients, idx: torch.Tensor) -> torch.Tensor:
     """[len(clients), len(idx)] host copy of the client rows' torch-order
     coordinates idx (one row converted at a time)."""
@@ -271,14 +307,20 @@ def test_c4_round_trimmed_mean_vit_bert(cuda):
     P = eng.trainer.P
     idx, lay = tensor_sample(param_layout(spec))
     sub = _sample_rows(eng, range(K), idx)
-    want, t = orc.trimmed_mean([[sub[k]] for k in range(K)], 0.1)
+    want, t = _trimmed_cascade(sub)
     assert t == 25
     got = new[idx.to(cuda)].cpu()
-    agg_rep = aggregate_report(got, want[0], glob[idx], lay)
+    agg_rep = aggregate_report(got, want, glob[idx], lay)
+    tail = _tail_param_report(eng, spec, new, range(K), glob)
     _record("c4_trimmed_round.json", {"config": "C4: K=256 trimmed mean (t=25), ViT-S/4 + BERT-mini, B=8, 1 step",
                                       "P": P, "coords_checked": int(idx.numel()),
-                                      "aggregate_rel_err": _rel(got, want[0]), "aggregate_per_tensor": agg_rep})
+                                      "aggregate_rel_err": _rel(got, want), "aggregate_per_tensor": agg_rep,
+                                      "tail_parameter": tail})
+    # per tensor: Δ_agg within the bar of the oracle's aggregate of the same rows
+    # (bit-identical expected: the same sort, torch's cascade order)
     check_delta({"aggregate": agg_rep})
+    assert agg_rep["bit_identical_coords"] == agg_rep["coords"], agg_rep["bit_identical_coords"]
+    assert tail["ok"], tail
 
 
 @pytest.mark.timeout(900)
@@ -348,17 +390,21 @@ def test_c5_round_backdoor_krum_trimmed_mean(cuda):
     sel = eng.defense.selected_clients
     idx, lay = tensor_sample(param_layout(spec))
     sub = _sample_rows(eng, sel, idx)  # in selection (score) order, as the reference stacks them
-    want, t = orc.trimmed_mean([[sub[i]] for i in range(len(sel))], 0.1)
+    want, t = _trimmed_cascade(sub)
     assert t == eng.defense.num_trimmed_per_end == 25
     got = new[idx.to(cuda)].cpu()
-    agg_rep = aggregate_report(got, want[0], glob[idx], lay)
+    agg_rep = aggregate_report(got, want, glob[idx], lay)
+    tail = _tail_param_report(eng, spec, new, sel, glob)
     _record("c5_backdoor_round.json", {
         "config": "C5: K=512, backdoor clients 0..101, Multi-Krum (multi_k=256) + trimmed mean (t=25), "
                   "ViT-S/4 + BERT-mini, B=32, 1 step",
         "P": P, "distance_rel_err_gpu_vs_fp64": dist_err, "D_pairs_bit_identical_to_reference": row_pairs,
-        "coords_checked": int(idx.numel()), "aggregate_rel_err": _rel(got, want[0]),
-        "aggregate_per_tensor": agg_rep, "backdoor_clients_selected": sorted(set(sel) & set(range(f))), **rep})
+        "coords_checked": int(idx.numel()), "aggregate_rel_err": _rel(got, want),
+        "aggregate_per_tensor": agg_rep, "tail_parameter": tail,
+        "backdoor_clients_selected": sorted(set(sel) & set(range(f))), **rep})
     check_delta({"aggregate": agg_rep})
+    assert agg_rep["bit_identical_coords"] == agg_rep["coords"], agg_rep["bit_identical_coords"]
+    assert tail["ok"], tail
 
 
 @pytest.mark.timeout(900)
@@ -379,12 +425,13 @@ def test_c4_round_bench_shape_update_parity(cuda):
     reps = _check_clients(eng, spec, glob, [3, 250], eng.batches, eng.masks, losses=True)
     idx, lay = tensor_sample(param_layout(spec), 2048)
     sub = _sample_rows(eng, range(K), idx)
-    want, t = orc.trimmed_mean([[sub[k]] for k in range(K)], 0.1)
+    want, t = _trimmed_cascade(sub)
     got = new[idx.to(cuda)].cpu()
-    agg_rep = aggregate_report(got, want[0], glob[idx], lay)
+    agg_rep = aggregate_report(got, want, glob[idx], lay)
     _record("c4_update_parity_bench_shape.json", {"config": "C4 round at the bench shape: K=256 trimmed mean, "
                                                             "ViT-S/4 + BERT-mini, B=32, 5 local steps",
-                                                  "aggregate_rel_err": _rel(got, want[0]),
+                                                  "aggregate_rel_err": _rel(got, want),
                                                   "aggregate_per_tensor": agg_rep, **reps})
     check_delta(reps)
     check_delta({"aggregate": agg_rep})
+    assert agg_rep["bit_identical_coords"] == agg_rep["coords"], agg_rep["bit_identical_coords"]

@@ -47,8 +47,8 @@ def test_fedavg_fallback_when_defense_raises(cuda):
     strict = RoundEngine(TINY, RoundConfig(defense="krum", **kw), TrainConfig(local_steps=1), cuda)
     with pytest.raises(ValueError):
         strict.run_round()
-    # a device / library failure: loud by default (fallback_device_errors=False);
-    # fallback_device_errors=True falls back as the reference's `except Exception`
+    # a device / library failure: falls back by default, as the reference's
+    # `except Exception` (fallback_device_errors=True); False keeps it loud
     from flr._capi import FlrError
 
     def _fail(*a, **k):
@@ -70,14 +70,20 @@ def test_round_refine_overflow_raises(cuda):
     """K = 300 with 140 sign-flipped clients — more far-cluster rows
     than the Gram path refines.  The round raises on its own device path
     (run_round never calls publish), instead of ranking a NaN matrix; with the
-    FedAvg fallback on, device errors stay loud by default."""
+    FedAvg fallback on it falls back (the default, as the reference's `except
+    Exception`) unless fallback_device_errors=False."""
     from flr._capi import FlrError
     kw = dict(num_clients=300, batch=4, defense="krum", attack="sign_flip", num_attackers=140, graph=False,
               defense_cfg={"pairwise_method": "gram"})
-    for fb in (False, True):
-        eng = RoundEngine(TINY, RoundConfig(fallback_fedavg=fb, **kw), TrainConfig(local_steps=1), cuda)
+    for fb, dev in ((False, True), (True, False)):
+        eng = RoundEngine(TINY, RoundConfig(fallback_fedavg=fb, fallback_device_errors=dev, **kw),
+                          TrainConfig(local_steps=1), cuda)
         with pytest.raises(FlrError):
             eng.run_round()
+    # the default with the fallback on: FedAvg, as the reference's `except Exception`
+    eng = RoundEngine(TINY, RoundConfig(fallback_fedavg=True, **kw), TrainConfig(local_steps=1), cuda)
+    eng.run_round()
+    assert eng.fell_back and eng.fallback_error == "FlrError"
 
 
 def test_fltrust_round(cuda):
