@@ -1685,6 +1685,9 @@ __device__ __forceinline__ int zimg(int row, int c) {
 #ifndef FLR_SG_OCC
 #define FLR_SG_OCC 2
 #endif
+#ifndef FLR_FRAG_AHEAD
+#define FLR_FRAG_AHEAD 1
+#endif
 template <class P> struct has_k8 : std::false_type {};
 template <> struct has_k8<FwdT> : std::true_type {};
 template <> struct has_k8<DgradT> : std::true_type {};
@@ -1868,10 +1871,43 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
 #pragma unroll
       for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(&Ls[ST][MS + j][t][zimg(srowB, skB >> 3)]) = pb[j][t];
   };
+  // FLR_FRAG_AHEAD (default): both k-steps' fragments are read before the
+  // first MFMA, so the second k-step's LDS latency runs under the first's MFMAs
+  // and the reads are complete by the barrier that follows (the compiler keeps
+  // the reads ahead of that barrier and moves the second k-step's MFMAs after
+  // it); 0: read per k-step (A/B build).  Same operands, same MFMA order.
   auto compute_tile = [&](auto stc) {
       constexpr int ST = decltype(stc)::value;
+      constexpr int NKS = BK / 16;
+#if FLR_FRAG_AHEAD
+      bf16x8 fa[NKS][MSW][3], fb[NKS][NS][3];
 #pragma unroll
-      for (int s = 0; s < BK / 16; ++s) {
+      for (int s = 0; s < NKS; ++s) {
+        const int ko = 16 * s + 8 * h;
+#pragma unroll
+        for (int i = 0; i < MSW; ++i)
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            fa[s][i][q] = *reinterpret_cast<const bf16x8*>(&Ls[ST][a_sub(i)][q][zimg(a_row(i), ko >> 3)]);
+#pragma unroll
+        for (int j = 0; j < NS; ++j)
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            fb[s][j][q] = *reinterpret_cast<const bf16x8*>(&Ls[ST][MS + j][q][zimg(b_row(), ko >> 3)]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the scheduler would sink the second k-step's reads again
+#define FLR_SX(TA, TB)                                                                              \
+  _Pragma("unroll") for (int i = 0; i < MSW; ++i) _Pragma("unroll") for (int j = 0; j < NS; ++j) \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i][TA], fb[s][j][TB], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        // product-major, small terms first (term 0 = hi, 1 = mid, 2 = lo)
+        FLR_SX(1, 1) FLR_SX(0, 2) FLR_SX(2, 0) FLR_SX(0, 1) FLR_SX(1, 0) FLR_SX(0, 0)
+      }
+#undef FLR_SX
+#else
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
         bf16x8 fa[MSW][3], fb[NS][3];
         const int ko = 16 * s + 8 * h;
 #pragma unroll
@@ -1891,6 +1927,7 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
         FLR_SX(1, 1) FLR_SX(0, 2) FLR_SX(2, 0) FLR_SX(0, 1) FLR_SX(1, 0) FLR_SX(0, 0)
 #undef FLR_SX
       }
+#endif
   };
   const int ntile = rend > rbeg ? (rend - rbeg + BK - 1) / BK : 0;
   using Q0 = std::integral_constant<int, 0>;
