@@ -67,6 +67,22 @@ def gram_traffic(K: int, P: int):
     return (2.0 * t["fetch_kib"] + t["write_kib"]) * 1024.0
 
 
+def ref_traffic(K: int, P: int):
+    """HBM bytes of one reference-exact distance call (the transposes, the tap
+    rewrite, the chains and the finish) from the committed rocprofv3 PMC
+    passes (profiles/r6_ref/ref_traffic.json: FETCH_SIZE and WRITE_SIZE in KiB
+    per call, separate passes, FETCH_SIZE doubled per MI355X_MICROARCH.md's
+    gfx950 correction for 16-B-per-lane reads); None unless measured at this
+    exact shape."""
+    path = os.path.join(ROOT, "profiles", "r6_ref", "ref_traffic.json")
+    if not os.path.exists(path):
+        return None
+    t = json.load(open(path))
+    if t.get("K") != K or t.get("P") != P:
+        return None
+    return (2.0 * t["fetch_kib_per_call"] + t["write_kib_per_call"]) * 1024.0
+
+
 COMMITTED_C3_STATS = "profiles/r4_c3_kernel_stats_serial.txt"  # FLR_TEXT_STREAM=0: per-kernel durations without the text stream beside them
 # the C4 bench's rocprofv3 summary (gemm_mfma_from_profile of an unmodified C4 line)
 COMMITTED_C4_STATS = "profiles/r3_c4_kernel_stats.txt"
@@ -597,7 +613,8 @@ def main() -> None:
             "kernel": "reference-exact distance phase (chain_transpose_kernel + tap_chain_kernel + ref_chain_kernel "
                       "+ ref_finish_kernel)",
             "bound": "valu", "unit": "Gop/s", "achieved": phase["valu_lane_ops"] / (phase["ms"] * 1e-3) / 1e9,
-            "peak": VALU_PEAK_OPS / 1e9, "frac": phase["valu_frac"], "traffic": None,
+            "peak": VALU_PEAK_OPS / 1e9, "frac": phase["valu_frac"],
+            "traffic": ref_traffic(K, P) if world == 1 else None,
             "kernel_ms": phase["ms"], "lane_ops": phase["valu_lane_ops"],
             "one_wave_issue_frac": phase["valu_frac"] * 2.0,
             "note": "lane-ops = 2 (v_sub + v_fma) x 8 chains x K(K-1)/2 pairs x P/8 steps; peak = fp32 VALU at "
