@@ -359,7 +359,14 @@ def round_collectives(eng, defense: str, K: int, P: int, world: int):
         ld = eng.xchg.plan.ld
         out.append({"op": "all_to_all", "what": "client rows -> coordinate ranges",
                     "bytes_sent_per_gpu": 4 * (world - 1) * kl * ld})
-        if defense in ("krum", "multi_krum", "krum_trimmed_mean"):
+        if defense in ("krum", "multi_krum", "krum_trimmed_mean") and \
+                getattr(eng.defense, "pairwise_method", "gram") == "reference":
+            # the chains handed rank to rank (ops.pairwise_l2_reference_sharded), D broadcast
+            out += [{"op": "send/recv", "what": "8 chain sums per pair [8, K, K] to the next rank",
+                     "bytes_sent_per_gpu": 4 * 8 * K * K},
+                    {"op": "broadcast", "what": "distance matrix [K, K] fp64 from the last rank",
+                     "bytes_per_gpu": 8 * K * K}]
+        elif defense in ("krum", "multi_krum", "krum_trimmed_mean"):
             S = int(_capi.lib().flr_pairwise_sample_len(P))
             glen = int(_capi.lib().flr_pairwise_gsum_len(K))
             out += [{"op": "all_reduce", "what": "pivot sample [K, S]",
@@ -551,14 +558,16 @@ def main() -> None:
     # (HIP events around its launch, on the stream it runs on); sharded: this
     # GPU's coordinates.  Timed for every config (the Krum roofline line).
     kms = []
-    for _ in range(reps):
+    # (not at tap-block-aligned rank boundaries: the Gram records need the canonical slices)
+    gram_timed = not (sharded and eng.slice.plan.bounds is not None)
+    for _ in range(reps if gram_timed else 0):
         ev = HipEventPair()
         if sharded:
             ops.pairwise_l2_sharded(eng.slice, events=ev.handles)
         else:
             ops.pairwise_l2(eng.full.X, "gram", events=ev.handles)
         kms.append(ev.elapsed_ms())
-    kernel_ms = sum(kms) / len(kms)
+    kernel_ms = sum(kms) / len(kms) if kms else None
     # the whole Krum distance phase: every kernel that produces D —
     # Gram: pivot sample + Gram + far-cluster refine + reductions, HBM-bound;
     # reference: chain-major transposes + chains + finish, VALU-issue-bound
@@ -593,9 +602,9 @@ def main() -> None:
             phase["bound"] = "hbm"
     n_coords = eng.slice.n if sharded else P
     pair_bytes = 4.0 * K * n_coords + 8.0 * K * K
-    achieved = pair_bytes / (kernel_ms * 1e-3) / 1e9
+    achieved = pair_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None
     traffic = gram_traffic(K, n_coords)
-    gram_roofline = {
+    gram_roofline = None if not gram_timed else {
         "kernel": "gram_partials_kernel (Krum pairwise, centred Gram on MFMA)" + (
             " — the --pairwise gram path, timed here beside the round" if phase and phase["method"] == "reference"
             else ""),

@@ -142,6 +142,14 @@ int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx,
 int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t P, int64_t ldx,
                                   const int64_t* taps, int64_t ntaps, double* D, void* ws,
                                   size_t ws_bytes, int64_t part, int64_t nparts, void* stream);
+/* The same with dead taps: dead[b] bit t set = tap t of block b is not in X
+ * (FLR_TC_DEFER_DEAD): its slab is read from gdead at the same training-order
+ * offset, negated on rows k < nneg — the values flr_resnet_gru_fill_dead
+ * writes, so D is bit-identical to the call on the filled X. */
+int flr_pairwise_l2_reference_tap_dead(const float* X, int64_t K, int64_t P, int64_t ldx,
+                                       const int64_t* taps, int64_t ntaps, const uint64_t* dead,
+                                       const float* gdead, int64_t nneg, double* D, void* ws,
+                                       size_t ws_bytes, int64_t part, int64_t nparts, void* stream);
 /* The same split over coordinate ranges held by different ranks (the
  * coordinate-sharded exchange): each range continues the chains where the
  * previous range left them.  _partial: `steps` chain steps of X (coordinates
@@ -156,6 +164,14 @@ int flr_pairwise_l2_reference_partial(const float* X, int64_t K, int64_t steps, 
                                       int first, void* ws, size_t ws_bytes, void* stream);
 int flr_pairwise_l2_reference_finish(const float* Xtail, int64_t K, int64_t ntail, int64_t ldx,
                                      int chains, const void* ws, double* D, void* stream);
+/* The same partial chains over a TRAINING-ORDER coordinate slice (a rank of
+ * a training-order round at G > 1): taps {off, Cout, Cin, KK} name the
+ * tap-major blocks inside the slice (offsets from X, each wholly inside
+ * [0, 8 steps)), as flr_pairwise_l2_reference_tap; the slice must hold whole
+ * blocks (the round engine aligns its rank boundaries to them). */
+int flr_pairwise_l2_reference_partial_tap(const float* X, int64_t K, int64_t steps, int64_t ldx,
+                                          const int64_t* taps, int64_t ntaps, int first, void* ws,
+                                          size_t ws_bytes, void* stream);
 
 /* Direct-difference VALU variant (same contract, exact fp32 differences);
  * a slower second implementation used to cross-check the MFMA path. */
@@ -770,8 +786,14 @@ int flr_train_clients(const flr_resnet_gru_spec* spec, const float* global, floa
  *   common coordinate permutation, so the last optimizer step writes X's rows
  *   directly (no export pass), the untrained dead-tap ranges are copied from
  *   `global`, and only the aggregated P-vector is permuted back.
+ * FLR_TC_DEFER_DEAD (with FLR_TC_TRAIN_ORDER) — the dead-tap ranges are left
+ *   unwritten; the caller writes them with flr_resnet_gru_fill_dead before
+ *   anything reads them (the round engine: on a side stream beside the Krum
+ *   chains, whose tap rewrite reads those taps from `global` itself,
+ *   flr_pairwise_l2_reference_tap_dead).
  * Flag 0 is flr_train_clients. */
 #define FLR_TC_TRAIN_ORDER 1u
+#define FLR_TC_DEFER_DEAD 2u
 int flr_train_clients_ex(const flr_resnet_gru_spec* spec, const float* global, float* X,
                          int64_t ld, const float* images, const int64_t* tokens,
                          const int64_t* labels, const float* dropout_masks, int64_t steps,
@@ -786,6 +808,16 @@ int flr_resnet_gru_reorder(const flr_resnet_gru_spec* spec, const float* src, fl
  * read zero padding at this image size; exact-zero gradients) when
  * weight_decay == 0, else P. */
 int64_t flr_resnet_gru_live_params(const flr_resnet_gru_spec* spec, float weight_decay);
+/* The dead-tap ranges of a training-order row ([off[r], off[r] + n[r]), whole
+ * tap slabs of tap-major weights, ascending): their count, the first
+ * min(count, cap) written (cap = 0: count only); -1 on a bad spec. */
+int64_t flr_resnet_gru_dead_ranges(const flr_resnet_gru_spec* spec, float weight_decay, int64_t* off,
+                                   int64_t* n, int64_t cap);
+/* X's dead-tap ranges (rows 0 .. K-1, training order) <- gtrain's, rows
+ * k < nneg negated: what flr_train_clients_ex writes last without
+ * FLR_TC_DEFER_DEAD. */
+int flr_resnet_gru_fill_dead(const flr_resnet_gru_spec* spec, float weight_decay, const float* gtrain,
+                             float* X, int64_t ld, int64_t K, int64_t nneg, void* stream);
 
 /* ---- a1 for the C4/C5 family: flr_train_vit_bert ---------------------------
  * The same client-plugin local update (run_experiments.py:193-240,

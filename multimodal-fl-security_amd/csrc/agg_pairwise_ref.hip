@@ -212,7 +212,8 @@ static_assert(TAP_CO * TAP_ROWS < (1 << 14), "dense write items exact in fp32");
 template <int KKT, bool VEC>  // KKT: 9, 1, or 0 = KK at run time; VEC: 16-B aligned tile rows
 __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict__ X, int64_t ldx, int64_t off,
                                                         int Cout, int Cin, int KKr, int64_t r0, int64_t steps,
-                                                        int64_t ldc, float* __restrict__ Xc) {
+                                                        int64_t ldc, float* __restrict__ Xc,
+                                                        const float* __restrict__ gdead, uint64_t dead, int nneg) {
   constexpr int TCO = TAP_CO, TROWS = TAP_ROWS;
   __shared__ float tile[TROWS][TCO + 1];
   const int KK = KKT > 0 ? KKT : KKr;
@@ -226,6 +227,13 @@ __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict_
   const int nci = min(CI, Cin - ci0), nco_v = min(TCO, Cout - co0);
   const int k = blockIdx.y;
   const float* row = X + (int64_t)k * ldx + off;
+  // dead taps (flr_pairwise_l2_reference_tap_dead): read from the global
+  // vector at the same offset, negated on the sign-flipped rows
+  const float* grow = gdead ? gdead + off : row;
+  const float gs = k < nneg ? -1.f : 1.f;
+  auto is_dead = [&](int t) { return t < 64 && ((dead >> t) & 1); };
+  auto src = [&](int t) { return is_dead(t) ? grow : row; };
+  auto sgn = [&](int t) { return is_dead(t) ? gs : 1.f; };  // (x * 1 == x, -x exact)
   const int nrows = KK * CI;
   // load: tile row r = t * CI + ci, column = output channel; every load of a
   // thread issued before its LDS stores
@@ -237,10 +245,13 @@ __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict_
 #pragma unroll
     for (int q = 0; q < IT; ++q) {
       const int r = rr + RPP * q, t = r / CI, ci = r - t * CI;
-      v[q] = (r < nrows && ci < nci)
-                 ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(
-                       row + ((int64_t)t * Cin + ci0 + ci) * Cout + co0 + 4 * sub))
-                 : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int64_t e = ((int64_t)t * Cin + ci0 + ci) * Cout + co0 + 4 * sub;
+      if (!(r < nrows && ci < nci))
+        v[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      else if (is_dead(t))  // the global vector, re-read by every client: cached loads
+        v[q] = *reinterpret_cast<const f32x4*>(grow + e) * gs;
+      else
+        v[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + e));
     }
 #pragma unroll
     for (int q = 0; q < IT; ++q) {
@@ -252,7 +263,7 @@ __global__ __launch_bounds__(256) void tap_chain_kernel(const float* __restrict_
   } else {
     for (int e = threadIdx.x; e < nrows * TCO; e += 256) {
       const int co = e % TCO, r = e / TCO, t = r / CI, ci = r % CI;
-      if (ci < nci && co < nco_v) tile[r][co] = row[((int64_t)t * Cin + ci0 + ci) * Cout + co0 + co];
+      if (ci < nci && co < nco_v) tile[r][co] = src(t)[((int64_t)t * Cin + ci0 + ci) * Cout + co0 + co] * sgn(t);
     }
   }
   __syncthreads();
@@ -405,6 +416,54 @@ __device__ __forceinline__ float chain_chunk(f32x4 xv, const f32x4 (&v)[NQ], flo
 #undef FLR_CHAIN_BLOCK
 #undef FLR_CHAIN16
 
+// Two chains per lane (K >= 256, off-diagonal tiles, ref_chain2_kernel): the
+// lane's pairs (i, j) and (i + 4, j) share the staged x_j; per step two
+// v_sub_f32_dpp (x_i and x_i2 broadcast by row_newbcast, as above) and two
+// v_fmac, the previous step's squares one slot behind its subtraction.
+#define FLR_STEP2(XA, XB, J, L, TA, TB, PA, PB) \
+  "v_sub_f32_dpp %[" #TA "], %[" #XA "], %[" #J "] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_sub_f32_dpp %[" #TB "], %[" #XB "], %[" #J "] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f32 %[acc], %[" #PA "], %[" #PA "]\n\t" \
+  "v_fmac_f32 %[acc2], %[" #PB "], %[" #PB "]\n\t"
+#define FLR_STEP2_FIRST(XA, XB, J, L, TA, TB) \
+  "v_sub_f32_dpp %[" #TA "], %[" #XA "], %[" #J "] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_sub_f32_dpp %[" #TB "], %[" #XB "], %[" #J "] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+#define FLR_CHAIN16_2(A, B, C, D, NOP) \
+  NOP \
+  FLR_STEP2_FIRST(x0, y0, j0, A, a0, b0) \
+  FLR_STEP2(x1, y1, j1, A, a1, b1, a0, b0) FLR_STEP2(x2, y2, j2, A, a0, b0, a1, b1) \
+  FLR_STEP2(x3, y3, j3, A, a1, b1, a0, b0) FLR_STEP2(x0, y0, j4, B, a0, b0, a1, b1) \
+  FLR_STEP2(x1, y1, j5, B, a1, b1, a0, b0) FLR_STEP2(x2, y2, j6, B, a0, b0, a1, b1) \
+  FLR_STEP2(x3, y3, j7, B, a1, b1, a0, b0) FLR_STEP2(x0, y0, j8, C, a0, b0, a1, b1) \
+  FLR_STEP2(x1, y1, j9, C, a1, b1, a0, b0) FLR_STEP2(x2, y2, j10, C, a0, b0, a1, b1) \
+  FLR_STEP2(x3, y3, j11, C, a1, b1, a0, b0) FLR_STEP2(x0, y0, j12, D, a0, b0, a1, b1) \
+  FLR_STEP2(x1, y1, j13, D, a1, b1, a0, b0) FLR_STEP2(x2, y2, j14, D, a0, b0, a1, b1) \
+  FLR_STEP2(x3, y3, j15, D, a1, b1, a0, b0) \
+  "v_fmac_f32 %[acc], %[a1], %[a1]\n\t" \
+  "v_fmac_f32 %[acc2], %[b1], %[b1]\n\t"
+#define FLR_CHAIN_BLOCK2(b, A, B, C, D, NOP)                                                                   \
+  asm volatile(FLR_CHAIN16_2(A, B, C, D, NOP)                                                                 \
+               : [acc] "+v"(acc), [acc2] "+v"(acc2), [a0] "=&v"(a0), [b0] "=&v"(b0), [a1] "=&v"(a1),          \
+                 [b1] "=&v"(b1)                                                                              \
+               : [x0] "v"(xv[0]), [x1] "v"(xv[1]), [x2] "v"(xv[2]), [x3] "v"(xv[3]), [y0] "v"(yv[0]),           \
+                 [y1] "v"(yv[1]), [y2] "v"(yv[2]), [y3] "v"(yv[3]), [j0] "v"(v[4 * (b) + 0][0]),              \
+                 [j1] "v"(v[4 * (b) + 0][1]), [j2] "v"(v[4 * (b) + 0][2]), [j3] "v"(v[4 * (b) + 0][3]),        \
+                 [j4] "v"(v[4 * (b) + 1][0]), [j5] "v"(v[4 * (b) + 1][1]), [j6] "v"(v[4 * (b) + 1][2]),        \
+                 [j7] "v"(v[4 * (b) + 1][3]), [j8] "v"(v[4 * (b) + 2][0]), [j9] "v"(v[4 * (b) + 2][1]),        \
+                 [j10] "v"(v[4 * (b) + 2][2]), [j11] "v"(v[4 * (b) + 2][3]), [j12] "v"(v[4 * (b) + 3][0]),     \
+                 [j13] "v"(v[4 * (b) + 3][1]), [j14] "v"(v[4 * (b) + 3][2]), [j15] "v"(v[4 * (b) + 3][3]))
+__device__ __forceinline__ void chain_chunk2(f32x4 xv, f32x4 yv, const f32x4 (&v)[NQ], float& acc, float& acc2) {
+  float a0, b0, a1, b1;
+  FLR_CHAIN_BLOCK2(0, 0, 1, 2, 3, "s_nop 1\n\t");
+  FLR_CHAIN_BLOCK2(1, 4, 5, 6, 7, "");
+  FLR_CHAIN_BLOCK2(2, 8, 9, 10, 11, "");
+  FLR_CHAIN_BLOCK2(3, 12, 13, 14, 15, "");
+}
+#undef FLR_CHAIN_BLOCK2
+#undef FLR_CHAIN16_2
+#undef FLR_STEP2_FIRST
+#undef FLR_STEP2
+
 template <class F, int... U>
 __device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, U...>) {
   (f(std::integral_constant<int, U>{}), ...);
@@ -427,11 +486,18 @@ __device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, U..
 // with explicit waits (the compiler's waitcnt pass, merging across the
 // rotated registers, drained vmcnt(0) every chunk).  No workgroup barrier:
 // the wave is the workgroup and reads only what it staged.
-template <bool DIAG>
+// NST: the ring's stages (the loop's unroll); TWO: two chains per lane, pairs
+// (i, j) and (i + 4, j) of an off-diagonal tile (ref_chain2_kernel).
+template <bool DIAG, int NST = NSTAGE, bool TWO = false>
 __device__ __forceinline__ void ref_chain_tile(float* lds, const Tile T, const int c, const float* __restrict__ Xc,
                                                int64_t ldc, int K, int64_t steps, int first,
                                                float* __restrict__ A) {
   using S = Staging<DIAG>;
+  static_assert(!(TWO && DIAG), "two chains per lane on off-diagonal tiles only");
+  static_assert(NST % 2 == 0 && NST >= 4, "two register buffers");
+  constexpr int NXI = TWO ? 2 : 1;               // x_i loads per body
+  constexpr int OPB = S::DPW + NXI;              // vector-memory ops per body
+  static_assert((NST - 2) * OPB + NXI < 64, "vmcnt counts to 63");
   const int lane = threadIdx.x & 63, r = lane >> 4, jl = lane & 15;
   // this lane's pair (i, j) and the staged row it reads
   int i, j, srow;
@@ -443,21 +509,28 @@ __device__ __forceinline__ void ref_chain_tile(float* lds, const Tile T, const i
     srow = r + jl;
     keep = o < SB / 2 || a < SB / 2;  // the antipodal pair once
   } else {
-    i = SB * T.X + IW * T.g + r;
+    i = SB * T.X + (TWO ? 2 * IW : IW) * T.g + r;  // TWO: I rows 8g + r and 8g + 4 + r
     j = SB * T.Y + JW * T.h + jl;
     srow = jl;
   }
+  const int i2 = i + IW;  // TWO: the lane's second pair (i2, j), i2 < j
+  const bool valid2 = TWO && i2 < K && j < K;
   const bool valid = keep && i < K && j < K;
   const int lo = i < j ? i : j, hi = i < j ? j : i;  // A holds the pair at [lo][hi]
   const int64_t rs = 8 * ldc;
 
   // the running sum of the previous segments: an asm load and a full wait
   // before any DMA, so no compiler-tracked load reaches into the loop
-  float acc = 0.f;
+  float acc = 0.f, acc2 = 0.f;
   if (!first) {
     const float* ap = A + ((int64_t)c * K + (lo < K ? lo : K - 1)) * K + (hi < K ? hi : K - 1);
     asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(acc) : "v"(ap) : "memory");
     acc = valid ? acc : 0.f;
+    if constexpr (TWO) {
+      const float* ap2 = A + ((int64_t)c * K + (i2 < K ? i2 : K - 1)) * K + (j < K ? j : K - 1);
+      asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(acc2) : "v"(ap2) : "memory");
+      acc2 = valid2 ? acc2 : 0.f;
+    }
   }
 
   // staging: DMA instruction u moves staged rows RPD u .. RPD u + 3, lane ->
@@ -479,13 +552,17 @@ __device__ __forceinline__ void ref_chain_tile(float* lds, const Tile T, const i
     voj[u] = (uint32_t)((int64_t)(gj - jrow0) * rs * 4 + 16 * ((lane % NQ) ^ slot_swz(s)) - 1024 * (u - 2) + 2048);
   }
   // x_i: lane jl of DPP row r loads steps 4 jl .. 4 jl + 3 of the row's I row
-  const int irow0 = min(SB * T.X + IW * T.g, K - 1);
+  const int irow0 = min(DIAG ? SB * T.X + IW * T.g : i - r, K - 1);
   const char* sbi = reinterpret_cast<const char*>(Xc + (int64_t)irow0 * rs + (int64_t)c * ldc);
   const uint32_t voi = (uint32_t)((int64_t)((i < K ? i : K - 1) - irow0) * rs * 4 + 16 * jl);
-  const int ngroup = (int)((steps + XC_GROUP - 1) / XC_GROUP);  // zero-filled past `steps`
+  const uint32_t voi2 = (uint32_t)((int64_t)((i2 < K ? i2 : K - 1) - irow0) * rs * 4 + 16 * jl);
+  // whole loop trips of NST chunks inside the zero-filled streams (padded to
+  // XC_GROUP steps, a multiple of NST * CS)
+  static_assert(XC_GROUP % (NST * CS) == 0, "trips inside the zero fill");
+  const int ngroup = (int)((steps + NST * CS - 1) / (NST * CS));
   // DMA(ch) into stage `slot`, then x_i(ch) into register set x (inline asm:
   // hipcc built 64-bit addresses per DMA instead of the saddr form)
-  auto issue = [&](int ch, int slot, f32x4& x) {
+  auto issue = [&](int ch, int slot, f32x4& x, f32x4& x2) {
     // the chunk's byte offset in a stream: the prefetch runs up to NSTAGE - 1
     // chunks past the last one (reads nothing consumes; the workspace carries
     // XC_SLACK bytes past the last stream)
@@ -513,6 +590,7 @@ __device__ __forceinline__ void ref_chain_tile(float* lds, const Tile T, const i
 #undef FLR_DMA
     static_assert(S::DPW == 4 || S::DPW == 5, "the DMA statements above");
     asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x) : "v"(voi), "s"(sbi + co) : "memory");
+    if constexpr (TWO) asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x2) : "v"(voi2), "s"(sbi + co) : "memory");
   };
   // per-lane LDS byte addresses of staged row srow's 16 swizzled pieces in stage 0
   const int rsw = slot_swz(srow);
@@ -528,27 +606,31 @@ __device__ __forceinline__ void ref_chain_tile(float* lds, const Tile T, const i
   };
 
   f32x4 va[NQ], vb[NQ];
-  f32x4 xs[NSTAGE];
+  f32x4 xs[NST], xs2[NST];
   auto body = [&](auto U, int ch, f32x4(&vc)[NQ], f32x4(&vn)[NQ]) {
     constexpr int u = decltype(U)::value;
     // DMA(ch + 1) was issued in body ch + 2 - NSTAGE; younger than it: its
     // x_i load and the NSTAGE - 3 bodies since (x_i(ch) is older: covered)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 3) * S::OPB + 1) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 3) * OPB + NXI) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // chunk ch's x_j
     // chunk ch's operands arrived at the waits above: tie them to here
     asm volatile("" : "+v"(vc[0]), "+v"(vc[1]), "+v"(vc[2]), "+v"(vc[3]), "+v"(vc[4]), "+v"(vc[5]), "+v"(vc[6]),
                  "+v"(vc[7]), "+v"(vc[8]), "+v"(vc[9]), "+v"(vc[10]), "+v"(vc[11]), "+v"(vc[12]), "+v"(vc[13]),
                  "+v"(vc[14]), "+v"(vc[15]), "+v"(xs[u]));
-    issue(ch + NSTAGE - 1, (u + NSTAGE - 1) % NSTAGE, xs[(u + NSTAGE - 1) % NSTAGE]);
-    rows(std::integral_constant<int, (u + 1) % NSTAGE>{}, vn, ra);
-    if (FLR_REF_ABL != 5) acc = chain_chunk(xs[u], vc, acc);
+    if constexpr (TWO) asm volatile("" : "+v"(xs2[u]));
+    issue(ch + NST - 1, (u + NST - 1) % NST, xs[(u + NST - 1) % NST], xs2[(u + NST - 1) % NST]);
+    rows(std::integral_constant<int, (u + 1) % NST>{}, vn, ra);
+    if constexpr (TWO)
+      chain_chunk2(xs[u], xs2[u], vc, acc, acc2);
+    else if (FLR_REF_ABL != 5)
+      acc = chain_chunk(xs[u], vc, acc);
   };
   // prologue = the issues of bodies -(NSTAGE-1) .. -1, then chunk 0's rows
 #pragma unroll
-  for (int u = 0; u < NSTAGE - 1; ++u) issue(u, u, xs[u]);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * S::OPB + 1) : "memory");  // DMA(0)
+  for (int u = 0; u < NST - 1; ++u) issue(u, u, xs[u], xs2[u]);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * OPB + NXI) : "memory");  // DMA(0)
   rows(std::integral_constant<int, 0>{}, va, ra);
-  for (int ch = 0; ch < ngroup * NSTAGE; ch += NSTAGE)
+  for (int ch = 0; ch < ngroup * NST; ch += NST)
     static_for(
         [&](auto U) {
           constexpr int u = decltype(U)::value;
@@ -557,9 +639,10 @@ __device__ __forceinline__ void ref_chain_tile(float* lds, const Tile T, const i
           else
             body(U, ch + u, vb, va);
         },
-        std::make_integer_sequence<int, NSTAGE>{});
+        std::make_integer_sequence<int, NST>{});
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (valid) A[((int64_t)c * K + lo) * K + hi] = acc;
+  if (valid2) A[((int64_t)c * K + i2) * K + j] = acc2;
 }
 
 // grid 8 x (t1 - t0) one-wave workgroups: chain c = blockIdx % 8 (the XCD),
@@ -575,6 +658,53 @@ __global__ __launch_bounds__(64) void ref_chain_kernel(const float* __restrict__
     ref_chain_tile<true>(lds, T, c, Xc, ldc, K, steps, first, A);
   else
     ref_chain_tile<false>(lds, T, c, Xc, ldc, K, steps, first, A);
+}
+
+// K >= 256 (more tiles than SIMDs: the chains are throughput-bound, not
+// latency-bound): off-diagonal super-block pairs as 8 waves of 8 I rows x 16 J
+// rows, two chains per lane sharing the staged x_j (half the LDS reads per chain
+// step), diagonal super-blocks as the 1-I circulant tiles above; a 4-stage ring
+// (20 KB) and at most 256 VGPRs, so two waves per SIMD.  Tiles per Y: the
+// off-diagonal pairs X = 0 .. Y-1 (8 waves each: w = 2g + h), then the diagonal.
+constexpr int NST2 = 4;
+__host__ __device__ inline int tiles2_before(int Y) { return 4 * Y * (Y + 1); }
+__host__ __device__ inline int ntiles2_of(int K) { return tiles2_before((K + SB - 1) / SB); }
+__host__ __device__ inline Tile tile2_of(int t) {
+  int Y = 0;
+  while (tiles2_before(Y + 1) <= t) ++Y;
+  const int local = t - tiles2_before(Y);
+  Tile r;
+  r.Y = Y;
+  if (local < 8 * Y) {
+    r.X = local / 8;
+    r.g = (local % 8) >> 1;
+    r.h = local & 1;
+    r.diag = false;
+  } else {
+    r.X = Y;
+    r.g = local - 8 * Y;
+    r.h = 0;
+    r.diag = true;
+  }
+  return r;
+}
+__global__ __launch_bounds__(64, 2) void ref_chain2_kernel(const float* __restrict__ Xc, int64_t ldc, int K,
+                                                           int64_t steps, int first, float* __restrict__ A) {
+  __shared__ __attribute__((aligned(16))) float lds[NST2 * STAGE];
+  const int c = (int)(blockIdx.x & 7);
+  const Tile T = tile2_of((int)(blockIdx.x >> 3));
+  if (T.diag)
+    ref_chain_tile<true, NST2, false>(lds, T, c, Xc, ldc, K, steps, first, A);
+  else
+    ref_chain_tile<false, NST2, true>(lds, T, c, Xc, ldc, K, steps, first, A);
+}
+
+// the two-chain form, opt-in (FLR_REF_2I=1, from two super-blocks, K > 32):
+// measured -6 % at K=512 P=2M but +10 % at K=256 P=4M and +6 % on the C5
+// distances (profiles/r6_ref/two_chain_ab.json), so off by default
+inline bool use_two_chains(int64_t K) {
+  const char* e = flr::knob("FLR_REF_2I");
+  return e && e[0] == '1' && K > SB;
 }
 
 // D[i][j] = D[j][i] for the pairs of tiles [t0, t1): chains summed 0..7 in
@@ -691,7 +821,8 @@ static WaveRuns wave_runs(const int64_t* taps, int64_t ntaps, int64_t r0, int64_
 // per segment the chain-major transpose (skipping the tap-major blocks), the
 // tap blocks' rewrite, the chain kernel.
 static int run_chains(const float* X, int64_t K, int64_t steps_total, int64_t ldx, const int64_t* taps, int64_t ntaps,
-                      int first, float* A, void* ws, size_t ws_bytes, int t0, int t1, hipStream_t st) {
+                      const uint64_t* dead, const float* gdead, int64_t nneg, int first, float* A, void* ws,
+                      size_t ws_bytes, int t0, int t1, hipStream_t st) {
   const size_t na = a_bytes(K);
   if (ws_bytes < na) return FLR_ERR_WORKSPACE;
   const int64_t R = steps_total;
@@ -720,17 +851,24 @@ static int run_chains(const float* X, int64_t K, int64_t steps_total, int64_t ld
       auto kern = kk == 9 ? (vec ? tap_chain_kernel<9, true> : tap_chain_kernel<9, false>)
                 : kk == 1 ? (vec ? tap_chain_kernel<1, true> : tap_chain_kernel<1, false>)
                           : (vec ? tap_chain_kernel<0, true> : tap_chain_kernel<0, false>);
+      const uint64_t dm = dead ? dead[b] : 0;
       hipLaunchKernelGGL(kern, dim3((unsigned)tiles, (unsigned)K), dim3(256), 0, st, X, ldx, off, (int)co, (int)ci,
-                         (int)kk, r0, steps, ldc, Xc);
+                         (int)kk, r0, steps, ldc, Xc, dm ? gdead : nullptr, dm, (int)std::min<int64_t>(nneg, K));
       if ((rc = launch_status("tap_chain_kernel")) != FLR_OK) return rc;
     }
     const int64_t padded = (steps + XC_GROUP - 1) / XC_GROUP * XC_GROUP;  // <= Rs <= ldc
     if (padded > steps &&
         hipMemset2DAsync(Xc + steps, (size_t)ldc * 4, 0, (size_t)(padded - steps) * 4, (size_t)(K * 8), st) != hipSuccess)
       return FLR_ERR_HIP;
-    hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(64), 0, st, Xc, ldc, (int)K, steps, t0,
-                       (first && seg == 0) ? 1 : 0, A);
-    rc = launch_status("ref_chain_kernel");
+    if (t0 == 0 && t1 == ntiles_of((int)K) && use_two_chains(K)) {  // every pair: the two-chain tiles
+      hipLaunchKernelGGL(ref_chain2_kernel, dim3(8 * ntiles2_of((int)K)), dim3(64), 0, st, Xc, ldc, (int)K, steps,
+                         (first && seg == 0) ? 1 : 0, A);
+      rc = launch_status("ref_chain2_kernel");
+    } else {
+      hipLaunchKernelGGL(ref_chain_kernel, dim3(8 * (t1 - t0)), dim3(64), 0, st, Xc, ldc, (int)K, steps, t0,
+                         (first && seg == 0) ? 1 : 0, A);
+      rc = launch_status("ref_chain_kernel");
+    }
     if (rc != FLR_OK) return rc;
   }
   return FLR_OK;
@@ -742,13 +880,20 @@ static int check_rows(const float* X, int64_t K, int64_t n, int64_t ldx) {
   return FLR_OK;
 }
 
-extern "C" int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t P, int64_t ldx,
-                                             const int64_t* taps, int64_t ntaps, double* D, void* ws, size_t ws_bytes,
-                                             int64_t part, int64_t nparts, void* stream) {
+extern "C" int flr_pairwise_l2_reference_tap_dead(const float* X, int64_t K, int64_t P, int64_t ldx,
+                                                  const int64_t* taps, int64_t ntaps, const uint64_t* dead,
+                                                  const float* gdead, int64_t nneg, double* D, void* ws,
+                                                  size_t ws_bytes, int64_t part, int64_t nparts, void* stream) {
   if (K < 1 || P < 0 || ldx < P || !D || (K > 1 && P > 0 && !X) || nparts < 1 || part < 0 || part >= nparts)
     return FLR_ERR_ARG;
   if (K > (1 << 15)) return FLR_ERR_UNSUPPORTED;
-  if (ntaps < 0 || (ntaps > 0 && !taps)) return FLR_ERR_ARG;
+  if (ntaps < 0 || (ntaps > 0 && !taps) || nneg < 0) return FLR_ERR_ARG;
+  bool any_dead = false;
+  for (int64_t b = 0; dead && b < ntaps; ++b) {  // bit t names tap t < min(KK, 64)
+    if (taps[4 * b + 3] < 64 && (dead[b] >> taps[4 * b + 3]) != 0) return FLR_ERR_ARG;
+    any_dead |= dead[b] != 0;
+  }
+  if (any_dead && !gdead) return FLR_ERR_ARG;
   // tap-major blocks: {off, Cout, Cin, KK}, inside [0, P), ascending, disjoint
   for (int64_t b = 0, end = 0; b < ntaps; ++b) {
     const int64_t off = taps[4 * b], co = taps[4 * b + 1], ci = taps[4 * b + 2], kk = taps[4 * b + 3];
@@ -766,7 +911,8 @@ extern "C" int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t 
   const int t0 = (int)(part * ntiles / nparts), t1 = (int)((part + 1) * ntiles / nparts);
   float* A = reinterpret_cast<float*>(ws);
   if (K > 1 && R > 0 && t1 > t0 &&
-      (rc = run_chains(X, K, R, ldx, taps, ntaps, 1, A, ws, ws_bytes, t0, t1, st)) != FLR_OK)
+      (rc = run_chains(X, K, R, ldx, taps, ntaps, any_dead ? dead : nullptr, gdead, nneg, 1, A, ws, ws_bytes, t0, t1,
+                       st)) != FLR_OK)
     return rc;
   // the tail coordinates' columns (identity outside the tap-major blocks)
   TailCols tc;
@@ -780,10 +926,25 @@ extern "C" int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t 
     }
     tc.c[u - 8 * R] = c;
   }
+  // the finish kernel reads the tail columns from X: none of them may be a dead tap
+  for (int64_t u = 8 * R; any_dead && u < P; ++u)
+    for (int64_t b = 0; b < ntaps; ++b) {
+      const int64_t off = taps[4 * b], co = taps[4 * b + 1], ci = taps[4 * b + 2], kk = taps[4 * b + 3];
+      if (u < off || u >= off + co * ci * kk) continue;
+      const int64_t t = (u - off) % kk;
+      if (t < 64 && ((dead[b] >> t) & 1)) return FLR_ERR_ARG;
+    }
   const int64_t kk = K * K;
   hipLaunchKernelGGL(ref_finish_kernel, dim3((unsigned)((kk + 255) / 256)), dim3(256), 0, st, A, R > 0 ? 1 : 0, X, tc,
                      (int)K, P, ldx, R, t0, t1, D);
   return launch_status("ref_finish_kernel");
+}
+
+extern "C" int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t P, int64_t ldx,
+                                             const int64_t* taps, int64_t ntaps, double* D, void* ws, size_t ws_bytes,
+                                             int64_t part, int64_t nparts, void* stream) {
+  return flr_pairwise_l2_reference_tap_dead(X, K, P, ldx, taps, ntaps, nullptr, nullptr, 0, D, ws, ws_bytes, part,
+                                            nparts, stream);
 }
 
 extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx, double* D, void* ws,
@@ -791,9 +952,18 @@ extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, i
   return flr_pairwise_l2_reference_tap(X, K, P, ldx, nullptr, 0, D, ws, ws_bytes, part, nparts, stream);
 }
 
-extern "C" int flr_pairwise_l2_reference_partial(const float* X, int64_t K, int64_t steps, int64_t ldx, int first,
-                                                 void* ws, size_t ws_bytes, void* stream) {
+extern "C" int flr_pairwise_l2_reference_partial_tap(const float* X, int64_t K, int64_t steps, int64_t ldx,
+                                                     const int64_t* taps, int64_t ntaps, int first, void* ws,
+                                                     size_t ws_bytes, void* stream) {
   if (K < 1 || steps < 0 || ldx < 8 * steps || (K > 1 && steps > 0 && !X)) return FLR_ERR_ARG;
+  if (ntaps < 0 || (ntaps > 0 && !taps)) return FLR_ERR_ARG;
+  for (int64_t b = 0, end = 0; b < ntaps; ++b) {  // ascending, disjoint, wholly inside the slice's chain steps
+    const int64_t off = taps[4 * b], co = taps[4 * b + 1], ci = taps[4 * b + 2], kk = taps[4 * b + 3];
+    if (off < end || co < 1 || ci < 1 || kk < 1 || kk > TAP_ROWS || co > INT32_MAX || ci > INT32_MAX ||
+        off + co * ci * kk > 8 * steps)
+      return FLR_ERR_ARG;
+    end = off + co * ci * kk;
+  }
   if (K > (1 << 15)) return FLR_ERR_UNSUPPORTED;
   int rc = check_rows(X, K, 8 * steps, ldx);
   if (rc != FLR_OK) return rc;
@@ -806,7 +976,13 @@ extern "C" int flr_pairwise_l2_reference_partial(const float* X, int64_t K, int6
       return launch_status("reference distances: zero the chains");
     return FLR_OK;
   }
-  return run_chains(X, K, steps, ldx, nullptr, 0, first, A, ws, ws_bytes, 0, ntiles_of((int)K), st);
+  return run_chains(X, K, steps, ldx, taps, ntaps, nullptr, nullptr, 0, first, A, ws, ws_bytes, 0, ntiles_of((int)K),
+                    st);
+}
+
+extern "C" int flr_pairwise_l2_reference_partial(const float* X, int64_t K, int64_t steps, int64_t ldx, int first,
+                                                 void* ws, size_t ws_bytes, void* stream) {
+  return flr_pairwise_l2_reference_partial_tap(X, K, steps, ldx, nullptr, 0, first, ws, ws_bytes, stream);
 }
 
 extern "C" int flr_pairwise_l2_reference_finish(const float* Xtail, int64_t K, int64_t ntail, int64_t ldx,

@@ -455,6 +455,21 @@ class Net {
     return flush();
   }
 
+  // the dead-tap ranges of a training-order row, ascending (dead_ranges' table)
+  void dead_list(std::vector<std::pair<int64_t, int64_t>>& out) const {
+    for (size_t j = 0; j < ps_.size(); ++j) {
+      const Param& p = ps_[j];
+      if (!p.dead) continue;
+      int64_t e = 0;
+      for (const auto& b : blocks_opt_) {
+        if (b.j != (int)j) continue;
+        if (b.o > e) out.push_back({p.off + e, b.o - e});
+        e = b.o + b.n;
+      }
+      if (p.n > e) out.push_back({p.off + e, p.n - e});
+    }
+  }
+
   // X's dead-tap ranges (training order) <- gtrain, rows k < nneg negated: one
   // launch over the range table when it fits and the rows are 16-B aligned
   // (was one broadcast per range: 57 launches per C3 round), else per range.
@@ -1078,7 +1093,8 @@ extern "C" int flr_train_clients_ex(const flr_resnet_gru_spec* spec, const float
                                     void* stream) {
   if (!spec || !global || !X || !images || !tokens || !labels || !loss_out || steps < 1 || K < 1 || B < 1 || nneg < 0)
     return FLR_ERR_ARG;
-  if (flags & ~(unsigned)FLR_TC_TRAIN_ORDER) return FLR_ERR_ARG;
+  if (flags & ~(unsigned)(FLR_TC_TRAIN_ORDER | FLR_TC_DEFER_DEAD)) return FLR_ERR_ARG;
+  if ((flags & FLR_TC_DEFER_DEAD) && !(flags & FLR_TC_TRAIN_ORDER)) return FLR_ERR_ARG;
   if (!workspace || workspace_bytes < flr_train_clients_workspace(spec, K, B, steps)) return FLR_ERR_WORKSPACE;
   char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
   tc::Net net(*spec, K, B, weight_decay, max_norm, base);
@@ -1118,9 +1134,37 @@ extern "C" int flr_train_clients_ex(const flr_resnet_gru_spec* spec, const float
                   step_loss + s * K, lr, momentum, st);
     if (rc != FLR_OK) return rc;
   }
-  rc = train_order ? net.dead_ranges(global, X, ld, nneg, st) : net.export_rows(X, ld, nneg, st);
+  if (!train_order) {
+    rc = net.export_rows(X, ld, nneg, st);
+  } else if (!(flags & FLR_TC_DEFER_DEAD)) {
+    rc = net.dead_ranges(global, X, ld, nneg, st);
+  }
   if (rc != FLR_OK) return rc;
   return flr_mean_rows(step_loss, steps, K, loss_out, st);
+}
+
+extern "C" int64_t flr_resnet_gru_dead_ranges(const flr_resnet_gru_spec* spec, float weight_decay, int64_t* off,
+                                              int64_t* n, int64_t cap) {
+  if (!spec || cap < 0 || (cap > 0 && (!off || !n))) return -1;
+  tc::Net net(*spec, 1, 1, weight_decay, 0.f, nullptr);
+  if (net.layout() != FLR_OK) return -1;
+  std::vector<std::pair<int64_t, int64_t>> r;
+  net.dead_list(r);
+  for (int64_t i = 0; i < cap && i < (int64_t)r.size(); ++i) {
+    off[i] = r[i].first;
+    n[i] = r[i].second;
+  }
+  return (int64_t)r.size();
+}
+
+extern "C" int flr_resnet_gru_fill_dead(const flr_resnet_gru_spec* spec, float weight_decay, const float* gtrain,
+                                        float* X, int64_t ld, int64_t K, int64_t nneg, void* stream) {
+  if (!spec || !gtrain || !X || K < 1 || nneg < 0) return FLR_ERR_ARG;
+  tc::Net net(*spec, K, 1, weight_decay, 0.f, nullptr);
+  const int rc = net.layout();
+  if (rc != FLR_OK) return rc;
+  if (ld < net.P()) return FLR_ERR_ARG;
+  return net.dead_ranges(gtrain, X, ld, nneg, as_stream(stream));
 }
 
 extern "C" int flr_resnet_gru_reorder(const flr_resnet_gru_spec* spec, const float* src, float* dst, int to_train,

@@ -54,7 +54,11 @@ SIGNATURES = {
                                          _c_void_p]),
     "flr_pairwise_l2_reference_tap": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p, _c_void_p,
                                              _size_t, _i64, _i64, _c_void_p]),
+    "flr_pairwise_l2_reference_tap_dead": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                                  _i64, _c_void_p, _c_void_p, _size_t, _i64, _i64, _c_void_p]),
     "flr_pairwise_l2_reference_partial": (_int, [_c_void_p, _i64, _i64, _i64, _int, _c_void_p, _size_t, _c_void_p]),
+    "flr_pairwise_l2_reference_partial_tap": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _int, _c_void_p,
+                                                     _size_t, _c_void_p]),
     "flr_pairwise_l2_reference_finish": (_int, [_c_void_p, _i64, _i64, _i64, _int, _c_void_p, _c_void_p, _c_void_p]),
     "flr_pairwise_l2_direct_workspace": (_size_t, [_i64, _i64]),
     "flr_pairwise_l2_direct": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
@@ -98,6 +102,8 @@ SIGNATURES = {
                                     _c_void_p]),
     "flr_resnet_gru_reorder": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p]),
     "flr_resnet_gru_live_params": (_i64, [_c_void_p, ctypes.c_float]),
+    "flr_resnet_gru_dead_ranges": (_i64, [_c_void_p, ctypes.c_float, _c_void_p, _c_void_p, _i64]),
+    "flr_resnet_gru_fill_dead": (_int, [_c_void_p, ctypes.c_float, _c_void_p, _c_void_p, _i64, _i64, _i64, _c_void_p]),
     "flr_vit_bert_num_params": (_i64, [_c_void_p]),
     "flr_train_vit_bert_workspace": (_size_t, [_c_void_p, _i64, _i64, _i64, _i64]),
     "flr_train_vit_bert": (_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p,

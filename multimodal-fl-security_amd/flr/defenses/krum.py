@@ -113,9 +113,8 @@ class KrumDefense(BaseDefense):
         if self.pairwise_method == "reference":
             if cs.comm.world == 1:  # the one slice is the whole matrix
                 return ops.pairwise_l2(cs.X, "reference", tap_blocks=self.tap_blocks)
-            if self.tap_blocks:
-                raise ValueError("reference-exact distances over coordinate slices need torch-order slices")
-            return ops.pairwise_l2_reference_sharded(cs)
+            # training order: the rank boundaries are tap-block aligned (shard.aligned_bounds)
+            return ops.pairwise_l2_reference_sharded(cs, self.tap_blocks)
         if self.pairwise_method != "gram":
             raise ValueError(f"pairwise_method {self.pairwise_method!r} has no coordinate-sharded form")
         return ops.pairwise_l2_sharded(cs, events=events)

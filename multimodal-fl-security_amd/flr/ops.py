@@ -252,7 +252,7 @@ def _ws(nbytes: int, device) -> Tuple[torch.Tensor, int]:
     return ws, ws.data_ptr() + (-ws.data_ptr()) % 256
 
 
-def pairwise_l2_reference_sharded(cs) -> torch.Tensor:
+def pairwise_l2_reference_sharded(cs, tap_blocks=None) -> torch.Tensor:
     """The reference-exact distances (pairwise_l2 "reference") from coordinate
     slices (flr.shard.CoordSlice, the reference's coordinate order): the
     chains run through the ranks in order — rank r continues every pair's 8
@@ -262,7 +262,11 @@ def pairwise_l2_reference_sharded(cs) -> torch.Tensor:
     operation in the same order as on one GPU, so D is bit-identical to
     pairwise_l2(X, "reference") at every world size.  A chain cannot be split,
     so the ranks run one after another: the phase costs about the one-GPU
-    chain time at any G, with only this rank's 1/G of the rows transposed."""
+    chain time at any G, with only this rank's 1/G of the rows transposed.
+    tap_blocks (a training-order round): the matrix's tap-major blocks
+    [(off, Cout, Cin, KK), ...]; the rank boundaries must not cut one
+    (shard.aligned_bounds), and the blocks inside this slice are read in
+    place (flr_pairwise_l2_reference_partial_tap)."""
     lib = _capi.lib()
     K, P, dev = cs.K, cs.P, cs.data.device
     X, ld = cs.data, cs.data.stride(0)
@@ -274,6 +278,16 @@ def pairwise_l2_reference_sharded(cs) -> torch.Tensor:
         raise ValueError("coordinate slices must start at a multiple of 8 coordinates")
     if X.data_ptr() % 16 or ld % 4:
         raise ValueError("coordinate slice rows must be 16-B aligned")
+    taps = []
+    for o, co, ci, kk in (tap_blocks or ()):
+        e = o + co * ci * kk
+        if e <= cs.begin or o >= cs.end:
+            continue
+        if o < cs.begin or e > cs.begin + 8 * steps:
+            raise ValueError(f"tap block [{o}, {e}) crosses this rank's chain range [{cs.begin}, "
+                             f"{cs.begin + 8 * steps}): the rank boundaries must be tap-block aligned")
+        taps += [o - cs.begin, co, ci, kk]
+    tarr = (ctypes.c_int64 * max(1, len(taps)))(*taps)
     nbytes = int(lib.flr_pairwise_l2_reference_workspace(K, 8 * steps))
     ws, wp = _ws(nbytes, dev)
     st = _stream(X)
@@ -282,7 +296,8 @@ def pairwise_l2_reference_sharded(cs) -> torch.Tensor:
         A = torch.as_strided(ws, (8 * K * K * 4,), (1,), (wp - ws.data_ptr())).view(torch.float32)
         if rank > 0:
             comm.recv(A, rank - 1)
-        _capi.call("flr_pairwise_l2_reference_partial", X.data_ptr(), K, steps, ld, int(rank == 0), wp, nbytes, st)
+        _capi.call("flr_pairwise_l2_reference_partial_tap", X.data_ptr(), K, steps, ld, ctypes.addressof(tarr),
+                   len(taps) // 4, int(rank == 0), wp, nbytes, st)
         if rank < world - 1:
             comm.send(A, rank + 1)
     D = torch.empty((K, K), dtype=torch.float64, device=dev)
@@ -299,6 +314,9 @@ def pairwise_l2_sharded(cs, events=None) -> torch.Tensor:
     every rank ends with the same D, bit-identical to pairwise_l2 on the
     whole matrix.  Collectives: one exact sum of the pivot sample, one exact
     sum of the tail term, one all-gather of the per-slice Gram sums."""
+    if cs.plan.bounds is not None:
+        raise ValueError("the Gram path's per-slice records need the canonical rank boundaries "
+                         "(this slice's are tap-block aligned: a training-order reference-exact round)")
     lib = _capi.lib()
     K, P, dev = cs.K, cs.P, cs.data.device
     X, ld = cs.data, cs.data.stride(0)

@@ -31,7 +31,7 @@ from . import ops
 from .attacks import Backdoor, poison_batches_
 from .defenses import get_defense
 from .matrix import ClientMatrix
-from .shard import PW_SLICES, Comm, CoordExchange
+from .shard import PW_SLICES, Comm, CoordExchange, aligned_bounds
 from .models.multimodal import ModelSpec, model_class, param_layout
 from .train import ClientBatchTrainer, TrainConfig, make_dropout_masks, synthetic_batches
 
@@ -100,14 +100,6 @@ class RoundEngine:
         self.full = None
         self.xchg = None
         self.slice = None
-        if mode == "alltoall":
-            self.xchg = CoordExchange(K, self.hi - self.lo, self.trainer.P, self.device, Comm())
-        else:
-            self.full = self.trainer.X if world == 1 else ClientMatrix.empty(K, shapes, self.device)
-            if world > 1 and hasattr(self.defense, "comm"):
-                # whole rows on every rank: the reference-exact Krum distances
-                # split their pair tiles over the ranks (one 8·K² all-reduce)
-                self.defense.comm = Comm()
         self.global_flat = initial_global(spec, rcfg.seed, self.device)
         steps = tcfg.local_steps
         self.batches = synthetic_batches(spec, steps, range(self.lo, self.hi), rcfg.batch, self.device)
@@ -127,16 +119,27 @@ class RoundEngine:
         # gtrain is the global model in that order (FLR_ORDER=torch: off)
         self.train_order = (getattr(self.defense, "order_free", False) and not self._wants_global
                             and os.environ.get("FLR_ORDER", "train") != "torch")
-        if (self.train_order and getattr(self.defense, "needs_tap_blocks", False) and self.exchange == "alltoall"
-                and world > 1):
-            # coordinate slices of the reference-exact chains: torch-order slices
-            self.train_order = False
+        bounds = None
         if self.train_order and getattr(self.defense, "needs_tap_blocks", False):
             # the reference-exact distances read the training-order matrix,
             # told which blocks are tap-major (no torch-order copy)
             ok, taps = self._tap_blocks()
+            if ok and self.exchange == "alltoall" and world > 1:
+                # the chains run through the ranks' coordinate ranges in torch
+                # order: rank boundaries moved off the tap-major blocks, so each
+                # range holds whole blocks (the same set in either order)
+                bounds = aligned_bounds(self.trainer.P, world, taps)
+                ok = bounds is not None
             self.train_order = ok
             self.defense.tap_blocks = taps if ok else None
+        if mode == "alltoall":
+            self.xchg = CoordExchange(K, self.hi - self.lo, self.trainer.P, self.device, Comm(), bounds=bounds)
+        else:
+            self.full = self.trainer.X if world == 1 else ClientMatrix.empty(K, shapes, self.device)
+            if world > 1 and hasattr(self.defense, "comm"):
+                # whole rows on every rank: the reference-exact Krum distances
+                # split their pair tiles over the ranks (one 8·K² all-reduce)
+                self.defense.comm = Comm()
         self.gtrain = self.trainer.to_train_order(self.global_flat) if self.train_order else None
         self.round_index = 0
         self.fell_back = False

@@ -43,9 +43,15 @@ def slice_chunks(P: int, q: int) -> Tuple[int, int]:
 
 @dataclass(frozen=True)
 class CoordPlan:
-    """Who owns which coordinates when the K×P matrix is split by columns."""
+    """Who owns which coordinates when the K×P matrix is split by columns.
+    bounds (world + 1 ascending offsets, 0 .. P): explicit rank boundaries
+    instead of the canonical slices' — a training-order round of the
+    reference-exact Krum distances aligns them to the tap-major blocks
+    (aligned_bounds); the Gram path's per-slice records need the canonical
+    ones."""
     P: int
     world: int
+    bounds: Optional[Tuple[int, ...]] = None
 
     def __post_init__(self):
         if PW_SLICES % self.world != 0:
@@ -61,6 +67,8 @@ class CoordPlan:
 
     def coords(self, rank: int) -> Tuple[int, int]:
         """[begin, end) of the coordinates rank owns (tail goes to the last rank)."""
+        if self.bounds is not None:
+            return self.bounds[rank], self.bounds[rank + 1]
         c0, c1 = self.chunks(rank)
         end = self.P if rank == self.world - 1 else c1 * CHUNK
         return c0 * CHUNK, end
@@ -70,6 +78,42 @@ class CoordPlan:
         """Row stride of every exchanged block: the longest range, 64-aligned."""
         n = max(e - b for b, e in (self.coords(r) for r in range(self.world)))
         return max(CHUNK, (n + CHUNK - 1) // CHUNK * CHUNK)
+
+
+def aligned_bounds(P: int, world: int, blocks) -> Optional[Tuple[int, ...]]:
+    """Rank boundaries for a training-order round whose reference-exact chains
+    run through the ranks (ops.pairwise_l2_reference_sharded): every rank's
+    range must hold whole tap-major blocks (then it is the same SET of
+    coordinates in training and in torch order) and start at a chain step.
+    Each canonical boundary moves to the nearest 64-coordinate chunk edge
+    outside every block, kept strictly increasing where the gaps allow (a
+    block longer than a canonical slice can leave a rank an empty range).
+    None when a block reaches the last P mod 8 coordinates (the chains' tail)."""
+    plan = CoordPlan(P, world)
+    spans = sorted((o, o + co * ci * kk) for o, co, ci, kk in blocks)
+    if any(e > P - P % 8 for _, e in spans):
+        return None
+    # the gaps a boundary may sit in: [lo, hi], both chunk edges
+    gaps, prev = [], 0
+    for o, e in spans + [(P, P)]:
+        lo, hi = -(-prev // CHUNK) * CHUNK, (o // CHUNK) * CHUNK
+        if o == P:  # the last rank starts at a chunk edge before the tail
+            hi = (P // CHUNK) * CHUNK
+        if lo <= hi:
+            gaps.append((lo, hi))
+        prev = max(prev, e)
+    out = [0]
+    for r in range(1, world):
+        t = plan.coords(r)[0]
+        cands = []
+        for lo, hi in gaps:
+            c = min(max(t, lo), hi)
+            cands.append((abs(c - t), c))
+        cands.sort()
+        pick = next((c for _, c in cands if c > out[-1]), None)
+        out.append(pick if pick is not None else out[-1])
+    out.append(P)
+    return tuple(out)
 
 
 class Comm:
@@ -222,9 +266,10 @@ class CoordExchange:
     and a write of the whole local matrix per round).  Only this rank's own
     block is copied, local -> recv."""
 
-    def __init__(self, K: int, K_local: int, P: int, device, comm: Optional[Comm] = None):
+    def __init__(self, K: int, K_local: int, P: int, device, comm: Optional[Comm] = None,
+                 bounds: Optional[Tuple[int, ...]] = None):
         self.comm = comm or Comm()
-        self.plan = CoordPlan(P, self.comm.world)
+        self.plan = CoordPlan(P, self.comm.world, bounds)
         self.K, self.K_local = K, K_local
         ld = self.plan.ld
         world = self.comm.world

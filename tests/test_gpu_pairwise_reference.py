@@ -62,6 +62,20 @@ def test_reference_mode_large_vs_c_oracle(cuda, K, P):
     assert np.array_equal(D, normref.distance_matrix(X.numpy()))
 
 
+@pytest.mark.parametrize("K,P,two", [(33, 4099, "1"), (64, 65_537, "1"), (100, 20_011, "1"), (127, 3001, "1"),
+                                     (300, 20_011, "0"), (257, 1000, "1")])
+def test_reference_mode_two_chain_tiles(cuda, knob, K, P, two):
+    """The K >= 256 form (ref_chain2_kernel: two chains per lane on the
+    off-diagonal tiles, the 1-I circulant diagonal tiles, a 4-stage ring at two
+    waves per SIMD) forced on below 256 (FLR_REF_2I=1) and off above it (=0):
+    D bit-identical to the C restatement either way, ragged super-blocks
+    included."""
+    knob("FLR_REF_2I", two)
+    X, data = _matrix(K, P, 31 + K, cuda)
+    D = ops.pairwise_l2(data[:, :P], "reference").cpu().numpy()
+    assert np.array_equal(D, normref.distance_matrix(X.numpy()))
+
+
 @pytest.mark.parametrize("path", golden_files("c3krum"), ids=lambda p: p.split("/")[-1])
 def test_reference_mode_c3_fixtures(cuda, path):
     """The C3-shaped fixtures (K = 128, f = 25 sign-flipped, multi_k = 64):

@@ -113,7 +113,7 @@ def _free_port():
     return p
 
 
-def _round_worker(rank, world, port, defense, q, exchange="alltoall"):
+def _round_worker(rank, world, port, defense, q, exchange="alltoall", spec="TINY"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
@@ -126,7 +126,8 @@ def _round_worker(rank, world, port, defense, q, exchange="alltoall"):
     if defense == "krum_ref":  # the reference-exact distances: pair tiles split over the ranks
         defense, cfg = "krum", {"pairwise_method": "reference"}
     rc = RoundConfig(num_clients=8, batch=4, defense=defense, num_attackers=1, exchange=exchange, defense_cfg=cfg)
-    eng = RoundEngine(TINY, rc, TrainConfig(local_steps=2), torch.device("cuda:0"), rank, world)
+    eng = RoundEngine(TINY if spec == "TINY" else MID, rc, TrainConfig(local_steps=2), torch.device("cuda:0"),
+                      rank, world)
     for _ in range(2):
         g = eng.run_round()
     torch.cuda.synchronize()
@@ -134,18 +135,19 @@ def _round_worker(rank, world, port, defense, q, exchange="alltoall"):
     if defense == "krum":
         eng.defense.publish()
         sel = (eng.defense.selected_clients, eng.defense.distances.cpu().numpy().tobytes())
-    q.put((rank, g.cpu().numpy(), sel))
+    q.put((rank, g.cpu().numpy(), sel, eng.train_order,
+           eng.xchg.plan.coords(rank) if eng.xchg is not None else None))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def _run(world, defense, exchange="alltoall"):
+def _run(world, defense, exchange="alltoall", spec="TINY"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_round_worker, args=(r, world, port, defense, q, exchange)) for r in range(world)]
+    procs = [ctx.Process(target=_round_worker, args=(r, world, port, defense, q, exchange, spec)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in procs], key=lambda r: r[0])
@@ -205,3 +207,34 @@ def test_reference_distances_split_over_ranks(cuda, world, exchange):
     many = _run(world, "krum_ref", exchange)
     for r in range(world):
         assert np.array_equal(one[0][1], many[r][1]) and one[0][2] == many[r][2], r
+
+
+def _mid_spec():
+    from flr.models.multimodal import ModelSpec
+    # 64-wide stages: tap-major blocks (up to 36,864 coordinates) longer than
+    # the canonical boundaries' distance to them at every world size
+    return ModelSpec(widths=(64, 64, 64, 64), blocks=(1, 1, 1, 1), vocab=50, embed=8, hidden=16, fusion=16,
+                     dropout=0.0)
+
+
+MID = _mid_spec()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("spec", ["TINY", "MID"])
+def test_reference_training_order_over_ranks(cuda, spec, world):
+    """The reference-exact Krum distances of a TRAINING-ORDER round (tap-major
+    convolution weights, no torch-order copy) over 2 / 4 / 8 ranks: the rank
+    boundaries are moved off the tap-major blocks (shard.aligned_bounds; at
+    MID they differ from the canonical slices'), every rank keeps
+    train_order, and the global model, selection and distance matrix equal
+    the one-rank round's bit for bit."""
+    one = _run(1, "krum_ref", "alltoall", spec)
+    assert one[0][3] is True
+    many = _run(world, "krum_ref", "alltoall", spec)
+    for r in range(world):
+        assert many[r][3] is True, r
+        assert np.array_equal(one[0][1], many[r][1]) and one[0][2] == many[r][2], r
+    P = one[0][1].size
+    moved = any(many[r][4] != CoordPlan(P, world).coords(r) for r in range(world))
+    assert moved == (spec == "MID")
