@@ -145,11 +145,16 @@ int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t P, int64_t 
 /* The same with dead taps: dead[b] bit t set = tap t of block b is not in X
  * (FLR_TC_DEFER_DEAD): its slab is read from gdead at the same training-order
  * offset, negated on rows k < nneg — the values flr_resnet_gru_fill_dead
- * writes, so D is bit-identical to the call on the filled X. */
+ * writes, so D is bit-identical to the call on the filled X.  No dead column
+ * may lie in the last P mod 8 (read from X): FLR_ERR_ARG.  after_rewrite
+ * (a hipEvent_t, or NULL): recorded on the stream once the call has read
+ * X for the last time (before the chain kernel of the last segment): the
+ * dead slabs may be written from then on, beside the chains. */
 int flr_pairwise_l2_reference_tap_dead(const float* X, int64_t K, int64_t P, int64_t ldx,
                                        const int64_t* taps, int64_t ntaps, const uint64_t* dead,
                                        const float* gdead, int64_t nneg, double* D, void* ws,
-                                       size_t ws_bytes, int64_t part, int64_t nparts, void* stream);
+                                       size_t ws_bytes, int64_t part, int64_t nparts,
+                                       void* after_rewrite, void* stream);
 /* The same split over coordinate ranges held by different ranks (the
  * coordinate-sharded exchange): each range continues the chains where the
  * previous range left them.  _partial: `steps` chain steps of X (coordinates

@@ -822,7 +822,7 @@ static WaveRuns wave_runs(const int64_t* taps, int64_t ntaps, int64_t r0, int64_
 // tap blocks' rewrite, the chain kernel.
 static int run_chains(const float* X, int64_t K, int64_t steps_total, int64_t ldx, const int64_t* taps, int64_t ntaps,
                       const uint64_t* dead, const float* gdead, int64_t nneg, int first, float* A, void* ws,
-                      size_t ws_bytes, int t0, int t1, hipStream_t st) {
+                      size_t ws_bytes, int t0, int t1, hipStream_t st, hipEvent_t after_rewrite = nullptr) {
   const size_t na = a_bytes(K);
   if (ws_bytes < na) return FLR_ERR_WORKSPACE;
   const int64_t R = steps_total;
@@ -860,6 +860,9 @@ static int run_chains(const float* X, int64_t K, int64_t steps_total, int64_t ld
     if (padded > steps &&
         hipMemset2DAsync(Xc + steps, (size_t)ldc * 4, 0, (size_t)(padded - steps) * 4, (size_t)(K * 8), st) != hipSuccess)
       return FLR_ERR_HIP;
+    // every read of X done (the last segment's rewrite): the caller may now
+    // write X's dead-tap slabs beside the chains (flr_pairwise_l2_reference_tap_dead)
+    if (after_rewrite && seg == nseg - 1 && hipEventRecord(after_rewrite, st) != hipSuccess) return FLR_ERR_HIP;
     if (t0 == 0 && t1 == ntiles_of((int)K) && use_two_chains(K)) {  // every pair: the two-chain tiles
       hipLaunchKernelGGL(ref_chain2_kernel, dim3(8 * ntiles2_of((int)K)), dim3(64), 0, st, Xc, ldc, (int)K, steps,
                          (first && seg == 0) ? 1 : 0, A);
@@ -883,7 +886,8 @@ static int check_rows(const float* X, int64_t K, int64_t n, int64_t ldx) {
 extern "C" int flr_pairwise_l2_reference_tap_dead(const float* X, int64_t K, int64_t P, int64_t ldx,
                                                   const int64_t* taps, int64_t ntaps, const uint64_t* dead,
                                                   const float* gdead, int64_t nneg, double* D, void* ws,
-                                                  size_t ws_bytes, int64_t part, int64_t nparts, void* stream) {
+                                                  size_t ws_bytes, int64_t part, int64_t nparts, void* after_rewrite,
+                                                  void* stream) {
   if (K < 1 || P < 0 || ldx < P || !D || (K > 1 && P > 0 && !X) || nparts < 1 || part < 0 || part >= nparts)
     return FLR_ERR_ARG;
   if (K > (1 << 15)) return FLR_ERR_UNSUPPORTED;
@@ -912,8 +916,12 @@ extern "C" int flr_pairwise_l2_reference_tap_dead(const float* X, int64_t K, int
   float* A = reinterpret_cast<float*>(ws);
   if (K > 1 && R > 0 && t1 > t0 &&
       (rc = run_chains(X, K, R, ldx, taps, ntaps, any_dead ? dead : nullptr, gdead, nneg, 1, A, ws, ws_bytes, t0, t1,
-                       st)) != FLR_OK)
+                       st, static_cast<hipEvent_t>(after_rewrite))) != FLR_OK)
     return rc;
+  // no chains ran (K < 2, no full step, no tiles here): X's dead slabs are free now
+  if (after_rewrite && !(K > 1 && R > 0 && t1 > t0) &&
+      hipEventRecord(static_cast<hipEvent_t>(after_rewrite), st) != hipSuccess)
+    return FLR_ERR_HIP;
   // the tail coordinates' columns (identity outside the tap-major blocks)
   TailCols tc;
   for (int64_t u = 8 * R; u < 8 * R + 8; ++u) {
@@ -944,7 +952,7 @@ extern "C" int flr_pairwise_l2_reference_tap(const float* X, int64_t K, int64_t 
                                              const int64_t* taps, int64_t ntaps, double* D, void* ws, size_t ws_bytes,
                                              int64_t part, int64_t nparts, void* stream) {
   return flr_pairwise_l2_reference_tap_dead(X, K, P, ldx, taps, ntaps, nullptr, nullptr, 0, D, ws, ws_bytes, part,
-                                            nparts, stream);
+                                            nparts, nullptr, stream);
 }
 
 extern "C" int flr_pairwise_l2_reference(const float* X, int64_t K, int64_t P, int64_t ldx, double* D, void* ws,

@@ -473,7 +473,7 @@ class Net {
   // X's dead-tap ranges (training order) <- gtrain, rows k < nneg negated: one
   // launch over the range table when it fits and the rows are 16-B aligned
   // (was one broadcast per range: 57 launches per C3 round), else per range.
-  int dead_ranges(const float* gtrain, float* X, int64_t ld, int64_t nneg, hipStream_t st) {
+  int dead_ranges(const float* gtrain, float* X, int64_t ld, int64_t nneg, hipStream_t st, int64_t gx = 0) {
     int rc;
     DeadTable t;
     t.cnt = 0;
@@ -500,7 +500,8 @@ class Net {
     }
     if (fits) {
       if (t.cnt == 0) return FLR_OK;
-      const int64_t g = std::max<int64_t>(1, std::min<int64_t>(256, (total / 4 + THREADS - 1) / THREADS));
+      // gx > 0: that many workgroups per row (a fill beside other kernels, throttled)
+      const int64_t g = gx > 0 ? gx : std::max<int64_t>(1, std::min<int64_t>(256, (total / 4 + THREADS - 1) / THREADS));
       hipLaunchKernelGGL(dead_ranges_kernel, dim3((unsigned)g, (unsigned)K_), dim3(THREADS), 0, st, t, gtrain, X, ld,
                          (int)std::min<int64_t>(nneg, K_));
       return launch_status("train_clients: dead ranges");
@@ -1164,7 +1165,14 @@ extern "C" int flr_resnet_gru_fill_dead(const flr_resnet_gru_spec* spec, float w
   const int rc = net.layout();
   if (rc != FLR_OK) return rc;
   if (ld < net.P()) return FLR_ERR_ARG;
-  return net.dead_ranges(gtrain, X, ld, nneg, as_stream(stream));
+  // FLR_FILL_GRID: workgroups per row (0: the training phase's grid); 1 or 4
+  // beside the Krum chains measured slower still (profiles/r6_dead/)
+  static const int64_t gx = [] {
+    const char* e = flr::knob("FLR_FILL_GRID");
+    const int v = e ? atoi(e) : 0;
+    return (int64_t)(v >= 0 && v <= 256 ? v : 0);
+  }();
+  return net.dead_ranges(gtrain, X, ld, nneg, as_stream(stream), gx);
 }
 
 extern "C" int flr_resnet_gru_reorder(const flr_resnet_gru_spec* spec, const float* src, float* dst, int to_train,

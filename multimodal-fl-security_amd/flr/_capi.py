@@ -55,7 +55,8 @@ SIGNATURES = {
     "flr_pairwise_l2_reference_tap": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p, _c_void_p,
                                              _size_t, _i64, _i64, _c_void_p]),
     "flr_pairwise_l2_reference_tap_dead": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _c_void_p, _c_void_p,
-                                                  _i64, _c_void_p, _c_void_p, _size_t, _i64, _i64, _c_void_p]),
+                                                  _i64, _c_void_p, _c_void_p, _size_t, _i64, _i64, _c_void_p,
+                                                  _c_void_p]),
     "flr_pairwise_l2_reference_partial": (_int, [_c_void_p, _i64, _i64, _i64, _int, _c_void_p, _size_t, _c_void_p]),
     "flr_pairwise_l2_reference_partial_tap": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _int, _c_void_p,
                                                      _size_t, _c_void_p]),

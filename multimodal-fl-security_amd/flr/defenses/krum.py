@@ -33,6 +33,11 @@ class KrumDefense(BaseDefense):
         # reference mode over a training-order client matrix: its tap-major
         # convolution blocks [(off, Cout, Cin, KK), ...] (set by RoundEngine)
         self.tap_blocks = None
+        # ... and its dead-tap slabs not yet in X (masks per block, training-order
+        # global vector, negated rows; RoundEngine: FLR_TC_DEFER_DEAD), with the
+        # call that makes X whole before rows are read (the side-stream fill joined)
+        self.tap_dead = None
+        self.before_rows = None
         self.selected_clients: List[int] = []
         self.rejected_clients: List[int] = []
         self.client_scores: List[float] = []
@@ -47,8 +52,10 @@ class KrumDefense(BaseDefense):
         if n < 2 * f + 3:  # krum.py:153-157
             raise ValueError(
                 f"Krum requires n >= 2f + 3. Got n={n}, f={f}. Need at least {2 * f + 3} clients.")
+        ref = self.pairwise_method == "reference"
         self.distances = ops.pairwise_l2(cm.X, self.pairwise_method, comm=self.comm,
-                                         tap_blocks=self.tap_blocks if self.pairwise_method == "reference" else None)
+                                         tap_blocks=self.tap_blocks if ref else None,
+                                         dead=self.tap_dead if ref and self.tap_blocks else None)
         self._check_refine_capacity(n)
         self.scores_device, self.order_device = ops.krum_select(self.distances, f)
         return self.order_device
@@ -70,6 +77,8 @@ class KrumDefense(BaseDefense):
         order = self.select(cm)
         if publish:
             self.publish()
+        if self.before_rows is not None:
+            self.before_rows()
         if self.multi_k == 1:
             return cm.data[int(order[0].item()), : cm.P]
         return ops.rows_mean(cm.X, order[: min(self.multi_k, cm.K)], divisor=self.multi_k)
@@ -105,6 +114,8 @@ class KrumDefense(BaseDefense):
         self.scores_device, self.order_device = ops.krum_select(self.distances, f)
         if publish:
             self.publish()
+        if self.before_rows is not None:
+            self.before_rows()
         if self.multi_k == 1:
             return cs.data[self.order_device[0].long(), : cs.n]
         return ops.rows_mean(cs.X, self.order_device[: min(self.multi_k, n)], divisor=self.multi_k)
@@ -112,7 +123,10 @@ class KrumDefense(BaseDefense):
     def _sharded_distances(self, cs, events=None):
         if self.pairwise_method == "reference":
             if cs.comm.world == 1:  # the one slice is the whole matrix
-                return ops.pairwise_l2(cs.X, "reference", tap_blocks=self.tap_blocks)
+                return ops.pairwise_l2(cs.X, "reference", tap_blocks=self.tap_blocks,
+                                       dead=self.tap_dead if self.tap_blocks else None)
+            if self.tap_dead is not None:
+                raise ValueError("deferred dead taps are a one-GPU mode")
             # training order: the rank boundaries are tap-block aligned (shard.aligned_bounds)
             return ops.pairwise_l2_reference_sharded(cs, self.tap_blocks)
         if self.pairwise_method != "gram":

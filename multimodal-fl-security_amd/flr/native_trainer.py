@@ -8,7 +8,7 @@ same symbol over ctypes / cgo / N-API."""
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 
@@ -138,6 +138,29 @@ class NativeRoundTrainer:
         self._global = None   # the vector the next local_update starts from, and its order
         self._order = 0
         self._bound = None    # (key, stacked copies) when the inputs are not views of one buffer
+        # training order: leave X's dead-tap slabs to fill_dead (FLR_TC_DEFER_DEAD; RoundEngine)
+        self.defer_dead = False
+
+    def dead_ranges(self) -> List[Tuple[int, int]]:
+        """[(off, n), ...]: the dead-tap ranges of a training-order row (the
+        untrained slabs the trainer copies from the global vector)."""
+        if self.vit:
+            return []
+        lib, sp, wd = _capi.lib(), ctypes.byref(self._sp), self.cfg.weight_decay
+        n = int(lib.flr_resnet_gru_dead_ranges(sp, wd, None, None, 0))
+        if n < 0:
+            raise ValueError("flr_resnet_gru_dead_ranges: bad spec")
+        off, ln = (ctypes.c_int64 * max(1, n))(), (ctypes.c_int64 * max(1, n))()
+        lib.flr_resnet_gru_dead_ranges(sp, wd, off, ln, n)
+        return [(int(off[i]), int(ln[i])) for i in range(n)]
+
+    def fill_dead(self, gtrain: torch.Tensor, negate_rows: int = 0) -> None:
+        """X's dead-tap ranges <- gtrain's (rows < negate_rows negated), on the
+        current stream: what a local_update with defer_dead left out."""
+        if gtrain.numel() < self.P or gtrain.dtype != torch.float32 or gtrain.device != self.device:
+            raise ValueError("fill_dead: a float32 training-order P-vector on the trainer's device")
+        _capi.call("flr_resnet_gru_fill_dead", ctypes.byref(self._sp), self.cfg.weight_decay, gtrain.data_ptr(),
+                   self.X.data.data_ptr(), self.X.data.stride(0), self.K, int(negate_rows), self._stream())
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -234,6 +257,7 @@ class NativeRoundTrainer:
         _capi.call("flr_train_clients_ex", ctypes.byref(self._sp), g.data_ptr(), self.X.data.data_ptr(),
                    self.X.data.stride(0), imgs.data_ptr(), toks.data_ptr(), labs.data_ptr(),
                    None if m is None else m.data_ptr(), steps, self.K, self.B, c.lr, c.momentum, c.weight_decay,
-                   c.clip, int(negate_rows), self.loss.data_ptr(), self.norms.data_ptr(), self._order,
+                   c.clip, int(negate_rows), self.loss.data_ptr(), self.norms.data_ptr(),
+                   self._order | (2 if self._order == 1 and self.defer_dead else 0),
                    self._ws.data_ptr(), self._ws_bytes, self._stream())
         return self.loss

@@ -38,7 +38,7 @@ def _check_matrix(X: torch.Tensor, name: str = "X") -> Tuple[int, int, int]:
 
 
 def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None, comm=None,
-                tap_blocks: Optional[Sequence[Tuple[int, int, int, int]]] = None) -> torch.Tensor:
+                tap_blocks: Optional[Sequence[Tuple[int, int, int, int]]] = None, dead=None) -> torch.Tensor:
     """K×K float64 distances, D[i][j] = fp32 ||X_i - X_j|| (krum.py:73-99).
 
     method: "gram" (centred Gram on MFMA), "direct" (exact fp32 differences,
@@ -51,11 +51,20 @@ def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None, comm=None,
     main MFMA kernel (flr.timing.HipEventPair).
     comm: optional flr.shard.Comm for the reference mode: every rank holds the
     whole X, computes 1/world of the pair tiles and one all-reduce (sum, exact:
-    one non-zero term per pair) of the 8·K² bytes of D gives every rank D."""
+    one non-zero term per pair) of the 8·K² bytes of D gives every rank D.
+    dead: optional (masks, gdead, nneg[, mark]) with tap_blocks — X's dead-tap
+    slabs are not written yet (FLR_TC_DEFER_DEAD): bit t of masks[b] reads tap
+    t of block b from the training-order vector gdead, negated on rows < nneg
+    (flr_pairwise_l2_reference_tap_dead; the same D as on the filled X).
+    mark: an object with .event (a recorded-once torch.cuda.Event): recorded
+    on the stream once X has been read for the last time, then mark.recorded
+    = True (the round engine writes the slabs beside the chains from there)."""
     K, P, ldx = _check_matrix(X)
     D = torch.empty((K, K), dtype=torch.float64, device=X.device)
     if method == "reference":
         if X.data_ptr() % 16 or ldx % 4:  # the kernels load 16-B pieces of 16-B aligned rows
+            if dead is not None:
+                raise ValueError("pairwise_l2(dead=): the rows must be 16-B aligned (read in place)")
             Xa = torch.zeros((K, (P + 63) // 64 * 64), dtype=torch.float32, device=X.device)
             Xa[:, :P].copy_(X)
             X, ldx = Xa, Xa.stride(0)
@@ -63,8 +72,21 @@ def pairwise_l2(X: torch.Tensor, method: str = "gram", events=None, comm=None,
         wp, nbytes = _ref_workspace(K, P, X.device, _stream(X))
         taps = [int(v) for blk in (tap_blocks or ()) for v in blk]
         tarr = (ctypes.c_int64 * max(1, len(taps)))(*taps)
-        _capi.call("flr_pairwise_l2_reference_tap", X.data_ptr(), K, P, ldx, ctypes.addressof(tarr), len(taps) // 4,
-                   D.data_ptr(), wp, nbytes, part, nparts, _stream(X))
+        if dead is None:
+            _capi.call("flr_pairwise_l2_reference_tap", X.data_ptr(), K, P, ldx, ctypes.addressof(tarr),
+                       len(taps) // 4, D.data_ptr(), wp, nbytes, part, nparts, _stream(X))
+        else:
+            masks, gdead, nneg = dead[:3]
+            mark = dead[3] if len(dead) > 3 else None
+            if len(masks) != len(taps) // 4 or gdead.device != X.device or gdead.dtype != torch.float32 \
+                    or gdead.numel() < P:
+                raise ValueError("pairwise_l2(dead=): one mask per tap block and a float32 P-vector on X's device")
+            marr = (ctypes.c_uint64 * max(1, len(masks)))(*[int(m) for m in masks])
+            _capi.call("flr_pairwise_l2_reference_tap_dead", X.data_ptr(), K, P, ldx, ctypes.addressof(tarr),
+                       len(taps) // 4, ctypes.addressof(marr), gdead.data_ptr(), int(nneg), D.data_ptr(), wp,
+                       nbytes, part, nparts, None if mark is None else mark.event.cuda_event, _stream(X))
+            if mark is not None:
+                mark.recorded = True
         if nparts > 1:
             comm.all_reduce_sum(D)
         return D

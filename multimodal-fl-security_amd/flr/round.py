@@ -64,6 +64,25 @@ def initial_global(spec: ModelSpec, seed: int, device) -> torch.Tensor:
     return torch.cat([p.detach().reshape(-1) for p in m.parameters()]).to(device)
 
 
+class _DeadFill:
+    """The deferred dead-tap fill of a round (RoundEngine, FLR_DEFER_DEAD):
+    side stream, the distances' 'X read for the last time' mark, the fill's
+    done event, per-block dead-tap masks; state 0 idle, 1 due this round."""
+
+    class _Mark:
+        def __init__(self, device):
+            self.event = torch.cuda.Event()
+            self.event.record(torch.cuda.current_stream(device))  # created now: a handle to pass down
+            self.recorded = False
+
+    def __init__(self, device, masks):
+        self.side = torch.cuda.Stream(device)
+        self.mark = _DeadFill._Mark(device)
+        self.done = torch.cuda.Event()
+        self.masks = masks
+        self.state = 0
+
+
 class RoundEngine:
     def __init__(self, spec: ModelSpec, rcfg: RoundConfig, tcfg: TrainConfig = TrainConfig(), device="cuda",
                  rank: int = 0, world: int = 1):
@@ -141,6 +160,19 @@ class RoundEngine:
                 # split their pair tiles over the ranks (one 8·K² all-reduce)
                 self.defense.comm = Comm()
         self.gtrain = self.trainer.to_train_order(self.global_flat) if self.train_order else None
+        # FLR_DEFER_DEAD=1 (opt-in): the dead-tap slabs (copies of the global
+        # model, 58 % of P at C3) written by a side stream under the Krum chains
+        # instead of last in the training phase, the tap rewrite reading them from
+        # gtrain meanwhile.  Bit-identical, but the chains slow by more than the
+        # fill saves (profiles/r6_dead/): off by default
+        self._fill = None
+        if (self.train_order and world == 1 and self.defense.__dict__.get("tap_blocks")
+                and hasattr(self.trainer, "fill_dead") and os.environ.get("FLR_DEFER_DEAD", "0") == "1"):
+            masks = self._dead_masks(self.defense.tap_blocks)
+            if masks is not None and any(masks):
+                self.trainer.defer_dead = True
+                self._fill = _DeadFill(self.device, masks)
+
         self.round_index = 0
         self.fell_back = False
         self.fallback_error: Optional[str] = None   # exception type of the last FedAvg fallback
@@ -172,6 +204,49 @@ class RoundEngine:
         if not torch.equal(got.to(torch.int64), want):
             return False, None
         return True, blocks
+
+    def _dead_masks(self, taps):
+        """Per tap block the bitmask of its dead taps (the trainer's dead ranges,
+        each a whole tap slab of one block), or None when a range is not (or a
+        dead coordinate falls in the last P mod 8, which the distances read
+        from X directly)."""
+        ranges = self.trainer.dead_ranges()
+        P = self.trainer.P
+        masks = [0] * len(taps)
+        for o, n in ranges:
+            if o + n > P - P % 8:
+                return None
+            for b, (off, co, ci, kk) in enumerate(taps):
+                slab = co * ci
+                if off <= o and o + n <= off + kk * slab:
+                    if (o - off) % slab or n % slab or kk > 64:
+                        return None
+                    for t in range((o - off) // slab, (o - off + n) // slab):
+                        masks[b] |= 1 << t
+                    break
+            else:
+                return None
+        return masks
+
+    def _join_fill(self) -> None:
+        """X whole on the current stream: this round's dead-tap fill launched
+        if it is not yet (on the side stream, after the distances' last read
+        of X when they marked it, else after everything so far) and waited for.
+        Idempotent; a no-op without a pending fill."""
+        f = self._fill
+        if f is None or f.state == 0:
+            return
+        main = torch.cuda.current_stream(self.device)
+        if f.state == 1:
+            if f.mark.recorded:
+                f.side.wait_event(f.mark.event)
+            else:
+                f.side.wait_stream(main)
+            with torch.cuda.stream(f.side):
+                self.trainer.fill_dead(self.gtrain, self._num_flipped())
+                f.done.record(f.side)
+        main.wait_event(f.done)
+        f.state = 0
 
     def _num_flipped(self) -> int:
         """Local rows of sign-flip attackers (clients 0..f-1): they submit
@@ -226,6 +301,22 @@ class RoundEngine:
             self.losses = self._graph_losses
         else:
             self.losses = self._train_phase()
+        if self._fill is not None:
+            # the dead-tap slabs are written by the side stream under the Krum
+            # chains (launched by _join_fill before the rows are read); until
+            # then the distances read those taps from gtrain (ops.pairwise_l2 dead=)
+            f = self._fill
+            f.state, f.mark.recorded = 1, False
+            self.defense.tap_dead = (f.masks, self.gtrain, self._num_flipped(), f.mark)
+            self.defense.before_rows = self._join_fill
+        try:
+            return self._aggregate_phase()
+        finally:
+            self._join_fill()  # X is whole for every later reader
+            if self._fill is not None:
+                self.defense.tap_dead = self.defense.before_rows = None
+
+    def _aggregate_phase(self) -> torch.Tensor:
         kw = {"publish": False} if hasattr(self.defense, "publish") else {}
         self.fell_back = False
         self.fallback_error = None
@@ -235,6 +326,7 @@ class RoundEngine:
                 part = self.defense.aggregate_sharded(self.slice, self.num_examples, **kw)
             except Exception as e:  # noqa: BLE001 - the reference catches any exception
                 part = self._fallback(e, self.slice.X)
+            self._join_fill()  # gtrain is overwritten next: the fill has read it
             self.slice.gather_vector(part, self.gtrain if self.train_order else self.global_flat)
             return self._publish()
         fdist.allgather_rows(self.trainer.X.data, self.full.data)
@@ -244,6 +336,7 @@ class RoundEngine:
             agg = self.defense.aggregate_flat(self.full, self.num_examples, **kw)
         except Exception as e:  # noqa: BLE001
             agg = self._fallback(e, self.full.X)
+        self._join_fill()
         return self._publish(agg)
 
     def _fallback(self, err: Exception, X: torch.Tensor) -> torch.Tensor:
@@ -253,6 +346,7 @@ class RoundEngine:
         = False keeps device / library failures (kernel launch, workspace, HIP or
         RCCL errors, out of memory) loud instead."""
         from ._capi import FlrError
+        self._join_fill()
         device_error = isinstance(err, (FlrError, torch.cuda.OutOfMemoryError))
         if not self.rcfg.fallback_fedavg or (device_error and (not self.rcfg.fallback_device_errors
                                                                or self.world > 1)):

@@ -190,3 +190,47 @@ def test_reference_mode_tap_blocks_segmented(cuda):
     want = ops.pairwise_l2(data[:, :P], "reference").cpu().numpy()
     assert np.array_equal(D.cpu().numpy(), want)
     assert np.array_equal(want, normref.distance_matrix(X.numpy()))
+
+
+@pytest.mark.parametrize("K,blocks,masks,nneg", [
+    (16, [(5, 64, 64, 9), (36_869 + 7, 64, 3, 9), (36_869 + 7 + 1728 + 3, 128, 64, 1)],
+     [0b110101011, 0b000010000, 0b1], 3),
+    (33, [(0, 128, 64, 9), (73_728 + 1, 40, 24, 9)], [0b011111110, 0b000000011], 0),
+    (9, [(3, 64, 8, 9)], [0b000011111], 9)])
+def test_reference_mode_deferred_dead_taps(cuda, K, blocks, masks, nneg):
+    """flr_pairwise_l2_reference_tap_dead (the round engine's FLR_TC_DEFER_DEAD
+    rounds): the dead-tap slabs are NaN in X and read from the global vector
+    instead, negated on rows < nneg — D bit-identical to the call on the matrix
+    with those slabs filled as flr_resnet_gru_fill_dead fills them."""
+    P = max(o + co * ci * kk for o, co, ci, kk in blocks) + (5 if K != 9 else 0)
+    X, data = _matrix(K, P, 31 + K, cuda)
+    train = data.clone()
+    for o, co, ci, kk in blocks:
+        w = data[:, o:o + co * ci * kk].reshape(K, co, ci, kk)
+        train[:, o:o + co * ci * kk] = w.permute(0, 3, 2, 1).reshape(K, -1)
+    g = torch.randn(P, generator=torch.Generator().manual_seed(5)).to(cuda)
+    filled, holes = train.clone(), train.clone()
+    for (o, co, ci, kk), m in zip(blocks, masks):
+        for t in range(kk):
+            if m >> t & 1:
+                sl = slice(o + t * ci * co, o + (t + 1) * ci * co)
+                filled[:, sl] = g[sl]
+                filled[:nneg, sl] = -g[sl]
+                holes[:, sl] = float("nan")
+    D = ops.pairwise_l2(holes[:, :P], "reference", tap_blocks=blocks, dead=(masks, g, nneg)).cpu().numpy()
+    want = ops.pairwise_l2(filled[:, :P], "reference", tap_blocks=blocks).cpu().numpy()
+    assert np.isfinite(want).all() and np.array_equal(D, want)
+
+
+def test_reference_mode_dead_tap_in_the_tail_rejected(cuda):
+    """The finish kernel reads the last P mod 8 coordinates from X itself: a
+    dead tap among them is refused (the engine then writes the slabs first)."""
+    from flr._capi import FlrError
+    K, blocks = 9, [(3, 64, 8, 9)]
+    P = 3 + 64 * 8 * 9  # tail: block columns of taps 6, 7, 8
+    _, data = _matrix(K, P, 3, cuda)
+    g = torch.zeros(P, device=cuda)
+    with pytest.raises((FlrError, ValueError)):
+        ops.pairwise_l2(data[:, :P], "reference", tap_blocks=blocks, dead=([1 << 8], g, 0))
+    with pytest.raises((FlrError, ValueError)):  # a bit past the block's taps
+        ops.pairwise_l2(data[:, :P], "reference", tap_blocks=blocks, dead=([1 << 9], g, 0))

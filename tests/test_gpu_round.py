@@ -185,3 +185,33 @@ def test_native_trainer_round_equals_python_trainer(cuda, monkeypatch, order):
     assert torch.equal(la, lb)
     assert torch.equal(xa, xb)
     assert torch.equal(ga, gb)
+
+
+@pytest.mark.parametrize("multi_k", [4, 1])
+def test_deferred_dead_taps_bit_identical(cuda, monkeypatch, multi_k):
+    """FLR_DEFER_DEAD=1 (opt-in): the training phase leaves X's dead-tap slabs
+    to a side-stream fill beside the reference-exact Krum distances, which
+    read those taps from the global vector meanwhile.  Against the slabs
+    written last in the training phase (FLR_DEFER_DEAD=0): the same distance
+    matrix, selection, client matrix and global model bit for bit, over 2
+    rounds of HIP-graph replay with sign-flip attackers, on the full
+    ResNet-18 + GRU model (dead taps in layers 3-4)."""
+    from flr.models.multimodal import ModelSpec
+    spec = ModelSpec()
+    rc = RoundConfig(num_clients=8, batch=4, defense="krum", attack="sign_flip", num_attackers=1,
+                     defense_cfg={"pairwise_method": "reference", "multi_k": multi_k})
+    res = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("FLR_DEFER_DEAD", defer)
+        eng = RoundEngine(spec, rc, TrainConfig(local_steps=2), cuda)
+        assert eng.train_order and (eng._fill is not None) == (defer == "1")
+        for _ in range(2):
+            eng.run_round()
+        eng.defense.publish()
+        res.append((eng.global_flat.clone().cpu(), eng.defense.distances.clone().cpu(),
+                    list(eng.defense.selected_clients), eng.trainer.X.X.clone().cpu()))
+    (ga, da, sa, xa), (gb, db, sb, xb) = res
+    assert torch.isfinite(ga).all() and torch.isfinite(da).all()
+    assert torch.equal(da, db) and sa == sb
+    assert torch.equal(xa, xb)
+    assert torch.equal(ga, gb)
