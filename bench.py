@@ -83,7 +83,7 @@ def ref_traffic(K: int, P: int):
     return (2.0 * t["fetch_kib_per_call"] + t["write_kib_per_call"]) * 1024.0
 
 
-COMMITTED_C3_STATS = "profiles/r4_c3_kernel_stats_serial.txt"  # FLR_TEXT_STREAM=0: per-kernel durations without the text stream beside them
+COMMITTED_C3_STATS = "profiles/r6_prof/c3_kernel_stats_serial.txt"  # FLR_TEXT_STREAM=0 FLR_WGRAD_STREAM=0: per-kernel durations with nothing beside them
 # the C4 bench's rocprofv3 summary (gemm_mfma_from_profile of an unmodified C4 line)
 COMMITTED_C4_STATS = "profiles/r3_c4_kernel_stats.txt"
 
