@@ -18,6 +18,14 @@ SHAPES = [  # name, M, N, R, mode (fwd: x W^T | dx: dy W | dw: dy^T x)
 ]
 
 
+
+def _set_knobs(env):
+    """The library reads FLR_* switches once at load: variants go through flr_set_knob."""
+    from flr import _capi
+    for k, v in env.items():
+        if k.startswith("FLR_"):
+            _capi.set_knob(k, v)
+
 def operands(M, N, R, mode):
     if mode in ("fwd", "fwdb", "fwda"):   # A = x [M, R], B = W [N, R] (fwdb: + bias [K, N]; fwda: + addend)
         return torch.randn(K, M, R, device="cuda"), torch.randn(K, N, R, device="cuda")
@@ -44,6 +52,7 @@ def main():
         for var in variants:
             old = {k: os.environ.get(k) for k in var}
             os.environ.update(var)
+            _set_knobs(var)
             for _ in range(3):
                 fnn.bgemm(A, B, bias=bias, add=addt, out=out)
             torch.cuda.synchronize()
@@ -61,6 +70,7 @@ def main():
                     os.environ.pop(k, None)
                 else:
                     os.environ[k] = v
+            _set_knobs(old)
         print(f"{name:12s} {M:5d} {N:5d} {R:5d} {mode:4s} | " + " | ".join(cells), flush=True)
 
 

@@ -26,6 +26,14 @@ LAYERS = [  # name, Cin, H, Cout, k, stride, pad
 ]
 
 
+
+def _set_knobs(env):
+    """The library reads FLR_* switches once at load: variants go through flr_set_knob."""
+    from flr import _capi
+    for k, v in env.items():
+        if k.startswith("FLR_"):
+            _capi.set_knob(k, v)
+
 def taps(H, k, s, p):
     Ho = (H + 2 * p - k) // s + 1
     v = [kh for kh in range(k) if any(0 <= o * s - p + kh < H for o in range(Ho))]
@@ -74,6 +82,7 @@ def main():
             for vi, env in enumerate(variants):
                 saved = {k: os.environ.get(k) for k in env}
                 os.environ.update(env)
+                _set_knobs(env)
                 fn()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -87,6 +96,7 @@ def main():
                         os.environ.pop(k, None)
                     else:
                         os.environ[k] = v
+                _set_knobs(saved)
                 us = e0.elapsed_time(e1) * 1e3 / reps
                 tot[vi] += us
                 cols.append(f"{us:9.1f} us {flops / us / 1e6:7.1f} TF/s")
