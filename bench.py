@@ -517,6 +517,7 @@ def main() -> None:
     elapsed = fdist.max_over_ranks(time.perf_counter() - t0, device)
 
     # ---- untimed diagnostics after the timed region ----
+    eng.materialize()  # (FLR_DEFER_DEAD=2: the client matrix's dead-tap ranges, for the diagnostics below)
     reps = 5
     sharded = eng.exchange == "alltoall"
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -210,6 +210,14 @@ int flr_krum_select(const double* D, int64_t K, int64_t f, double* scores,
 int flr_rows_mean(const float* X, int64_t K, int64_t P, int64_t ldx,
                   const int32_t* rows, int64_t m, int64_t divisor, float* out,
                   void* stream);
+/* The same over a training-order matrix whose dead-tap ranges [dead_off[r],
+ * + dead_n[r]) are not written (the round engine's FLR_DEFER_DEAD=2): row k's
+ * value there is gdead's, negated for k < nneg, summed in the same order —
+ * bit-identical to flr_rows_mean over the filled rows; X's dead ranges are not
+ * read (the float4 groups wholly inside them).  16-B aligned rows and out. */
+int flr_rows_mean_dead(const float* X, int64_t K, int64_t P, int64_t ldx, const int32_t* rows,
+                       int64_t m, int64_t divisor, const int64_t* dead_off, const int64_t* dead_n,
+                       int64_t ndead, const float* gdead, int64_t nneg, float* out, void* stream);
 
 /* ---- a14: FedAvg -------------------------------------------------------
  * Replaces NoDefense.aggregate (src/defenses/base_defense.py:80-97) and the

@@ -64,6 +64,8 @@ SIGNATURES = {
     "flr_pairwise_l2_direct_workspace": (_size_t, [_i64, _i64]),
     "flr_pairwise_l2_direct": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "flr_krum_select": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),
+    "flr_rows_mean_dead": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64,
+                                  _c_void_p, _i64, _c_void_p, _c_void_p]),
     "flr_rows_mean": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _i64, _i64, _c_void_p, _c_void_p]),
     "flr_fedavg": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _c_void_p]),
     "flr_trimmed_mean": (_int, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p]),

@@ -38,6 +38,9 @@ class KrumDefense(BaseDefense):
         # call that makes X whole before rows are read (the side-stream fill joined)
         self.tap_dead = None
         self.before_rows = None
+        # FLR_DEFER_DEAD=2: X's dead-tap ranges never written — (ranges, gtrain,
+        # nneg) for the Multi-Krum mean and the selected row
+        self.rows_dead = None
         self.selected_clients: List[int] = []
         self.rejected_clients: List[int] = []
         self.client_scores: List[float] = []
@@ -80,8 +83,12 @@ class KrumDefense(BaseDefense):
         if self.before_rows is not None:
             self.before_rows()
         if self.multi_k == 1:
-            return cm.data[int(order[0].item()), : cm.P]
-        return ops.rows_mean(cm.X, order[: min(self.multi_k, cm.K)], divisor=self.multi_k)
+            i = int(order[0].item())
+            if self.rows_dead is not None:
+                ranges, g, nneg = self.rows_dead
+                return ops.fill_dead_ranges(cm.data[i, : cm.P].clone(), ranges, g, i < nneg)
+            return cm.data[i, : cm.P]
+        return ops.rows_mean(cm.X, order[: min(self.multi_k, cm.K)], divisor=self.multi_k, dead=self.rows_dead)
 
     # pairwise_method="reference" reproduces the reference's torch.norm
     # accumulation, which runs over the whole vector in parameters() order:
@@ -117,8 +124,13 @@ class KrumDefense(BaseDefense):
         if self.before_rows is not None:
             self.before_rows()
         if self.multi_k == 1:
+            if self.rows_dead is not None:  # one GPU: the slice is the whole matrix
+                i = int(self.order_device[0].item())
+                ranges, g, nneg = self.rows_dead
+                return ops.fill_dead_ranges(cs.data[i, : cs.n].clone(), ranges, g, i < nneg)
             return cs.data[self.order_device[0].long(), : cs.n]
-        return ops.rows_mean(cs.X, self.order_device[: min(self.multi_k, n)], divisor=self.multi_k)
+        return ops.rows_mean(cs.X, self.order_device[: min(self.multi_k, n)], divisor=self.multi_k,
+                             dead=self.rows_dead)
 
     def _sharded_distances(self, cs, events=None):
         if self.pairwise_method == "reference":

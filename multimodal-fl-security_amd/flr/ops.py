@@ -120,17 +120,37 @@ def krum_select(D: torch.Tensor, f: int) -> Tuple[torch.Tensor, torch.Tensor]:
 
 
 def rows_mean(X: torch.Tensor, rows: torch.Tensor, divisor: Optional[int] = None,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Ordered fp32 sum of X[rows] divided by `divisor` (krum.py:182-192)."""
+              out: Optional[torch.Tensor] = None, dead=None) -> torch.Tensor:
+    """Ordered fp32 sum of X[rows] divided by `divisor` (krum.py:182-192).
+    dead: optional (ranges [(off, n), ...], gdead, nneg) — X's dead-tap ranges
+    are not written (FLR_DEFER_DEAD=2): row k's value there is gdead's, negated
+    for k < nneg (flr_rows_mean_dead; the same bits as over the filled rows)."""
     K, P, ldx = _check_matrix(X)
     rows = rows.to(device=X.device, dtype=torch.int32).contiguous()
     m = rows.numel()
     divisor = m if divisor is None else int(divisor)
     if out is None:
         out = torch.empty(P, dtype=torch.float32, device=X.device)
-    _capi.call("flr_rows_mean", X.data_ptr(), K, P, ldx, rows.data_ptr(), m, divisor, out.data_ptr(),
-               _stream(X))
+    if dead is None:
+        _capi.call("flr_rows_mean", X.data_ptr(), K, P, ldx, rows.data_ptr(), m, divisor, out.data_ptr(),
+                   _stream(X))
+        return out
+    ranges, gdead, nneg = dead
+    off = (ctypes.c_int64 * max(1, len(ranges)))(*[int(o) for o, _ in ranges])
+    ln = (ctypes.c_int64 * max(1, len(ranges)))(*[int(n) for _, n in ranges])
+    _capi.call("flr_rows_mean_dead", X.data_ptr(), K, P, ldx, rows.data_ptr(), m, divisor, ctypes.addressof(off),
+               ctypes.addressof(ln), len(ranges), gdead.data_ptr(), int(nneg), out.data_ptr(), _stream(X))
     return out
+
+
+def fill_dead_ranges(vec: torch.Tensor, ranges, gdead: torch.Tensor, negate: bool) -> torch.Tensor:
+    """vec's dead-tap ranges <- gdead's (negated when `negate`): one row of a
+    FLR_DEFER_DEAD=2 matrix made whole (flr_copy_rows_neg per range)."""
+    st = _stream(vec)
+    for o, n in ranges:
+        _capi.call("flr_copy_rows_neg", gdead.data_ptr() + 4 * o, n, n, vec.data_ptr() + 4 * o, n, 1,
+                   1 if negate else 0, st)
+    return vec
 
 
 def fedavg(X: torch.Tensor, num_examples, out: Optional[torch.Tensor] = None) -> torch.Tensor:

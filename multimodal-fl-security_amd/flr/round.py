@@ -26,6 +26,7 @@ from typing import Dict, Optional
 
 import torch
 
+from . import _capi
 from . import dist as fdist
 from . import ops
 from .attacks import Backdoor, poison_batches_
@@ -165,13 +166,28 @@ class RoundEngine:
         # instead of last in the training phase, the tap rewrite reading them from
         # gtrain meanwhile.  Bit-identical, but the chains slow by more than the
         # fill saves (profiles/r6_dead/): off by default
+        # FLR_DEFER_DEAD=2 (default): never written at all — the distances read
+        # them from the round's global vector, the Multi-Krum mean too
+        # (flr_rows_mean_dead): C3 15.65-15.73 -> 15.94-15.99 rounds/s, the
+        # same bits (profiles/r6_dead/); materialize() writes them for any other
+        # reader of X; =0: written last in the training phase
         self._fill = None
+        self._lazy = None
+        self._x_stale = False
+        defer = os.environ.get("FLR_DEFER_DEAD", "2")
         if (self.train_order and world == 1 and self.defense.__dict__.get("tap_blocks")
-                and hasattr(self.trainer, "fill_dead") and os.environ.get("FLR_DEFER_DEAD", "0") == "1"):
+                and hasattr(self.trainer, "fill_dead") and defer in ("1", "2")):
             masks = self._dead_masks(self.defense.tap_blocks)
             if masks is not None and any(masks):
                 self.trainer.defer_dead = True
-                self._fill = _DeadFill(self.device, masks)
+                if defer == "1":
+                    self._fill = _DeadFill(self.device, masks)
+                elif hasattr(self.defense, "rows_dead"):
+                    # the global vector the round trained from (gtrain is overwritten by the publish)
+                    self._lazy = (masks, self.trainer.dead_ranges(),
+                                  torch.empty(self.trainer.P, dtype=torch.float32, device=self.device))
+                else:
+                    self.trainer.defer_dead = False
 
         self.round_index = 0
         self.fell_back = False
@@ -227,6 +243,13 @@ class RoundEngine:
             else:
                 return None
         return masks
+
+    def materialize(self) -> None:
+        """X's dead-tap ranges written (FLR_DEFER_DEAD=2 leaves them out): call
+        before reading the client matrix outside the round's own Krum."""
+        if self._lazy is not None and self._x_stale:
+            self.trainer.fill_dead(self._lazy[2], self._num_flipped())
+            self._x_stale = False
 
     def _join_fill(self) -> None:
         """X whole on the current stream: this round's dead-tap fill launched
@@ -309,12 +332,22 @@ class RoundEngine:
             f.state, f.mark.recorded = 1, False
             self.defense.tap_dead = (f.masks, self.gtrain, self._num_flipped(), f.mark)
             self.defense.before_rows = self._join_fill
+        if self._lazy is not None:
+            masks, ranges, gprev = self._lazy
+            _capi.call("flr_copy_rows", self.gtrain.data_ptr(), self.trainer.P, self.trainer.P, gprev.data_ptr(),
+                       self.trainer.P, 1, torch.cuda.current_stream(self.device).cuda_stream)
+            nneg = self._num_flipped()
+            self._x_stale = True
+            self.defense.tap_dead = (masks, gprev, nneg)
+            self.defense.rows_dead = (ranges, gprev, nneg)
         try:
             return self._aggregate_phase()
         finally:
             self._join_fill()  # X is whole for every later reader
             if self._fill is not None:
                 self.defense.tap_dead = self.defense.before_rows = None
+            if self._lazy is not None:
+                self.defense.tap_dead = self.defense.rows_dead = None
 
     def _aggregate_phase(self) -> torch.Tensor:
         kw = {"publish": False} if hasattr(self.defense, "publish") else {}
@@ -347,6 +380,7 @@ class RoundEngine:
         RCCL errors, out of memory) loud instead."""
         from ._capi import FlrError
         self._join_fill()
+        self.materialize()
         device_error = isinstance(err, (FlrError, torch.cuda.OutOfMemoryError))
         if not self.rcfg.fallback_fedavg or (device_error and (not self.rcfg.fallback_device_errors
                                                                or self.world > 1)):

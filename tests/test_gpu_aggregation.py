@@ -394,3 +394,33 @@ def test_krum_trimmed_mean_vs_oracle(cuda, K, P):
     assert d.selected_clients == sel and d.rejected_clients == rej
     assert d.num_trimmed_per_end == t
     torch.testing.assert_close(got[0].cpu(), want[0], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("K,P,ranges,nneg,m", [
+    (12, 4096 + 13, [(64, 512), (1024, 1000), (3000, 3)], 3, 6),
+    (40, 70_001, [(1, 7), (100, 40_000), (60_000, 10_001)], 0, 17),
+    (8, 1029, [(1024, 5)], 8, 8)])
+def test_rows_mean_dead_ranges(cuda, K, P, ranges, nneg, m):
+    """flr_rows_mean_dead (FLR_DEFER_DEAD=2): the dead ranges are NaN in X and
+    come from the global vector (negated on rows < nneg) — bit-identical to
+    flr_rows_mean over the filled rows, also in the float4 groups a range
+    only partly covers and in the scalar tail; and the selected-row fill
+    (ops.fill_dead_ranges) equals the filled row."""
+    g = torch.Generator().manual_seed(K + P)
+    ld = padded_ld(P)
+    data = torch.zeros(K, ld)
+    data[:, :P] = torch.randn(K, P, generator=g)
+    gv = torch.randn(P, generator=g)
+    filled, holes = data.clone(), data.clone()
+    for o, n in ranges:
+        filled[:, o:o + n] = gv[o:o + n]
+        filled[:nneg, o:o + n] = -gv[o:o + n]
+        holes[:, o:o + n] = float("nan")
+    filled, holes, gvd = filled.to(cuda), holes.to(cuda), gv.to(cuda)
+    rows = torch.randperm(K, generator=g)[:m].to(torch.int32).to(cuda)
+    want = ops.rows_mean(filled[:, :P], rows, divisor=m + 1)
+    got = ops.rows_mean(holes[:, :P], rows, divisor=m + 1, dead=(ranges, gvd, nneg))
+    assert torch.isfinite(want).all() and torch.equal(got, want)
+    for i in (0, K - 1):
+        row = ops.fill_dead_ranges(holes[i, :P].clone(), ranges, gvd, i < nneg)
+        assert torch.equal(row, filled[i, :P])

@@ -132,6 +132,7 @@ def test_c3_trained_round_krum_indices_vs_reference_norms(cuda):
     glob = eng.global_flat.clone().cpu()
     new = eng.run_round().clone().cpu()
     eng.defense.publish()
+    eng.materialize()  # the client matrix whole (the dead-tap ranges, FLR_DEFER_DEAD)
     torch.cuda.synchronize()
     P = eng.trainer.P
     X = eng.trainer.X.data[:, :P]
@@ -256,6 +257,7 @@ def _tail_param_report(eng, spec, new, rows, glob, name="fc2.bias"):
 def _sample_rows(eng, clients, idx: torch.Tensor) -> torch.Tensor:
     """[len(clients), len(idx)] host copy of the client rows' torch-order
     coordinates idx (one row converted at a time)."""
+    eng.materialize()
     X = eng.trainer.X.data[:, : eng.trainer.P]
     di = idx.to(X.device)
     out = []
@@ -269,6 +271,7 @@ def _check_clients(eng, spec, glob, clients, batches_dev, masks_dev, negate=(), 
     """Sampled clients' rows vs the oracle loop: whole vector at 1e-5 and the
     per-tensor update report (tests/parity.py); returns the reports."""
     reps = {}
+    eng.materialize()
     for k in clients:
         j = k - eng.lo
         cb = [(im[j].cpu(), tk[j].cpu(), lb[j].cpu()) for im, tk, lb in batches_dev]

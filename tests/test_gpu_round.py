@@ -187,27 +187,31 @@ def test_native_trainer_round_equals_python_trainer(cuda, monkeypatch, order):
     assert torch.equal(ga, gb)
 
 
-@pytest.mark.parametrize("multi_k", [4, 1])
-def test_deferred_dead_taps_bit_identical(cuda, monkeypatch, multi_k):
+@pytest.mark.parametrize("defer,multi_k", [("1", 4), ("1", 1), ("2", 4), ("2", 1)])
+def test_deferred_dead_taps_bit_identical(cuda, monkeypatch, defer, multi_k):
     """FLR_DEFER_DEAD=1 (opt-in): the training phase leaves X's dead-tap slabs
     to a side-stream fill beside the reference-exact Krum distances, which
-    read those taps from the global vector meanwhile.  Against the slabs
-    written last in the training phase (FLR_DEFER_DEAD=0): the same distance
-    matrix, selection, client matrix and global model bit for bit, over 2
-    rounds of HIP-graph replay with sign-flip attackers, on the full
-    ResNet-18 + GRU model (dead taps in layers 3-4)."""
+    read those taps from the global vector meanwhile; =2: never written — the
+    distances and the Multi-Krum mean (flr_rows_mean_dead; the selected row
+    itself at multi_k = 1) read them from the round's global vector, and
+    materialize() writes them for other readers.  Against the slabs written
+    last in the training phase (FLR_DEFER_DEAD=0): the same distance matrix,
+    selection, client matrix and global model bit for bit, over 2 rounds of
+    HIP-graph replay with sign-flip attackers, on the full ResNet-18 + GRU
+    model (dead taps in layers 3-4)."""
     from flr.models.multimodal import ModelSpec
     spec = ModelSpec()
     rc = RoundConfig(num_clients=8, batch=4, defense="krum", attack="sign_flip", num_attackers=1,
                      defense_cfg={"pairwise_method": "reference", "multi_k": multi_k})
     res = []
-    for defer in ("0", "1"):
-        monkeypatch.setenv("FLR_DEFER_DEAD", defer)
+    for d in ("0", defer):
+        monkeypatch.setenv("FLR_DEFER_DEAD", d)
         eng = RoundEngine(spec, rc, TrainConfig(local_steps=2), cuda)
-        assert eng.train_order and (eng._fill is not None) == (defer == "1")
+        assert eng.train_order and (eng._fill is not None) == (d == "1") and (eng._lazy is not None) == (d == "2")
         for _ in range(2):
             eng.run_round()
         eng.defense.publish()
+        eng.materialize()
         res.append((eng.global_flat.clone().cpu(), eng.defense.distances.clone().cpu(),
                     list(eng.defense.selected_clients), eng.trainer.X.X.clone().cpu()))
     (ga, da, sa, xa), (gb, db, sb, xb) = res

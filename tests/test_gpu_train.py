@@ -314,6 +314,7 @@ def test_c3_round_multikrum_signflip(cuda):
     glob = eng.global_flat.clone().cpu()
     eng.run_round()
     eng.defense.publish()
+    eng.materialize()  # the client matrix whole (the dead-tap ranges, FLR_DEFER_DEAD)
     X = eng.trainer.X.data[:, : eng.trainer.P]
     batches = synthetic_batches(spec, steps, [0, 24, 25, 127], B, "cpu")
     masks = make_dropout_masks(spec, steps, [0, 24, 25, 127], B, "cpu", seed=rc.seed + 7919)
