@@ -103,6 +103,10 @@ class KrumDefense(BaseDefense):
     def order_free(self) -> bool:
         return True
 
+    # the round engine may leave X's dead-tap ranges unwritten (FLR_DEFER_DEAD):
+    # this defense reads them through tap_dead / rows_dead / before_rows
+    supports_dead_rows = True
+
     @property
     def needs_tap_blocks(self) -> bool:
         """A training-order client matrix needs tap_blocks set (reference mode)."""
@@ -207,6 +211,9 @@ class KrumTrimmedMeanDefense(KrumDefense):
         super().__init__(defense_config)
         self.trim_ratio = defense_config.get("trim_ratio", 0.1)
         self.num_trimmed_per_end = 0
+
+    # the trimmed mean reads the selected rows whole: no dead-tap deferral
+    supports_dead_rows = False
 
     def _combine(self, X: torch.Tensor, order: torch.Tensor) -> torch.Tensor:
         m = min(self.multi_k, X.shape[0])

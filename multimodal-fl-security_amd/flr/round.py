@@ -176,18 +176,17 @@ class RoundEngine:
         self._x_stale = False
         defer = os.environ.get("FLR_DEFER_DEAD", "2")
         if (self.train_order and world == 1 and self.defense.__dict__.get("tap_blocks")
+                and getattr(self.defense, "supports_dead_rows", False)
                 and hasattr(self.trainer, "fill_dead") and defer in ("1", "2")):
             masks = self._dead_masks(self.defense.tap_blocks)
             if masks is not None and any(masks):
                 self.trainer.defer_dead = True
                 if defer == "1":
                     self._fill = _DeadFill(self.device, masks)
-                elif hasattr(self.defense, "rows_dead"):
+                else:
                     # the global vector the round trained from (gtrain is overwritten by the publish)
                     self._lazy = (masks, self.trainer.dead_ranges(),
                                   torch.empty(self.trainer.P, dtype=torch.float32, device=self.device))
-                else:
-                    self.trainer.defer_dead = False
 
         self.round_index = 0
         self.fell_back = False

@@ -219,3 +219,28 @@ def test_deferred_dead_taps_bit_identical(cuda, monkeypatch, defer, multi_k):
     assert torch.equal(da, db) and sa == sb
     assert torch.equal(xa, xb)
     assert torch.equal(ga, gb)
+
+
+def test_dead_deferral_only_where_the_defense_reads_it(cuda, monkeypatch):
+    """The dead-tap deferral (FLR_DEFER_DEAD=2, default) is on only for a
+    defense that reads the unwritten ranges through the global vector (Krum /
+    Multi-Krum, `supports_dead_rows`); Krum + trimmed mean reads the selected
+    rows whole, so its rounds keep the slabs written — the same global model
+    as with the deferral switched off."""
+    from flr.models.multimodal import ModelSpec
+    spec = ModelSpec()
+    monkeypatch.delenv("FLR_DEFER_DEAD", raising=False)
+    kw = dict(num_clients=8, batch=4, attack="sign_flip", num_attackers=1)
+    eng = RoundEngine(spec, RoundConfig(defense="krum", defense_cfg={"multi_k": 4}, **kw),
+                      TrainConfig(local_steps=1), cuda)
+    assert eng._lazy is not None and eng.trainer.defer_dead
+    outs = []
+    for d in (None, "0"):
+        if d is not None:
+            monkeypatch.setenv("FLR_DEFER_DEAD", d)
+        eng = RoundEngine(spec, RoundConfig(defense="krum_trimmed_mean", defense_cfg={"multi_k": 6,
+                                                                                       "trim_ratio": 0.2}, **kw),
+                          TrainConfig(local_steps=1), cuda)
+        assert eng.train_order and eng._lazy is None and eng._fill is None and not eng.trainer.defer_dead
+        outs.append(eng.run_round().clone().cpu())
+    assert torch.isfinite(outs[0]).all() and torch.equal(outs[0], outs[1])
