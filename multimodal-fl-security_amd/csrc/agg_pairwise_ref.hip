@@ -50,6 +50,7 @@ namespace flr {
 namespace pwref {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int IW = 4;              // I rows per wave: its 16-lane DPP rows
 constexpr int JW = 16;             // J rows per wave: the lanes of a DPP row
@@ -707,6 +708,459 @@ inline bool use_two_chains(int64_t K) {
   return e && e[0] == '1' && K > SB;
 }
 
+// K >= 480 (every pair, no tap-major blocks): the throughput form.  Measured
+// on gfx950 (tools/hip/pk_rate.hip, profiles/r6_ref/pk_rate.json): at two waves
+// per SIMD a plain v_fmac_f32 costs the SIMD 2.3 cycles, a v_sub_f32_dpp about
+// 6.6, and packed f32 ops no fewer cycles per element than plain ones; so once
+// there are two waves per SIMD to run, the cheapest chain step is a plain
+// v_sub_f32 with x_i as an SGPR operand and a plain v_fmac_f32 — 2 SIMD issue
+// slots of 2.3 cycles.  A wave holds 8 I rows (wave-uniform, scalar loads) x 64
+// J rows (one per lane): 8 chains per lane, each x_j element serves 8 chain
+// steps, so the chip's L2 traffic stays at 0.56 B per chain step.
+// Operand layout (per segment, quad_transpose_kernel): Xq[c][b][k][e] =
+// X[k][8 (r0 + 4 b + e) + c] — per chain c and 4-step block b, the Kp rows'
+// 16-B pieces contiguous: lane j's x_j is one coalesced 1-KB load per wave,
+// the 8 I rows' block 128 contiguous bytes (two s_load_dwordx16).
+constexpr int QJ = 64;   // J rows per wave (lanes)
+constexpr int QTB = 16;  // transpose tile: rows x 4-step blocks
+constexpr int QD = 8;    // x_j blocks in flight per lane
+static_assert(XC_GROUP % (4 * QTB) == 0 && XC_GROUP % (4 * QD) == 0, "padded segments hold whole tiles / trips");
+__host__ __device__ inline int64_t quad_rows(int64_t K) { return (K + QJ - 1) / QJ * QJ; }
+// tiles of J block q (rows 64 q .. 64 q + 63): I blocks of ni rows a = 0 ..
+// min(64 / ni (q + 1), ceil(K / ni)) - 1
+__host__ __device__ inline int quad_ni(int q, int K, int ni) {
+  const int a = QJ / ni * (q + 1), b = (K + ni - 1) / ni;
+  return a < b ? a : b;
+}
+// bytes past a segment's last block the x_j / x_i prefetches may read
+inline int64_t quad_slack(int64_t K) { return (QD + 4) * quad_rows(K) * 16; }
+inline int quad_ntiles(int K, int ni) {
+  int n = 0;
+  for (int q = 0; q * QJ < K; ++q) n += quad_ni(q, K, ni);
+  return n;
+}
+
+// Xq tile: rows k0 .. k0 + 15 x blocks b0 .. b0 + 15 (64 steps = 512 coordinates
+// = 2 KB of each row): coalesced 1-KB row reads into LDS, then thread (k, block)
+// takes its row's 32 coordinates of the block and stores 8 chain pieces (16 B:
+// 4 steps each), 256-B runs of consecutive rows.  Steps past `steps` are 0.
+__global__ __launch_bounds__(256) void quad_transpose_kernel(const float* __restrict__ X, int64_t ldx, int K,
+                                                             int64_t r0, int64_t steps, int64_t NB, int64_t Kp,
+                                                             float* __restrict__ Xq) {
+  __shared__ f32x4 t[QTB][QTB * 8 + 1];
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * QTB;
+  const int k0 = blockIdx.y * QTB;
+  const int64_t u0 = 8 * (r0 + 4 * b0), uend = 8 * (r0 + steps);  // this tile's first coordinate, the segment's end
+  f32x4 v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int idx = q * 256 + tid, row = idx >> 7, p = idx & 127;
+    const int64_t u = u0 + 4 * p;
+    v[q] = (k0 + row < K && u < uend)
+               ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(X + (int64_t)(k0 + row) * ldx + u))
+               : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int idx = q * 256 + tid;
+    t[idx >> 7][idx & 127] = v[q];
+  }
+  __syncthreads();
+  const int k = tid & 15, bl = tid >> 4;
+  if (k0 + k >= K) return;  // rows past K: never a valid pair's operand
+  f32x4 w[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) w[q] = t[k][8 * bl + q];
+  // coordinate 32 bl + 4 q + m = 8 (4 bl + e) + c: step e = q / 2, chain c = 4 (q % 2) + m
+  float* out = Xq + ((b0 + bl) * Kp + k0 + k) * 4;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int h = c >> 2, m = c & 3;
+    *reinterpret_cast<f32x4*>(out + (int64_t)c * NB * Kp * 4) = f32x4{w[h][m], w[2 + h][m], w[4 + h][m], w[6 + h][m]};
+  }
+}
+
+// One wave: chain c = blockIdx % 8 (the XCD) of tile blockIdx / 8 — J block q,
+// I block a: lane l's pairs (NI a + r, 64 q + l), r < NI, valid where i < j < K.
+// x_j: one 16-B load per lane and 4-step block, QD blocks in flight (vmcnt, in
+// order).  x_i: NI rows x 4 steps x BT blocks per scalar round trip (NI BT / 4
+// s_load_dwordx16 into one of two SGPR buffers).  Scalar loads return out of
+// order, so a wait for one buffer waits for every scalar load issued: the next
+// buffer's loads go out right AFTER the wait for the current one, and the
+// latency they can hide is one buffer's compute, 2 NI 4 BT VALU — the reason for
+// BT > 1 at NI = 4 (measured: NI = 8, BT = 1 stalled ~650 cycles per buffer,
+// profiles/r6_ref/).  Per step the NI chains d = fl(x_i - x_j),
+// acc = fma(d, d, acc): the reference's operations in its order.
+// one step of the NI chains: plain v_sub_f32 (x_i an SGPR operand) and
+// v_fmac_f32, each square one slot behind its difference (inline asm: the
+// compiler otherwise SLP-packs the rows into v_pk_* ops whose SGPR pairs cost an
+// s_mov per operand).  g0: rows 0-3 of the block (row r's step e at 4 r + e), g1:
+// rows 4-7
+template <int E>
+__device__ __forceinline__ void sgpr_step(float (&acc)[4], const i32x16& g0, const i32x16&, float xjv) {
+  float t0, t1;
+  asm volatile(
+      "v_sub_f32 %[t0], %[s0], %[x]\n\t"
+      "v_sub_f32 %[t1], %[s1], %[x]\n\t"
+      "v_fmac_f32 %[a0], %[t0], %[t0]\n\t"
+      "v_sub_f32 %[t0], %[s2], %[x]\n\t"
+      "v_fmac_f32 %[a1], %[t1], %[t1]\n\t"
+      "v_sub_f32 %[t1], %[s3], %[x]\n\t"
+      "v_fmac_f32 %[a2], %[t0], %[t0]\n\t"
+      "v_fmac_f32 %[a3], %[t1], %[t1]\n\t"
+      : [a0] "+v"(acc[0]), [a1] "+v"(acc[1]), [a2] "+v"(acc[2]), [a3] "+v"(acc[3]), [t0] "=&v"(t0), [t1] "=&v"(t1)
+      : [s0] "s"(g0[E]), [s1] "s"(g0[4 + E]), [s2] "s"(g0[8 + E]), [s3] "s"(g0[12 + E]), [x] "v"(xjv));
+}
+template <int E>
+__device__ __forceinline__ void sgpr_step(float (&acc)[8], const i32x16& g0, const i32x16& g1, float xjv) {
+  float t0, t1;
+  asm volatile(
+      "v_sub_f32 %[t0], %[s0], %[x]\n\t"
+      "v_sub_f32 %[t1], %[s1], %[x]\n\t"
+      "v_fmac_f32 %[a0], %[t0], %[t0]\n\t"
+      "v_sub_f32 %[t0], %[s2], %[x]\n\t"
+      "v_fmac_f32 %[a1], %[t1], %[t1]\n\t"
+      "v_sub_f32 %[t1], %[s3], %[x]\n\t"
+      "v_fmac_f32 %[a2], %[t0], %[t0]\n\t"
+      "v_sub_f32 %[t0], %[s4], %[x]\n\t"
+      "v_fmac_f32 %[a3], %[t1], %[t1]\n\t"
+      "v_sub_f32 %[t1], %[s5], %[x]\n\t"
+      "v_fmac_f32 %[a4], %[t0], %[t0]\n\t"
+      "v_sub_f32 %[t0], %[s6], %[x]\n\t"
+      "v_fmac_f32 %[a5], %[t1], %[t1]\n\t"
+      "v_sub_f32 %[t1], %[s7], %[x]\n\t"
+      "v_fmac_f32 %[a6], %[t0], %[t0]\n\t"
+      "v_fmac_f32 %[a7], %[t1], %[t1]\n\t"
+      : [a0] "+v"(acc[0]), [a1] "+v"(acc[1]), [a2] "+v"(acc[2]), [a3] "+v"(acc[3]), [a4] "+v"(acc[4]),
+        [a5] "+v"(acc[5]), [a6] "+v"(acc[6]), [a7] "+v"(acc[7]), [t0] "=&v"(t0), [t1] "=&v"(t1)
+      : [s0] "s"(g0[E]), [s1] "s"(g0[4 + E]), [s2] "s"(g0[8 + E]), [s3] "s"(g0[12 + E]), [s4] "s"(g1[E]),
+        [s5] "s"(g1[4 + E]), [s6] "s"(g1[8 + E]), [s7] "s"(g1[12 + E]), [x] "v"(xjv));
+}
+
+// FLR_REF_S_ABL (tools build, timing only, wrong results): 1 no x_j loads in the
+// loop, 2 no x_i loads, 3 no chain arithmetic, 4 x_i loaded but never waited for
+#ifndef FLR_REF_S_ABL
+#define FLR_REF_S_ABL 0
+#endif
+template <int NI, int BT>
+__global__ __launch_bounds__(64) void ref_chain_s_kernel(const float* __restrict__ Xq, int64_t NB, int64_t Kp, int K,
+                                                         int first, float* __restrict__ A) {
+  static_assert(NI == 4 || NI == 8, "the step forms above");
+  constexpr int NL = NI * BT / 4;  // s_load_dwordx16 per buffer
+  static_assert(QD % (2 * BT) == 0, "whole ping-pong pairs of buffers per trip");
+  const int c = (int)(blockIdx.x & 7), lane = threadIdx.x;
+  int t = (int)(blockIdx.x >> 3), q = 0;
+  for (int n = quad_ni(0, K, NI); t >= n; n = quad_ni(q, K, NI)) {
+    t -= n;
+    ++q;
+  }
+  const int i0 = NI * t, j = QJ * q + lane;
+  const float* __restrict__ base = Xq + (int64_t)c * NB * Kp * 4;
+  float acc[NI];
+  if (first) {
+#pragma unroll
+    for (int r = 0; r < NI; ++r) acc[r] = 0.f;
+  } else {  // asm loads and a full wait: no compiler-tracked load reaches into the loop
+#pragma unroll
+    for (int r = 0; r < NI; ++r) {
+      const float* ap = A + ((int64_t)c * K + i0 + r) * K + (j < K ? j : K - 1);
+      asm volatile("global_load_dword %0, %1, off" : "=v"(acc[r]) : "v"(ap) : "memory");
+    }
+    // the wait ties the loaded values: nothing reads them above it
+    if constexpr (NI == 4)
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]) : : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)"
+                   : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
+                     "+v"(acc[6]), "+v"(acc[7])
+                   :
+                   : "memory");
+#pragma unroll
+    for (int r = 0; r < NI; ++r) acc[r] = (i0 + r < j && j < K) ? acc[r] : 0.f;
+  }
+  // uniform block pointers advanced per block (the prefetches run up to QD
+  // blocks past the segment's last: the workspace's quad slack) and the lane's
+  // 32-bit byte offset (the saddr load form)
+  const int64_t bb = Kp * 16;  // bytes per block
+  const uint32_t voff = (uint32_t)j * 16;
+  const char* pjn = reinterpret_cast<const char*>(base);                      // the next x_j block to load
+  const char* pin = reinterpret_cast<const char*>(base) + (int64_t)i0 * 16;  // the next x_i buffer
+  auto ldj = [&](f32x4& x) {
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x) : "v"(voff), "s"(pjn) : "memory");
+    pjn += bb;
+    asm volatile("" : "+s"(pjn));  // one running pointer, not QD precomputed ones
+  };
+  // buffer: block u's 4-row groups at buf[u NI / 4 ..]
+  auto ldi = [&](i32x16(&buf)[NL]) {
+    const char* pu = pin;
+#pragma unroll
+    for (int u = 0; u < BT; ++u) {
+#pragma unroll
+      for (int h = 0; h < NI / 4; ++h)
+        asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(buf[u * (NI / 4) + h]) : "s"(pu), "n"(64 * h) : "memory");
+      pu += bb;
+      asm volatile("" : "+s"(pu));
+    }
+    pin = pu;
+  };
+  f32x4 xj[QD];
+  i32x16 xa[NL], xb[NL];
+#pragma unroll
+  for (int u = 0; u < QD; ++u) ldj(xj[u]);
+  ldi(xa);
+  // a buffer's BT blocks: x_i(buffer) landed, then the next buffer issued;
+  // per block x_j(b) landed, its 4 steps, x_j(b + QD) issued into the freed registers
+  auto trip = [&](auto U0, const i32x16(&cur)[NL], i32x16(&nxt)[NL]) {
+    constexpr int u0 = decltype(U0)::value;
+    if (FLR_REF_S_ABL != 2 && FLR_REF_S_ABL != 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (FLR_REF_S_ABL != 2) ldi(nxt);
+#pragma unroll
+    for (int v = 0; v < BT; ++v) {
+      f32x4& x = xj[u0 + v];
+      if (FLR_REF_S_ABL != 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QD - 1) : "memory");
+      asm volatile("" : "+v"(x));  // x arrived at the wait above
+      const i32x16& g0 = cur[v * (NI / 4)];
+      const i32x16& g1 = cur[v * (NI / 4) + (NI / 4) - 1];
+      if (FLR_REF_S_ABL != 3) {
+        sgpr_step<0>(acc, g0, g1, x[0]);
+        sgpr_step<1>(acc, g0, g1, x[1]);
+        sgpr_step<2>(acc, g0, g1, x[2]);
+        sgpr_step<3>(acc, g0, g1, x[3]);
+      }
+      if (FLR_REF_S_ABL != 1) ldj(x);
+    }
+  };
+  for (int64_t b0 = 0; b0 < NB; b0 += QD)
+    static_for(
+        [&](auto P) {
+          constexpr int p = decltype(P)::value;
+          trip(std::integral_constant<int, 2 * BT * p>{}, xa, xb);
+          trip(std::integral_constant<int, 2 * BT * p + BT>{}, xb, xa);
+        },
+        std::make_integer_sequence<int, QD / (2 * BT)>{});
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int r = 0; r < NI; ++r) {
+    const int i = i0 + r;
+    if (i < j && j < K) A[((int64_t)c * K + i) * K + j] = acc[r];
+  }
+}
+
+// The workgroup form (default for the throughput path): 4 waves = 4 I blocks
+// (32 rows) of one J block share its x_j through LDS.  Measured, the one-wave
+// form above is bound by its x_j stream, not its arithmetic (without any chain
+// arithmetic it ran 21.5 of 22.1 ms at K = 512, P = 2M, profiles/r6_sgpr/): its
+// waves drift apart, the L2 no longer serves one J block to the many waves that
+// read it, and the chip streams ~7.7 TB/s.  Here a 4-wave workgroup stages each
+// chunk of WCB blocks of its J rows (WCB KB) once by LDS-DMA into a ring of WNS
+// stages — one barrier per chunk keeps its waves together — and each lane reads
+// its row's 16-B piece per block with ds_read_b128 (1 KB per wave: ~4 LDS cycles
+// per 64 VALU).  x_i as above (SGPR operands, one block ahead).
+constexpr int WCB = 8;  // 4-step blocks per staged chunk (WCB KB: one 1-KB DMA per block)
+constexpr int WNS = 4;  // ring stages
+static_assert(WCB % 8 == 0 && (XC_GROUP / 4) % WCB == 0, "two DMAs per wave per chunk; whole chunks per segment");
+__host__ __device__ inline int wg_groups(int q, int K) { return (quad_ni(q, K, 8) + 3) / 4; }
+inline int wg_ntiles(int K) {
+  int n = 0;
+  for (int q = 0; q * QJ < K; ++q) n += wg_groups(q, K);
+  return n;
+}
+// the step with x_i in VGPRs (XL: every lane holds the same value, read from LDS)
+template <int E>
+__device__ __forceinline__ void vgpr_step(float (&acc)[8], const f32x4 (&xi)[8], float xjv) {
+  float t0, t1;
+  asm volatile(
+      "v_sub_f32 %[t0], %[s0], %[x]\n\t"
+      "v_sub_f32 %[t1], %[s1], %[x]\n\t"
+      "v_fmac_f32 %[a0], %[t0], %[t0]\n\t"
+      "v_sub_f32 %[t0], %[s2], %[x]\n\t"
+      "v_fmac_f32 %[a1], %[t1], %[t1]\n\t"
+      "v_sub_f32 %[t1], %[s3], %[x]\n\t"
+      "v_fmac_f32 %[a2], %[t0], %[t0]\n\t"
+      "v_sub_f32 %[t0], %[s4], %[x]\n\t"
+      "v_fmac_f32 %[a3], %[t1], %[t1]\n\t"
+      "v_sub_f32 %[t1], %[s5], %[x]\n\t"
+      "v_fmac_f32 %[a4], %[t0], %[t0]\n\t"
+      "v_sub_f32 %[t0], %[s6], %[x]\n\t"
+      "v_fmac_f32 %[a5], %[t1], %[t1]\n\t"
+      "v_sub_f32 %[t1], %[s7], %[x]\n\t"
+      "v_fmac_f32 %[a6], %[t0], %[t0]\n\t"
+      "v_fmac_f32 %[a7], %[t1], %[t1]\n\t"
+      : [a0] "+v"(acc[0]), [a1] "+v"(acc[1]), [a2] "+v"(acc[2]), [a3] "+v"(acc[3]), [a4] "+v"(acc[4]),
+        [a5] "+v"(acc[5]), [a6] "+v"(acc[6]), [a7] "+v"(acc[7]), [t0] "=&v"(t0), [t1] "=&v"(t1)
+      : [s0] "v"(xi[0][E]), [s1] "v"(xi[1][E]), [s2] "v"(xi[2][E]), [s3] "v"(xi[3][E]), [s4] "v"(xi[4][E]),
+        [s5] "v"(xi[5][E]), [s6] "v"(xi[6][E]), [s7] "v"(xi[7][E]), [x] "v"(xjv));
+}
+
+// XL: x_i staged through LDS too (the group's 32 I rows, 512 B per block) and
+// read as broadcast ds_read_b128 into VGPR operands — no scalar loads (their
+// round trip, ~600 cycles under load, bounded the SGPR form: one block's
+// compute is all a scalar prefetch can hide, as they complete out of order)
+template <bool XL>
+__global__ __launch_bounds__(256, 3) void ref_chain_w_kernel(const float* __restrict__ Xq, int64_t NB, int64_t Kp,
+                                                             int K, int first, float* __restrict__ A) {
+  constexpr int SJ = WCB * QJ * 16;              // x_j bytes per stage
+  constexpr int SI = XL ? WCB * 32 * 16 : 0;     // x_i bytes per stage
+  constexpr int NDMA = XL ? 3 : 2;               // DMA instructions per wave per chunk
+  __shared__ __attribute__((aligned(16))) float xs[WNS * (SJ + SI) / 4];  // [stage]{[block][row][4] x_j, x_i}
+  const int c = (int)(blockIdx.x & 7), lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform (SGPR operands)
+  int t = (int)(blockIdx.x >> 3), q = 0;
+  for (int n = wg_groups(0, K); t >= n; n = wg_groups(q, K)) {
+    t -= n;
+    ++q;
+  }
+  // this wave's I block; past the J block's last one (a ragged group) the wave
+  // still stages and meets every barrier, and stores nothing
+  const int a = 4 * t + wave, na = quad_ni(q, K, 8);
+  const bool live = a < na;
+  const int i0 = 8 * (live ? a : na - 1), j = QJ * q + lane;
+  const float* __restrict__ base = Xq + (int64_t)c * NB * Kp * 4;
+  float acc[8];
+  if (first || !live) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = 0.f;
+  } else {  // asm loads and a full wait: no compiler-tracked load reaches into the loop
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float* ap = A + ((int64_t)c * K + i0 + r) * K + (j < K ? j : K - 1);
+      asm volatile("global_load_dword %0, %1, off" : "=v"(acc[r]) : "v"(ap) : "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
+                   "+v"(acc[7])
+                 :
+                 : "memory");
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = (i0 + r < j && j < K) ? acc[r] : 0.f;
+  }
+  const int64_t bb = Kp * 16;   // bytes per block
+  const int64_t nch = NB / WCB;  // chunks in the segment
+  // staging: wave w moves x_j blocks 2w, 2w + 1 of a chunk (the J block's 64
+  // rows, 1 KB contiguous each) and (XL) the x_i of the same two blocks (the
+  // group's 32 rows, 512 B each: lanes 0-31 block 2w, 32-63 block 2w + 1)
+  const char* jsrc = reinterpret_cast<const char*>(base) + (int64_t)(QJ * q) * 16;
+  const char* isrc = reinterpret_cast<const char*>(base) + (int64_t)(32 * t) * 16;
+  const uint32_t vj = (uint32_t)lane * 16;
+  const uint32_t vi = (uint32_t)(((lane >> 5) * Kp + (lane & 31)) * 16);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)xs;
+  auto dma = [&](int64_t ch) {
+    const int64_t cc = ch < nch ? ch : nch - 1;  // past the last chunk: the last again (nothing reads it)
+    const uint32_t sb = lds0 + (uint32_t)((int)(ch % WNS) * (SJ + SI));
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int blk = 2 * wave + v;
+      const char* src = jsrc + (cc * WCB + blk) * bb;
+      const uint32_t m = sb + (uint32_t)(blk * QJ * 16);
+      // M0 written in the statement that reads it; nothing else in the kernel reads M0
+      asm volatile("s_mov_b32 m0, %[m]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[v], %[s] offset:0"
+                   :
+                   : [m] "s"(m), [v] "v"(vj), [s] "s"(src)
+                   : "memory");
+    }
+    if constexpr (XL) {
+      const char* src = isrc + (cc * WCB + 2 * wave) * bb;
+      const uint32_t m = sb + SJ + (uint32_t)(2 * wave * 32 * 16);
+      asm volatile("s_mov_b32 m0, %[m]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[v], %[s] offset:0"
+                   :
+                   : [m] "s"(m), [v] "v"(vi), [s] "s"(src)
+                   : "memory");
+    }
+  };
+  const char* pin = reinterpret_cast<const char*>(base) + (int64_t)i0 * 16;  // the next x_i block (SGPR form)
+  auto ldi = [&](i32x16& lo, i32x16& hi) {
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40" : "=s"(lo), "=s"(hi) : "s"(pin) : "memory");
+    pin += bb;
+    asm volatile("" : "+s"(pin));
+  };
+  auto rdj = [&](f32x4& x, uint32_t addr, auto U) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x) : "v"(addr), "n"(decltype(U)::value * QJ * 16) : "memory");
+  };
+  // XL: row r of this wave's 8 at byte 16 (32 u + 8 wave + r) of the stage's x_i
+  // (the same address in every lane: a broadcast)
+  auto rdi = [&](f32x4(&x)[8], uint32_t addr, auto U) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      asm volatile("ds_read_b128 %0, %1 offset:%2"
+                   : "=v"(x[r])
+                   : "v"(addr), "n"(SJ + decltype(U)::value * 32 * 16 + 16 * r)
+                   : "memory");
+  };
+  i32x16 al, ah, bl, bh;
+  f32x4 j0, j1, ia[8], ib[8];
+#pragma unroll
+  for (int p = 0; p < WNS - 1; ++p) dma(p);
+  if constexpr (!XL) ldi(al, ah);
+  // block u of chunk ch: x_i(b) and x_j(b) landed; x_i(b + 1) issued (the SGPR
+  // form: always; XL: inside the chunk, like x_j(b + 1)); the block's 4 steps
+  auto body = [&](auto U, uint32_t sbase, uint32_t ibase, f32x4& xc, f32x4& xn, const i32x16& cl,
+                  const i32x16& ch_, i32x16& nl, i32x16& nh, f32x4(&ic)[8], f32x4(&in)[8]) {
+    constexpr int u = decltype(U)::value;
+    if constexpr (XL) {
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(xc), "+v"(ic[0]), "+v"(ic[1]), "+v"(ic[2]), "+v"(ic[3]), "+v"(ic[4]), "+v"(ic[5]),
+                     "+v"(ic[6]), "+v"(ic[7])
+                   :
+                   : "memory");
+      if constexpr (u + 1 < WCB) {
+        rdj(xn, sbase, std::integral_constant<int, u + 1>{});
+        rdi(in, ibase, std::integral_constant<int, u + 1>{});
+      }
+      vgpr_step<0>(acc, ic, xc[0]);
+      vgpr_step<1>(acc, ic, xc[1]);
+      vgpr_step<2>(acc, ic, xc[2]);
+      vgpr_step<3>(acc, ic, xc[3]);
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xc) : : "memory");
+      ldi(nl, nh);
+      if constexpr (u + 1 < WCB) rdj(xn, sbase, std::integral_constant<int, u + 1>{});
+      sgpr_step<0>(acc, cl, ch_, xc[0]);
+      sgpr_step<1>(acc, cl, ch_, xc[1]);
+      sgpr_step<2>(acc, cl, ch_, xc[2]);
+      sgpr_step<3>(acc, cl, ch_, xc[3]);
+    }
+  };
+  static_assert(WCB % 2 == 0, "x_i / x_j ping-pong");
+  for (int64_t ch = 0; ch < nch; ++ch) {
+    // this wave's DMAs of chunk ch landed (the younger ones: chunks ch + 1 ..
+    // ch + WNS - 2), then every wave's (the barrier), which also marks every
+    // wave done with chunk ch - 1, whose stage the next DMA refills
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NDMA * (WNS - 2)) : "memory");
+    dma(ch + WNS - 1);
+    const uint32_t st = lds0 + (uint32_t)((int)(ch % WNS) * (SJ + SI));
+    const uint32_t sbase = st + vj;
+    const uint32_t ibase = st + (uint32_t)(wave * 8 * 16);  // uniform: a broadcast address
+    rdj(j0, sbase, std::integral_constant<int, 0>{});
+    if constexpr (XL) rdi(ia, ibase, std::integral_constant<int, 0>{});
+    static_for(
+        [&](auto P) {
+          constexpr int p = decltype(P)::value;
+          body(std::integral_constant<int, 2 * p>{}, sbase, ibase, j0, j1, al, ah, bl, bh, ia, ib);
+          body(std::integral_constant<int, 2 * p + 1>{}, sbase, ibase, j1, j0, bl, bh, al, ah, ib, ia);
+        },
+        std::make_integer_sequence<int, WCB / 2>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (live) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = i0 + r;
+      if (i < j && j < K) A[((int64_t)c * K + i) * K + j] = acc[r];
+    }
+  }
+}
+
+// the throughput form: every pair in one call, no tap-major blocks, K >= 480
+// (at least two waves per SIMD); FLR_REF_SGPR=0 off, =1 from K > 64
+inline bool use_quad(int64_t K, int64_t ntaps, bool all_tiles) {
+  if (!all_tiles || ntaps > 0 || K <= QJ) return false;
+  const char* e = flr::knob("FLR_REF_SGPR");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return K >= 480;
+}
+
 // D[i][j] = D[j][i] for the pairs of tiles [t0, t1): chains summed 0..7 in
 // order, the tail, correctly rounded sqrt; the other pairs 0 (the ranks' parts
 // are then summed: exactly one rank holds each pair), the diagonal 0.
@@ -769,10 +1223,11 @@ extern "C" size_t flr_pairwise_l2_reference_workspace(int64_t K, int64_t P) {
   size_t n = a_bytes(K);
   if (K < 2 || R == 0) return n;
   const int64_t Rc = (R + XC_GROUP - 1) / XC_GROUP * XC_GROUP;
-  const int64_t per_step = K * 8 * 4;
+  // the throughput form's segments hold K rounded up to 64 rows (use_quad)
+  const int64_t per_step = (K > QJ ? quad_rows(K) : K) * 8 * 4;
   const int64_t nseg = (per_step * Rc + XC_CAP - 1) / XC_CAP;
   const int64_t Rs = ((R + nseg - 1) / nseg + XC_GROUP - 1) / XC_GROUP * XC_GROUP;
-  return n + (size_t)(per_step * Rs + XC_SLACK);
+  return n + (size_t)(per_step * Rs + XC_SLACK + (K > QJ ? quad_slack(K) : 0));
 }
 
 extern "C" int flr_pairwise_l2_reference_tiles(int64_t K) {
@@ -826,8 +1281,48 @@ static int run_chains(const float* X, int64_t K, int64_t steps_total, int64_t ld
   const size_t na = a_bytes(K);
   if (ws_bytes < na) return FLR_ERR_WORKSPACE;
   const int64_t R = steps_total;
-  const int64_t per_step = K * 8 * 4;
   if (ws_bytes < na + (size_t)XC_SLACK) return FLR_ERR_WORKSPACE;
+  if (use_quad(K, ntaps, t0 == 0 && t1 == ntiles_of((int)K))) {  // the throughput form (Xq segments)
+    const int64_t Kp = quad_rows(K), qstep = Kp * 8 * 4;
+    const char* rows_knob = flr::knob("FLR_REF_SGPR_ROWS");  // 4 (default) or 8 I rows per wave
+    const bool eight = rows_knob && rows_knob[0] == '8';
+    const char* form_knob = flr::knob("FLR_REF_SGPR_FORM");  // "wave": the one-wave forms (A/B)
+    const bool wg = !(form_knob && form_knob[0] == 'w' && form_knob[1] == 'a');
+    const bool xl = !(form_knob && form_knob[0] == 's');  // "sgpr": the workgroup form with scalar x_i
+    if (ws_bytes < na + (size_t)(XC_SLACK + quad_slack(K))) return FLR_ERR_WORKSPACE;
+    const int64_t cap =
+        (int64_t)((ws_bytes - na - XC_SLACK - quad_slack(K)) / (size_t)qstep) / XC_GROUP * XC_GROUP;
+    if (cap < XC_GROUP) return FLR_ERR_WORKSPACE;
+    const int64_t nseg = (R + cap - 1) / cap;
+    const int64_t Rs = ((R + nseg - 1) / nseg + XC_GROUP - 1) / XC_GROUP * XC_GROUP;  // <= cap
+    float* Xq = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + na);
+    for (int64_t seg = 0; seg < nseg; ++seg) {
+      const int64_t r0 = seg * Rs, steps = (R - r0 < Rs) ? R - r0 : Rs;
+      if (steps <= 0) break;
+      const int64_t NB = (steps + XC_GROUP - 1) / XC_GROUP * XC_GROUP / 4;
+      hipLaunchKernelGGL(quad_transpose_kernel, dim3((unsigned)(NB / QTB), (unsigned)((K + QTB - 1) / QTB)), dim3(256),
+                         0, st, X, ldx, (int)K, r0, steps, NB, Kp, Xq);
+      int rc = launch_status("quad_transpose_kernel");
+      if (rc != FLR_OK) return rc;
+      if (after_rewrite && seg == nseg - 1 && hipEventRecord(after_rewrite, st) != hipSuccess) return FLR_ERR_HIP;
+      const int fst = (first && seg == 0) ? 1 : 0;
+      if (wg && xl)
+        hipLaunchKernelGGL(ref_chain_w_kernel<true>, dim3((unsigned)(8 * wg_ntiles((int)K))), dim3(256), 0, st, Xq, NB,
+                           Kp, (int)K, fst, A);
+      else if (wg)
+        hipLaunchKernelGGL(ref_chain_w_kernel<false>, dim3((unsigned)(8 * wg_ntiles((int)K))), dim3(256), 0, st, Xq,
+                           NB, Kp, (int)K, fst, A);
+      else if (eight)
+        hipLaunchKernelGGL((ref_chain_s_kernel<8, 1>), dim3((unsigned)(8 * quad_ntiles((int)K, 8))), dim3(64), 0, st,
+                           Xq, NB, Kp, (int)K, fst, A);
+      else
+        hipLaunchKernelGGL((ref_chain_s_kernel<4, 2>), dim3((unsigned)(8 * quad_ntiles((int)K, 4))), dim3(64), 0, st,
+                           Xq, NB, Kp, (int)K, fst, A);
+      if ((rc = launch_status("ref_chain_s_kernel")) != FLR_OK) return rc;
+    }
+    return FLR_OK;
+  }
+  const int64_t per_step = K * 8 * 4;
   const int64_t ldc = (int64_t)((ws_bytes - na - XC_SLACK) / (size_t)per_step) / XC_GROUP * XC_GROUP;
   if (ldc < XC_GROUP) return FLR_ERR_WORKSPACE;
   const int64_t nseg = (R + ldc - 1) / ldc;

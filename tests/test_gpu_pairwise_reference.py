@@ -76,6 +76,65 @@ def test_reference_mode_two_chain_tiles(cuda, knob, K, P, two):
     assert np.array_equal(D, normref.distance_matrix(X.numpy()))
 
 
+@pytest.mark.parametrize("K,P,on,form", [(65, 4099, "1", "wg"), (100, 20_011, "1", "wg"), (130, 65_537, "1", "wg"),
+                                         (200, 8, "1", "wg"), (300, 20_011, "1", "wg"), (480, 3001, "", "wg"),
+                                         (512, 20_011, "", "wg"), (520, 1007, "", "wg"), (512, 2053, "0", "wg"),
+                                         (100, 20_011, "1", "sg"), (520, 1007, "", "sg"),
+                                         (65, 4099, "1", "4"), (300, 20_011, "1", "4"), (520, 1007, "", "4"),
+                                         (70, 4099, "1", "8"), (130, 20_011, "1", "8"), (520, 1007, "", "8")])
+def test_reference_mode_sgpr_tiles(cuda, knob, K, P, on, form):
+    """The throughput form (quad_transpose_kernel, then ref_chain_w_kernel: 4-wave
+    workgroups of 8 I rows per wave x one 64-row J block, both staged through
+    LDS; FLR_REF_SGPR_FORM=sgpr: x_i as SGPR operands instead; =wave: the
+    one-wave ref_chain_s_kernel with 4 or FLR_REF_SGPR_ROWS=8 I rows), K >= 480, forced on below it
+    (FLR_REF_SGPR=1) and off at K = 512 (=0): D bit-identical to the C
+    restatement, ragged J blocks and workgroups (K not a multiple of 64) and a
+    single step (P = 8) included."""
+    if on:
+        knob("FLR_REF_SGPR", on)
+    if form == "sg":
+        knob("FLR_REF_SGPR_FORM", "sgpr")
+    elif form != "wg":
+        knob("FLR_REF_SGPR_FORM", "wave")
+        knob("FLR_REF_SGPR_ROWS", form)
+    X, data = _matrix(K, P, 57 + K, cuda)
+    D = ops.pairwise_l2(data[:, :P], "reference").cpu().numpy()
+    assert np.array_equal(D, normref.distance_matrix(X.numpy()))
+
+
+@pytest.mark.parametrize("K,form", [(96, "wg"), (520, "wg"), (96, "4"), (100, "8")])
+def test_reference_mode_sgpr_segmented(cuda, knob, K, form):
+    """The throughput form over a workspace of 1024 chain steps: several
+    segments, each chain continued from A (first = 0), the last segment
+    zero-filled to 512 steps; D bit-identical to the one-segment call."""
+    import ctypes
+    from flr import _capi
+    knob("FLR_REF_SGPR", "1")
+    if form == "sg":
+        knob("FLR_REF_SGPR_FORM", "sgpr")
+    elif form != "wg":
+        knob("FLR_REF_SGPR_FORM", "wave")
+        knob("FLR_REF_SGPR_ROWS", form)
+    P = 8 * 2900 + 3
+    X, data = _matrix(K, P, 23 + K, cuda)
+    lib = _capi.lib()
+    Kp = (K + 63) // 64 * 64
+    a_bytes = (8 * K * K * 4 + 255) // 256 * 256
+    nbytes = a_bytes + Kp * 32 * 1024 + 4096 + 12 * Kp * 16
+    assert nbytes < int(lib.flr_pairwise_l2_reference_workspace(K, P))
+    ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=cuda)
+    wp = (ws.data_ptr() + 255) // 256 * 256
+    D = torch.empty((K, K), dtype=torch.float64, device=cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    _capi.call("flr_pairwise_l2_reference", data.data_ptr(), K, P, data.stride(0), D.data_ptr(), wp, nbytes, 0, 1,
+               st)
+    torch.cuda.synchronize()
+    want = ops.pairwise_l2(data[:, :P], "reference").cpu().numpy()
+    assert np.array_equal(D.cpu().numpy(), want)
+    if K < 128:
+        assert np.array_equal(want, normref.distance_matrix(X.numpy()))
+
+
 @pytest.mark.parametrize("path", golden_files("c3krum"), ids=lambda p: p.split("/")[-1])
 def test_reference_mode_c3_fixtures(cuda, path):
     """The C3-shaped fixtures (K = 128, f = 25 sign-flipped, multi_k = 64):
