@@ -1,0 +1,19 @@
+#!/bin/bash
+# round 6 final (part 1): the -m gpu suite on the final library, in three
+# pytest runs (each under its own limit), then smoke
+set -o pipefail
+O=gpurun_out/r6s
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 700 python -u -m pytest tests/ -x -q -m gpu --timeout 600 --timeout-method thread --ignore=tests/test_gpu_shard.py --ignore=tests/test_gpu_configs.py > $O/gpu_tests_a.log 2>&1 || { echo "gpu tests a failed"; grep -E "^E |FAILED|passed|failed" $O/gpu_tests_a.log | head -20; exit 1; }
+tail -1 $O/gpu_tests_a.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_shard.py -x -q -m gpu --timeout 300 --timeout-method thread > $O/gpu_tests_shard.log 2>&1 || { echo "shard tests failed"; grep -E "^E |FAILED|passed|failed" $O/gpu_tests_shard.log | head -20; exit 1; }
+tail -1 $O/gpu_tests_shard.log
+timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py -x -q -m gpu --timeout 500 --timeout-method thread > $O/gpu_tests_configs.log 2>&1 || { echo "config tests failed"; grep -E "^E |FAILED|passed|failed" $O/gpu_tests_configs.log | head -20; exit 1; }
+tail -1 $O/gpu_tests_configs.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -5 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/c3_bench.json 2> $O/c3_bench.err || { echo "c3 bench failed"; tail -5 $O/c3_bench.err; exit 1; }
+python -c "import json; d=json.loads(open('$O/c3_bench.json').read().strip().splitlines()[-1]); print('C3', d['value'], d.get('sha_matches_reference_run'), d['roofline']['frac'])"
+timeout -k 10 500 python -u bench.py --config C5 --steps 2 --warmup 1 > $O/c5_bench.json 2> $O/c5_bench.err || { echo "c5 bench failed"; tail -5 $O/c5_bench.err; exit 1; }
+python -c "import json; d=json.loads(open('$O/c5_bench.json').read().strip().splitlines()[-1]); print('C5', d['value'], {k: v for k, v in d.items() if 'aggregate' in k or 'distance' in k})"
