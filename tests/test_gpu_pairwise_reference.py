@@ -181,14 +181,17 @@ def test_reference_mode_round_engine(cuda):
 @pytest.mark.parametrize("K,blocks", [
     (16, [(5, 64, 64, 9), (36_869 + 7, 64, 3, 9), (36_869 + 7 + 1728 + 3, 128, 64, 1)]),
     (33, [(0, 128, 64, 9), (73_728 + 1, 40, 24, 9)]),
-    (128, [(100, 512, 256, 9), (100 + 1_179_648 + 13, 64, 64, 1)])])
+    (128, [(100, 512, 256, 9), (100 + 1_179_648 + 13, 64, 64, 1)]),
+    (16, [(0, 64, 64, 9), (36_864, 128, 64, 1), (45_056, 64, 128, 9), (118_784 + 32, 256, 128, 9)]),
+    (24, [(32, 128, 128, 9), (32 + 147_456, 256, 128, 1)])])
 def test_reference_mode_tap_major_blocks(cuda, K, blocks):
     """A training-order matrix (convolution weights stored tap-major, column
     off + (t * Cin + ci) * Cout + co for reference coordinate
     off + (co * Cin + ci) * KK + t) read through flr_pairwise_l2_reference_tap:
     D bit-identical to the reference-order matrix's.  Blocks at odd offsets
     (chain steps shared with the plain columns beside them), partial 32-channel
-    tiles, KK 9 and 1, a block reaching the tail."""
+    tiles, KK 9 and 1, a block reaching the tail; blocks at multiples of 32
+    coordinates (every one of C3's: the 16-B store form of the dense writes)."""
     P = max(o + co * ci * kk for o, co, ci, kk in blocks) + 5
     X, data = _matrix(K, P, 13 + K, cuda)
     train = data.clone()
