@@ -191,9 +191,24 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& hi, bf16x8& 
 // FLR_GEMM=f32 selects the exact-f32 MFMA (A/B timing, cross-checks); read per
 // launch so one process can compare both forms.
 // FLR_XCD=0 turns the XCD-aware tile order off (A/B timing).
+// bit 0: the XCD-aware tile order; A/B (split-at-stash kernels): bits 8-15
+// FLR_GEMM_STAGGER = n, workgroups of odd XCD slot start n x 512 cycles late;
+// bit 16 FLR_GEMM_SPRIO=1, those workgroups at s_setprio 1 for the whole loop
 inline int xcd_remap() {
   const char* e = flr::knob("FLR_XCD");
-  return (e && e[0] == '0') ? 0 : 1;
+  int r = (e && e[0] == '0') ? 0 : 1;
+  const char* st = flr::knob("FLR_GEMM_STAGGER");
+  if (st) r |= (std::min(255, std::max(0, atoi(st))) << 8);
+  const char* sp = flr::knob("FLR_GEMM_SPRIO");
+  if (sp && sp[0] == '1') r |= 1 << 16;
+  return r;
+}
+// the A/B controls above, at the start of a split-at-stash kernel
+__device__ __forceinline__ void odd_slot_controls(int remap) {
+  const int lid = (int)blockIdx.x + (int)gridDim.x * ((int)blockIdx.y + (int)gridDim.y * (int)blockIdx.z);
+  if (((lid >> 3) & 1) == 0) return;
+  if ((remap >> 16) & 1) __builtin_amdgcn_s_setprio(1);
+  for (int i = (remap >> 8) & 255; i > 0; --i) __builtin_amdgcn_s_sleep(8);
 }
 
 // Wave priority raised around each MFMA cluster (FLR_PRIO=0: off, for A/B).
@@ -1372,7 +1387,7 @@ __global__ __launch_bounds__(THREADS, 2) void tgemm_kernel(const Plan pl, int S,
   __shared__ __attribute__((aligned(16))) float As[2][MS][TILE];
   __shared__ __attribute__((aligned(16))) float Bs[2][NS][TILE];
   int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
-  if (remap) xcd_tile(bx, by, bz);
+  if (remap & 1) xcd_tile(bx, by, bz);
   const int k = bz / S, split = bz % S;
   const int M = pl.M(), N = pl.N(), R = pl.R();
   const int ktiles = cdiv(R, BK);
@@ -1808,7 +1823,8 @@ __device__ __forceinline__ void sgemm_body(const Plan& pl, int S, float* __restr
   constexpr int NST = 1;
   __shared__ __attribute__((aligned(16))) __bf16 Ls[NST][MS + NS][3][TERM_B];
   int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
-  if (remap) xcd_tile(bx, by, bz);
+  if (remap & 1) xcd_tile(bx, by, bz);
+  if (remap >> 8) odd_slot_controls(remap);
   const int k = bz / S, split = bz % S;
   const int M = pl.M(), N = pl.N(), R = pl.R();
   const int ktiles = cdiv(R, BK);
@@ -1997,7 +2013,7 @@ __global__ __launch_bounds__(THREADS, 2) void dsgemm_kernel(const Plan pl, int S
   constexpr int MSW = 2, NS = 2;
   __shared__ __attribute__((aligned(16))) float Lf[2][2][DG_IMG];  // [stage][A, B]
   int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
-  if (remap) xcd_tile(bx, by, bz);
+  if (remap & 1) xcd_tile(bx, by, bz);
   const int k = bz / S, split = bz % S;
   const int M = pl.M(), N = pl.N(), R = pl.R();
   const int ktiles = cdiv(R, BK);
@@ -2172,7 +2188,7 @@ __global__ __launch_bounds__(THREADS, 2) void psgemm_kernel(const Plan pl, int S
   constexpr int MSW = 2, NS = 2;
   __shared__ __attribute__((aligned(16))) __bf16 L[PS_NST * PS_STAGE];  // one array: no compiler vmcnt(0)
   int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
-  if (remap) xcd_tile(bx, by, bz);
+  if (remap & 1) xcd_tile(bx, by, bz);
   const int k = bz / S, split = bz % S;
   const int M = pl.M(), N = pl.N(), R = pl.R();
   const int ktiles = cdiv(R, BK);
@@ -2295,7 +2311,8 @@ __global__ __launch_bounds__(THREADS, FLR_SG_OCC) void wsgemm_kernel(const Plan 
   constexpr int IMG = (TA || TB) && !(TA && TB) ? TERM_B : (TA ? TIMG : TERM_B);
   __shared__ __attribute__((aligned(16))) __bf16 Lt[MS + NS][3][IMG];
   int bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
-  if (remap) xcd_tile(bx, by, bz);
+  if (remap & 1) xcd_tile(bx, by, bz);
+  if (remap >> 8) odd_slot_controls(remap);
   const int k = bz / S, split = bz % S;
   const int M = pl.M(), N = pl.N(), R = pl.R();
   const int ktiles = cdiv(R, BK);
